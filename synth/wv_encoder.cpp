@@ -1,0 +1,1171 @@
+// wv_encoder.cpp -- synthetic WavPack-4 stream generator (test/bench input
+// infrastructure; never part of the decode path).
+//
+// There is no WavPack encoder, library or .wv file anywhere in this image and
+// the reference ships none, so every test vector is made
+// here.  Each encode step is derived as the exact inverse of the reference
+// decode step it feeds:
+//   * get_words (WordsUtils.cs:272-511): the same median / holding / zero-run /
+//     escape / hybrid error_limit state machine, run forwards, choosing bits;
+//   * decorr passes (UnpackUtils.cs:688-1240): each pass inverted per frame;
+//   * joint stereo (UnpackUtils.cs:615) inverted;
+//   * metadata written so that the reference readers (UnpackUtils.cs:156-360,
+//     WordsUtils.cs:75-187) reconstruct exactly the encoder's start state --
+//     including the read_decorr_samples "last term" quirk (Appendix B-7),
+//     which the encoder simulates instead of assuming;
+//   * DSD modes 0/1/3 (DsdUtils.cs): range encoders mirroring decode_fast /
+//     decode_high bit for bit.
+// The hybrid path is closed-loop: the encoder decorrelates against the
+// decoder's reconstruction, so decode(encode(x)) is what the reference returns.
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../wavpackdecoder_amd/csrc/wv_format.h"
+
+using namespace wvf;
+
+extern "C" {
+struct wvenc_params {
+    int32_t nch;               // 1 or 2 input channels
+    int32_t bytes_per_sample;  // 1..4 (BYTES_STORED + 1)
+    int32_t shift;             // header SHIFT field; input low `shift` bits must be 0
+    int32_t joint_stereo;
+    int32_t false_stereo;      // nch == 2 with L == R, written as a mono FALSE_STEREO block
+    int32_t num_terms;
+    int32_t terms[16];         // encoder order (the decoder's reversed)
+    int32_t deltas[16];
+    int32_t block_samples;
+    int32_t sample_rate;
+    int32_t version;           // 0x402..0x410
+    int32_t hybrid;
+    int32_t hybrid_bitrate;
+    int32_t hybrid_balance;
+    int32_t bitrate_x256;      // hybrid bitrate in 8.8 log2 units (e.g. 3.5 bits -> 896)
+    int32_t float_data;        // input ints are float mantissas (see synth/wvsynth.py)
+    int32_t float_flags, float_shift, float_max_exp, float_norm_exp;
+    int32_t int32_zeros;       // INT32_DATA with `zeros` trailing zero bits
+    int32_t write_riff;        // RIFF header/trailer sub-blocks
+    int32_t config_flags;      // CONFIG_BLOCK payload (0 = none)
+    int32_t write_history;     // DECORR_SAMPLES carried from the previous block
+    int32_t reset_state;       // 1: every block starts from zero weights/medians
+    int32_t block_index_start;
+    int32_t total_unknown;     // write total_samples = 0xFFFFFFFF
+    int32_t extras;            // bit0: DUMMY sub-block, bit1: unknown optional sub-block, bit2: NEW_CONFIG
+    int32_t mag_override;      // >= 0 forces the MAG field
+};
+
+struct wvenc_dsd_params {
+    int32_t nch;           // 1 or 2
+    int32_t false_stereo;  // nch == 2 with identical channels
+    int32_t mode;          // 0 raw, 1 fast, 3 high
+    int32_t block_samples; // DSD bytes per channel per block
+    int32_t rate_multiplier_log2;  // first DSD_BLOCK byte
+    int32_t sample_rate;   // header sample rate (44100 typical)
+    int32_t history_bits;  // mode 1: 0..5
+    int32_t rle_tables;    // mode 1: RLE-coded probability tables (else raw 0xFF form)
+    int32_t rate_i;        // mode 3
+};
+}
+
+namespace {
+
+// -------------------------------------------------------------------------
+// bit writer: LSB-first within bytes, the order BitsUtils.getbit reads
+// -------------------------------------------------------------------------
+struct BitWriter {
+    std::vector<uint8_t> out;
+    uint64_t acc = 0;
+    int n = 0;
+    void put(uint64_t bits, int count) {
+        while (count > 0) {
+            int take = count > 32 ? 32 : count;
+            acc |= (bits & ((take == 64) ? ~0ull : ((1ull << take) - 1))) << n;
+            n += take;
+            bits >>= take;
+            count -= take;
+            while (n >= 8) {
+                out.push_back((uint8_t)acc);
+                acc >>= 8;
+                n -= 8;
+            }
+        }
+    }
+    void bit(int b) { put((uint64_t)(b & 1), 1); }
+    void ones(uint32_t count) {
+        while (count >= 32) {
+            put(0xffffffffull, 32);
+            count -= 32;
+        }
+        if (count) put((1ull << count) - 1, (int)count);
+    }
+    std::vector<uint8_t> finish() {
+        if (n > 0) out.push_back((uint8_t)acc);
+        acc = 0;
+        n = 0;
+        return out;
+    }
+};
+
+// Elias-gamma-like count (decoder: WordsUtils.cs:321-335 and 391-405)
+void put_gamma(BitWriter &bw, uint32_t v) {
+    if (v < 2) {
+        bw.ones(v);
+        bw.bit(0);
+        return;
+    }
+    int cb = count_bits_u32(v);
+    bw.ones((uint32_t)cb);
+    bw.bit(0);
+    bw.put(v, cb - 1);  // low cb-1 bits, LSB first; top bit implied
+}
+
+// unary ones_count with the LIMIT_ONES escape (WordsUtils.cs:354-409)
+void put_unary(BitWriter &bw, uint32_t u) {
+    if (u < (uint32_t)LIMIT_ONES) {
+        bw.ones(u);
+        bw.bit(0);
+    } else {
+        bw.ones(LIMIT_ONES);
+        bw.bit(0);
+        put_gamma(bw, u - LIMIT_ONES);
+    }
+}
+
+struct EntropyState {
+    int32_t med[2][3] = {{0, 0, 0}, {0, 0, 0}};
+    int32_t slow_level[2] = {0, 0};
+    int32_t error_limit[2] = {0, 0};
+    int64_t bitrate_acc[2] = {0, 0};
+    int64_t bitrate_delta[2] = {0, 0};
+};
+
+int32_t get_med(int32_t m) { return add32(m >> 4, 1); }
+
+// ones_count of a folded value without touching state (the decoder's
+// low/high ladder, WordsUtils.cs:433-475)
+uint32_t ones_for(const int32_t *med, uint32_t u) {
+    uint32_t m0 = (uint32_t)get_med(med[0]);
+    if (u < m0) return 0;
+    uint32_t rem = u - m0;
+    uint32_t m1 = (uint32_t)get_med(med[1]);
+    if (rem < m1) return 1;
+    rem -= m1;
+    uint32_t m2 = (uint32_t)get_med(med[2]);
+    if (rem < m2) return 2;
+    return 2 + rem / m2;
+}
+
+// mirror of update_error_limit (WordsUtils.cs:195-261)
+void update_error_limit(EntropyState &w, uint32_t flags) {
+    int bitrate_0 = (int)((w.bitrate_acc[0] += w.bitrate_delta[0]) >> 16);
+    if (flags & MONO_DATA) {
+        if (flags & HYBRID_BITRATE) {
+            int slow_log_0 = add32(w.slow_level[0], SLO) >> SLS;
+            w.error_limit[0] = (slow_log_0 - bitrate_0 > -0x100) ? exp2s_host(slow_log_0 - bitrate_0 + 0x100) : 0;
+        } else
+            w.error_limit[0] = exp2s_host(bitrate_0);
+    } else {
+        int bitrate_1 = (int)((w.bitrate_acc[1] += w.bitrate_delta[1]) >> 16);
+        if (flags & HYBRID_BITRATE) {
+            int slow_log_0 = add32(w.slow_level[0], SLO) >> SLS;
+            int slow_log_1 = add32(w.slow_level[1], SLO) >> SLS;
+            if (flags & HYBRID_BALANCE) {
+                int balance = (slow_log_1 - slow_log_0 + bitrate_1 + 1) >> 1;
+                if (balance > bitrate_0) {
+                    bitrate_1 = bitrate_0 * 2;
+                    bitrate_0 = 0;
+                } else if (-balance > bitrate_0) {
+                    bitrate_0 = bitrate_0 * 2;
+                    bitrate_1 = 0;
+                } else {
+                    bitrate_1 = bitrate_0 + balance;
+                    bitrate_0 = bitrate_0 - balance;
+                }
+            }
+            w.error_limit[0] = (slow_log_0 - bitrate_0 > -0x100) ? exp2s_host(slow_log_0 - bitrate_0 + 0x100) : 0;
+            w.error_limit[1] = (slow_log_1 - bitrate_1 > -0x100) ? exp2s_host(slow_log_1 - bitrate_1 + 0x100) : 0;
+        } else {
+            w.error_limit[0] = exp2s_host(bitrate_0);
+            w.error_limit[1] = exp2s_host(bitrate_1);
+        }
+    }
+}
+
+// -------------------------------------------------------------------------
+// Entropy encoder: get_words run forwards.  Words are fed one at a time in
+// decode order; a normal word's unary code needs the next word's ones_count
+// (the holding_one/holding_zero pairing), so it is emitted one word late.
+// -------------------------------------------------------------------------
+struct WordEncoder {
+    BitWriter bw;
+    EntropyState w;
+    uint32_t flags;
+    bool mono;
+    bool H1 = false, H0 = false;  // decoder's holding_one / holding_zero before the next word
+    int64_t run = 0;              // zeros accumulated in the current run (zeros_acc)
+    bool in_run = false;
+    // pending normal word
+    bool pend = false;
+    uint32_t pend_ubase = 0;
+    uint64_t pend_tail = 0;
+    int pend_tail_n = 0;
+    int64_t csamples = 0;  // word counter inside the block (parity picks the channel)
+
+    explicit WordEncoder(uint32_t f) : flags(f), mono((f & MONO_DATA) != 0) {}
+
+    int chan_of(int64_t cs) const { return mono ? 0 : (int)(cs & 1); }
+
+    bool run_check() const {
+        return (w.med[0][0] & ~1) == 0 && !H0 && !H1 && (w.med[1][0] & ~1) == 0;
+    }
+
+    void flush_pending(int b) {
+        if (!pend) return;
+        put_unary(bw, pend_ubase + (uint32_t)b);
+        bw.put(pend_tail, pend_tail_n);
+        pend = false;
+    }
+    void flush_run() {
+        if (in_run) {
+            put_gamma(bw, (uint32_t)run);
+            in_run = false;
+            run = 0;
+        }
+    }
+
+    // Encode one residual; returns the decoder's reconstruction of it.
+    int32_t word(int32_t value) {
+        int c = chan_of(csamples);
+        int64_t cs = csamples++;
+
+        // a pending normal word learns whether this word's ones_count >= 1
+        if (pend) {
+            uint32_t u = value < 0 ? ~(uint32_t)value : (uint32_t)value;
+            uint32_t ones_next = ones_for(w.med[c], u);
+            int b = ones_next >= 1 ? 1 : 0;
+            flush_pending(b);
+            H1 = b;
+            H0 = !b;
+        }
+
+        if (run_check() || in_run) {
+            // zero-run mode (WordsUtils.cs:304-352)
+            if (in_run) {
+                if (value == 0) {
+                    w.slow_level[c] = sub32(w.slow_level[c], add32(w.slow_level[c], SLO) >> SLS);
+                    run++;
+                    return 0;
+                }
+                flush_run();  // the decoder falls through on this word with zeros_acc == 0
+            } else if (value == 0) {
+                in_run = true;
+                run = 1;
+                w.slow_level[c] = sub32(w.slow_level[c], add32(w.slow_level[c], SLO) >> SLS);
+                for (int k = 0; k < 3; k++) w.med[0][k] = w.med[1][k] = 0;
+                return 0;
+            } else {
+                put_gamma(bw, 0);  // zeros_acc == 0: normal word follows
+            }
+        }
+
+        uint32_t u = value < 0 ? ~(uint32_t)value : (uint32_t)value;
+        int sign = value < 0 ? 1 : 0;
+        bool h0_word = H0;
+        uint32_t ones;
+        uint32_t ubase = 0;
+        if (h0_word) {
+            H0 = false;
+            ones = 0;
+            if (ones_for(w.med[c], u) != 0) throw std::runtime_error("holding_zero violated");
+        } else {
+            ones = ones_for(w.med[c], u);
+            uint32_t h = H1 ? 1 : 0;
+            ubase = 2 * (ones - h);
+        }
+
+        if ((flags & HYBRID_FLAG) && (mono || (cs & 1) == 0)) update_error_limit(w, flags);
+
+        // low/high + median adaptation, exactly as the decoder
+        int32_t *m = w.med[c];
+        int64_t low, high;
+        if (ones == 0) {
+            low = 0;
+            high = (int64_t)get_med(m[0]) - 1;
+            m[0] = sub32(m[0], mul32(add32(m[0], 128 - 2) >> 7, 2));
+        } else {
+            low = get_med(m[0]);
+            m[0] = add32(m[0], mul32(add32(m[0], 128) >> 7, 5));
+            if (ones == 1) {
+                high = low + get_med(m[1]) - 1;
+                m[1] = sub32(m[1], mul32(add32(m[1], 64 - 2) >> 6, 2));
+            } else {
+                low += get_med(m[1]);
+                m[1] = add32(m[1], mul32(add32(m[1], 64) >> 6, 5));
+                if (ones == 2) {
+                    high = low + get_med(m[2]) - 1;
+                    m[2] = sub32(m[2], mul32(add32(m[2], 32 - 2) >> 5, 2));
+                } else {
+                    low += (int64_t)mul32((int32_t)ones - 2, get_med(m[2]));
+                    high = low + get_med(m[2]) - 1;
+                    m[2] = add32(m[2], mul32(add32(m[2], 32) >> 5, 5));
+                }
+            }
+        }
+
+        BitWriter tail;
+        int64_t mid;
+        if (w.error_limit[c] == 0) {
+            // read_code inverse (WordsUtils.cs:546-570)
+            uint32_t maxcode = (uint32_t)(high - low), code = (uint32_t)(u - (uint32_t)low);
+            if ((int64_t)u < low || (int64_t)u > high) throw std::runtime_error("value outside code interval");
+            int bitcount = count_bits_u32(maxcode);
+            if (bitcount) {
+                uint32_t extras = (uint32_t)((1ull << bitcount) - maxcode - 1);
+                if (code < extras)
+                    tail.put(code, bitcount - 1);
+                else {
+                    tail.put((code + extras) >> 1, bitcount - 1);
+                    tail.bit((code + extras) & 1);
+                }
+            }
+            mid = u;
+        } else {
+            mid = (high + low + 1) >> 1;
+            while (high - low > w.error_limit[c]) {
+                if ((int64_t)u < mid) {
+                    tail.bit(0);
+                    high = mid - 1;
+                    mid = (high + low + 1) >> 1;
+                } else {
+                    tail.bit(1);
+                    low = mid;
+                    mid = (high + low + 1) >> 1;
+                }
+            }
+        }
+        tail.bit(sign);
+        uint64_t tbits = tail.acc;
+        int tn = tail.n;
+        // tail never exceeds 64 bits: collect bytes already flushed
+        if (!tail.out.empty()) {
+            uint64_t all = 0;
+            int pos = 0;
+            for (uint8_t byte : tail.out) {
+                all |= (uint64_t)byte << pos;
+                pos += 8;
+            }
+            all |= tbits << pos;
+            tbits = all;
+            tn += pos;
+        }
+
+        if (flags & HYBRID_BITRATE)
+            w.slow_level[c] = add32(sub32(w.slow_level[c], add32(w.slow_level[c], SLO) >> SLS), mylog2_host(mid));
+
+        if (h0_word) {
+            bw.put(tbits, tn);  // no unary part; H0 = H1 = false for the next word
+        } else {
+            pend = true;
+            pend_ubase = ubase;
+            pend_tail = tbits;
+            pend_tail_n = tn;
+        }
+        return sign ? (int32_t)~(uint32_t)mid : (int32_t)mid;
+    }
+
+    std::vector<uint8_t> finish() {
+        flush_pending(0);
+        flush_run();
+        return bw.finish();
+    }
+};
+
+// -------------------------------------------------------------------------
+// decorrelation passes (decoder order), forward = decoder, inverse = encoder
+// -------------------------------------------------------------------------
+struct Pass {
+    int term = 0, delta = 0;
+    int32_t wA = 0, wB = 0;
+    int32_t sA[8] = {0}, sB[8] = {0};  // decoder representation (see UnpackUtils.cs:688-944)
+};
+
+inline void upd(int32_t &w, int32_t s, int32_t b, int delta) {
+    if (s != 0 && b != 0) w += ((s ^ b) < 0) ? -delta : delta;
+}
+inline void updc(int32_t &w, int32_t s, int32_t b, int delta) {
+    if ((s ^ b) < 0) {
+        if (s != 0 && b != 0 && (w -= delta) < -1024) w = w < 0 ? -1024 : 1024;
+    } else {
+        if (s != 0 && b != 0 && (w += delta) > 1024) w = w < 0 ? -1024 : 1024;
+    }
+}
+
+// prediction source of a positive-term pass for one channel
+inline int32_t pos_pred(const int32_t *s, int term) {
+    if (term == 17) return sub32(mul32(2, s[0]), s[1]);
+    if (term == 18) return sub32(mul32(3, s[0]), s[1]) >> 1;
+    return s[0];  // ring kept shifted so s[0] is `term` frames back
+}
+inline void pos_push(int32_t *s, int term, int32_t out) {
+    if (term >= 17) {
+        s[1] = s[0];
+        s[0] = out;
+    } else {
+        // s[i] = output (term - i) frames back, i < term; shift left
+        for (int i = 0; i < term - 1; i++) s[i] = s[i + 1];
+        s[term - 1] = out;
+    }
+}
+
+// decoder step of one stereo pass on one frame: in -> out (UnpackUtils.cs:688-944)
+inline void pass_fwd_stereo(Pass &p, int32_t inL, int32_t inR, int32_t &outL, int32_t &outR) {
+    int d = p.delta;
+    switch (p.term) {
+    case -1: {
+        outL = add32(inL, apply_weight(p.wA, p.sA[0]));
+        updc(p.wA, p.sA[0], inL, d);
+        outR = add32(inR, apply_weight(p.wB, outL));
+        updc(p.wB, outL, inR, d);
+        p.sA[0] = outR;
+        break;
+    }
+    case -2: {
+        outR = add32(inR, apply_weight(p.wB, p.sB[0]));
+        updc(p.wB, p.sB[0], inR, d);
+        outL = add32(inL, apply_weight(p.wA, outR));
+        updc(p.wA, outR, inL, d);
+        p.sB[0] = outL;
+        break;
+    }
+    case -3: {
+        outL = add32(inL, apply_weight(p.wA, p.sA[0]));
+        updc(p.wA, p.sA[0], inL, d);
+        outR = add32(inR, apply_weight(p.wB, p.sB[0]));
+        updc(p.wB, p.sB[0], inR, d);
+        p.sB[0] = outL;
+        p.sA[0] = outR;
+        break;
+    }
+    default: {
+        int32_t pa = pos_pred(p.sA, p.term), pb = pos_pred(p.sB, p.term);
+        outL = add32(apply_weight(p.wA, pa), inL);
+        upd(p.wA, pa, inL, d);
+        outR = add32(apply_weight(p.wB, pb), inR);
+        upd(p.wB, pb, inR, d);
+        pos_push(p.sA, p.term, outL);
+        pos_push(p.sB, p.term, outR);
+    }
+    }
+}
+
+// encoder inverse, no state update: out -> in
+inline void pass_inv_stereo(const Pass &p, int32_t outL, int32_t outR, int32_t &inL, int32_t &inR) {
+    switch (p.term) {
+    case -1:
+        inL = sub32(outL, apply_weight(p.wA, p.sA[0]));
+        inR = sub32(outR, apply_weight(p.wB, outL));
+        break;
+    case -2:
+        inR = sub32(outR, apply_weight(p.wB, p.sB[0]));
+        inL = sub32(outL, apply_weight(p.wA, outR));
+        break;
+    case -3:
+        inL = sub32(outL, apply_weight(p.wA, p.sA[0]));
+        inR = sub32(outR, apply_weight(p.wB, p.sB[0]));
+        break;
+    default:
+        inL = sub32(outL, apply_weight(p.wA, pos_pred(p.sA, p.term)));
+        inR = sub32(outR, apply_weight(p.wB, pos_pred(p.sB, p.term)));
+    }
+}
+
+inline int32_t pass_fwd_mono(Pass &p, int32_t in) {
+    int32_t pa = pos_pred(p.sA, p.term);
+    int32_t out = add32(apply_weight(p.wA, pa), in);
+    upd(p.wA, pa, in, p.delta);
+    pos_push(p.sA, p.term, out);
+    return out;
+}
+inline int32_t pass_inv_mono(const Pass &p, int32_t out) { return sub32(out, apply_weight(p.wA, pos_pred(p.sA, p.term))); }
+
+// convert between the encoder's shifted ring (s[0] = oldest needed) and the
+// decoder's post-call representation (identical for m == 0; UnpackUtils.cs:900-917)
+// -- they coincide: decoder slot i holds output (term - i) frames back.
+
+// -------------------------------------------------------------------------
+// metadata helpers
+// -------------------------------------------------------------------------
+void put_subblock(std::vector<uint8_t> &blk, uint8_t id, const std::vector<uint8_t> &data) {
+    size_t len = data.size();
+    size_t words = (len + 1) / 2;
+    uint8_t idb = id;
+    if (len & 1) idb |= ID_ODD_SIZE;
+    if (words > 255) {
+        idb |= ID_LARGE;
+        blk.push_back(idb);
+        blk.push_back((uint8_t)words);
+        blk.push_back((uint8_t)(words >> 8));
+        blk.push_back((uint8_t)(words >> 16));
+    } else {
+        blk.push_back(idb);
+        blk.push_back((uint8_t)words);
+    }
+    blk.insert(blk.end(), data.begin(), data.end());
+    if (len & 1) blk.push_back(0);
+}
+
+void le16(std::vector<uint8_t> &v, int x) {
+    v.push_back((uint8_t)x);
+    v.push_back((uint8_t)(x >> 8));
+}
+
+int srate_index(int rate) {
+    static const int rates[15] = {6000,  8000,  9600,  11025, 12000, 16000, 22050, 24000,
+                                  32000, 44100, 48000, 64000, 88200, 96000, 192000};
+    for (int i = 0; i < 15; i++)
+        if (rates[i] == rate) return i;
+    return 15;
+}
+
+void write_header(std::vector<uint8_t> &blk, int version, int64_t total, int64_t block_index, uint32_t block_samples,
+                  uint32_t flags, int32_t crc, bool total_unknown) {
+    uint32_t ck = (uint32_t)(blk.size() - 8);
+    uint8_t *h = blk.data();
+    memcpy(h, "wvpk", 4);
+    h[4] = (uint8_t)ck;
+    h[5] = (uint8_t)(ck >> 8);
+    h[6] = (uint8_t)(ck >> 16);
+    h[7] = (uint8_t)(ck >> 24);
+    h[8] = (uint8_t)version;
+    h[9] = (uint8_t)(version >> 8);
+    uint64_t ts = total_unknown ? 0xFFFFFFFFull : (uint64_t)total;
+    h[10] = (uint8_t)((uint64_t)block_index >> 32);
+    h[11] = (uint8_t)(ts >> 32);
+    h[12] = (uint8_t)ts;
+    h[13] = (uint8_t)(ts >> 8);
+    h[14] = (uint8_t)(ts >> 16);
+    h[15] = (uint8_t)(ts >> 24);
+    h[16] = (uint8_t)block_index;
+    h[17] = (uint8_t)(block_index >> 8);
+    h[18] = (uint8_t)(block_index >> 16);
+    h[19] = (uint8_t)(block_index >> 24);
+    h[20] = (uint8_t)block_samples;
+    h[21] = (uint8_t)(block_samples >> 8);
+    h[22] = (uint8_t)(block_samples >> 16);
+    h[23] = (uint8_t)(block_samples >> 24);
+    h[24] = (uint8_t)flags;
+    h[25] = (uint8_t)(flags >> 8);
+    h[26] = (uint8_t)(flags >> 16);
+    h[27] = (uint8_t)(flags >> 24);
+    h[28] = (uint8_t)crc;
+    h[29] = (uint8_t)(crc >> 8);
+    h[30] = (uint8_t)(crc >> 16);
+    h[31] = (uint8_t)(crc >> 24);
+}
+
+std::vector<uint8_t> riff_header(int nch, int bps, int bits, int rate, int64_t frames) {
+    std::vector<uint8_t> h(44);
+    uint32_t data = (uint32_t)(frames * nch * bps);
+    auto w32 = [&](int o, uint32_t v) {
+        h[o] = (uint8_t)v;
+        h[o + 1] = (uint8_t)(v >> 8);
+        h[o + 2] = (uint8_t)(v >> 16);
+        h[o + 3] = (uint8_t)(v >> 24);
+    };
+    memcpy(&h[0], "RIFF", 4);
+    w32(4, data + 36);
+    memcpy(&h[8], "WAVEfmt ", 8);
+    w32(16, 16);
+    h[20] = 1;
+    h[22] = (uint8_t)nch;
+    w32(24, (uint32_t)rate);
+    w32(28, (uint32_t)(rate * nch * bps));
+    h[32] = (uint8_t)(nch * bps);
+    h[34] = (uint8_t)bits;
+    memcpy(&h[36], "data", 4);
+    w32(40, data);
+    return h;
+}
+
+// -------------------------------------------------------------------------
+// PCM file encoder
+// -------------------------------------------------------------------------
+struct PcmEncoder {
+    const wvenc_params &P;
+    std::vector<Pass> passes;  // decoder order
+    EntropyState ent;
+    // previous block's final outputs per pass (for history metadata)
+    explicit PcmEncoder(const wvenc_params &p) : P(p) {}
+
+    int nterms() const { return P.num_terms; }
+
+    std::vector<uint8_t> encode(const int32_t *x, int64_t frames) {
+        std::vector<uint8_t> file;
+        const bool mono_block = P.nch == 1 || P.false_stereo;
+        const int wch = mono_block ? 1 : 2;  // channels actually coded
+        const int n = P.num_terms;
+        passes.assign(n, Pass());
+        for (int d = 0; d < n; d++) {
+            int e = n - 1 - d;
+            passes[d].term = P.terms[e];
+            passes[d].delta = P.deltas[e];
+        }
+        const int64_t B = P.block_samples;
+        int64_t nblocks = frames == 0 ? 0 : (frames + B - 1) / B;
+        int zeros = P.int32_zeros;
+        for (int64_t bi = 0; bi < nblocks; bi++) {
+            int64_t f0 = bi * B;
+            int64_t nf = std::min<int64_t>(B, frames - f0);
+            if (P.reset_state) {
+                for (auto &p : passes) {
+                    p.wA = p.wB = 0;
+                    memset(p.sA, 0, sizeof(p.sA));
+                    memset(p.sB, 0, sizeof(p.sB));
+                }
+                ent = EntropyState();
+            }
+            {   // read_entropy_vars builds a fresh words_data (WordsUtils.cs:80): only
+                // the medians (and, via HYBRID_PROFILE, slow_level/bitrate) survive
+                EntropyState fresh;
+                memcpy(fresh.med, ent.med, sizeof(fresh.med));
+                if (P.hybrid && P.hybrid_bitrate) memcpy(fresh.slow_level, ent.slow_level, sizeof(fresh.slow_level));
+                ent = fresh;
+            }
+            // ---- flags
+            uint32_t flags = (uint32_t)(P.bytes_per_sample - 1) & BYTES_STORED;
+            if (P.nch == 1) flags |= MONO_FLAG;
+            if (P.false_stereo) flags |= FALSE_STEREO;
+            if (!mono_block && P.joint_stereo) flags |= JOINT_STEREO;
+            for (int k = 0; k < n; k++)
+                if (P.terms[k] < 0) flags |= CROSS_DECORR;
+            if (P.hybrid) flags |= HYBRID_FLAG;
+            if (P.hybrid && P.hybrid_bitrate) flags |= HYBRID_BITRATE;
+            if (P.hybrid && P.hybrid_balance && !mono_block) flags |= HYBRID_BALANCE;
+            if (P.float_data) flags |= FLOAT_DATA;
+            if (zeros) flags |= INT32_DATA;
+            flags |= INITIAL_BLOCK | FINAL_BLOCK;
+            flags |= ((uint32_t)P.shift << SHIFT_LSB) & SHIFT_MASK;
+            flags |= (uint32_t)srate_index(P.sample_rate) << SRATE_LSB;
+
+            // ---- metadata reflecting the start state (quantized the way the
+            // decoder will restore it)
+            std::vector<uint8_t> md;
+            if (bi == 0 && P.write_riff) {
+                int bps = P.float_data ? 4 : P.bytes_per_sample;
+                int bits = P.float_data ? 32 : P.bytes_per_sample * 8 - P.shift;
+                put_subblock(md, ID_RIFF_HEADER, riff_header(P.nch, bps, bits, P.sample_rate, frames));
+            }
+            if (bi == 0 && P.config_flags) {
+                std::vector<uint8_t> cfg = {(uint8_t)(P.config_flags >> 8), (uint8_t)(P.config_flags >> 16),
+                                            (uint8_t)(P.config_flags >> 24)};
+                put_subblock(md, ID_CONFIG_BLOCK, cfg);
+            }
+            if (P.extras & 4) put_subblock(md, ID_NEW_CONFIG_BLOCK, std::vector<uint8_t>{0, 0});
+            if (P.extras & 1) put_subblock(md, ID_DUMMY, std::vector<uint8_t>{1, 2, 3, 4});
+            if (P.extras & 2) put_subblock(md, ID_OPTIONAL_DATA | 0x1d, std::vector<uint8_t>{9, 9, 9});
+            if (srate_index(P.sample_rate) == 15) {
+                std::vector<uint8_t> sr = {(uint8_t)P.sample_rate, (uint8_t)(P.sample_rate >> 8),
+                                           (uint8_t)(P.sample_rate >> 16)};
+                put_subblock(md, ID_SAMPLE_RATE, sr);
+            }
+            {  // terms (encoder order)
+                std::vector<uint8_t> t;
+                for (int e = 0; e < n; e++) t.push_back((uint8_t)(((P.terms[e] + 5) & 0x1f) | ((P.deltas[e] & 7) << 5)));
+                put_subblock(md, ID_DECORR_TERMS, t);
+            }
+            if (n) {  // weights, encoder order; the decoder fills from its last pass
+                std::vector<uint8_t> wt;
+                for (int e = 0; e < n; e++) {
+                    Pass &p = passes[n - 1 - e];
+                    int8_t a = store_weight(p.wA);
+                    wt.push_back((uint8_t)a);
+                    p.wA = restore_weight(a);
+                    if (!mono_block) {
+                        int8_t b = store_weight(p.wB);
+                        wt.push_back((uint8_t)b);
+                        p.wB = restore_weight(b);
+                    } else
+                        p.wB = 0;
+                }
+                put_subblock(md, ID_DECORR_WEIGHTS, wt);
+            }
+            if (n && P.write_history) {
+                // Entries for every pass, decoder index n-1 down to 0, all in the
+                // layout of the decoder's LAST pass term (quirk B-7); then the
+                // start state is whatever read_decorr_samples rebuilds.
+                int T0 = passes[n - 1].term;
+                std::vector<uint8_t> sm;
+                for (int d = n - 1; d >= 0; d--) {
+                    Pass &p = passes[d];
+                    auto put_log = [&](int32_t v) { le16(sm, (int16_t)log2s_host(v)); };
+                    if (T0 > MAX_TERM) {
+                        put_log(p.sA[0]);
+                        put_log(p.sA[1]);
+                        if (!mono_block) {
+                            put_log(p.sB[0]);
+                            put_log(p.sB[1]);
+                        }
+                    } else if (T0 < 0) {
+                        put_log(p.sA[0]);
+                        put_log(p.sB[0]);
+                    } else {
+                        for (int m = 0; m < T0; m++) {
+                            put_log(p.sA[m]);
+                            if (!mono_block) put_log(p.sB[m]);
+                        }
+                    }
+                }
+                put_subblock(md, ID_DECORR_SAMPLES, sm);
+                // simulate UnpackUtils.cs:250-360 on those bytes
+                int32_t tA[8] = {0}, tB[8] = {0};
+                size_t c = 0;
+                auto rd = [&](size_t o) { return exp2s_host((int16_t)(sm[o] | (sm[o + 1] << 8))); };
+                for (int d = n - 1; d >= 0; d--) {
+                    if (T0 > MAX_TERM) {
+                        tA[0] = rd(c);
+                        tA[1] = rd(c + 2);
+                        c += 4;
+                        if (!mono_block) {
+                            tB[0] = rd(c);
+                            tB[1] = rd(c + 2);
+                            c += 4;
+                        }
+                    } else if (T0 < 0) {
+                        tA[0] = rd(c);
+                        tB[0] = rd(c + 2);
+                        c += 4;
+                    } else {
+                        for (int m = 0; m < T0; m++) {
+                            tA[m] = rd(c);
+                            c += 2;
+                            if (!mono_block) {
+                                tB[m] = rd(c);
+                                c += 2;
+                            }
+                        }
+                    }
+                    memcpy(passes[d].sA, tA, sizeof(tA));
+                    memcpy(passes[d].sB, tB, sizeof(tB));
+                }
+            } else {
+                for (auto &p : passes) {
+                    memset(p.sA, 0, sizeof(p.sA));
+                    memset(p.sB, 0, sizeof(p.sB));
+                }
+            }
+            {  // entropy medians (stored as mylog2, restored with exp2s)
+                std::vector<uint8_t> ev;
+                for (int c = 0; c < (mono_block ? 1 : 2); c++)
+                    for (int k = 0; k < 3; k++) {
+                        int lg = mylog2_host((uint32_t)ent.med[c][k]);
+                        le16(ev, lg);
+                        ent.med[c][k] = exp2s_host(lg);
+                    }
+                if (mono_block)
+                    for (int k = 0; k < 3; k++) ent.med[1][k] = 0;
+                put_subblock(md, ID_ENTROPY_VARS, ev);
+            }
+            if (P.hybrid) {
+                std::vector<uint8_t> hp;
+                if (P.hybrid_bitrate) {
+                    for (int c = 0; c < (mono_block ? 1 : 2); c++) {
+                        int lg = mylog2_host((uint32_t)ent.slow_level[c]);
+                        le16(hp, lg);
+                        ent.slow_level[c] = exp2s_host(lg);
+                    }
+                }
+                for (int c = 0; c < (mono_block ? 1 : 2); c++) {
+                    le16(hp, P.bitrate_x256);
+                    ent.bitrate_acc[c] = (int64_t)shl32(P.bitrate_x256 & 0xffff, 16);
+                    ent.bitrate_delta[c] = 0;
+                }
+                put_subblock(md, ID_HYBRID_PROFILE, hp);
+            } else {
+                ent.bitrate_acc[0] = ent.bitrate_acc[1] = 0;
+                ent.bitrate_delta[0] = ent.bitrate_delta[1] = 0;
+                ent.error_limit[0] = ent.error_limit[1] = 0;
+            }
+            if (P.float_data) {
+                std::vector<uint8_t> fi = {(uint8_t)P.float_flags, (uint8_t)P.float_shift, (uint8_t)P.float_max_exp,
+                                           (uint8_t)P.float_norm_exp};
+                put_subblock(md, ID_FLOAT_INFO, fi);
+            }
+            if (zeros) put_subblock(md, ID_INT32_INFO, std::vector<uint8_t>{0, (uint8_t)zeros, 0, 0});
+
+            // ---- samples: pre-fixup domain values
+            WordEncoder we(flags);
+            we.w = ent;
+            int32_t crc = -1;
+            uint32_t maxabs = 0;
+            std::vector<int32_t> inres(n + 1);
+            for (int64_t f = 0; f < nf; f++) {
+                const int32_t *xf = x + (f0 + f) * P.nch;
+                int32_t L = xf[0], R = P.nch == 2 ? xf[1] : 0;
+                int sh = P.shift + zeros;
+                if (sh) {
+                    L = sar32(L, sh);
+                    R = sar32(R, sh);
+                }
+                if (mono_block) {
+                    int32_t t = L;
+                    for (int d = n - 1; d >= 0; d--) t = pass_inv_mono(passes[d], t);
+                    int32_t r = we.word(t);
+                    int32_t y = r;
+                    for (int d = 0; d < n; d++) y = pass_fwd_mono(passes[d], y);
+                    crc = add32(mul32(crc, 3), y);
+                    uint32_t a = y < 0 ? (uint32_t)(-(int64_t)y) : (uint32_t)y;
+                    if (a > maxabs) maxabs = a;
+                } else {
+                    int32_t Ld = L, Rd = R;
+                    if (P.joint_stereo) {
+                        Ld = sub32(L, R);
+                        Rd = add32(R, Ld >> 1);
+                    }
+                    int32_t tL = Ld, tR = Rd;
+                    for (int d = n - 1; d >= 0; d--) {
+                        int32_t iL, iR;
+                        pass_inv_stereo(passes[d], tL, tR, iL, iR);
+                        // propagate targets through the remaining inverse passes
+                        tL = iL;
+                        tR = iR;
+                    }
+                    int32_t rL = we.word(tL);
+                    int32_t rR = we.word(tR);
+                    int32_t yL = rL, yR = rR;
+                    for (int d = 0; d < n; d++) {
+                        int32_t oL, oR;
+                        pass_fwd_stereo(passes[d], yL, yR, oL, oR);
+                        yL = oL;
+                        yR = oR;
+                    }
+                    if (P.joint_stereo) {
+                        yR = sub32(yR, yL >> 1);
+                        yL = add32(yL, yR);
+                    }
+                    crc = add32(mul32(add32(mul32(crc, 3), yL), 3), yR);
+                    uint32_t a = yL < 0 ? (uint32_t)(-(int64_t)yL) : (uint32_t)yL;
+                    uint32_t b = yR < 0 ? (uint32_t)(-(int64_t)yR) : (uint32_t)yR;
+                    if (a > maxabs) maxabs = a;
+                    if (b > maxabs) maxabs = b;
+                    if (!P.hybrid && (yL != L || yR != R)) throw std::runtime_error("lossless reconstruction mismatch");
+                }
+                for (auto &p : passes)
+                    if (p.wA > 32767 || p.wA < -32768 || p.wB > 32767 || p.wB < -32768)
+                        throw std::runtime_error("decorr weight left int16 range");
+            }
+            std::vector<uint8_t> bits = we.finish();
+            ent = we.w;
+            if (bits.empty()) bits.push_back(0);
+            put_subblock(md, ID_WV_BITSTREAM, bits);
+            if (bi == nblocks - 1 && P.write_riff) put_subblock(md, ID_RIFF_TRAILER, std::vector<uint8_t>{'t', 'r'});
+
+            int mag = P.mag_override >= 0 ? P.mag_override : count_bits_u32(maxabs);
+            if (mag > 31) mag = 31;
+            flags |= ((uint32_t)mag << MAG_LSB) & MAG_MASK;
+
+            std::vector<uint8_t> blk(32);
+            blk.insert(blk.end(), md.begin(), md.end());
+            write_header(blk, P.version, frames, P.block_index_start + f0, (uint32_t)nf, flags, crc, P.total_unknown);
+            file.insert(file.end(), blk.begin(), blk.end());
+        }
+        return file;
+    }
+};
+
+// -------------------------------------------------------------------------
+// DSD encoders (inverse of DsdUtils.cs decode_fast / decode_high)
+// -------------------------------------------------------------------------
+struct RangeOut {
+    std::vector<uint8_t> &o;
+    explicit RangeOut(std::vector<uint8_t> &v) : o(v) {}
+    void b(uint32_t x) { o.push_back((uint8_t)x); }
+};
+
+// init_ptable (DsdUtils.cs:321-341)
+void init_ptable(int32_t *table, int rate_i, int rate_s) {
+    int value = 0x808000, rate = rate_i << 8, c, i;
+    for (c = (rate + 128) >> 8; c > 0; c--) value += (0x00010000 - value) >> 8;
+    for (i = 0; i < 128; ++i) {
+        table[i] = value;
+        table[255 - i] = 0x100ffff - value;
+        if (value > 0x010000) {
+            rate += (rate * rate_s + 128) >> 8;
+            for (c = (rate + 64) >> 7; c > 0; c--) value += (0x00010000 - value) >> 8;
+        }
+    }
+}
+
+struct DsdFilters {
+    int32_t value, filter0, filter1, filter2, filter3, filter4, filter5, filter6, factor, bytei;
+};
+
+std::vector<uint8_t> dsd_high_payload(const uint8_t *x, int64_t nf, int wch, int nch_in, int rate_i) {
+    std::vector<uint8_t> o;
+    o.push_back((uint8_t)rate_i);
+    o.push_back(20);  // RATE_S
+    DsdFilters sp[2];
+    memset(sp, 0, sizeof(sp));
+    for (int c = 0; c < wch; c++) {
+        for (int k = 0; k < 5; k++) o.push_back(0);  // filter1..5 = 0
+        o.push_back(0);
+        o.push_back(0);  // factor
+    }
+    int32_t ptable[256];
+    init_ptable(ptable, rate_i, 20);
+    uint32_t low = 0, high = 0xFFFFFFFFu;
+    const int32_t UP = 0x010000FE, DOWN = 0x00010000;
+    for (int64_t f = 0; f < nf; f++) {
+        sp[0].value = sp[0].filter1 - sp[0].filter5 + ((sp[0].filter6 * sp[0].factor) >> 2);
+        if (wch == 2) sp[1].value = sp[1].filter1 - sp[1].filter5 + ((sp[1].filter6 * sp[1].factor) >> 2);
+        uint8_t byt[2] = {x[f * nch_in], wch == 2 ? x[f * nch_in + 1] : (uint8_t)0};
+        for (int bitn = 7; bitn >= 0; bitn--) {
+            for (int c = 0; c < wch; c++) {
+                DsdFilters *q = &sp[c];
+                int bit = (byt[c] >> bitn) & 1;
+                int pp = (q->value >> 8) & 255;
+                uint32_t split = low + ((high - low) >> 8) * ((uint32_t)ptable[pp] >> 16);
+                if (bit) {
+                    high = split;
+                    ptable[pp] += (UP - ptable[pp]) >> 8;
+                    q->filter0 = -1;
+                } else {
+                    low = split + 1;
+                    ptable[pp] += (DOWN - ptable[pp]) >> 8;
+                    q->filter0 = 0;
+                }
+                while (((high ^ low) & 0xFF000000u) == 0) {
+                    o.push_back((uint8_t)(high >> 24));
+                    high = (high << 8) | 0xFF;
+                    low <<= 8;
+                }
+                q->value += q->filter6 * 8;
+                q->bytei = (int32_t)((uint32_t)q->bytei << 1) | (q->filter0 & 1);
+                q->factor += (((q->value ^ q->filter0) >> 31) | 1) & ((q->value ^ (q->value - (q->filter6 * 16))) >> 31);
+                q->filter1 += ((q->filter0 & (1 << 20)) - q->filter1) >> 6;
+                q->filter2 += ((q->filter0 & (1 << 20)) - q->filter2) >> 4;
+                q->filter3 += (q->filter2 - q->filter3) >> 4;
+                q->filter4 += (q->filter3 - q->filter4) >> 4;
+                q->value = (q->filter4 - q->filter5) >> 4;
+                q->filter5 += q->value;
+                q->filter6 += (q->value - q->filter6) >> 3;
+                q->value = q->filter1 - q->filter5 + ((q->filter6 * q->factor) >> 2);
+            }
+        }
+        sp[0].factor -= (sp[0].factor + 512) >> 10;
+        if (wch == 2) sp[1].factor -= (sp[1].factor + 512) >> 10;
+    }
+    // flush: 4 bytes of low pin the final interval
+    for (int i = 0; i < 4; i++) {
+        o.push_back((uint8_t)(low >> 24));
+        low <<= 8;
+    }
+    return o;
+}
+
+std::vector<uint8_t> dsd_fast_payload(const uint8_t *x, int64_t nf, int wch, int nch_in, int history_bits, bool rle) {
+    const int bins = 1 << history_bits;
+    // context histograms
+    std::vector<uint32_t> hist((size_t)bins * 256, 0);
+    int p0 = 0, p1 = 0;
+    std::vector<uint8_t> sym;
+    sym.reserve((size_t)(nf * wch));
+    for (int64_t f = 0; f < nf; f++)
+        for (int c = 0; c < wch; c++) sym.push_back(x[f * nch_in + c]);
+    for (size_t i = 0; i < sym.size(); i++) {
+        hist[(size_t)p0 * 256 + sym[i]]++;
+        if (wch == 1)
+            p0 = sym[i] & (bins - 1);
+        else {
+            p0 = p1;
+            p1 = sym[i] & (bins - 1);
+        }
+    }
+    // scale each bin so that max <= 254 and sum <= 1280 (MAX_BYTES_PER_BIN),
+    // keeping every used symbol >= 1
+    std::vector<uint8_t> prob((size_t)bins * 256, 0);
+    for (int b = 0; b < bins; b++) {
+        uint64_t tot = 0;
+        for (int s = 0; s < 256; s++) tot += hist[(size_t)b * 256 + s];
+        if (!tot) continue;
+        for (double target = 1000.0;; target *= 0.9) {
+            double scale = target / (double)tot;
+            int sum = 0;
+            for (int s = 0; s < 256; s++) {
+                uint32_t h = hist[(size_t)b * 256 + s];
+                int q = 0;
+                if (h) {
+                    q = (int)std::lround(h * scale);
+                    if (q < 1) q = 1;
+                    if (q > 254) q = 254;
+                }
+                prob[(size_t)b * 256 + s] = (uint8_t)q;
+                sum += q;
+            }
+            if (sum <= 1200) break;  // total per bin must stay <= MAX_BYTES_PER_BIN (DsdUtils.cs:216)
+        }
+    }
+    std::vector<uint8_t> o;
+    o.push_back((uint8_t)history_bits);
+    if (rle) {
+        uint8_t maxp = 0;
+        for (uint8_t p : prob) maxp = std::max(maxp, p);
+        if (maxp < 1) maxp = 1;
+        o.push_back(maxp);
+        size_t i = 0;
+        while (i < prob.size()) {
+            if (prob[i] == 0) {
+                size_t z = 0;
+                while (i + z < prob.size() && prob[i + z] == 0 && z < (size_t)(255 - maxp)) z++;
+                o.push_back((uint8_t)(maxp + z));
+                i += z;
+            } else {
+                o.push_back(prob[i]);
+                i++;
+            }
+        }
+        o.push_back(0);  // terminator (DsdUtils.cs:193)
+    } else {
+        o.push_back(0xFF);
+        o.insert(o.end(), prob.begin(), prob.end());
+    }
+    // cumulative tables as the decoder builds them
+    std::vector<uint16_t> cum((size_t)bins * 256);
+    for (int b = 0; b < bins; b++) {
+        uint16_t s = 0;
+        for (int k = 0; k < 256; k++) {
+            s = (uint16_t)(s + prob[(size_t)b * 256 + k]);
+            cum[(size_t)b * 256 + k] = s;
+        }
+    }
+    uint32_t low = 0, high = 0xFFFFFFFFu;
+    p0 = p1 = 0;
+    std::vector<uint8_t> body;
+    for (size_t i = 0; i < sym.size(); i++) {
+        int code = sym[i];
+        uint32_t tot = cum[(size_t)p0 * 256 + 255];
+        uint32_t mult = (high - low) / tot;
+        if (mult == 0) {
+            // decoder reloads a fresh 32-bit window (DsdUtils.cs:262-274)
+            for (int k = 0; k < 4; k++) {
+                body.push_back((uint8_t)(low >> 24));
+                low <<= 8;
+            }
+            low = 0;
+            high = 0xFFFFFFFFu;
+            mult = high / tot;
+        }
+        if (code > 0) low += cum[(size_t)p0 * 256 + code - 1] * mult;
+        high = low + prob[(size_t)p0 * 256 + code] * mult - 1;
+        if (wch == 1)
+            p0 = code & (bins - 1);
+        else {
+            p0 = p1;
+            p1 = code & (bins - 1);
+        }
+        while (((high ^ low) & 0xFF000000u) == 0) {
+            body.push_back((uint8_t)(high >> 24));
+            high = (high << 8) | 0xFF;
+            low <<= 8;
+        }
+    }
+    for (int k = 0; k < 4; k++) {
+        body.push_back((uint8_t)(low >> 24));
+        low <<= 8;
+    }
+    o.insert(o.end(), body.begin(), body.end());
+    return o;
+}
+
+std::vector<uint8_t> encode_dsd(const wvenc_dsd_params &P, const uint8_t *x, int64_t frames) {
+    std::vector<uint8_t> file;
+    const bool mono_block = P.nch == 1 || P.false_stereo;
+    const int wch = mono_block ? 1 : 2;
+    const int64_t B = P.block_samples;
+    int64_t nblocks = frames == 0 ? 0 : (frames + B - 1) / B;
+    for (int64_t bi = 0; bi < nblocks; bi++) {
+        int64_t f0 = bi * B, nf = std::min<int64_t>(B, frames - f0);
+        const uint8_t *xb = x + f0 * P.nch;
+        uint32_t flags = DSD_FLAG | INITIAL_BLOCK | FINAL_BLOCK;  // BYTES_STORED = 0
+        if (P.nch == 1) flags |= MONO_FLAG;
+        if (P.false_stereo) flags |= FALSE_STEREO;
+        flags |= (uint32_t)srate_index(P.sample_rate) << SRATE_LSB;
+        std::vector<uint8_t> payload;
+        payload.push_back((uint8_t)P.rate_multiplier_log2);
+        payload.push_back((uint8_t)P.mode);
+        std::vector<uint8_t> body;
+        if (P.mode == 0) {
+            for (int64_t f = 0; f < nf; f++)
+                for (int c = 0; c < wch; c++) body.push_back(xb[f * P.nch + c]);
+        } else if (P.mode == 1) {
+            body = dsd_fast_payload(xb, nf, wch, P.nch, P.history_bits, P.rle_tables != 0);
+        } else {
+            body = dsd_high_payload(xb, nf, wch, P.nch, P.rate_i);
+        }
+        payload.insert(payload.end(), body.begin(), body.end());
+        int32_t crc = -1;
+        for (int64_t f = 0; f < nf; f++)
+            for (int c = 0; c < wch; c++) crc = add32(crc, add32(shl32(crc, 1), xb[f * P.nch + c]));
+        std::vector<uint8_t> md;
+        put_subblock(md, ID_DSD_BLOCK, payload);
+        std::vector<uint8_t> blk(32);
+        blk.insert(blk.end(), md.begin(), md.end());
+        write_header(blk, 0x410, frames, f0, (uint32_t)nf, flags, crc, false);
+        file.insert(file.end(), blk.begin(), blk.end());
+    }
+    return file;
+}
+
+thread_local std::string g_err;
+
+}  // namespace
+
+extern "C" {
+
+// Encode interleaved int32 PCM (`frames` x nch) into a .wv byte stream.
+// Returns the byte count, or -(needed) if cap is too small, or -1 on error
+// (message via wvenc_last_error).  Passing out == NULL queries the size.
+int64_t wvenc_encode_pcm(const int32_t *samples, int64_t frames, const wvenc_params *p, uint8_t *out, int64_t cap) {
+    try {
+        if (p->nch < 1 || p->nch > 2) throw std::runtime_error("nch must be 1 or 2");
+        if (p->num_terms < 0 || p->num_terms > 16) throw std::runtime_error("num_terms");
+        if (p->block_samples <= 0) throw std::runtime_error("block_samples");
+        for (int e = 0; e < p->num_terms; e++) {
+            int t = p->terms[e];
+            bool ok = (t >= 1 && t <= 8) || t == 17 || t == 18 || ((t >= -3 && t <= -1) && p->nch == 2 && !p->false_stereo);
+            if (!ok) throw std::runtime_error("unsupported term for this channel layout");
+        }
+        PcmEncoder enc(*p);
+        std::vector<uint8_t> f = enc.encode(samples, frames);
+        if (!out) return (int64_t)f.size();
+        if ((int64_t)f.size() > cap) return -(int64_t)f.size();
+        memcpy(out, f.data(), f.size());
+        return (int64_t)f.size();
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
+int64_t wvenc_encode_dsd(const uint8_t *samples, int64_t frames, const wvenc_dsd_params *p, uint8_t *out, int64_t cap) {
+    try {
+        if (p->nch < 1 || p->nch > 2) throw std::runtime_error("nch must be 1 or 2");
+        if (p->mode != 0 && p->mode != 1 && p->mode != 3) throw std::runtime_error("mode");
+        std::vector<uint8_t> f = encode_dsd(*p, samples, frames);
+        if (!out) return (int64_t)f.size();
+        if ((int64_t)f.size() > cap) return -(int64_t)f.size();
+        memcpy(out, f.data(), f.size());
+        return (int64_t)f.size();
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
+const char *wvenc_last_error(void) { return g_err.c_str(); }
+}

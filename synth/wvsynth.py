@@ -1,0 +1,246 @@
+"""Synthetic WavPack corpora for tests and bench (input generation only).
+
+Wraps synth/wv_encoder.cpp (a WavPack-4 encoder derived as the inverse of the
+reference decode path) and the signal models of SURVEY.md §8d:
+  C1  one 44.1 kHz 16-bit stereo file, default terms {18,18,2,3,-2}
+  C2  1,024 blocks x 22,050 frames, 16-bit stereo, fast terms {17,17}
+  C3  4,096 blocks x 44,100 frames, 24-bit stereo, high 16-term chain
+  C4  hybrid lossy float32 (FLOAT_DATA|HYBRID|HYBRID_BITRATE)
+  C5  mixed corpus (mono/stereo, 16/24-bit, DSD modes 0/1/3)
+Seeds are fixed and recorded by the callers.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from dataclasses import dataclass, field
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "libwvenc.so")
+_lib = None
+
+TERMS_FAST = [17, 17]
+TERMS_DEFAULT = [18, 18, 2, 3, -2]
+TERMS_HIGH = [18, 18, 2, 3, -2, 18, 2, 4, 7, 5, 3, 6, 8, -1, 18, 2]
+TERMS_MONO_HIGH = [18, 18, 2, 3, 18, 2, 4, 7, 5, 3, 6, 8, 18, 2, 17, 1]
+
+
+class _Params(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "nch", "bytes_per_sample", "shift", "joint_stereo", "false_stereo", "num_terms")] + [
+        ("terms", ctypes.c_int32 * 16), ("deltas", ctypes.c_int32 * 16)] + [
+        (n, ctypes.c_int32) for n in (
+            "block_samples", "sample_rate", "version", "hybrid", "hybrid_bitrate", "hybrid_balance",
+            "bitrate_x256", "float_data", "float_flags", "float_shift", "float_max_exp", "float_norm_exp",
+            "int32_zeros", "write_riff", "config_flags", "write_history", "reset_state", "block_index_start",
+            "total_unknown", "extras", "mag_override")]
+
+
+class _DsdParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "nch", "false_stereo", "mode", "block_samples", "rate_multiplier_log2", "sample_rate",
+        "history_bits", "rle_tables", "rate_i")]
+
+
+@dataclass
+class EncParams:
+    nch: int = 2
+    bytes_per_sample: int = 2
+    shift: int = 0
+    joint_stereo: bool = True
+    false_stereo: bool = False
+    terms: list = field(default_factory=lambda: list(TERMS_FAST))
+    deltas: list | None = None
+    block_samples: int = 22050
+    sample_rate: int = 44100
+    version: int = 0x407
+    hybrid: bool = False
+    hybrid_bitrate: bool = False
+    hybrid_balance: bool = False
+    bitrate_x256: int = 0
+    float_data: bool = False
+    float_flags: int = 0
+    float_shift: int = 0
+    float_max_exp: int = 126
+    float_norm_exp: int = 127
+    int32_zeros: int = 0
+    write_riff: bool = False
+    config_flags: int = 0
+    write_history: bool = True
+    reset_state: bool = False
+    block_index_start: int = 0
+    total_unknown: bool = False
+    extras: int = 0
+    mag_override: int = -1
+
+    def to_c(self) -> _Params:
+        p = _Params()
+        p.nch, p.bytes_per_sample, p.shift = self.nch, self.bytes_per_sample, self.shift
+        p.joint_stereo, p.false_stereo = int(self.joint_stereo), int(self.false_stereo)
+        p.num_terms = len(self.terms)
+        deltas = self.deltas if self.deltas is not None else [2] * len(self.terms)
+        for i, t in enumerate(self.terms):
+            p.terms[i] = t
+            p.deltas[i] = deltas[i]
+        for n in ("block_samples", "sample_rate", "version", "bitrate_x256", "float_flags", "float_shift",
+                  "float_max_exp", "float_norm_exp", "int32_zeros", "config_flags", "block_index_start",
+                  "extras", "mag_override"):
+            setattr(p, n, int(getattr(self, n)))
+        for n in ("hybrid", "hybrid_bitrate", "hybrid_balance", "float_data", "write_riff", "write_history",
+                  "reset_state", "total_unknown"):
+            setattr(p, n, int(bool(getattr(self, n))))
+        return p
+
+
+def build() -> str:
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.wvenc_encode_pcm.restype = ctypes.c_int64
+        L.wvenc_encode_pcm.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(_Params), ctypes.c_void_p,
+                                       ctypes.c_int64]
+        L.wvenc_encode_dsd.restype = ctypes.c_int64
+        L.wvenc_encode_dsd.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(_DsdParams),
+                                       ctypes.c_void_p, ctypes.c_int64]
+        L.wvenc_last_error.restype = ctypes.c_char_p
+        _lib = L
+    return _lib
+
+
+def encode_pcm(samples: np.ndarray, params: EncParams) -> bytes:
+    """samples: int32 array shaped (frames, nch) (or flat interleaved)."""
+    x = np.ascontiguousarray(samples, dtype=np.int32).reshape(-1)
+    frames = x.size // params.nch
+    p = params.to_c()
+    L = lib()
+    n = L.wvenc_encode_pcm(x.ctypes.data, frames, ctypes.byref(p), None, 0)
+    if n < 0:
+        raise RuntimeError("wvenc: " + L.wvenc_last_error().decode())
+    out = np.empty(n, dtype=np.uint8)
+    m = L.wvenc_encode_pcm(x.ctypes.data, frames, ctypes.byref(p), out.ctypes.data, n)
+    if m != n:
+        raise RuntimeError("wvenc: size mismatch " + L.wvenc_last_error().decode())
+    return out.tobytes()
+
+
+@dataclass
+class DsdParams:
+    nch: int = 2
+    false_stereo: bool = False
+    mode: int = 3
+    block_samples: int = 44100
+    rate_multiplier_log2: int = 0
+    sample_rate: int = 44100
+    history_bits: int = 5
+    rle_tables: bool = False
+    rate_i: int = 3
+
+    def to_c(self) -> _DsdParams:
+        p = _DsdParams()
+        for n in ("nch", "mode", "block_samples", "rate_multiplier_log2", "sample_rate", "history_bits", "rate_i"):
+            setattr(p, n, int(getattr(self, n)))
+        p.false_stereo = int(self.false_stereo)
+        p.rle_tables = int(self.rle_tables)
+        return p
+
+
+def encode_dsd(samples: np.ndarray, params: DsdParams) -> bytes:
+    x = np.ascontiguousarray(samples, dtype=np.uint8).reshape(-1)
+    frames = x.size // params.nch
+    p = params.to_c()
+    L = lib()
+    n = L.wvenc_encode_dsd(x.ctypes.data, frames, ctypes.byref(p), None, 0)
+    if n < 0:
+        raise RuntimeError("wvenc: " + L.wvenc_last_error().decode())
+    out = np.empty(n, dtype=np.uint8)
+    m = L.wvenc_encode_dsd(x.ctypes.data, frames, ctypes.byref(p), out.ctypes.data, n)
+    assert m == n
+    return out.tobytes()
+
+
+# ---------------------------------------------------------------------------
+# signal models
+# ---------------------------------------------------------------------------
+def _one_channel(rng: np.random.Generator, frames: int, rate: float, full_scale: float, sigma: float) -> np.ndarray:
+    t = np.arange(frames, dtype=np.float64) / rate
+    y = np.zeros(frames, dtype=np.float64)
+    for _ in range(4):
+        f = np.exp(rng.uniform(np.log(40.0), np.log(6000.0)))
+        a_db = rng.uniform(-20.0, -3.0)
+        ph = rng.uniform(0, 2 * np.pi)
+        y += (10 ** (a_db / 20.0)) * 0.25 * np.sin(2 * np.pi * f * t + ph)
+    return y * full_scale + rng.normal(0.0, sigma, frames)
+
+
+def audio_like(frames: int, nch: int = 2, bits: int = 16, seed: int = 0, sigma: float | None = None,
+               kind: str = "music") -> np.ndarray:
+    """int32 (frames, nch): 4 sinusoids + Gaussian noise; R = 0.7 L + 0.3 indep.
+
+    kind: "music" (the model above), "zeros" (digital silence, exercises the
+    zero-run coder), "noise" (full-scale white noise, exercises escapes)."""
+    rng = np.random.default_rng(seed)
+    fs = float(2 ** (bits - 1) - 1)
+    lo, hi = -(2 ** (bits - 1)), 2 ** (bits - 1) - 1
+    if kind == "zeros":
+        return np.zeros((frames, nch), dtype=np.int32)
+    if kind == "noise":
+        return rng.integers(lo, hi + 1, size=(frames, nch), dtype=np.int64).astype(np.int32)
+    if sigma is None:
+        sigma = 64.0 * (2 ** (bits - 16)) if bits >= 16 else 1.0
+    left = _one_channel(rng, frames, 44100.0, fs, sigma)
+    if nch == 1:
+        chans = [left]
+    else:
+        other = _one_channel(rng, frames, 44100.0, fs, sigma)
+        chans = [left, 0.7 * left + 0.3 * other]
+    x = np.stack(chans, axis=1)
+    return np.clip(np.rint(x), lo, hi).astype(np.int32)
+
+
+def float_mantissas(x: np.ndarray, max_exp: int = 126) -> np.ndarray:
+    """float32 in [-1, 1) -> the integer values a FLOAT_DATA block carries:
+    round(f * 2^(150 - max_exp)); the decoder returns v << (max_exp - 127)
+    clipped to 24 bits (FloatUtils.cs:32-56)."""
+    v = np.rint(x.astype(np.float64) * float(2 ** (150 - max_exp)))
+    return np.clip(v, -(2 ** 30), 2 ** 30).astype(np.int32)
+
+
+def dsd_like(frames: int, nch: int = 2, seed: int = 0) -> np.ndarray:
+    """1-bit sigma-delta modulation of a slow sine mix, packed MSB first."""
+    rng = np.random.default_rng(seed)
+    nbits = frames * 8
+    t = np.arange(nbits, dtype=np.float64)
+    out = []
+    for c in range(nch):
+        f1, f2 = rng.uniform(1e-5, 4e-4, size=2)
+        s = 0.4 * np.sin(2 * np.pi * f1 * t) + 0.2 * np.sin(2 * np.pi * f2 * t + c)
+        # first-order sigma-delta
+        bits = np.empty(nbits, dtype=np.uint8)
+        acc = 0.0
+        for i in range(0, nbits, 65536):
+            seg = s[i:i + 65536]
+            b = np.empty(seg.size, dtype=np.uint8)
+            for j, v in enumerate(seg):
+                acc += v - (1.0 if acc > 0 else -1.0)
+                b[j] = 1 if acc > 0 else 0
+            bits[i:i + seg.size] = b
+        out.append(np.packbits(bits.reshape(-1, 8), axis=1, bitorder="big").reshape(-1))
+    return np.stack(out, axis=1).astype(np.uint8)
+
+
+def dsd_random_like(frames: int, nch: int = 2, seed: int = 0, density: float = 0.5) -> np.ndarray:
+    """Fast DSD-ish bytes: biased random bits (no Python loops)."""
+    rng = np.random.default_rng(seed)
+    bits = (rng.random((frames * 8, nch)) < density).astype(np.uint8)
+    packed = np.packbits(bits.T.reshape(nch, frames, 8), axis=2, bitorder="big").reshape(nch, frames)
+    return np.ascontiguousarray(packed.T)
