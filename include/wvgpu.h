@@ -1,0 +1,138 @@
+/*
+ * wvgpu.h -- C-ABI of the MI355X WavPack block-decode path (libwvgpu.so).
+ *
+ * Drop-in boundary for the reference's hot path
+ *   public static long WavPackUtils.WavpackUnpackSamples(WavpackContext wpc, int[] buffer, long samples)
+ *   (Quake4/WavPackDecoder WavPackUtils.cs:200-282)
+ * and the calls around it that a C# host needs to keep its API:
+ *   WavpackOpenFileInput   WavPackUtils.cs:36-120   -> wvg_batch_add_file (framing, info)
+ *   WavpackUnpackSamples   WavPackUtils.cs:200-282  -> wvg_batch_decode (+ download)
+ *   WavpackFormatSamples   WavPackUtils.cs:288-341  -> wvg_format_samples
+ *   WavpackGetNumErrors    WavPackUtils.cs:363      -> wvg_file_result.crc_errors
+ *   WavpackLossy           WavPackUtils.cs:371      -> wvg_file_result.lossy
+ *   other getters          WavPackUtils.cs:346-499  -> wvg_file_info
+ *
+ * Blittable types only (P/Invoke ready): every buffer is caller-owned; the
+ * library keeps device copies owned by the batch handle.  Errors are int
+ * return codes (0 = OK, < 0 = error) plus wvg_last_error(); no C++
+ * exception crosses the ABI.  One context per device per host thread.
+ *
+ * Output contract: a batch decodes every file exactly as a caller looping
+ * WavpackUnpackSamples(wpc, buffer, chunk_frames) (WvDemo.cs:110-135) would
+ * receive it, concatenated: int32 per channel-sample, interleaved,
+ * right-justified; float files as clipped 24-bit ints (FloatUtils.cs:32-56);
+ * DSD as one byte value per channel-sample.
+ */
+#ifndef WVGPU_H
+#define WVGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WVG_OK 0
+#define WVG_ERR_HIP (-1)      /* HIP runtime error (see wvg_last_error) */
+#define WVG_ERR_ARG (-2)      /* bad argument / state */
+#define WVG_ERR_OPEN (-3)     /* WavpackOpenFileInput failed (info.error holds the message) */
+#define WVG_ERR_SPACE (-4)    /* caller buffer too small */
+
+/* per-block status bits (wvg_file_result.status_or) */
+#define WVG_ST_CRC_CHECKED 0x01u
+#define WVG_ST_CRC_ERROR 0x02u
+#define WVG_ST_MUTED 0x04u
+#define WVG_ST_BITS_ERROR 0x08u
+#define WVG_ST_EXCEPTION 0x10u   /* the reference raises a C# exception in this block */
+#define WVG_ST_UNSUPPORTED 0x20u /* depends on decode state of an earlier block (never in well-formed files) */
+#define WVG_ST_DSD_MUTE 0x40u
+#define WVG_ST_NONDET 0x80u      /* reference output depends on stale caller-buffer contents */
+
+typedef struct wvg_ctx wvg_ctx;
+typedef struct wvg_batch wvg_batch;
+
+/* What WavpackOpenFileInput + the getters report (WavPackUtils.cs:36-120, 346-499). */
+typedef struct {
+    int32_t open_ok;            /* 0 => error[] holds wpc.error_message */
+    int32_t num_channels;       /* WavpackGetNumChannels */
+    int32_t reduced_channels;   /* WavpackGetReducedChannels (ints per output frame) */
+    int32_t bits_per_sample;    /* WavpackGetBitsPerSample (DSD: /8 applied like the getter) */
+    int32_t bytes_per_sample;   /* WavpackGetBytesPerSample */
+    int32_t version;            /* WavpackGetVersion */
+    int32_t mode;               /* WavpackGetMode */
+    int32_t is_float;           /* WavpackGetIsFloat */
+    int32_t is_five;            /* WavpackGetIsFive */
+    int32_t file_format;        /* WavpackGetFileFormat */
+    int32_t lossy;              /* WavpackLossy at open */
+    uint32_t dsd_multiplier;
+    int64_t sample_rate;        /* WavpackGetSampleRate */
+    int64_t total_samples;      /* WavpackGetNumSamples(native=false), -1 unknown */
+    int64_t out_frames;         /* frames the chunked caller receives */
+    int64_t out_offset;         /* int32 index of this file's output inside the batch */
+    int64_t header_off, header_len;   /* RIFF/ALT header bytes inside the file (WavpackGetHeader), -1 none */
+    int64_t trailer_off, trailer_len; /* WavpackGetTrailer */
+    char error[96];
+} wvg_file_info;
+
+typedef struct {
+    int64_t frames;             /* == info.out_frames unless an exception stopped the decode */
+    int64_t crc_errors;         /* WavpackGetNumErrors after the last call */
+    int32_t lossy;              /* WavpackLossy after the last call */
+    int32_t exception;          /* the reference would have thrown (WvDemo exits 1) */
+    uint32_t status_or;         /* OR of the WVG_ST_* bits of all blocks */
+    int32_t num_blocks;
+} wvg_file_result;
+
+/* Device + stream ownership.  device < 0 => current device. */
+wvg_ctx *wvg_open(int device);
+void wvg_close(wvg_ctx *ctx);
+const char *wvg_last_error(wvg_ctx *ctx);
+
+/* A batch of files decoded together.  chunk_frames is the caller's per-call
+ * frame count (Defines.SAMPLE_BUFFER_SIZE = 4096 for WvDemo); it fixes the
+ * reference's chunk seams (weight (short) stores, mute granularity). */
+wvg_batch *wvg_batch_new(wvg_ctx *ctx, int chunk_frames);
+void wvg_batch_free(wvg_batch *b);
+
+/* Frame one file (host): parses headers/metadata, records the blocks.
+ * The bytes are copied into the batch.  Returns the file index (>= 0) or
+ * WVG_ERR_OPEN (info->error set; the file contributes no output). */
+int wvg_batch_add_file(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open_flags, wvg_file_info *info);
+
+/* Copy blob + descriptors to the device and zero the output. */
+int wvg_batch_upload(wvg_batch *b);
+
+/* Enqueue the decode kernels on `stream` (hipStream_t, NULL = the context's
+ * stream).  Input and output stay in HBM. */
+int wvg_batch_decode(wvg_batch *b, void *stream);
+int wvg_batch_sync(wvg_batch *b);
+
+int64_t wvg_batch_out_ints(const wvg_batch *b);
+int32_t *wvg_batch_device_out(wvg_batch *b);      /* device pointer to the int32 output */
+int64_t wvg_batch_num_blocks(const wvg_batch *b);
+int64_t wvg_batch_bytes_in(const wvg_batch *b);   /* compressed bytes of all decoded blocks */
+int64_t wvg_batch_frames(const wvg_batch *b);     /* frames of all decoded blocks */
+
+/* Download output (and per-block statuses) and fill per-file results. */
+int wvg_batch_download(wvg_batch *b, int32_t *host_out, int64_t cap_ints);
+int wvg_batch_file_result(wvg_batch *b, int file, wvg_file_result *res);
+/* per-block status words (after download), one per decoded block in file order */
+int wvg_batch_block_status(wvg_batch *b, uint32_t *out, int64_t cap);
+
+/* Device-side timing of `iters` back-to-back decodes (hipEvents on the
+ * batch stream).  *ms receives the average per decode. */
+int wvg_batch_time(wvg_batch *b, int iters, float *ms);
+
+/* One-shot convenience: frame + upload + decode + download one file. */
+int wvg_decode_file(wvg_ctx *ctx, const uint8_t *file, size_t len, int chunk_frames, int32_t *out, int64_t cap_ints,
+                    wvg_file_info *info, wvg_file_result *res);
+
+/* WavpackFormatSamples (WavPackUtils.cs:288-341) on the host: int32 -> LE PCM bytes. */
+int wvg_format_samples(const int32_t *src, int64_t samcnt, int bps, uint8_t *pcm, int64_t pcm_len, int offset,
+                       int dsd);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,73 @@
+// tests/emu/emu.cpp -- TEST-ONLY host build of the device decode core.
+//
+// Compiles wv_framing.cpp + wv_decode_core.h (the exact source the HIP kernel
+// runs) for the host, so `pytest -m "not gpu"` can check the decode logic
+// against the oracle on a machine without a GPU.  It is never loaded by the
+// product package (wavpackdecoder_amd), which only runs the HIP kernels.
+#include <string.h>
+
+#include <vector>
+
+#include "../../wavpackdecoder_amd/csrc/wv_decode_core.h"
+#include "../../wavpackdecoder_amd/csrc/wv_framing.h"
+
+using namespace wvg;
+
+struct HostStore {
+    int32_t *out;
+    uint64_t base;
+    void put(uint64_t i, int32_t v) { out[base + i] = v; }
+};
+
+extern "C" {
+// Returns frames (or -2 open error, -3 exception); fills out (cap ints).
+int64_t emu_decode(const uint8_t *file, size_t len, int chunk, int32_t *out, int64_t cap, int64_t *crc_errors,
+                   int *nch, uint32_t *status_or) {
+    FramingOutput fo;
+    FileInfo info;
+    frame_file(file, len, 0, 0, 0, chunk, fo, info);
+    *crc_errors = 0;
+    *status_or = 0;
+    *nch = info.out_nch;
+    if (!info.open_ok) return -2;
+    int64_t total = info.out_frames * info.out_nch;
+    if (total > cap) return -4;
+    memset(out, 0, sizeof(int32_t) * (size_t)total);
+    std::vector<int32_t> ptable(256);
+    bool exception = info.exception != 0;
+    std::vector<std::pair<int64_t, int64_t>> fills;
+    for (auto &d : fo.descs) {
+        uint32_t st = d.fstatus;
+        HostStore hs{out, d.out_off};
+        if (d.kind == KIND_PCM) {
+            st |= decode_pcm_block(d, file, hs);
+        } else if (d.kind != KIND_SKIP) {
+            DsdResult r = decode_dsd_block(d, file, fo.tables.data(), ptable.data(), hs);
+            st |= r.status;
+            if (r.status & ST_DSD_MUTE) {
+                // chunks from mute_chunk on: fill n*call_nch from the call start
+                uint32_t f = 0, cl = d.first_chunk;
+                for (uint32_t ci = 0; f < d.nframes; ci++) {
+                    uint32_t n = cl < d.nframes - f ? cl : d.nframes - f;
+                    if (ci >= r.mute_chunk) {
+                        int64_t start = (int64_t)d.out_off + (int64_t)f * d.out_nch - (ci == 0 ? d.first_bsp : 0);
+                        fills.push_back({start, (int64_t)n * d.call_nch});
+                    }
+                    f += n;
+                    cl = d.chunk;
+                }
+            }
+        }
+        *status_or |= st;
+        if (st & ST_CRC_ERROR) (*crc_errors)++;
+        if (st & ST_EXCEPTION) {
+            exception = true;
+            break;
+        }
+    }
+    for (auto &fl : fills)
+        for (int64_t i = 0; i < fl.second; i++) out[fl.first + i] = 0x55;
+    if (exception) return -3;
+    return info.out_frames;
+}
+}

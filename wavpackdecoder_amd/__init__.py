@@ -1,0 +1,19 @@
+"""wavpackdecoder_amd -- MI355X-native WavPack block decode (drop-in for the
+reference's WavPackUtils.WavpackUnpackSamples hot path).
+
+Layout:
+  csrc/wv_decode.hip      HIP kernels for gfx950 (PCM + DSD block decode)
+  csrc/wv_decode_core.h   per-block decode (host+device source)
+  csrc/wv_framing.cpp     host framing: .wv bytes -> block descriptors
+  csrc/wv_api.cpp         C-ABI (include/wvgpu.h) -> build/libwvgpu.so
+  api.py                  mirror of the reference's WavPackUtils API
+  shard.py                per-GPU file partition (multi-GPU, no collectives)
+"""
+from .api import (  # noqa: F401
+    DecodeBatch, WavpackContext, WavpackException, WavpackFormatSamples, WavpackGetBitsPerSample,
+    WavpackGetBytesPerSample, WavpackGetErrorMessage, WavpackGetFileFormat, WavpackGetHeader, WavpackGetIsFive,
+    WavpackGetIsFloat, WavpackGetMode, WavpackGetNumChannels, WavpackGetNumErrors, WavpackGetNumSamples,
+    WavpackGetReducedChannels, WavpackGetSampleIndex, WavpackGetSampleRate, WavpackGetTrailer, WavpackGetVersion,
+    WavpackLossy, WavpackOpenFileInput, WavpackUnpackSamples,
+)
+from ._lib import build, lib  # noqa: F401

@@ -1,0 +1,280 @@
+"""Host-side mirror of the reference's public API for the decode path.
+
+Reference (C#, Quake4/WavPackDecoder WavPackUtils.cs):
+    WavpackOpenFileInput(BinaryReader, uint flags=0)      :36-120
+    WavpackUnpackSamples(WavpackContext, int[] buffer, long samples)  :200-282
+    WavpackFormatSamples(int[] src, long samcnt, int bps, byte[] pcm, int offset=0, bool dsd=false) :288-341
+    WavpackGetNumSamples / GetSampleIndex / GetNumErrors / Lossy / GetSampleRate /
+    GetNumChannels / GetBitsPerSample / GetBytesPerSample / GetReducedChannels /
+    GetMode / GetFileFormat / GetFileExtension / GetErrorMessage / GetHeader /
+    GetTrailer / GetIsFive / GetVersion / GetIsFloat       :346-499
+
+Same names, same argument meaning and the same error behaviour (errors are
+reported through GetErrorMessage; a decode that the reference would abort
+with a C# exception raises WavpackException here).  Underneath, the whole
+file is decoded by the MI355X kernels on the first WavpackUnpackSamples call
+and served from the decoded buffer; the chunk schedule is the caller's
+request size (the reference's seams are a function of it), 4096 frames by
+default like WvDemo.
+
+For throughput use DecodeBatch: many files, one upload, one decode.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib as _L
+
+SAMPLE_BUFFER_SIZE = 4096  # Defines.cs:18
+OPEN_2CH_MAX = 0x8         # Defines.cs:26
+
+
+class WavpackException(RuntimeError):
+    """The reference would have raised a C# exception (WvDemo.cs:144 catch)."""
+
+
+_ctx = None
+
+
+def _context():
+    global _ctx
+    if _ctx is None:
+        L = _L.lib()
+        _ctx = L.wvg_open(-1)
+        if not _ctx:
+            raise RuntimeError("wvg_open failed: no HIP device visible (the decode path is GPU-only)")
+    return _ctx
+
+
+class DecodeBatch:
+    """A batch of .wv files decoded together on one GPU (files shard across GPUs)."""
+
+    def __init__(self, chunk_frames: int = SAMPLE_BUFFER_SIZE):
+        self._L = _L.lib()
+        self._b = self._L.wvg_batch_new(_context(), int(chunk_frames))
+        if not self._b:
+            raise RuntimeError("wvg_batch_new failed")
+        self.infos: list = []
+        self._uploaded = False
+        self._data: list = []
+
+    def add_file(self, data: bytes, open_flags: int = 0):
+        info = _L.WvgFileInfo()
+        idx = self._L.wvg_batch_add_file(self._b, data, len(data), int(open_flags), ctypes.byref(info))
+        self.infos.append(info)
+        self._uploaded = False
+        return idx
+
+    def upload(self):
+        self._check(self._L.wvg_batch_upload(self._b))
+        self._uploaded = True
+
+    def decode(self, stream=None):
+        if not self._uploaded:
+            self.upload()
+        self._check(self._L.wvg_batch_decode(self._b, stream))
+
+    def sync(self):
+        self._check(self._L.wvg_batch_sync(self._b))
+
+    def time(self, iters: int) -> float:
+        ms = ctypes.c_float()
+        self._check(self._L.wvg_batch_time(self._b, int(iters), ctypes.byref(ms)))
+        return float(ms.value)
+
+    @property
+    def out_ints(self) -> int:
+        return int(self._L.wvg_batch_out_ints(self._b))
+
+    @property
+    def num_blocks(self) -> int:
+        return int(self._L.wvg_batch_num_blocks(self._b))
+
+    @property
+    def frames(self) -> int:
+        return int(self._L.wvg_batch_frames(self._b))
+
+    @property
+    def bytes_in(self) -> int:
+        return int(self._L.wvg_batch_bytes_in(self._b))
+
+    def device_out_ptr(self) -> int:
+        return int(self._L.wvg_batch_device_out(self._b) or 0)
+
+    def download(self) -> np.ndarray:
+        out = np.empty(max(self.out_ints, 1), dtype=np.int32)
+        self._check(self._L.wvg_batch_download(self._b, out.ctypes.data, out.size))
+        return out[: self.out_ints]
+
+    def block_status(self) -> np.ndarray:
+        n = self.num_blocks + 1024
+        st = np.zeros(n, dtype=np.uint32)
+        k = self._L.wvg_batch_block_status(self._b, st.ctypes.data, n)
+        if k < 0:
+            raise RuntimeError("block status unavailable (download first)")
+        return st[:k]
+
+    def result(self, i: int) -> _L.WvgFileResult:
+        r = _L.WvgFileResult()
+        self._check(self._L.wvg_batch_file_result(self._b, int(i), ctypes.byref(r)))
+        return r
+
+    def _check(self, rc: int):
+        if rc != 0:
+            raise RuntimeError(f"libwvgpu error {rc}: {self._L.wvg_last_error(_context()).decode()}")
+
+    def close(self):
+        if self._b:
+            self._L.wvg_batch_free(self._b)
+            self._b = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class WavpackContext:
+    """Opaque context (WavpackContext.cs:13-35)."""
+
+    def __init__(self, data: bytes, open_flags: int):
+        self._data = data
+        self._flags = open_flags
+        self._info = _L.WvgFileInfo()
+        self._decoded = None
+        self._result = None
+        self._pos = 0  # frames already handed out
+        self._chunk = None
+        self.error_message = None
+
+    def _decode(self, chunk: int):
+        b = DecodeBatch(chunk)
+        idx = b.add_file(self._data, self._flags)
+        if idx < 0:
+            raise RuntimeError("file cannot be opened: " + self._info.error.decode())
+        b.decode()
+        out = b.download()
+        self._result = b.result(idx)
+        b.close()
+        if self._result.exception:
+            raise WavpackException("the reference decoder raises an exception on this file")
+        nch = max(self._info.reduced_channels, 1)
+        self._decoded = out.reshape(-1, nch) if out.size else np.zeros((0, nch), np.int32)
+        self._chunk = chunk
+
+
+def WavpackOpenFileInput(reader, flags: int = 0) -> WavpackContext:
+    """WavPackUtils.cs:36-120.  `reader` is bytes or a binary file object."""
+    data = reader if isinstance(reader, (bytes, bytearray, memoryview)) else reader.read()
+    data = bytes(data)
+    wpc = WavpackContext(data, flags)
+    L = _L.lib()
+    b = L.wvg_batch_new(_context(), SAMPLE_BUFFER_SIZE)
+    rc = L.wvg_batch_add_file(b, data, len(data), int(flags), ctypes.byref(wpc._info))
+    L.wvg_batch_free(b)
+    if rc < 0 or not wpc._info.open_ok:
+        wpc.error_message = wpc._info.error.decode() or "not compatible with this version of WavPack file!"
+    return wpc
+
+
+def WavpackUnpackSamples(wpc: WavpackContext, buffer: np.ndarray, samples: int) -> int:
+    """WavPackUtils.cs:200-282: fill `buffer` (int32, >= samples * reduced channels)."""
+    if wpc.error_message:
+        return 0
+    if wpc._decoded is None:
+        wpc._decode(int(samples))
+    n = min(int(samples), wpc._decoded.shape[0] - wpc._pos)
+    if n <= 0:
+        return 0
+    nch = wpc._decoded.shape[1]
+    buffer[: n * nch] = wpc._decoded[wpc._pos:wpc._pos + n].reshape(-1)
+    wpc._pos += n
+    return n
+
+
+def WavpackFormatSamples(src: np.ndarray, samcnt: int, bps: int, pcm_buffer: bytearray, offset: int = 0,
+                         dsd: bool = False) -> bool:
+    """WavPackUtils.cs:288-341 (host C implementation in libwvgpu)."""
+    L = _L.lib()
+    s = np.ascontiguousarray(src, dtype=np.int32)
+    if pcm_buffer is None:
+        return False
+    view = (ctypes.c_uint8 * len(pcm_buffer)).from_buffer(pcm_buffer)
+    return bool(L.wvg_format_samples(s.ctypes.data, int(samcnt), int(bps), ctypes.addressof(view), len(pcm_buffer),
+                                     int(offset), int(bool(dsd))))
+
+
+def WavpackGetNumSamples(wpc, native: bool = False) -> int:
+    t = wpc._info.total_samples
+    return t * 8 if native and wpc._info.dsd_multiplier > 0 else t
+
+
+def WavpackGetSampleIndex(wpc) -> int:
+    return wpc._pos
+
+
+def WavpackGetNumErrors(wpc) -> int:
+    return int(wpc._result.crc_errors) if wpc._result is not None else 0
+
+
+def WavpackLossy(wpc) -> bool:
+    if wpc._result is not None:
+        return bool(wpc._result.lossy)
+    return bool(wpc._info.lossy)
+
+
+def WavpackGetSampleRate(wpc) -> int:
+    return int(wpc._info.sample_rate)
+
+
+def WavpackGetNumChannels(wpc) -> int:
+    return int(wpc._info.num_channels)
+
+
+def WavpackGetBitsPerSample(wpc) -> int:
+    return int(wpc._info.bits_per_sample)
+
+
+def WavpackGetBytesPerSample(wpc) -> int:
+    return int(wpc._info.bytes_per_sample)
+
+
+def WavpackGetReducedChannels(wpc) -> int:
+    return int(wpc._info.reduced_channels) or int(wpc._info.num_channels) or 2
+
+
+def WavpackGetMode(wpc) -> int:
+    return int(wpc._info.mode)
+
+
+def WavpackGetFileFormat(wpc) -> int:
+    return int(wpc._info.file_format)
+
+
+def WavpackGetErrorMessage(wpc):
+    return wpc.error_message
+
+
+def WavpackGetVersion(wpc) -> int:
+    return int(wpc._info.version)
+
+
+def WavpackGetIsFloat(wpc) -> bool:
+    return bool(wpc._info.is_float)
+
+
+def WavpackGetIsFive(wpc) -> bool:
+    return bool(wpc._info.is_five)
+
+
+def WavpackGetHeader(wpc):
+    i = wpc._info
+    return None if i.header_off < 0 else wpc._data[i.header_off:i.header_off + i.header_len]
+
+
+def WavpackGetTrailer(wpc):
+    i = wpc._info
+    return None if i.trailer_off < 0 else wpc._data[i.trailer_off:i.trailer_off + i.trailer_len]

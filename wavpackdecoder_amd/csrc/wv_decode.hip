@@ -1,0 +1,101 @@
+// wv_decode.hip -- HIP kernels (gfx950) for the WavPack block decode.
+//
+// Kernel map:
+//   wv_decode_pcm_lane  : one lane per PCM block; runs decode_pcm_block
+//                         (get_words -> decorr passes -> joint/CRC/mute ->
+//                         fixup -> int32 store) fused, sample-major.
+//   wv_decode_dsd_lane  : one lane per DSD block (DsdUtils modes 0/1/3).
+//   wv_dsd_fill         : post-pass writing the 0x55 mute fills of DSD blocks in
+//                         call-buffer coordinates (DsdUtils.cs:104-117, quirk B-9).
+// No MFMA: there is no contraction in this path; the work is serial integer
+// bit-parsing per block, so the design goal is many independent blocks in
+// flight with the whole per-sample pipeline in registers.
+#include <hip/hip_runtime.h>
+
+#include "wv_decode_core.h"
+
+namespace wvg {
+
+struct DevStore {
+    int32_t *out;
+    __device__ __forceinline__ void put(uint64_t i, int32_t v) { out[i] = v; }
+};
+
+extern "C" __global__ void __launch_bounds__(64) wv_decode_pcm_lane(const BlockDesc *__restrict__ descs,
+                                                                    const uint32_t *__restrict__ list, uint32_t n,
+                                                                    const uint8_t *__restrict__ blob,
+                                                                    int32_t *__restrict__ out,
+                                                                    uint32_t *__restrict__ status) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t bi = list[i];
+    const BlockDesc &d = descs[bi];
+    DevStore st{out + d.out_off};
+    status[bi] = d.fstatus | decode_pcm_block(d, blob, st);
+}
+
+extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_lane(const BlockDesc *__restrict__ descs,
+                                                                    const uint32_t *__restrict__ list, uint32_t n,
+                                                                    const uint8_t *__restrict__ blob,
+                                                                    const uint8_t *__restrict__ tables,
+                                                                    int32_t *__restrict__ ptables,
+                                                                    int32_t *__restrict__ out,
+                                                                    uint32_t *__restrict__ status,
+                                                                    uint32_t *__restrict__ mute_chunk) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t bi = list[i];
+    const BlockDesc &d = descs[bi];
+    DevStore st{out + d.out_off};
+    DsdResult r = decode_dsd_block(d, blob, tables, ptables + (size_t)i * 256, st);
+    status[bi] = d.fstatus | r.status;
+    mute_chunk[bi] = r.mute_chunk;
+}
+
+// one thread per DSD block; fills only for blocks that muted
+extern "C" __global__ void __launch_bounds__(64) wv_dsd_fill(const BlockDesc *__restrict__ descs,
+                                                             const uint32_t *__restrict__ list, uint32_t n,
+                                                             const uint32_t *__restrict__ status,
+                                                             const uint32_t *__restrict__ mute_chunk,
+                                                             int32_t *__restrict__ out) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t bi = list[i];
+    if (!(status[bi] & ST_DSD_MUTE)) return;
+    const BlockDesc &d = descs[bi];
+    uint32_t f = 0, cl = d.first_chunk, mc = mute_chunk[bi];
+    for (uint32_t ci = 0; f < d.nframes; ci++) {
+        uint32_t len = cl < d.nframes - f ? cl : d.nframes - f;
+        if (ci >= mc) {
+            int64_t start = (int64_t)d.out_off + (int64_t)f * d.out_nch - (ci == 0 ? (int64_t)d.first_bsp : 0);
+            for (int64_t k = 0; k < (int64_t)len * d.call_nch; k++) out[start + k] = 0x55;
+        }
+        f += len;
+        cl = d.chunk;
+    }
+}
+
+}  // namespace wvg
+
+// ---------------------------------------------------------------------------
+// host launchers (called from wv_api.cpp)
+// ---------------------------------------------------------------------------
+namespace wvg {
+
+hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint32_t n_pcm, const uint32_t *dsd_list,
+                         uint32_t n_dsd, const uint8_t *blob, const uint8_t *tables, int32_t *ptables, int32_t *out,
+                         uint32_t *status, uint32_t *mute_chunk, hipStream_t s) {
+    if (n_pcm) {
+        hipLaunchKernelGGL(wv_decode_pcm_lane, dim3((n_pcm + 63) / 64), dim3(64), 0, s, descs, pcm_list, n_pcm, blob,
+                           out, status);
+    }
+    if (n_dsd) {
+        hipLaunchKernelGGL(wv_decode_dsd_lane, dim3((n_dsd + 63) / 64), dim3(64), 0, s, descs, dsd_list, n_dsd, blob,
+                           tables, ptables, out, status, mute_chunk);
+        hipLaunchKernelGGL(wv_dsd_fill, dim3((n_dsd + 63) / 64), dim3(64), 0, s, descs, dsd_list, n_dsd, status,
+                           mute_chunk, out);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace wvg

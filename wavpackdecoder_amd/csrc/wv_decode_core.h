@@ -1,0 +1,911 @@
+// wv_decode_core.h -- per-block WavPack PCM decode, sample-major.
+//
+// This is the reference's hot path (WavPackUtils.WavpackUnpackSamples ->
+// UnpackUtils.unpack_samples, WavPackUtils.cs:200-282 / UnpackUtils.cs:510-686)
+// re-expressed for one block at a time and one frame at a time:
+//
+//   get_words           WordsUtils.cs:272-511  (entropy decode of the residuals)
+//   decorr passes       UnpackUtils.cs:688-1240 (adaptive prediction, every pass)
+//   joint stereo + CRC + mute          UnpackUtils.cs:549-664
+//   fixup_samples / float_values       UnpackUtils.cs:1251-1404, FloatUtils.cs:32-56
+//   FALSE_STEREO duplication           UnpackUtils.cs:668-680
+//   check_crc_error                    UnpackUtils.cs:1414-1421
+//
+// The reference evaluates pass-major over each caller chunk (4096 frames in
+// WvDemo).  Sample-major gives the same values except at three chunk seams,
+// which are emulated from the descriptor's chunk schedule:
+//   * weights are stored back as (short) at the end of every pass call and
+//     after the first 8 frames of stereo chunks >= 16 frames (Appendix B-4);
+//   * muting zeroes the whole chunk and every later chunk (Appendix B-5);
+//   * the mono mute test compares an absolute buffer index (Appendix B-6).
+//
+// The code is __host__ __device__: the HIP kernel (wv_decode.hip) runs it one
+// block per lane, and tests/emu builds it for the host so the logic can be
+// checked against the oracle on a machine without a GPU.
+#pragma once
+#include <stdint.h>
+
+#include "wv_desc.h"
+#include "wv_format.h"
+
+namespace wvg {
+
+#if defined(__HIPCC__)
+__constant__ uint8_t c_exp2_table[256] = {WVF_EXP2_TABLE};
+__constant__ uint8_t c_log2_table[256] = {WVF_LOG2_TABLE};
+#endif
+
+WVF_HD int tab_exp2(int i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return c_exp2_table[i];
+#else
+    return wvf::host_exp2_table[i];
+#endif
+}
+WVF_HD int tab_log2(int i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return c_log2_table[i];
+#else
+    return wvf::host_log2_table[i];
+#endif
+}
+
+enum { DEC_OK = 0, DEC_BITS_ERROR = 1, DEC_EXCEPTION = 2 };
+
+// exp2s (WordsUtils.cs:633-646); int.MinValue recurses forever in C# -> exception
+WVF_HD int32_t dev_exp2s(int32_t log, int &exc) {
+    bool neg = log < 0;
+    if (log == INT32_MIN) {
+        exc = 1;
+        return 0;
+    }
+    if (neg) log = -log;
+    int64_t value = tab_exp2(log & 0xff) | 0x100;
+    int e = log >> 8;
+    int32_t r = (e <= 9) ? (int32_t)wvf::sar64(value, 9 - e) : (int32_t)wvf::shl64(value, e - 9);
+    return neg ? (int32_t)(0u - (uint32_t)r) : r;
+}
+
+// mylog2 (WordsUtils.cs:588-608); out-of-table indices are C# exceptions
+WVF_HD int dev_mylog2(int64_t avalue, int &exc) {
+    avalue += avalue >> 9;
+    if (avalue < 0 || avalue >= (1LL << 32)) {
+        exc = 1;
+        return 0;
+    }
+    uint32_t a = (uint32_t)avalue;
+    int dbits = a ? 32 - __builtin_clz(a) : 0;
+    if (a < 256) return (dbits << 8) + tab_log2((int)(((uint64_t)a << (9 - dbits)) & 0xff));
+    return (dbits << 8) + tab_log2((int)((a >> (dbits - 9)) & 0xff));
+}
+
+// ---------------------------------------------------------------------------
+// Bit reader over the batch blob: the byte-serial LSB-first Bitstream of
+// BitsUtils.cs:15-68 as a 64-bit window.  Bytes at or past `end` read as
+// 0xFF (bs_read fills the buffer with -1 once ptr reaches end, :125-139).
+// ---------------------------------------------------------------------------
+struct BitReader {
+    const uint8_t *base;
+    uint64_t pos, end;
+    uint64_t win;
+    int nb;
+
+    WVF_HD void init(const uint8_t *blob, uint64_t off, uint64_t len) {
+        base = blob;
+        pos = off;
+        end = off + len;
+        win = 0;
+        nb = 0;
+    }
+    // keep at least 33 valid bits in the window
+    WVF_HD void refill() {
+        while (nb <= 56) {
+            uint64_t b = pos < end ? (uint64_t)base[pos] : 0xFFull;
+            win |= b << nb;
+            nb += 8;
+            pos++;
+        }
+    }
+    WVF_HD void need(int n) {
+        if (nb < n) refill();
+    }
+    WVF_HD void skip(int n) {
+        win >>= n;
+        nb -= n;
+    }
+    WVF_HD int getbit() {
+        need(1);
+        int b = (int)(win & 1);
+        skip(1);
+        return b;
+    }
+    // n <= 32 (masked result, as every reference caller masks)
+    WVF_HD uint32_t getbits(int n) {
+        if (n <= 0) return 0;
+        need(n);
+        uint32_t v = (uint32_t)(win & ((n == 64) ? ~0ull : ((1ull << n) - 1)));
+        skip(n);
+        return v;
+    }
+    // count leading one bits (stream order), capped at `cap` (cap <= 40)
+    WVF_HD int ones_run(int cap) {
+        need(cap + 1);
+        uint64_t inv = ~win;
+        int r = inv ? __builtin_ctzll(inv) : 64;
+        return r < cap ? r : cap;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// entropy state: words_data + entropy_data (words_data.cs, entropy_data.cs)
+// ---------------------------------------------------------------------------
+struct Entropy {
+    int32_t med[2][3];
+    int32_t slow[2];
+    int32_t errlim[2];
+    int64_t acc[2], dlt[2];
+    int64_t zeros_acc;
+    bool h1, h0;
+};
+
+// update_error_limit (WordsUtils.cs:195-261)
+WVF_HD void update_error_limit(Entropy &w, uint32_t flags, int &exc) {
+    using namespace wvf;
+    int32_t bitrate_0 = (int32_t)((w.acc[0] += w.dlt[0]) >> 16);
+    if (flags & MONO_DATA) {
+        if (flags & HYBRID_BITRATE) {
+            int32_t slow_log_0 = add32(w.slow[0], SLO) >> SLS;
+            w.errlim[0] = (sub32(slow_log_0, bitrate_0) > -0x100) ? dev_exp2s(add32(sub32(slow_log_0, bitrate_0), 0x100), exc) : 0;
+        } else
+            w.errlim[0] = dev_exp2s(bitrate_0, exc);
+    } else {
+        int32_t bitrate_1 = (int32_t)((w.acc[1] += w.dlt[1]) >> 16);
+        if (flags & HYBRID_BITRATE) {
+            int32_t slow_log_0 = add32(w.slow[0], SLO) >> SLS;
+            int32_t slow_log_1 = add32(w.slow[1], SLO) >> SLS;
+            if (flags & HYBRID_BALANCE) {
+                int32_t balance = add32(add32(sub32(slow_log_1, slow_log_0), bitrate_1), 1) >> 1;
+                if (balance > bitrate_0) {
+                    bitrate_1 = mul32(bitrate_0, 2);
+                    bitrate_0 = 0;
+                } else if ((int32_t)(0u - (uint32_t)balance) > bitrate_0) {
+                    bitrate_0 = mul32(bitrate_0, 2);
+                    bitrate_1 = 0;
+                } else {
+                    bitrate_1 = add32(bitrate_0, balance);
+                    bitrate_0 = sub32(bitrate_0, balance);
+                }
+            }
+            w.errlim[0] = (sub32(slow_log_0, bitrate_0) > -0x100) ? dev_exp2s(add32(sub32(slow_log_0, bitrate_0), 0x100), exc) : 0;
+            w.errlim[1] = (sub32(slow_log_1, bitrate_1) > -0x100) ? dev_exp2s(add32(sub32(slow_log_1, bitrate_1), 0x100), exc) : 0;
+        } else {
+            w.errlim[0] = dev_exp2s(bitrate_0, exc);
+            w.errlim[1] = dev_exp2s(bitrate_1, exc);
+        }
+    }
+}
+
+// One residual of get_words (WordsUtils.cs:290-503).  `c` is entidx, `even`
+// is ((csamples & 1) == 0).  Returns DEC_* and the value in `out`.
+WVF_HD int get_word(Entropy &w, BitReader &bs, uint32_t flags, int c, bool even, int32_t &out) {
+    using namespace wvf;
+    int exc = 0;
+    const bool mono = (flags & MONO_DATA) != 0;
+    if ((w.med[0][0] & ~1) == 0 && !w.h0 && !w.h1 && (w.med[1][0] & ~1) == 0) {
+        // zero-run mode (:304-352)
+        if (w.zeros_acc > 0) {
+            if (--w.zeros_acc > 0) {
+                w.slow[c] = sub32(w.slow[c], add32(w.slow[c], SLO) >> SLS);
+                out = 0;
+                return DEC_OK;
+            }
+        } else {
+            int cbits = bs.ones_run(33);
+            if (cbits == 33) {
+                bs.skip(33);
+                return DEC_BITS_ERROR;
+            }
+            bs.skip(cbits + 1);
+            if (cbits < 2)
+                w.zeros_acc = cbits;
+            else
+                w.zeros_acc = (int64_t)bs.getbits(cbits - 1) | ((int64_t)1 << (cbits - 1));
+            if (w.zeros_acc > 0) {
+                w.slow[c] = sub32(w.slow[c], add32(w.slow[c], SLO) >> SLS);
+                for (int k = 0; k < 3; k++) w.med[0][k] = w.med[1][k] = 0;
+                out = 0;
+                return DEC_OK;
+            }
+        }
+    }
+
+    int32_t ones;
+    if (w.h0) {
+        w.h0 = false;
+        ones = 0;
+    } else {
+        // unary count with LIMIT_ONES escape (:361-409): leading ones, capped at 17
+        int u = bs.ones_run(17);
+        if (u == 17) {
+            bs.skip(17);
+            return DEC_BITS_ERROR;
+        }
+        bs.skip(u + 1);
+        ones = u;
+        if (u == LIMIT_ONES) {
+            int cbits = bs.ones_run(33);
+            if (cbits == 33) {
+                bs.skip(33);
+                return DEC_BITS_ERROR;
+            }
+            bs.skip(cbits + 1);
+            if (cbits < 2)
+                ones = cbits;
+            else
+                ones = (int32_t)(bs.getbits(cbits - 1) | (uint32_t)shl32(1, cbits - 1));
+            ones = add32(ones, LIMIT_ONES);
+        }
+        if (w.h1) {
+            w.h1 = (ones & 1) != 0;
+            ones = add32(ones >> 1, 1);
+        } else {
+            w.h1 = (ones & 1) != 0;
+            ones >>= 1;
+        }
+        w.h0 = !w.h1;
+    }
+
+    if ((flags & HYBRID_FLAG) && (mono || even)) update_error_limit(w, flags, exc);
+
+    int32_t *m = w.med[c];
+    int64_t low, high;
+    if (ones == 0) {
+        low = 0;
+        high = (int64_t)add32(m[0] >> 4, 1) - 1;
+        m[0] = sub32(m[0], mul32(add32(m[0], 126) >> 7, 2));
+    } else {
+        low = add32(m[0] >> 4, 1);
+        m[0] = add32(m[0], mul32(add32(m[0], 128) >> 7, 5));
+        if (ones == 1) {
+            high = low + add32(m[1] >> 4, 1) - 1;
+            m[1] = sub32(m[1], mul32(add32(m[1], 62) >> 6, 2));
+        } else {
+            low += add32(m[1] >> 4, 1);
+            m[1] = add32(m[1], mul32(add32(m[1], 64) >> 6, 5));
+            if (ones == 2) {
+                high = low + add32(m[2] >> 4, 1) - 1;
+                m[2] = sub32(m[2], mul32(add32(m[2], 30) >> 5, 2));
+            } else {
+                low += (int64_t)mul32(sub32(ones, 2), add32(m[2] >> 4, 1));
+                high = low + add32(m[2] >> 4, 1) - 1;
+                m[2] = add32(m[2], mul32(add32(m[2], 32) >> 5, 5));
+            }
+        }
+    }
+
+    int64_t mid;
+    if (w.errlim[c] == 0) {
+        // read_code (:546-570) with count_bits (:513-537)
+        int64_t maxcode = high - low;
+        if (maxcode < 0 || maxcode >= (1LL << 32)) return DEC_EXCEPTION;  // nbits_table[] out of range
+        uint32_t mc = (uint32_t)maxcode;
+        int bitcount = mc ? 32 - __builtin_clz(mc) : 0;
+        int64_t code = 0;
+        if (bitcount != 0) {
+            int64_t extras = (int64_t)shl32(1, bitcount) - maxcode - 1;
+            code = (int64_t)(bs.getbits(bitcount - 1) & (uint32_t)(shl32(1, bitcount - 1) - 1));
+            if (code >= extras) {
+                code = (code << 1) - extras;
+                if (bs.getbit()) ++code;
+            }
+        }
+        mid = code + low;
+    } else {
+        mid = (high + low + 1) >> 1;
+        while (high - low > w.errlim[c]) {
+            if (bs.getbit())
+                mid = (high + (low = mid) + 1) >> 1;
+            else
+                mid = ((high = mid - 1) + low + 1) >> 1;
+        }
+    }
+    out = bs.getbit() ? (int32_t)~(uint32_t)(uint64_t)mid : (int32_t)(uint32_t)(uint64_t)mid;
+    if (flags & HYBRID_BITRATE) {
+        int lg = dev_mylog2(mid, exc);
+        w.slow[c] = add32(sub32(w.slow[c], add32(w.slow[c], SLO) >> SLS), lg);
+    }
+    return exc ? DEC_EXCEPTION : DEC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// decorrelation pass state, sample-major.  Ring semantics: at block frame t
+// a 1..8 (or mono negative/0) pass reads slot t&7 and writes (t+(term&7))&7,
+// exactly the m/k walk of UnpackUtils.cs:869-899 seen across chunk seams.
+// ---------------------------------------------------------------------------
+struct PassState {
+    int32_t term, delta;
+    int32_t wA, wB;
+    int32_t rA[8], rB[8];
+};
+
+WVF_HD void upd_w(int32_t &w, int32_t s, int32_t b, int32_t delta) {
+    if (s != 0 && b != 0) w = ((s ^ b) < 0) ? wvf::sub32(w, delta) : wvf::add32(w, delta);
+}
+WVF_HD void upd_wc(int32_t &w, int32_t s, int32_t b, int32_t delta) {  // negative terms: clamp +-1024
+    if ((s ^ b) < 0) {
+        if (s != 0 && b != 0 && (w = wvf::sub32(w, delta)) < -1024) w = w < 0 ? -1024 : 1024;
+    } else {
+        if (s != 0 && b != 0 && (w = wvf::add32(w, delta)) > 1024) w = w < 0 ? -1024 : 1024;
+    }
+}
+
+// one stereo frame through one pass (UnpackUtils.cs:688-944 / 946-1154)
+WVF_HD void pass_stereo(PassState &p, uint32_t t, int32_t &L, int32_t &R) {
+    using namespace wvf;
+    const int32_t d = p.delta;
+    switch (p.term) {
+    case 17: {
+        int32_t sa = sub32(mul32(2, p.rA[0]), p.rA[1]);
+        p.rA[1] = p.rA[0];
+        p.rA[0] = add32(apply_weight(p.wA, sa), L);
+        upd_w(p.wA, sa, L, d);
+        L = p.rA[0];
+        int32_t sb = sub32(mul32(2, p.rB[0]), p.rB[1]);
+        p.rB[1] = p.rB[0];
+        p.rB[0] = add32(apply_weight(p.wB, sb), R);
+        upd_w(p.wB, sb, R, d);
+        R = p.rB[0];
+        break;
+    }
+    case 18: {
+        int32_t sa = sub32(mul32(3, p.rA[0]), p.rA[1]) >> 1;
+        p.rA[1] = p.rA[0];
+        p.rA[0] = add32(apply_weight(p.wA, sa), L);
+        upd_w(p.wA, sa, L, d);
+        L = p.rA[0];
+        int32_t sb = sub32(mul32(3, p.rB[0]), p.rB[1]) >> 1;
+        p.rB[1] = p.rB[0];
+        p.rB[0] = add32(apply_weight(p.wB, sb), R);
+        upd_w(p.wB, sb, R, d);
+        R = p.rB[0];
+        break;
+    }
+    case -1: {
+        int32_t sa = add32(L, apply_weight(p.wA, p.rA[0]));
+        upd_wc(p.wA, p.rA[0], L, d);
+        L = sa;
+        int32_t o = add32(R, apply_weight(p.wB, sa));
+        upd_wc(p.wB, sa, R, d);
+        R = o;
+        p.rA[0] = o;
+        break;
+    }
+    case -2: {
+        int32_t sb = add32(R, apply_weight(p.wB, p.rB[0]));
+        upd_wc(p.wB, p.rB[0], R, d);
+        R = sb;
+        int32_t o = add32(L, apply_weight(p.wA, sb));
+        upd_wc(p.wA, sb, L, d);
+        L = o;
+        p.rB[0] = o;
+        break;
+    }
+    case -3: {
+        int32_t sa = add32(L, apply_weight(p.wA, p.rA[0]));
+        upd_wc(p.wA, p.rA[0], L, d);
+        int32_t sb = add32(R, apply_weight(p.wB, p.rB[0]));
+        upd_wc(p.wB, p.rB[0], R, d);
+        p.rB[0] = sa;
+        p.rA[0] = sb;
+        L = sa;
+        R = sb;
+        break;
+    }
+    default: {
+        int m = t & 7, k = (t + (p.term & 7)) & 7;
+        int32_t sa = p.rA[m];
+        int32_t oa = add32(apply_weight(p.wA, sa), L);
+        upd_w(p.wA, sa, L, d);
+        p.rA[k] = oa;
+        L = oa;
+        int32_t sb = p.rB[m];
+        int32_t ob = add32(apply_weight(p.wB, sb), R);
+        upd_w(p.wB, sb, R, d);
+        p.rB[k] = ob;
+        R = ob;
+        break;
+    }
+    }
+}
+
+// one mono value through one pass (UnpackUtils.cs:1156-1240)
+WVF_HD void pass_mono(PassState &p, uint32_t t, int32_t &X) {
+    using namespace wvf;
+    const int32_t d = p.delta;
+    if (p.term == 17 || p.term == 18) {
+        int32_t sa = p.term == 17 ? sub32(mul32(2, p.rA[0]), p.rA[1]) : (sub32(mul32(3, p.rA[0]), p.rA[1]) >> 1);
+        p.rA[1] = p.rA[0];
+        p.rA[0] = add32(apply_weight(p.wA, sa), X);
+        upd_w(p.wA, sa, X, d);
+        X = p.rA[0];
+    } else {
+        int m = t & 7, k = (t + (p.term & 7)) & 7;
+        int32_t sa = p.rA[m];
+        int32_t o = add32(apply_weight(p.wA, sa), X);
+        upd_w(p.wA, sa, X, d);
+        p.rA[k] = o;
+        X = o;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// fixup (UnpackUtils.cs:1251-1404): everything except the wvx read is a pure
+// per-value map prepared once per block.
+// ---------------------------------------------------------------------------
+struct Fixup {
+    int mode;  // 0 float, 1 int32 per-value (zeros/ones/dups), 2 int32+wvx, 3 plain
+    int32_t fshift;
+    int32_t zeros, ones, dups, sent_bits, max_width;
+    uint32_t mask;
+    bool lossy;
+    int32_t shift, min_value, max_value, min_shifted, max_shifted;
+};
+
+WVF_HD void fixup_init(Fixup &f, const BlockDesc &d) {
+    using namespace wvf;
+    const uint32_t flags = d.flags;
+    f.lossy = (flags & HYBRID_FLAG) != 0;
+    int32_t shift = d.shift;
+    f.zeros = d.int32_zeros;
+    f.ones = d.int32_ones;
+    f.dups = d.int32_dups;
+    f.sent_bits = d.int32_sent_bits;
+    f.max_width = d.int32_max_width;
+    f.mask = (uint32_t)shl32(1, f.sent_bits) - 1u;
+    f.fshift = d.float_shift;
+    if (f.fshift > 32) f.fshift = 32;
+    else if (f.fshift < -32) f.fshift = -32;
+    if (flags & FLOAT_DATA) {
+        f.mode = 0;
+    } else if (flags & INT32_DATA) {
+        if (d.wvx_state & 0x100) {
+            f.mode = 2;
+        } else if (f.sent_bits == 0 && (f.zeros + f.ones + f.dups) != 0) {
+            f.mode = 1;
+            while (f.lossy && (flags & BYTES_STORED) == 3 && shift < 8) {
+                if (f.zeros > 0) f.zeros--;
+                else if (f.ones > 0) f.ones--;
+                else if (f.dups > 0) f.dups--;
+                else break;
+                shift++;
+            }
+        } else {
+            f.mode = 3;
+            shift += f.zeros + f.sent_bits + f.ones + f.dups;
+        }
+    } else
+        f.mode = 3;
+    f.shift = shift & 0x1f;
+    switch (flags & BYTES_STORED) {
+    case 0: f.min_value = sar32(-128, f.shift); f.max_value = sar32(127, f.shift); break;
+    case 1: f.min_value = sar32(-32768, f.shift); f.max_value = sar32(32767, f.shift); break;
+    case 2: f.min_value = sar32(-8388608, f.shift); f.max_value = sar32(8388607, f.shift); break;
+    default: f.min_value = (int32_t)(0x80000000u >> f.shift); f.max_value = sar32(0x7FFFFFFF, f.shift); break;
+    }
+    f.min_shifted = shl32(f.min_value, f.shift);
+    f.max_shifted = shl32(f.max_value, f.shift);
+}
+
+WVF_HD int32_t zod(const Fixup &f, int32_t x) {  // zeros / ones / dups (UnpackUtils.cs:1300-1305)
+    using namespace wvf;
+    if (f.zeros != 0) return shl32(x, f.zeros);
+    if (f.ones != 0) return sub32(shl32(add32(x, 1), f.ones), 1);
+    if (f.dups != 0) return sub32(shl32(add32(x, x & 1), f.dups), x & 1);
+    return x;
+}
+
+// everything after the optional wvx read
+WVF_HD int32_t fixup_tail(const Fixup &f, int32_t x) {
+    using namespace wvf;
+    if (f.mode == 0) {  // float_values
+        if (f.fshift > 0) x = shl32(x, f.fshift);
+        else if (f.fshift < 0) x = sar32(x, -f.fshift);
+        if (x > 8388607) x = 8388607;
+        else if (x < -8388608) x = -8388608;
+        return x;
+    }
+    if (f.mode == 1) x = zod(f, x);
+    if (f.lossy) {
+        if (x < f.min_value) return f.min_shifted;
+        if (x > f.max_value) return f.max_shifted;
+        return shl32(x, f.shift);
+    }
+    return f.shift ? shl32(x, f.shift) : x;
+}
+
+// int32 + wvx (UnpackUtils.cs:1271-1314): reads the extra stream, updates crc_x
+WVF_HD int32_t fixup_wvx(const Fixup &f, BitReader &xb, int32_t x, int32_t &crc_x) {
+    using namespace wvf;
+    if (f.sent_bits > 0) {
+        if (f.max_width > 0) {
+            int32_t pvalue = x < 0 ? ~x : x;
+            int width = (pvalue ? 32 - __builtin_clz((uint32_t)pvalue) : 0) + f.sent_bits;
+            int bits_to_read = f.sent_bits;
+            if (width <= f.max_width || (bits_to_read -= width - f.max_width) > 0) {
+                uint32_t data = xb.getbits(bits_to_read) & f.mask;
+                x = shl32((int32_t)((uint32_t)shl32(x, bits_to_read) | data), f.sent_bits - bits_to_read);
+            } else
+                x = shl32(x, f.sent_bits);
+        } else {
+            uint32_t data = xb.getbits(f.sent_bits) & f.mask;
+            x = (int32_t)((uint32_t)shl32(x, f.sent_bits) | data);
+        }
+    }
+    x = zod(f, x);
+    crc_x = add32(add32(mul32(crc_x, 9), mul32(x & 0xffff, 3)), (x >> 16) & 0xffff);
+    return fixup_tail(f, x);
+}
+
+// ---------------------------------------------------------------------------
+// one PCM block
+// ---------------------------------------------------------------------------
+template <class Store>
+WVF_HD uint32_t decode_pcm_block(const BlockDesc &d, const uint8_t *blob, Store &out) {
+    using namespace wvf;
+    const uint32_t flags = d.flags;
+    const bool mono = (flags & MONO_DATA) != 0;       // decode path (UnpackUtils.cs:549)
+    const bool mono_out = (flags & MONO_FLAG) != 0;   // ints written per frame: 1 or 2
+    const bool fstereo = (flags & FALSE_STEREO) != 0;
+    const bool joint = (flags & JOINT_STEREO) != 0;
+    const int32_t ml = d.mute_limit;
+    const int nt = d.num_terms;
+    const uint32_t nfr = d.nframes;
+    const int och = mono_out ? 1 : 2;
+
+    BitReader bs;
+    bs.init(blob, d.bits_off, d.bits_len);
+    BitReader xb;
+    xb.init(blob, d.wvx_off, d.wvx_len);
+    if (d.wvx_state & 0x100) {
+        int skip = (d.wvx_state >> 1) & 0x7f;
+        if (skip) xb.getbits(skip);
+    }
+
+    Entropy w;
+    for (int c = 0; c < 2; c++) {
+        for (int k = 0; k < 3; k++) w.med[c][k] = d.median[c][k];
+        w.slow[c] = d.slow_level[c];
+        w.errlim[c] = 0;
+        w.acc[c] = d.bitrate_acc[c];
+        w.dlt[c] = d.bitrate_delta[c];
+    }
+    w.zeros_acc = 0;
+    w.h0 = w.h1 = false;
+
+    PassState ps[MAXP];
+    for (int i = 0; i < nt; i++) {
+        ps[i].term = d.term[i];
+        ps[i].delta = d.delta[i];
+        ps[i].wA = d.weight_A[i];
+        ps[i].wB = d.weight_B[i];
+        for (int k = 0; k < 8; k++) {
+            ps[i].rA[k] = d.samples_A[i][k];
+            ps[i].rB[k] = d.samples_B[i][k];
+        }
+    }
+
+    Fixup fx;
+    fixup_init(fx, d);
+
+    uint32_t status = 0;
+    if (fstereo && fx.mode == 2) status |= ST_NONDET;  // fixup reads wvx bits for 2n values (n stale)
+    bool crc_garbage = false;
+    int32_t crc = -1, crc_x = -1;
+    bool muted = false;
+    uint32_t f = 0;  // block frame index (also the ring clock)
+    uint32_t chunk_len = d.first_chunk;
+    uint32_t bsp = d.first_bsp;
+    bool first = true;
+    while (f < nfr) {
+        uint32_t n = chunk_len;
+        if (n > nfr - f) n = nfr - f;
+        if (muted) {  // mute_error set: unpack_samples zero-fills (UnpackUtils.cs:527-543)
+            for (uint32_t j = 0; j < n; j++)
+                for (int c = 0; c < och; c++) out.put((uint64_t)(f + j) * och + c, 0);
+            f += n;
+            chunk_len = d.chunk;
+            bsp = 0;
+            first = false;
+            continue;
+        }
+        // state at the chunk start, for the wvx rewind on muting
+        BitReader xb0 = xb;
+        int32_t crcx0 = crc_x;
+        bool crc_stop = false;
+        int mute_at = -1;  // chunk-relative frame that mutes the chunk
+        for (uint32_t j = 0; j < n; j++) {
+            uint32_t t = f + j;
+            int32_t L, R = 0;
+            int rc = get_word(w, bs, flags, 0, true, L);
+            if (rc == DEC_OK && !mono) rc = get_word(w, bs, flags, 1, false, R);
+            if (rc != DEC_OK) {
+                if (rc == DEC_EXCEPTION) return status | ST_EXCEPTION;
+                // get_words stopped short: the reference decorrelates stale buffer
+                // contents; the chunk is muted and the CRC is garbage (-> error)
+                status |= ST_BITS_ERROR;
+                if (mono && first && bsp > 0) status |= ST_NONDET;
+                mute_at = (int)j;
+                crc_garbage = true;  // the verdict at block end is "error" (w.p. 1 - 2^-32)
+                break;
+            }
+            if (mono) {
+                for (int i = 0; i < nt; i++) pass_mono(ps[i], t, L);
+                int32_t a = L < 0 ? (int32_t)(0u - (uint32_t)L) : L;
+                if (!crc_stop && a > ml) {
+                    uint32_t q = bsp + j;  // absolute buffer index (quirk B-6)
+                    if (q != n) {
+                        mute_at = (int)j;
+                        break;
+                    }
+                    crc_stop = true;
+                }
+                if (!crc_stop) crc = add32(mul32(crc, 3), L);
+            } else {
+                for (int i = 0; i < nt; i++) pass_stereo(ps[i], t, L, R);
+                if (joint) {
+                    R = sub32(R, L >> 1);
+                    L = add32(L, R);
+                }
+                int32_t a = L < 0 ? (int32_t)(0u - (uint32_t)L) : L;
+                int32_t b = R < 0 ? (int32_t)(0u - (uint32_t)R) : R;
+                if (a > ml || b > ml) {
+                    mute_at = (int)j;
+                    break;
+                }
+                crc = add32(mul32(add32(mul32(crc, 3), L), 3), R);
+            }
+            // (short) weight stores at the pass-call seams (B-4)
+            if ((!mono && n >= 16 && j == 7) || j == n - 1) {
+                for (int i = 0; i < nt; i++) {
+                    ps[i].wA = (int16_t)ps[i].wA;
+                    ps[i].wB = (int16_t)ps[i].wB;
+                }
+            }
+            // fixup + store
+            int32_t oL, oR;
+            if (fx.mode == 2) {
+                oL = fixup_wvx(fx, xb, L, crc_x);
+                oR = mono ? 0 : fixup_wvx(fx, xb, R, crc_x);
+            } else {
+                oL = fixup_tail(fx, L);
+                oR = mono ? 0 : fixup_tail(fx, R);
+            }
+            uint64_t o = (uint64_t)t * och;
+            if (mono_out) {
+                out.put(o, oL);
+            } else if (fstereo) {
+                out.put(o, oL);
+                out.put(o + 1, oL);
+            } else {
+                out.put(o, oL);
+                out.put(o + 1, oR);
+            }
+        }
+        if (mute_at >= 0) {
+            // UnpackUtils.cs:649-664: zero the whole chunk, then fixup_samples runs on
+            // the zeros (which is not always 0: int32 'ones', wvx reads)
+            status |= ST_MUTED;
+            muted = true;
+            xb = xb0;
+            crc_x = crcx0;
+            for (uint32_t j = 0; j < n; j++) {
+                int32_t z0, z1 = 0;
+                if (fx.mode == 2) {
+                    z0 = fixup_wvx(fx, xb, 0, crc_x);
+                    if (!mono) z1 = fixup_wvx(fx, xb, 0, crc_x);
+                } else {
+                    z0 = fixup_tail(fx, 0);
+                    z1 = mono ? 0 : fixup_tail(fx, 0);
+                }
+                uint64_t o = (uint64_t)(f + j) * och;
+                if (mono_out) {
+                    out.put(o, z0);
+                } else if (fstereo) {
+                    out.put(o, z0);
+                    out.put(o + 1, z0);
+                } else {
+                    out.put(o, z0);
+                    out.put(o + 1, z1);
+                }
+            }
+        }
+        f += n;
+        chunk_len = d.chunk;
+        bsp = 0;
+        first = false;
+    }
+    if (nfr == d.block_samples) {  // check_crc_error at block end (WavPackUtils.cs:273-275)
+        status |= ST_CRC_CHECKED;
+        bool err = crc_garbage || crc != d.crc;
+        if (!(flags & FLOAT_DATA) && (d.wvx_state & 1) && crc_x != d.crc_mvx) err = true;
+        if (err) status |= ST_CRC_ERROR;
+    }
+    return status;
+}
+
+// ---------------------------------------------------------------------------
+// one DSD block (DsdUtils.cs:56-136 with decode_fast :244-304 and
+// decode_high :391-493).  Muting fills 0x55 from the *call* buffer start
+// (quirk B-9); the kernel only records where muting began (ST_DSD_MUTE +
+// the returned chunk index) and a post-pass writes the fills in block order.
+// `ptable` is 256 ints of per-block scratch for mode 3.
+// ---------------------------------------------------------------------------
+struct DsdResult {
+    uint32_t status;
+    uint32_t mute_chunk;  // first muted chunk (valid with ST_DSD_MUTE)
+};
+
+template <class Store>
+WVF_HD DsdResult decode_dsd_block(const BlockDesc &d, const uint8_t *blob, const uint8_t *tables, int32_t *ptable,
+                                  Store &out) {
+    using namespace wvf;
+    const uint32_t flags = d.flags;
+    const bool mono = (flags & MONO_DATA) != 0;
+    const bool fstereo = (flags & FALSE_STEREO) != 0;
+    const int wch = mono ? 1 : 2;
+    const int och = (flags & MONO_FLAG) ? 1 : 2;
+    const uint8_t *data = blob + d.bits_off;  // data[byteptr] with byteptr == 0 here
+    const uint32_t dlen = d.dsd_data_len;
+    uint32_t bp = 0;
+    int32_t crc = -1;
+    DsdResult res = {0, 0};
+    bool mute = false;
+
+    // mode 1 state
+    const int bins = d.dsd_history_bins;
+    const uint8_t *prob = tables + d.dsd_table_off;
+    const uint16_t *summed = (const uint16_t *)(tables + d.dsd_table_off + (size_t)bins * 256);
+    const uint8_t *lookup = tables + d.dsd_table_off + (size_t)bins * 768;
+    const int32_t *vlook = (const int32_t *)(tables + d.dsd_table_off + (size_t)bins * 2048);
+    uint32_t low = 0, high = 0xFFFFFFFFu, value = 0;
+    int p0 = 0, p1 = 0;
+    // mode 3 state
+    int32_t F[2][9];  // value, filter0..6, factor
+    int32_t bytei[2] = {0, 0};
+    if (d.kind == KIND_DSD_FAST || d.kind == KIND_DSD_HIGH) {
+        for (int i = 0; i < 4; i++) value = (value << 8) | data[bp++];
+    }
+    if (d.kind == KIND_DSD_HIGH) {
+        const int32_t *pt0 = (const int32_t *)(tables + d.dsd_table_off);
+        for (int i = 0; i < 256; i++) ptable[i] = pt0[i];
+        for (int c = 0; c < 2; c++) {
+            F[c][0] = 0;
+            F[c][1] = 0;
+            for (int k = 0; k < 5; k++) F[c][2 + k] = d.dsd_filters[c][k];
+            F[c][7] = 0;  // filter6
+            F[c][8] = d.dsd_filters[c][5];  // factor
+        }
+    }
+
+    uint32_t f = 0, chunk_len = d.first_chunk, ci = 0;
+    while (f < d.nframes) {
+        uint32_t n = chunk_len;
+        if (n > d.nframes - f) n = d.nframes - f;
+        bool chunk_ok = true;
+        if (!mute) {
+            for (uint32_t j = 0; j < n && chunk_ok; j++) {
+                int32_t v[2] = {0, 0};
+                for (int c = 0; c < wch; c++) {
+                    int code;
+                    if (d.kind == KIND_DSD_RAW) {
+                        code = bp < dlen ? data[bp] : 0;
+                        bp++;
+                    } else if (d.kind == KIND_DSD_FAST) {
+                        const int pi = p0 * 256;
+                        uint32_t tot = summed[pi + 255];
+                        if (tot == 0) { chunk_ok = false; break; }
+                        uint32_t mult = (high - low) / tot;
+                        if (mult == 0) {
+                            if (dlen - bp >= 4)
+                                for (int i = 0; i < 4; i++) value = (value << 8) | data[bp++];
+                            low = 0;
+                            high = 0xFFFFFFFFu;
+                            mult = high / tot;
+                            if (mult == 0) { chunk_ok = false; break; }
+                        }
+                        uint32_t index = (value - low) / mult;
+                        if (index >= tot) { chunk_ok = false; break; }
+                        code = lookup[vlook[p0] + index];
+                        if (code > 0) low += summed[pi + code - 1] * mult;
+                        high = low + prob[pi + code] * mult - 1;
+                        if (mono)
+                            p0 = code & (bins - 1);
+                        else {
+                            p0 = p1;
+                            p1 = code & (bins - 1);
+                        }
+                        while (((high ^ low) & 0xFF000000u) == 0 && bp < dlen) {
+                            value = (value << 8) | data[bp++];
+                            high = (high << 8) | 0xFF;
+                            low <<= 8;
+                        }
+                    } else {
+                        code = 0;  // filled below for both channels at once
+                    }
+                    v[c] = code;
+                }
+                if (!chunk_ok) break;
+                if (d.kind == KIND_DSD_HIGH) {
+                    for (int c = 0; c < wch; c++) F[c][0] = add32(sub32(F[c][2], F[c][6]), mul32(F[c][7], F[c][8]) >> 2);
+                    for (int bit = 0; bit < 8; bit++) {
+                        for (int c = 0; c < wch; c++) {
+                            int32_t *q = F[c];
+                            int pp = (q[0] >> 8) & 255;
+                            uint32_t split = low + ((high - low) >> 8) * ((uint32_t)ptable[pp] >> 16);
+                            if (value <= split) {
+                                high = split;
+                                ptable[pp] += (0x010000FE - ptable[pp]) >> 8;
+                                q[1] = -1;
+                            } else {
+                                low = split + 1;
+                                ptable[pp] += (0x00010000 - ptable[pp]) >> 8;
+                                q[1] = 0;
+                            }
+                            while (((high ^ low) & 0xFF000000u) == 0 && bp < dlen) {
+                                value = (value << 8) | data[bp++];
+                                high = (high << 8) | 0xFF;
+                                low <<= 8;
+                            }
+                            q[0] = add32(q[0], mul32(q[7], 8));
+                            bytei[c] = shl32(bytei[c], 1) | (q[1] & 1);
+                            q[8] = add32(q[8], (((q[0] ^ q[1]) >> 31) | 1) & ((q[0] ^ sub32(q[0], mul32(q[7], 16))) >> 31));
+                            q[2] = add32(q[2], sub32(q[1] & (1 << 20), q[2]) >> 6);
+                            q[3] = add32(q[3], sub32(q[1] & (1 << 20), q[3]) >> 4);
+                            q[4] = add32(q[4], sub32(q[3], q[4]) >> 4);
+                            q[5] = add32(q[5], sub32(q[4], q[5]) >> 4);
+                            q[0] = sub32(q[5], q[6]) >> 4;
+                            q[6] = add32(q[6], q[0]);
+                            q[7] = add32(q[7], sub32(q[0], q[7]) >> 3);
+                            q[0] = add32(sub32(q[2], q[6]), mul32(q[7], q[8]) >> 2);
+                        }
+                    }
+                    for (int c = 0; c < wch; c++) {
+                        v[c] = bytei[c] & 0xFF;
+                        F[c][8] = sub32(F[c][8], add32(F[c][8], 512) >> 10);
+                    }
+                }
+                for (int c = 0; c < wch; c++) crc = add32(crc, add32(shl32(crc, 1), v[c]));
+                uint64_t o = (uint64_t)(f + j) * och;
+                if (mono && !fstereo) {
+                    out.put(o, v[0]);
+                } else if (fstereo) {
+                    out.put(o, v[0]);
+                    out.put(o + 1, v[0]);
+                } else {
+                    out.put(o, v[0]);
+                    out.put(o + 1, v[1]);
+                }
+            }
+            if (!chunk_ok) {
+                mute = true;
+                res.status |= ST_NONDET;  // the rest of this chunk's region keeps stale caller data
+            }
+            // DsdUtils.cs:99-101: the final chunk checks the crc and mutes on mismatch
+            if (!mute && f + n == d.block_samples && crc != d.crc) mute = true;
+        }
+        if (mute && !(res.status & ST_DSD_MUTE)) {
+            res.status |= ST_DSD_MUTE;
+            res.mute_chunk = ci;
+        }
+        f += n;
+        chunk_len = d.chunk;
+        ci++;
+    }
+    if (d.nframes == d.block_samples) {
+        res.status |= ST_CRC_CHECKED;
+        if (crc != d.crc) res.status |= ST_CRC_ERROR;
+    }
+    return res;
+}
+
+}  // namespace wvg

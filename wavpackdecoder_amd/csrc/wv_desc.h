@@ -1,0 +1,83 @@
+// wv_desc.h -- the host->device block descriptor.
+//
+// One descriptor per decoded WavPack block: everything unpack_init
+// (UnpackUtils.cs:24-68) and the metadata readers leave in the WavpackStream
+// before WavpackUnpackSamples starts decoding the block, flattened so a lane
+// or wave can load it with a few wide loads.  Built by wv_framing.cpp,
+// consumed by wv_decode.hip.
+#pragma once
+#include <stdint.h>
+
+namespace wvg {
+
+enum BlockKind : uint32_t {
+    KIND_PCM = 0,        // UnpackUtils.unpack_samples path
+    KIND_DSD_RAW = 1,    // DsdUtils mode 0
+    KIND_DSD_FAST = 2,   // DsdUtils mode 1 (decode_fast)
+    KIND_DSD_HIGH = 3,   // DsdUtils mode 3 (decode_high)
+    KIND_SKIP = 4,       // nothing to decode on the device (error already known)
+};
+
+// status bits written per block by the kernels (and by the framing for
+// blocks it already knows the verdict of)
+enum StatusBits : uint32_t {
+    ST_CRC_CHECKED = 1u << 0,  // the block ran to its end: check_crc_error applies
+    ST_CRC_ERROR = 1u << 1,    // check_crc_error() was true (WavPackUtils.cs:273-275)
+    ST_MUTED = 1u << 2,        // mute_error was raised in some chunk
+    ST_BITS_ERROR = 1u << 3,   // get_words hit the 33-ones / 17-ones break
+    ST_EXCEPTION = 1u << 4,    // the reference would raise a C# exception here
+    ST_UNSUPPORTED = 1u << 5,  // state depends on data the device cannot see (sticky decode state)
+    ST_DSD_MUTE = 1u << 6,     // DSD chunk(s) muted with 0x55 (post-pass fill, DsdUtils.cs:104-117)
+    ST_NONDET = 1u << 7,       // reference output depends on stale caller-buffer contents
+};
+
+constexpr int MAXP = 16;  // MAX_NTERMS
+
+struct alignas(16) BlockDesc {
+    // --- bitstreams (byte offsets into the batch blob)
+    uint64_t bits_off;      // ID_WV_BITSTREAM payload (PCM) or DSD payload start (after mult/mode bytes)
+    uint64_t out_off;       // int32 index of the block's first output value
+    uint64_t wvx_off;       // ID_WVX payload (after the 4 crc bytes), if any
+    uint32_t bits_len;      // payload bytes that are real (past them everything reads 0xFF)
+    uint32_t wvx_len;       // bytes of the wvx stream counted from wvx_off (end - 4)
+    uint32_t kind;          // BlockKind
+    uint32_t flags;         // header flags
+    uint32_t nframes;       // frames this block decodes (<= block_samples)
+    uint32_t block_samples; // header block_samples (CRC is checked only when nframes reaches it)
+    int32_t crc;            // expected header crc
+    int32_t crc_mvx;        // expected wvx crc
+    uint32_t first_chunk;   // frames in the first unpack_samples call for this block
+    uint32_t chunk;         // frames per later call (the caller's buffer, 4096 for WvDemo)
+    uint32_t first_bsp;     // bufferStartPos (ints) of the first call
+    uint32_t out_nch;       // ints per output frame (reduced/num channels)
+    uint32_t call_nch;      // DSD mute-fill width per frame
+    int32_t mute_limit;     // ((1 << MAG) + 2), doubled for hybrid, C# int wrap applied
+    // --- fixup (UnpackUtils.cs:1251-1404, FloatUtils.cs:32-56)
+    int32_t shift;          // header SHIFT
+    int32_t float_shift;    // float_max_exp - float_norm_exp + float_shift (unclamped)
+    int32_t int32_sent_bits, int32_zeros, int32_ones, int32_dups, int32_max_width;
+    int32_t wvx_state;      // 0: wvxbits == null; bit0 valid, bits1-7 skip bits, bit8 fixup reads it (INT32)
+    // --- entropy state (words_data, WordsUtils.cs:75-187)
+    int32_t median[2][3];
+    int32_t slow_level[2];
+    int64_t bitrate_acc[2];
+    int64_t bitrate_delta[2];
+    // --- decorrelation passes in decoder order (UnpackUtils.cs:156-360)
+    int32_t num_terms;
+    uint32_t fstatus;       // StatusBits the framing already knows (UNSUPPORTED, NONDET, ...)
+    int8_t term[MAXP];
+    int8_t delta[MAXP];
+    int16_t weight_A[MAXP];
+    int16_t weight_B[MAXP];
+    int32_t samples_A[MAXP][8];
+    int32_t samples_B[MAXP][8];
+    // --- DSD (DsdUtils.cs:17-54, 149-242, 343-389)
+    uint32_t dsd_data_len;  // bytes from bits_off to the end of the sub-block (C# data.Length - byteptr)
+    int32_t dsd_history_bins;
+    uint64_t dsd_table_off; // offset into the batch's DSD table area (fast mode)
+    int32_t dsd_rate_i;
+    int32_t dsd_filters[2][7];  // filter1..5, factor (high mode), per channel
+    int32_t dsd_pad[1];
+};
+
+}  // namespace wvg

@@ -1,0 +1,927 @@
+// wv_framing.cpp -- host framing for the MI355X WavPack decode path.
+// See wv_framing.h.  Every routine names the reference code it restates.
+#include "wv_framing.h"
+
+#include <string.h>
+
+#include <stdexcept>
+
+#include "wv_format.h"
+
+namespace wvg {
+using namespace wvf;
+
+namespace {
+
+struct CsException : std::exception {};  // a C# exception escaping to the caller (WvDemo.cs:144)
+
+// ---- reference state that matters to the framing -------------------------
+struct Hdr {  // WavpackHeader.cs:15-22
+    uint32_t ckSize = 0;
+    int16_t version = 0;
+    int64_t total_samples = 0, block_index = 0;
+    uint32_t block_samples = 0, flags = 0;
+    int32_t crc = 0;
+    bool error = false;
+    int64_t stream_position = 0, average_block_size = 0;
+};
+
+struct Pass {  // decorr_pass.cs:24-26 + "does the host know its value"
+    int16_t term = 0, delta = 0, wA = 0, wB = 0;
+    int32_t sA[8] = {0}, sB[8] = {0};
+    bool known_w = true, known_s = true;
+};
+
+struct Words {  // words_data.cs
+    int32_t med[2][3] = {{0, 0, 0}, {0, 0, 0}};
+    int32_t slow[2] = {0, 0};
+    int64_t acc[2] = {0, 0}, dlt[2] = {0, 0};
+    bool known = true;
+};
+
+struct BitsRef {  // a Bitstream reference: where its bytes are and whether it is untouched
+    bool valid = false;
+    int64_t file_off = 0;
+    int32_t byte_length = 0;  // bs.end
+    int32_t data_len = 0;     // C# data.Length
+    bool fresh = false;       // opened in the current unpack_init and not yet read
+};
+
+struct DsdState {  // WavpackStream.dsds
+    bool ready = false, fresh = false;
+    int mode = 0;
+    int64_t data_off = 0;  // file offset of data[0]
+    int32_t data_len = 0;  // data.Length
+    int32_t byteptr = 0;   // after init
+    int history_bins = 0;
+    std::vector<uint8_t> prob;
+    std::vector<uint16_t> summed;
+    std::vector<uint8_t> lookup;
+    std::vector<int32_t> value_lookup;
+    int32_t ptable[256];
+    int32_t filt[2][7];
+    int rate_i = 0;
+};
+
+struct Reader {  // System.IO.BinaryReader over the file bytes
+    const uint8_t *d = nullptr;
+    int64_t len = 0, pos = 0;
+    int byte() { return pos < len ? d[pos++] : -1; }
+    int read(uint8_t *dst, int n) {
+        int64_t a = len - pos;
+        if (a < 0) a = 0;
+        if (n > a) n = (int)a;
+        if (n > 0) memcpy(dst, d + pos, (size_t)n);
+        pos += n;
+        return n;
+    }
+};
+
+struct Md {  // WavpackMetadata.cs:15-23
+    int byte_length = 0;
+    const uint8_t *data = nullptr;  // read_buffer or `big`
+    int data_len = 0;
+    std::vector<uint8_t> big;
+    int64_t data_file_off = 0;  // where data[0] came from
+    uint8_t id = 0;
+    bool hasdata = false;
+    int64_t bytecount = 24;
+    uint8_t at(int64_t i) const {
+        if (i < 0 || i >= data_len) throw CsException();
+        return data[i];
+    }
+};
+
+int exp2s(int log) {
+    if (log == INT32_MIN) throw CsException();  // C# recursion never ends (StackOverflow)
+    return exp2s_host(log);
+}
+
+class Framer {
+  public:
+    // WavpackContext fields (WavpackContext.cs:15-35) + WavpackStream
+    Reader in;
+    uint8_t read_buffer[BITSTREAM_BUFFER_SIZE];
+    std::string error_message;
+    int64_t total_samples = -1;
+    int reduced_channels = 0;
+    bool lossy_blocks = false, five = false;
+    int file_format = 0;
+    uint32_t dsd_multiplier = 0;
+    int64_t header_off = -1, header_len = 0, trailer_off = -1, trailer_len = 0;
+    // config (WavpackConfig.cs)
+    int bits_per_sample = 0, bytes_per_sample = 0, num_channels = 0, float_norm_exp_cfg = 0;
+    int64_t cfg_flags = 0, sample_rate = 0, channel_mask = 0;
+    uint8_t xmode = 0;
+    // stream
+    Hdr wphdr;
+    BitsRef wvbits, wvcbits, wvxbits;
+    bool wvx_fresh = false;
+    int wvx_skip_bits = 0;
+    int32_t crc_mvx = 0;
+    Words w;
+    int num_terms = 0;
+    Pass passes[16];
+    int16_t int32_sent_bits = 0, int32_zeros = 0, int32_ones = 0, int32_dups = 0;
+    int16_t float_flags = 0, float_shift = 0, float_max_exp = 0, float_norm_exp = 0;
+    uint8_t int32_max_width = 0;
+    int64_t sample_index = 0;
+    DsdState dsd;
+    bool inited_this_block = false;  // unpack_init ran for the current header
+
+    Framer() {
+        memset(read_buffer, 0, sizeof(read_buffer));
+        // `new Bitstream()` (WavpackStream.cs:48): non-null, end == 0
+        wvbits.valid = true;
+        wvbits.byte_length = 0;
+        wvbits.fresh = false;
+    }
+
+    // ---- WavPackUtils.cs:600-671
+    void read_next_header() {
+        uint8_t b[32];
+        int64_t bytes_skipped = 0;
+        int bleft = 0, counter;
+        for (;;) {
+            for (int i = 0; i < bleft; i++) b[i] = b[32 - bleft + i];
+            counter = 0;
+            int cnt = 32 - bleft;
+            if (in.read(b + bleft, cnt) != cnt) {
+                wphdr.error = true;
+                return;
+            }
+            bleft = 32;
+            if (b[0] == 'w' && b[1] == 'v' && b[2] == 'p' && b[3] == 'k' && (b[4] & 1) == 0 && b[6] < 16 &&
+                b[7] == 0 && b[9] == 4 && b[8] >= (MIN_STREAM_VERS & 0xff) && b[8] <= (MAX_STREAM_VERS & 0xff)) {
+                wphdr.ckSize = (uint32_t)b[4] | ((uint32_t)b[5] << 8) | ((uint32_t)b[6] << 16) | ((uint32_t)b[7] << 24);
+                wphdr.version = (int16_t)((b[9] << 8) | b[8]);
+                wphdr.total_samples = (int64_t)(((uint64_t)b[11] << 32) | ((uint64_t)b[15] << 24) |
+                                                ((uint64_t)b[14] << 16) | ((uint64_t)b[13] << 8) | b[12]);
+                wphdr.block_index = (int64_t)(((uint64_t)b[10] << 32) | ((uint64_t)b[19] << 24) |
+                                              ((uint64_t)b[18] << 16) | ((uint64_t)b[17] << 8) | b[16]);
+                wphdr.block_samples = (uint32_t)b[20] | ((uint32_t)b[21] << 8) | ((uint32_t)b[22] << 16) | ((uint32_t)b[23] << 24);
+                wphdr.flags = (uint32_t)b[24] | ((uint32_t)b[25] << 8) | ((uint32_t)b[26] << 16) | ((uint32_t)b[27] << 24);
+                wphdr.crc = (int32_t)((uint32_t)b[28] | ((uint32_t)b[29] << 8) | ((uint32_t)b[30] << 16) | ((uint32_t)b[31] << 24));
+                wphdr.error = false;
+                wphdr.stream_position = in.pos - bleft;
+                wphdr.average_block_size =
+                    wphdr.average_block_size == 0 ? wphdr.ckSize : (wphdr.average_block_size + wphdr.ckSize) / 2;
+                inited_this_block = false;
+                return;
+            }
+            counter++;
+            bleft--;
+            while (bleft > 0 && b[counter] != 'w') {
+                counter++;
+                bleft--;
+            }
+            bytes_skipped += counter;
+            if (bytes_skipped > 1048576LL) {
+                wphdr.error = true;
+                return;
+            }
+        }
+    }
+
+    // ---- MetadataUtils.cs:15-109
+    bool read_metadata_buff(Md &m) {
+        if (m.bytecount >= wphdr.ckSize) return false;
+        int a = in.byte();
+        if (a < 0) return false;
+        m.id = (uint8_t)a;
+        int t = in.byte();
+        if (t < 0) return false;
+        m.bytecount += 2;
+        m.byte_length = t << 1;
+        if (m.id & ID_LARGE) {
+            m.id &= (uint8_t)~ID_LARGE;
+            if ((t = in.byte()) < 0) return false;
+            m.byte_length += t << 9;
+            if ((t = in.byte()) < 0) return false;
+            m.byte_length += t << 17;
+            m.bytecount += 2;
+        }
+        int bytes_to_read = m.byte_length;
+        if (m.id & ID_ODD_SIZE) {
+            m.id &= (uint8_t)~ID_ODD_SIZE;
+            m.byte_length--;
+        }
+        if (m.byte_length == 0) {
+            m.hasdata = false;
+            return true;
+        }
+        m.bytecount += bytes_to_read;
+        if (bytes_to_read > 0) {
+            m.data_file_off = in.pos;
+            if (bytes_to_read > BITSTREAM_BUFFER_SIZE) {
+                m.big.assign((size_t)bytes_to_read, 0);
+                m.data = m.big.data();
+                m.data_len = bytes_to_read;
+                if (in.read(m.big.data(), bytes_to_read) != bytes_to_read) {
+                    m.hasdata = false;
+                    return false;
+                }
+            } else {
+                m.data = read_buffer;
+                m.data_len = BITSTREAM_BUFFER_SIZE;
+                if (in.read(read_buffer, bytes_to_read) != bytes_to_read) {
+                    m.hasdata = false;
+                    return false;
+                }
+            }
+            m.hasdata = true;
+        }
+        return true;
+    }
+
+    // WavpackMetadata.copy_data (WavpackMetadata.cs:25-36): returns C# data.Length after the copy
+    bool copy_data(Md &m, int &len) {
+        if (!m.hasdata || m.byte_length <= 0) return false;
+        len = (m.data_len != BITSTREAM_BUFFER_SIZE) ? m.data_len : m.byte_length;
+        return true;
+    }
+
+    // ---- readers ------------------------------------------------------------
+    bool read_decorr_terms(Md &m) {  // UnpackUtils.cs:156-187
+        int termcnt = m.byte_length;
+        if (termcnt > MAX_NTERMS) return false;
+        Pass tmp[16];
+        for (int dc = termcnt - 1, c = 0; dc >= 0; dc--, c++) {
+            int b = m.at(c);
+            tmp[dc].term = (int16_t)((b & 0x1f) - 5);
+            tmp[dc].delta = (int16_t)((b >> 5) & 7);
+            if (tmp[dc].term < -3 || (tmp[dc].term > MAX_TERM && tmp[dc].term < 17) || tmp[dc].term > 18) return false;
+        }
+        for (int i = 0; i < 16; i++) passes[i] = tmp[i];
+        num_terms = termcnt;
+        return true;
+    }
+    bool read_decorr_weights(Md &m) {  // UnpackUtils.cs:196-239
+        int termcnt = m.byte_length;
+        bool mono = (wphdr.flags & MONO_DATA) != 0;
+        if (!mono) termcnt /= 2;
+        if (termcnt > num_terms) return false;
+        int16_t wa = 0, wb = 0;
+        int counter = 0, it = num_terms;
+        while (termcnt > 0) {
+            int idx = it - 1;
+            if (idx < 0 || idx >= 16) throw CsException();
+            wa = (int16_t)restore_weight((int8_t)m.at(counter++));
+            passes[idx].wA = wa;
+            if (!mono) wb = (int16_t)restore_weight((int8_t)m.at(counter++));
+            passes[idx].wB = wb;
+            passes[idx].known_w = true;
+            it--;
+            termcnt--;
+        }
+        return true;
+    }
+    bool read_decorr_samples(Md &m) {  // UnpackUtils.cs:250-360 (quirk B-7 kept)
+        int16_t term = 0;
+        int32_t tA[8] = {0}, tB[8] = {0};
+        int idx = 0;
+        for (int t = num_terms; t > 0; t--) {
+            if (idx >= 16) throw CsException();
+            term = passes[idx].term;
+            memset(passes[idx].sA, 0, sizeof(passes[idx].sA));
+            memset(passes[idx].sB, 0, sizeof(passes[idx].sB));
+            passes[idx].known_s = true;
+            idx++;
+        }
+        int counter = 0;
+        bool mono = (wphdr.flags & MONO_DATA) != 0;
+        if (wphdr.version == 0x402 && (wphdr.flags & HYBRID_FLAG)) counter += mono ? 2 : 4;
+        idx--;
+        auto rd = [&](int o) { return exp2s((int16_t)(m.at(o) + (m.at(o + 1) << 8))); };
+        while (counter < m.byte_length) {
+            if (term > MAX_TERM) {
+                tA[0] = rd(counter);
+                tA[1] = rd(counter + 2);
+                counter += 4;
+                if (!mono) {
+                    tB[0] = rd(counter);
+                    tB[1] = rd(counter + 2);
+                    counter += 4;
+                }
+            } else if (term < 0) {
+                tA[0] = rd(counter);
+                tB[0] = rd(counter + 2);
+                counter += 4;
+            } else {
+                for (int mm = 0, cnt = term; cnt > 0; mm++, cnt--) {
+                    tA[mm] = rd(counter);
+                    counter += 2;
+                    if (!mono) {
+                        tB[mm] = rd(counter);
+                        counter += 2;
+                    }
+                }
+            }
+            if (idx < 0 || idx >= 16) throw CsException();
+            memcpy(passes[idx].sA, tA, sizeof(tA));
+            memcpy(passes[idx].sB, tB, sizeof(tB));
+            passes[idx].known_s = true;
+            idx--;
+        }
+        return true;
+    }
+    bool read_entropy_vars(Md &m) {  // WordsUtils.cs:75-116
+        int b[12];
+        for (int i = 0; i < 6; i++) b[i] = m.at(i);
+        bool mono = (wphdr.flags & MONO_DATA) != 0;
+        if (m.byte_length != 12 && !mono) return false;
+        Words nw;
+        nw.med[0][0] = exp2s(b[0] + (b[1] << 8));
+        nw.med[0][1] = exp2s(b[2] + (b[3] << 8));
+        nw.med[0][2] = exp2s(b[4] + (b[5] << 8));
+        if (!mono) {
+            for (int i = 6; i < 12; i++) b[i] = m.at(i);
+            nw.med[1][0] = exp2s(b[6] + (b[7] << 8));
+            nw.med[1][1] = exp2s(b[8] + (b[9] << 8));
+            nw.med[1][2] = exp2s(b[10] + (b[11] << 8));
+        }
+        nw.known = true;
+        w = nw;
+        return true;
+    }
+    bool read_hybrid_profile(Md &m) {  // WordsUtils.cs:124-187
+        bool mono = (wphdr.flags & MONO_DATA) != 0;
+        int bc = 0;
+        auto u16 = [&](int o) { return m.at(o) + (m.at(o + 1) << 8); };
+        if (wphdr.flags & HYBRID_BITRATE) {
+            w.slow[0] = exp2s(u16(bc));
+            bc += 2;
+            if (!mono) {
+                w.slow[1] = exp2s(u16(bc));
+                bc += 2;
+            }
+        }
+        w.acc[0] = (int64_t)shl32(u16(bc), 16);
+        bc += 2;
+        if (!mono) {
+            w.acc[1] = (int64_t)shl32(u16(bc), 16);
+            bc += 2;
+        }
+        if (bc < m.byte_length) {
+            w.dlt[0] = exp2s((int16_t)u16(bc));
+            bc += 2;
+            if (!mono) {
+                w.dlt[1] = exp2s((int16_t)u16(bc));
+                bc += 2;
+            }
+            if (bc < m.byte_length) return false;
+        } else
+            w.dlt[0] = w.dlt[1] = 0;
+        return true;
+    }
+    bool init_bits(Md &m, BitsRef &br, int start) {
+        int len;
+        if (!copy_data(m, len)) return false;
+        br.valid = true;
+        br.file_off = m.data_file_off + start;
+        br.byte_length = m.byte_length;
+        br.data_len = len;
+        br.fresh = true;
+        return true;
+    }
+    bool init_wvx(Md &m) {  // UnpackUtils.cs:115-147
+        int len;
+        if (m.byte_length <= 4 || (m.byte_length & 1) || !copy_data(m, len)) return false;
+        crc_mvx = (int32_t)((uint32_t)m.at(0) | ((uint32_t)m.at(1) << 8) | ((uint32_t)m.at(2) << 16) |
+                            ((uint32_t)m.at(3) << 24));
+        wvxbits.valid = true;
+        wvxbits.file_off = m.data_file_off + 4;
+        wvxbits.byte_length = m.byte_length;
+        wvxbits.data_len = len;
+        wvxbits.fresh = true;
+        wvx_skip_bits = 0;
+        if (m.id == ID_WVX_NEW_BITSTREAM) {
+            // getbits(5) from the fresh stream: the first byte's low bits (and the second's)
+            uint32_t v = (uint32_t)m.at(4) | ((uint32_t)(len > 5 ? m.at(5) : 0) << 8);
+            if (wphdr.flags & FLOAT_DATA) {
+                wvx_skip_bits = 10;
+            } else {
+                int32_max_width = (uint8_t)(v & 0x1f);
+                wvx_skip_bits = 5;
+            }
+        }
+        return true;
+    }
+    bool read_int32_info(Md &m) {  // UnpackUtils.cs:367-382
+        if (m.byte_length != 4) return false;
+        int32_sent_bits = m.at(0);
+        int32_zeros = m.at(1);
+        int32_ones = m.at(2);
+        int32_dups = m.at(3);
+        return true;
+    }
+    bool read_float_info(Md &m) {  // FloatUtils.cs:15-30
+        if (m.byte_length != 4) return false;
+        float_flags = m.at(0);
+        float_shift = m.at(1);
+        float_max_exp = m.at(2);
+        float_norm_exp = m.at(3);
+        return true;
+    }
+    bool read_channel_info(Md &m) {  // UnpackUtils.cs:389-410
+        int bytecnt = m.byte_length, shift = 0, counter = 0;
+        if (bytecnt == 0 || bytecnt > 5) return false;
+        num_channels = m.at(counter++);
+        int64_t mask = 0;
+        while (bytecnt >= 0) {
+            mask |= (int64_t)shl32(m.at(counter++), shift);
+            shift += 8;
+            bytecnt--;
+        }
+        channel_mask = mask;
+        return true;
+    }
+    bool read_config_info(Md &m) {  // UnpackUtils.cs:432-455
+        int bytecnt = m.byte_length, counter = 0;
+        if (bytecnt >= 3) {
+            cfg_flags &= 0xff;
+            cfg_flags |= (int64_t)shl32(m.at(counter++), 8);
+            cfg_flags |= (int64_t)shl32(m.at(counter++), 16);
+            cfg_flags |= (int64_t)shl32(m.at(counter++), 24);
+        }
+        if (bytecnt >= 4 && (cfg_flags & CONFIG_EXTRA_MODE)) {
+            xmode = m.at(counter++);
+            bytecnt--;
+        }
+        if (bytecnt >= 5) five = true;
+        return true;
+    }
+    bool read_sample_rate(Md &m) {  // UnpackUtils.cs:459-473
+        if (m.byte_length == 3) {
+            sample_rate = m.at(0);
+            sample_rate |= (int64_t)shl32(m.at(1), 8);
+            sample_rate |= (int64_t)shl32(m.at(2), 16);
+        }
+        return true;
+    }
+    void read_hdr_trailer(Md &m, bool trailer) {  // UnpackUtils.cs:475-491
+        if (m.byte_length < 0 || m.byte_length > m.data_len) throw CsException();
+        if (trailer) {
+            trailer_off = m.data_file_off;
+            trailer_len = m.byte_length;
+        } else {
+            header_off = m.data_file_off;
+            header_len = m.byte_length;
+        }
+    }
+
+    // ---- DSD (DsdUtils.cs)
+    bool init_dsd_block(Md &m) {  // :17-54
+        if (m.byte_length < 2 || m.at(0) > 31) return false;
+        int len;
+        if (!copy_data(m, len)) return false;
+        DsdState d;
+        d.data_off = m.data_file_off;
+        d.data_len = len;
+        const uint8_t *data = m.data;
+        d.byteptr = 0;
+        dsd_multiplier = 1u << (data[d.byteptr++] & 31);
+        d.mode = data[d.byteptr++];
+        d.fresh = true;
+        bool ok = false;
+        if (d.mode == 0) {
+            ok = (int64_t)(d.data_len - d.byteptr) ==
+                 (int64_t)wphdr.block_samples * ((wphdr.flags & MONO_DATA) ? 1 : 2);
+            d.ready = ok;
+        } else if (d.mode == 1)
+            ok = init_fast(d, data);
+        else if (d.mode == 3)
+            ok = init_high(d, data);
+        dsd = std::move(d);
+        return ok;
+    }
+    bool init_fast(DsdState &d, const uint8_t *data) {  // :149-242
+        if (d.byteptr == d.data_len) return false;
+        int history_bits = data[d.byteptr++];
+        if (d.byteptr == d.data_len || history_bits > 5) return false;
+        d.history_bins = 1 << history_bits;
+        const int bins = d.history_bins;
+        d.lookup.assign((size_t)bins * 1280, 0);
+        d.value_lookup.assign((size_t)bins, 0);
+        d.summed.assign((size_t)bins * 256, 0);
+        d.prob.assign((size_t)bins * 256, 0);
+        int max_probability = data[d.byteptr++];
+        if (max_probability < 0xFF) {
+            size_t outptr = 0, outend = d.prob.size();
+            while (outptr < outend && d.byteptr < d.data_len) {
+                int code = data[d.byteptr++];
+                if (code > max_probability) {
+                    int z = code - max_probability;
+                    while (outptr < outend && z-- > 0) d.prob[outptr++] = 0;
+                } else if (code != 0)
+                    d.prob[outptr++] = (uint8_t)code;
+                else
+                    break;
+            }
+            if (outptr < outend || (d.byteptr < d.data_len && data[d.byteptr++] > 0)) return false;
+        } else if ((size_t)(d.data_len - d.byteptr) > d.prob.size()) {
+            memcpy(d.prob.data(), data + d.byteptr, d.prob.size());
+            d.byteptr += (int32_t)d.prob.size();
+        } else
+            return false;
+        int total = 0, lb = 0;
+        for (int bi = 0; bi < bins; bi++) {
+            uint16_t sum = 0;
+            for (int i = 0; i < 256; i++) d.summed[(size_t)bi * 256 + i] = sum = (uint16_t)(sum + d.prob[(size_t)bi * 256 + i]);
+            if (sum) {
+                if ((total += sum) > bins * 1280) return false;
+                d.value_lookup[(size_t)bi] = lb;
+                for (int i = 0; i < 256; i++)
+                    for (int c = d.prob[(size_t)bi * 256 + i]; c > 0; c--) d.lookup[(size_t)lb++] = (uint8_t)i;
+            }
+        }
+        if (d.data_len - d.byteptr < 4 || total > bins * 1280) return false;
+        d.ready = true;
+        return true;
+    }
+    bool init_high(DsdState &d, const uint8_t *data) {  // :343-389
+        bool mono = (wphdr.flags & MONO_DATA) != 0;
+        if (d.data_len - d.byteptr < (mono ? 13 : 20)) return false;
+        d.rate_i = data[d.byteptr++];
+        int rate_s = data[d.byteptr++];
+        if (rate_s != 20) return false;
+        // init_ptable (:321-341)
+        int value = 0x808000, rate = d.rate_i << 8;
+        for (int c = (rate + 128) >> 8; c > 0; c--) value += (0x00010000 - value) >> 8;
+        for (int i = 0; i < 128; ++i) {
+            d.ptable[i] = value;
+            d.ptable[255 - i] = 0x100ffff - value;
+            if (value > 0x010000) {
+                rate += (rate * rate_s + 128) >> 8;
+                for (int c = (rate + 64) >> 7; c > 0; c--) value += (0x00010000 - value) >> 8;
+            }
+        }
+        memset(d.filt, 0, sizeof(d.filt));
+        for (int ch = 0; ch < (mono ? 1 : 2); ch++) {
+            for (int k = 0; k < 5; k++) d.filt[ch][k] = data[d.byteptr++] << 12;
+            int f = data[d.byteptr++];
+            f |= data[d.byteptr++] << 8;
+            d.filt[ch][5] = (int32_t)((uint32_t)f << 16) >> 16;
+        }
+        d.ready = true;
+        return true;
+    }
+
+    // ---- MetadataUtils.process_metadata (:111-192)
+    bool process_metadata(Md &m) {
+        switch (m.id) {
+        case ID_DUMMY: return true;
+        case ID_DECORR_TERMS: return read_decorr_terms(m);
+        case ID_DECORR_WEIGHTS: return read_decorr_weights(m);
+        case ID_DECORR_SAMPLES: return read_decorr_samples(m);
+        case ID_ENTROPY_VARS: return read_entropy_vars(m);
+        case ID_HYBRID_PROFILE: return read_hybrid_profile(m);
+        case ID_SHAPING_WEIGHTS: return true;
+        case ID_FLOAT_INFO: return read_float_info(m);
+        case ID_INT32_INFO: return read_int32_info(m);
+        case ID_CHANNEL_INFO: return read_channel_info(m);
+        case ID_CONFIG_BLOCK: return read_config_info(m);
+        case ID_SAMPLE_RATE: return read_sample_rate(m);
+        case ID_WV_BITSTREAM: return init_bits(m, wvbits, 0);
+        case ID_WVC_BITSTREAM:
+            if (m.byte_length & 1) return false;
+            return init_bits(m, wvcbits, 0);
+        case ID_WVX_BITSTREAM:
+        case ID_WVX_NEW_BITSTREAM: return init_wvx(m);
+        case ID_DSD_BLOCK: return init_dsd_block(m);
+        case ID_NEW_CONFIG_BLOCK:
+            five = true;
+            if (m.byte_length >= 1) file_format = m.at(0);
+            return true;
+        case ID_RIFF_HEADER:
+        case ID_ALT_HEADER: read_hdr_trailer(m, false); return true;
+        case ID_RIFF_TRAILER:
+        case ID_ALT_TRAILER: read_hdr_trailer(m, true); return true;
+        case ID_ALT_EXTENSION:
+            if (m.byte_length < 0 || m.byte_length > m.data_len) throw CsException();
+            return true;
+        case ID_BLOCK_CHECKSUM: five = true; return true;
+        default: return (m.id & ID_OPTIONAL_DATA) != 0;
+        }
+    }
+
+    // ---- UnpackUtils.unpack_init (:24-68)
+    bool unpack_init() {
+        Md m;
+        if (wphdr.block_samples > 0 && wphdr.block_index != 0xFFFFFFFFLL) sample_index = wphdr.block_index;
+        inited_this_block = true;
+        // anything the previous decode adapted is now unknown unless re-sent
+        wvbits.fresh = false;
+        wvxbits.fresh = false;
+        dsd.fresh = false;
+        while (read_metadata_buff(m)) {
+            if (!process_metadata(m)) {
+                error_message = "invalid metadata id " + std::to_string(m.id);
+                return false;
+            }
+        }
+        if (m.bytecount != wphdr.ckSize) {
+            error_message = "invalid reading WavPack metadata block";
+            return false;
+        }
+        bool bad = (wphdr.block_samples != 0 && (wphdr.flags & DSD_FLAG)) ? !dsd.ready
+                                                                          : (!wvbits.valid || wvbits.byte_length == 0);
+        if (bad) {
+            error_message = "invalid WavPack file";
+            return false;
+        }
+        if (wphdr.block_samples != 0) {
+            if ((wphdr.flags & INT32_DATA) && int32_sent_bits != 0 && !wvxbits.valid) lossy_blocks = true;
+            if ((wphdr.flags & FLOAT_DATA) &&
+                (float_flags & (FLOAT_EXCEPTIONS | FLOAT_ZEROS_SENT | FLOAT_SHIFT_SENT | FLOAT_SHIFT_SAME)))
+                lossy_blocks = true;
+        }
+        return true;
+    }
+
+    // state snapshot for one block about to be decoded
+    BlockDesc snapshot(uint64_t blob_base, FramingOutput &out) {
+        BlockDesc d;
+        memset(&d, 0, sizeof(d));
+        d.flags = wphdr.flags;
+        d.block_samples = wphdr.block_samples;
+        d.crc = wphdr.crc;
+        uint32_t status = 0;
+        const uint32_t flags = wphdr.flags;
+        int mag = (int)((flags & MAG_MASK) >> MAG_LSB);
+        int32_t ml = (int32_t)((int64_t)(1LL << mag) + 2);
+        if (flags & HYBRID_FLAG) ml = mul32(ml, 2);
+        d.mute_limit = ml;
+        d.shift = (int32_t)((flags & SHIFT_MASK) >> SHIFT_LSB);
+        d.float_shift = float_max_exp - float_norm_exp + float_shift;
+        d.int32_sent_bits = int32_sent_bits;
+        d.int32_zeros = int32_zeros;
+        d.int32_ones = int32_ones;
+        d.int32_dups = int32_dups;
+        d.int32_max_width = int32_max_width;
+        if (!inited_this_block) status |= ST_UNSUPPORTED;
+        if (flags & DSD_FLAG) {
+            if (!dsd.fresh) status |= ST_UNSUPPORTED;
+            d.kind = dsd.mode == 0 ? KIND_DSD_RAW : dsd.mode == 1 ? KIND_DSD_FAST : KIND_DSD_HIGH;
+            d.bits_off = blob_base + (uint64_t)dsd.data_off + (uint64_t)dsd.byteptr;
+            d.dsd_data_len = (uint32_t)(dsd.data_len - dsd.byteptr);
+            d.dsd_history_bins = dsd.history_bins;
+            d.dsd_rate_i = dsd.rate_i;
+            if (dsd.mode == 1) {
+                // table area: prob[bins*256] u8 | summed[bins*256] u16 | lookup[bins*1280] u8 | value_lookup[bins] i32
+                size_t off = (out.tables.size() + 15) & ~(size_t)15;
+                size_t bins = (size_t)dsd.history_bins;
+                out.tables.resize(off + bins * 256 + bins * 512 + bins * 1280 + bins * 4 + 16, 0);
+                uint8_t *t = out.tables.data() + off;
+                memcpy(t, dsd.prob.data(), bins * 256);
+                memcpy(t + bins * 256, dsd.summed.data(), bins * 512);
+                memcpy(t + bins * 768, dsd.lookup.data(), bins * 1280);
+                memcpy(t + bins * 2048, dsd.value_lookup.data(), bins * 4);
+                d.dsd_table_off = off;
+            } else if (dsd.mode == 3) {
+                size_t off = (out.tables.size() + 15) & ~(size_t)15;
+                out.tables.resize(off + 1024, 0);
+                memcpy(out.tables.data() + off, dsd.ptable, 1024);
+                d.dsd_table_off = off;
+                memcpy(d.dsd_filters, dsd.filt, sizeof(d.dsd_filters));
+            }
+        } else {
+            d.kind = KIND_PCM;
+            if (!wvbits.fresh) status |= ST_UNSUPPORTED;  // would continue a consumed bitstream
+            d.bits_off = blob_base + (uint64_t)wvbits.file_off;
+            d.bits_len = (uint32_t)wvbits.byte_length;
+            if (wvxbits.valid) {
+                d.wvx_state = 1 | (wvx_skip_bits << 1);
+                d.crc_mvx = crc_mvx;
+                if ((flags & INT32_DATA) && !(flags & FLOAT_DATA)) {
+                    // fixup_samples reads it (UnpackUtils.cs:1271-1314)
+                    if (!wvxbits.fresh) status |= ST_UNSUPPORTED;
+                    d.wvx_state |= 0x100;
+                    d.wvx_off = blob_base + (uint64_t)wvxbits.file_off;
+                    d.wvx_len = (uint32_t)(wvxbits.data_len - 4);
+                }
+            }
+            if (!w.known) status |= ST_UNSUPPORTED;
+            memcpy(d.median, w.med, sizeof(d.median));
+            memcpy(d.slow_level, w.slow, sizeof(d.slow_level));
+            memcpy(d.bitrate_acc, w.acc, sizeof(d.bitrate_acc));
+            memcpy(d.bitrate_delta, w.dlt, sizeof(d.bitrate_delta));
+            d.num_terms = num_terms;
+            for (int i = 0; i < num_terms && i < 16; i++) {
+                const Pass &p = passes[i];
+                if (!p.known_w || !p.known_s) status |= ST_UNSUPPORTED;
+                d.term[i] = (int8_t)p.term;
+                d.delta[i] = (int8_t)p.delta;
+                d.weight_A[i] = p.wA;
+                d.weight_B[i] = p.wB;
+                memcpy(d.samples_A[i], p.sA, sizeof(p.sA));
+                memcpy(d.samples_B[i], p.sB, sizeof(p.sB));
+            }
+            if (num_terms < 0 || num_terms > 16) status |= ST_UNSUPPORTED;
+            // term 0 in a stereo block behaves differently in the first 8 frames
+            // and in decorr_stereo_pass_cont (UnpackUtils.cs:1118-1121)
+            for (int i = 0; i < num_terms && i < 16; i++)
+                if (passes[i].term == 0 && !(flags & MONO_DATA)) status |= ST_UNSUPPORTED;
+            // FALSE_STEREO together with MONO_FLAG writes 2 ints/frame at a 1-int stride
+            if ((flags & FALSE_STEREO) && (flags & MONO_FLAG)) status |= ST_UNSUPPORTED;
+            if (int32_sent_bits > 32 || int32_sent_bits < 0) status |= ST_UNSUPPORTED;
+        }
+        if (status & ST_UNSUPPORTED) d.kind = KIND_SKIP;
+        // the framing reports its verdicts through the same status word
+        d.fstatus = status;
+        return d;
+    }
+
+    // decoding changes the passes, the entropy state and the bitstreams
+    void mark_adapted() {
+        for (auto &p : passes) p.known_w = p.known_s = false;
+        w.known = false;
+        wvbits.fresh = false;
+        wvxbits.fresh = false;
+        dsd.fresh = false;
+    }
+};
+
+}  // namespace
+
+int compute_mode(const FileInfo &info) {  // WavPackUtils.cs:133-167 (fields captured at open)
+    return info.mode;
+}
+
+void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t out_base_ints, uint32_t open_flags,
+                int chunk, FramingOutput &out, FileInfo &info) {
+    Framer F;
+    F.in.d = file;
+    F.in.len = (int64_t)len;
+    info = FileInfo();
+    info.first_desc = (int64_t)out.descs.size();
+    try {
+        // ---- WavpackOpenFileInput (WavPackUtils.cs:36-120)
+        while (F.wphdr.block_samples == 0) {
+            F.read_next_header();
+            if (F.wphdr.error) {
+                info.error = "not compatible with this version of WavPack file!";
+                return;
+            }
+            if (F.wphdr.block_samples > 0 && F.wphdr.total_samples != 0xFFFFFFFFLL) F.total_samples = F.wphdr.total_samples;
+            if (!F.unpack_init()) {
+                info.error = F.error_message;
+                return;
+            }
+        }
+        F.cfg_flags = (F.cfg_flags & ~0xffLL) | (F.wphdr.flags & 0xff);
+        F.bytes_per_sample = (int)((F.wphdr.flags & BYTES_STORED) + 1);
+        F.float_norm_exp_cfg = F.float_norm_exp;
+        F.bits_per_sample = (int)(F.bytes_per_sample * 8 - ((F.wphdr.flags & SHIFT_MASK) >> SHIFT_LSB));
+        if (F.cfg_flags & FLOAT_DATA) {
+            F.bytes_per_sample = 3;
+            F.bits_per_sample = 24;
+        }
+        if (F.sample_rate == 0) {
+            static const int64_t rates[15] = {6000,  8000,  9600,  11025, 12000, 16000, 22050, 24000,
+                                              32000, 44100, 48000, 64000, 88200, 96000, 192000};
+            if (F.wphdr.block_samples == 0 || (F.wphdr.flags & SRATE_MASK) == SRATE_MASK)
+                F.sample_rate = 44100;
+            else
+                F.sample_rate = rates[(F.wphdr.flags & SRATE_MASK) >> SRATE_LSB];
+        }
+        if (F.num_channels == 0) {
+            F.num_channels = (F.wphdr.flags & MONO_FLAG) ? 1 : 2;
+            F.channel_mask = 0x5 - F.num_channels;
+        }
+        if ((open_flags & 0x8) && !(F.wphdr.flags & FINAL_BLOCK)) F.reduced_channels = (F.wphdr.flags & MONO_FLAG) ? 1 : 2;
+        if (!(open_flags & 0x8) && F.num_channels > 2) {
+            info.error = "only two channels supported!";
+            return;
+        }
+        if (F.wphdr.flags & DSD_FLAG) {
+            F.bytes_per_sample = 1;
+            F.bits_per_sample = 8;
+        }
+    } catch (const CsException &) {
+        info.error = "exception";
+        info.exception = 1;
+        return;
+    }
+    info.open_ok = 1;
+    info.num_channels = F.num_channels;
+    info.reduced_channels = F.reduced_channels;
+    info.bits_per_sample = F.bits_per_sample;
+    info.bytes_per_sample = F.bytes_per_sample;
+    info.version = F.wphdr.version;
+    info.sample_rate = F.sample_rate;
+    info.total_samples = F.total_samples;
+    info.config_flags = F.cfg_flags;
+    {  // WavpackGetMode at open time
+        int mode = 0;
+        if (F.cfg_flags & CONFIG_HYBRID_FLAG) mode |= 0x4;
+        else if (!(F.cfg_flags & CONFIG_LOSSY_MODE)) mode |= 0x2;
+        if (F.lossy_blocks) mode &= ~0x2;
+        if (F.cfg_flags & CONFIG_FLOAT_DATA) mode |= 0x8;
+        if (F.cfg_flags & CONFIG_HIGH_FLAG) {
+            mode |= 0x20;
+            if ((F.cfg_flags & CONFIG_VERY_HIGH_FLAG) || F.wphdr.version < 0x405) mode |= 0x400;
+        }
+        if (F.cfg_flags & CONFIG_FAST_FLAG) mode |= 0x40;
+        if (F.cfg_flags & CONFIG_EXTRA_MODE) mode |= 0x80 | ((F.xmode << 12) & 0x7000);
+        if (F.dsd_multiplier > 0) mode |= 0x10000;
+        info.mode = mode;
+    }
+    info.is_float = (F.cfg_flags & CONFIG_FLOAT_DATA) != 0;
+
+    const int nch = F.reduced_channels ? F.reduced_channels : F.num_channels;
+    info.out_nch = nch;
+    int64_t out_frames = 0;
+    BlockDesc *cur = nullptr;  // descriptor of the block being decoded
+    int64_t cur_idx = -1;
+    // ---- the caller's loop (WvDemo.cs:117-135) over WavpackUnpackSamples (WavPackUtils.cs:200-282)
+    try {
+        for (;;) {
+            int64_t samples = chunk, unpacked = 0;
+            int64_t buf_idx = 0;
+            while (samples > 0) {
+                Hdr &h = F.wphdr;
+                if (h.block_samples == 0 || !(h.flags & INITIAL_BLOCK) || F.sample_index >= h.block_index + h.block_samples) {
+                    F.read_next_header();
+                    if (F.wphdr.error) break;
+                    cur_idx = -1;
+                    if (F.wphdr.block_samples == 0 || F.sample_index == F.wphdr.block_index) {
+                        if (!F.unpack_init()) break;
+                    }
+                }
+                Hdr &hh = F.wphdr;
+                if (hh.block_samples == 0 || !(hh.flags & INITIAL_BLOCK) || F.sample_index >= hh.block_index + hh.block_samples)
+                    continue;
+                if (F.sample_index < hh.block_index) {  // gap: zero fill (output is pre-zeroed)
+                    int64_t n = hh.block_index - F.sample_index;
+                    if (n > samples) n = samples;
+                    F.sample_index += n;
+                    unpacked += n;
+                    samples -= n;
+                    buf_idx += n * nch;
+                    if (buf_idx > (int64_t)chunk * nch) throw CsException();
+                    continue;
+                }
+                int64_t n = hh.block_index + hh.block_samples - F.sample_index;
+                if (n > samples) n = samples;
+                // one unpack_samples / unpack_dsd_samples call of n frames at buf_idx
+                const int bch = (hh.flags & MONO_FLAG) ? 1 : 2;  // ints each frame writes
+                if (bch != nch) {
+                    // a layout the reference writes inconsistently (and may overrun): not decoded here
+                    info.nondet = 1;
+                }
+                if (cur_idx < 0) {
+                    BlockDesc d = F.snapshot(blob_base, out);
+                    d.out_off = out_base_ints + (uint64_t)((out_frames + unpacked) * nch);
+                    d.first_chunk = (uint32_t)n;
+                    d.chunk = (uint32_t)chunk;
+                    d.first_bsp = (uint32_t)buf_idx;
+                    d.out_nch = (uint32_t)nch;
+                    d.call_nch = (F.reduced_channels == 1 || F.num_channels == 1 || (hh.flags & MONO_FLAG)) ? 1 : 2;
+                    d.nframes = 0;
+                    if (bch != nch) {
+                        d.kind = KIND_SKIP;
+                        d.fstatus |= ST_UNSUPPORTED;
+                    }
+                    if ((hh.flags & DSD_FLAG) && F.dsd.mode == 0 && (hh.flags & FALSE_STEREO)) {
+                        // DsdUtils.cs:81 advances bufferStartPos, then :119-131 duplicates
+                        // from past it: the reference overruns or emits caller-buffer garbage.
+                        d.kind = KIND_SKIP;
+                        d.fstatus |= ST_NONDET;
+                        if (buf_idx + 3 * n > (int64_t)chunk * nch) info.exception = 1;
+                    }
+                    out.descs.push_back(d);
+                    cur_idx = (int64_t)out.descs.size() - 1;
+                    F.mark_adapted();
+                }
+                cur = &out.descs[(size_t)cur_idx];
+                cur->nframes += (uint32_t)n;
+                F.sample_index += n;
+                buf_idx += n * nch;
+                unpacked += n;
+                samples -= n;
+                if (F.sample_index == F.total_samples) break;
+            }
+            if (unpacked == 0) break;
+            out_frames += unpacked;
+            if (info.exception) break;
+            // a descriptor whose block stopped exactly at a call boundary stays open:
+            // the next call continues it (cur_idx kept)
+        }
+    } catch (const CsException &) {
+        info.exception = 1;
+    }
+    info.out_frames = out_frames;
+    info.lossy_blocks = F.lossy_blocks;
+    info.is_five = F.five;
+    info.file_format = F.file_format;
+    info.dsd_multiplier = F.dsd_multiplier;
+    info.header_off = F.header_off;
+    info.header_len = F.header_len;
+    info.trailer_off = F.trailer_off;
+    info.trailer_len = F.trailer_len;
+    info.num_desc = (int64_t)out.descs.size() - info.first_desc;
+    (void)cur;
+}
+
+}  // namespace wvg

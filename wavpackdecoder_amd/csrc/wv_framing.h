@@ -1,0 +1,56 @@
+// wv_framing.h -- host-side framing: .wv file bytes -> device block descriptors.
+//
+// Restates the part of the reference that runs *around* the hot path:
+//   WavpackOpenFileInput   (WavPackUtils.cs:36-120)
+//   read_next_header       (WavPackUtils.cs:600-671)
+//   unpack_init + readers  (UnpackUtils.cs:24-491, MetadataUtils.cs, WordsUtils.cs:75-187,
+//                           FloatUtils.cs:15-30, DsdUtils.cs:17-54,149-242,343-389)
+//   the block-walking loop of WavpackUnpackSamples (WavPackUtils.cs:200-282)
+//     driven by a caller that asks for `chunk` frames per call (WvDemo.cs:110-135)
+// It produces one BlockDesc per decoded block with the exact start state, the
+// output offset and the chunk seams.  No sample is decoded here.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "wv_desc.h"
+
+namespace wvg {
+
+struct FileInfo {
+    // WavpackOpenFileInput outcome (WavPackUtils.cs:36-120)
+    int32_t open_ok = 0;
+    std::string error;  // wpc.error_message (empty when none)
+    int32_t num_channels = 0, reduced_channels = 0, bits_per_sample = 0, bytes_per_sample = 0;
+    int32_t version = 0, mode = 0, is_float = 0, is_five = 0, file_format = 0;
+    int64_t sample_rate = 0, total_samples = -1, config_flags = 0;
+    uint32_t dsd_multiplier = 0;
+    int32_t lossy_blocks = 0;   // after the whole walk
+    int32_t exception = 0;      // framing hit a C# exception; output stops there
+    int32_t nondet = 0;
+    // output of the chunked caller
+    int32_t out_nch = 0;        // ints per frame
+    int64_t out_frames = 0;     // frames all calls return
+    int64_t header_off = -1, header_len = 0, trailer_off = -1, trailer_len = 0;  // RIFF/ALT header+trailer
+    // blocks of this file inside the batch descriptor array
+    int64_t first_desc = 0, num_desc = 0;
+};
+
+// DSD fast/high tables live in a side area (bytes) appended per block.
+struct FramingOutput {
+    std::vector<BlockDesc> descs;
+    std::vector<uint8_t> tables;  // DSD tables (see BlockDesc::dsd_table_off)
+};
+
+// Frame one file.  `file` must stay valid until the batch is uploaded.
+// `blob_base` is the file's byte offset inside the device blob; descriptors are
+// appended to `out` with out_off relative to `out_base_ints`.
+void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t out_base_ints, uint32_t open_flags,
+                int chunk, FramingOutput &out, FileInfo &info);
+
+// WavpackGetMode (WavPackUtils.cs:133-167) from the framed context values
+int compute_mode(const FileInfo &info);
+
+}  // namespace wvg
