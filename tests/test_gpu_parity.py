@@ -11,8 +11,17 @@ from tests import vectors as V
 pytestmark = pytest.mark.gpu
 
 
-def _gpu_decode(files, chunk, batch_cls):
-    b = batch_cls(chunk)
+def _gpu_decode(files, chunk, batch_cls, force_lane=False):
+    import os
+    old = os.environ.get("WVG_FORCE_LANE")
+    os.environ["WVG_FORCE_LANE"] = "1" if force_lane else "0"
+    try:
+        b = batch_cls(chunk)
+    finally:
+        if old is None:
+            os.environ.pop("WVG_FORCE_LANE", None)
+        else:
+            os.environ["WVG_FORCE_LANE"] = old
     idx = [b.add_file(d) for d in files]
     b.decode()
     out = b.download()
@@ -22,9 +31,9 @@ def _gpu_decode(files, chunk, batch_cls):
     return out, res, infos
 
 
-def _check_one(data, chunk, batch_cls, name):
+def _check_one(data, chunk, batch_cls, name, force_lane=False):
     ref = O.decode_file(data, chunk=chunk)
-    out, res, infos = _gpu_decode([data], chunk, batch_cls)
+    out, res, infos = _gpu_decode([data], chunk, batch_cls, force_lane)
     r, info = res[0], infos[0]
     if ref.status == -2:
         assert not info.open_ok, name
@@ -40,10 +49,11 @@ def _check_one(data, chunk, batch_cls, name):
     np.testing.assert_array_equal(got, ref.samples, err_msg=name)
 
 
+@pytest.mark.parametrize("lane", [False, True], ids=["2wave", "lane"])
 @pytest.mark.parametrize("case", V.pcm_cases(), ids=lambda c: c[0])
-def test_pcm_modes(case, gpu_batch_cls):
+def test_pcm_modes(case, lane, gpu_batch_cls):
     name, data, chunk = case
-    _check_one(data, chunk, gpu_batch_cls, name)
+    _check_one(data, chunk, gpu_batch_cls, name, force_lane=lane)
 
 
 @pytest.mark.parametrize("case", V.dsd_cases(), ids=lambda c: c[0])
@@ -58,9 +68,10 @@ def test_corrupted_streams(gpu_batch_cls):
     m = S.audio_like(20000, 1, 16, seed=12)
     base = S.encode_pcm(x, S.EncParams(terms=S.TERMS_DEFAULT, block_samples=4000))
     basem = S.encode_pcm(m, S.EncParams(nch=1, terms=S.TERMS_MONO_HIGH, block_samples=3001))
-    for k in range(10):
-        _check_one(V.corrupt(base, k), 4096, gpu_batch_cls, f"stereo#{k}")
-        _check_one(V.corrupt(basem, 100 + k), 1000, gpu_batch_cls, f"mono#{k}")
+    for lane in (False, True):
+        for k in range(10):
+            _check_one(V.corrupt(base, k), 4096, gpu_batch_cls, f"stereo#{k}", lane)
+            _check_one(V.corrupt(basem, 100 + k), 1000, gpu_batch_cls, f"mono#{k}", lane)
 
 
 def test_batch_of_many_files_matches_per_file(gpu_batch_cls):

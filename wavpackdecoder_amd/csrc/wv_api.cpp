@@ -1,5 +1,6 @@
 // wv_api.cpp -- the C-ABI (include/wvgpu.h) over the framing and the HIP kernels.
 #include <hip/hip_runtime_api.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -14,6 +15,10 @@ namespace wvg {
 hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint32_t n_pcm, const uint32_t *dsd_list,
                          uint32_t n_dsd, const uint8_t *blob, const uint8_t *tables, int32_t *ptables, int32_t *out,
                          uint32_t *status, uint32_t *mute_chunk, hipStream_t s);
+int term_set_of(const BlockDesc &d);
+hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, uint32_t n, const uint8_t *blob,
+                        int32_t *out, uint32_t *status, hipStream_t s);
+constexpr int kMaxTermSets = 8;
 }
 
 using namespace wvg;
@@ -32,7 +37,10 @@ struct wvg_batch {
     std::vector<FileInfo> finfo;
     std::vector<wvg_file_info> infos;
     int64_t out_ints = 0;
-    std::vector<uint32_t> pcm_list, dsd_list;
+    std::vector<uint32_t> pcm_list, dsd_list;           // lane kernels (generic PCM, DSD)
+    std::vector<uint32_t> ts_list[kMaxTermSets];        // two-wave kernels per term set
+    uint32_t *d_ts[kMaxTermSets] = {nullptr};
+    int force_lane = 0;                                 // WVG_FORCE_LANE=1: everything on the lane kernel
     std::vector<uint32_t> h_status;
     int64_t bytes_in = 0, frames = 0;
     // device
@@ -88,6 +96,8 @@ wvg_batch *wvg_batch_new(wvg_ctx *c, int chunk_frames) {
     wvg_batch *b = new wvg_batch();
     b->ctx = c;
     b->chunk = chunk_frames;
+    const char *fl = getenv("WVG_FORCE_LANE");
+    b->force_lane = fl && fl[0] == '1';
     return b;
 }
 
@@ -101,6 +111,10 @@ static void free_dev(wvg_batch *b) {
     hipFree(b->d_mute);
     hipFree(b->d_pcm);
     hipFree(b->d_dsd);
+    for (int t = 0; t < kMaxTermSets; t++) {
+        hipFree(b->d_ts[t]);
+        b->d_ts[t] = nullptr;
+    }
     b->d_blob = b->d_tables = nullptr;
     b->d_descs = nullptr;
     b->d_out = b->d_ptables = nullptr;
@@ -153,7 +167,9 @@ int wvg_batch_add_file(wvg_batch *b, const uint8_t *file, size_t len, uint32_t o
     b->out_ints += fi.out_frames * fi.out_nch;
     for (int64_t k = fi.first_desc; k < fi.first_desc + fi.num_desc; k++) {
         const BlockDesc &d = b->fo.descs[(size_t)k];
-        if (d.kind == KIND_PCM) b->pcm_list.push_back((uint32_t)k);
+        int ts = (d.kind == KIND_PCM && !b->force_lane) ? term_set_of(d) : -1;
+        if (ts >= 0) b->ts_list[ts].push_back((uint32_t)k);
+        else if (d.kind == KIND_PCM) b->pcm_list.push_back((uint32_t)k);
         else if (d.kind != KIND_SKIP) b->dsd_list.push_back((uint32_t)k);
         b->frames += d.nframes;
     }
@@ -193,6 +209,12 @@ int wvg_batch_upload(wvg_batch *b) {
     if (np) HIPCHK(c, hipMemcpyAsync(b->d_pcm, b->pcm_list.data(), sizeof(uint32_t) * np, hipMemcpyHostToDevice, c->stream));
     if (ns) HIPCHK(c, hipMemcpyAsync(b->d_dsd, b->dsd_list.data(), sizeof(uint32_t) * ns, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMalloc(&b->d_ptables, sizeof(int32_t) * 256 * (ns ? ns : 1)));
+    for (int t = 0; t < kMaxTermSets; t++) {
+        size_t nl = b->ts_list[t].size();
+        if (!nl) continue;
+        HIPCHK(c, hipMalloc(&b->d_ts[t], sizeof(uint32_t) * nl));
+        HIPCHK(c, hipMemcpyAsync(b->d_ts[t], b->ts_list[t].data(), sizeof(uint32_t) * nl, hipMemcpyHostToDevice, c->stream));
+    }
     HIPCHK(c, hipStreamSynchronize(c->stream));
     b->uploaded = true;
     b->downloaded = false;
@@ -203,6 +225,10 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
     if (!b || !b->uploaded) return WVG_ERR_ARG;
     wvg_ctx *c = b->ctx;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    for (int t = 0; t < kMaxTermSets; t++)
+        if (!b->ts_list[t].empty())
+            HIPCHK(c, launch_2wave(t, b->d_descs, b->d_ts[t], (uint32_t)b->ts_list[t].size(), b->d_blob, b->d_out,
+                                   b->d_status, s));
     HIPCHK(c, launch_decode(b->d_descs, b->d_pcm, (uint32_t)b->pcm_list.size(), b->d_dsd, (uint32_t)b->dsd_list.size(),
                             b->d_blob, b->d_tables, b->d_ptables, b->d_out, b->d_status, b->d_mute, s));
     b->downloaded = false;
@@ -218,7 +244,7 @@ int wvg_batch_sync(wvg_batch *b) {
 
 int64_t wvg_batch_out_ints(const wvg_batch *b) { return b ? b->out_ints : 0; }
 int32_t *wvg_batch_device_out(wvg_batch *b) { return b ? b->d_out : nullptr; }
-int64_t wvg_batch_num_blocks(const wvg_batch *b) { return b ? (int64_t)(b->pcm_list.size() + b->dsd_list.size()) : 0; }
+int64_t wvg_batch_num_blocks(const wvg_batch *b) { return b ? (int64_t)b->fo.descs.size() : 0; }
 int64_t wvg_batch_bytes_in(const wvg_batch *b) { return b ? b->bytes_in : 0; }
 int64_t wvg_batch_frames(const wvg_batch *b) { return b ? b->frames : 0; }
 

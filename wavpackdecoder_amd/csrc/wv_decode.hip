@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include "wv_decode_core.h"
+#include "wv_wave2.h"
 
 namespace wvg {
 
@@ -73,6 +74,72 @@ extern "C" __global__ void __launch_bounds__(64) wv_dsd_fill(const BlockDesc *__
         f += len;
         cl = d.chunk;
     }
+}
+
+}  // namespace wvg
+
+// ---------------------------------------------------------------------------
+// two-wave PCM kernels, one instantiation per decorrelation term list
+// (decoder order, i.e. the reverse of the encoder's; see wv_wave2.h)
+// ---------------------------------------------------------------------------
+namespace wvg {
+
+template <int... Ts>
+__global__ void __launch_bounds__(128) wv_pcm_2wave(const BlockDesc *__restrict__ descs,
+                                                    const uint32_t *__restrict__ list,
+                                                    const uint8_t *__restrict__ blob, int32_t *__restrict__ out,
+                                                    uint32_t *__restrict__ status) {
+    w2::block_2wave<Ts...>(descs, list, blob, out, status);
+}
+
+#define WVG_TS_FAST 17, 17
+#define WVG_TS_DEFAULT -2, 3, 2, 18, 18
+#define WVG_TS_HIGH 2, 18, -1, 8, 6, 3, 5, 7, 4, 2, 18, -2, 3, 2, 18, 18
+#define WVG_TS_MHIGH 1, 17, 2, 18, 8, 6, 3, 5, 7, 4, 2, 18, 3, 2, 18, 18
+#define WVG_TS_M5 18, 3, 2, 18, 18
+
+static const int8_t kTermSets[][17] = {
+    // {count, terms...}
+    {2, WVG_TS_FAST},
+    {5, WVG_TS_DEFAULT},
+    {16, WVG_TS_HIGH},
+    {16, WVG_TS_MHIGH},
+    {5, WVG_TS_M5},
+};
+constexpr int kNumTermSets = 5;
+
+// which specialised kernel decodes this block (-1: the generic lane kernel)
+int term_set_of(const BlockDesc &d) {
+    using namespace wvf;
+    if (d.kind != KIND_PCM) return -1;
+    if (d.wvx_state & 0x100) return -1;  // int32 + wvx fixup reads a second stream
+    const bool mono = (d.flags & MONO_DATA) != 0;
+    for (int s = 0; s < kNumTermSets; s++) {
+        if (kTermSets[s][0] != d.num_terms) continue;
+        bool ok = true;
+        for (int i = 0; i < d.num_terms && ok; i++) {
+            int t = kTermSets[s][1 + i];
+            if (t != d.term[i]) ok = false;
+            if (mono && t < 0) ok = false;
+        }
+        if (ok) return s;
+    }
+    return -1;
+}
+
+hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, uint32_t n, const uint8_t *blob,
+                        int32_t *out, uint32_t *status, hipStream_t s) {
+    if (!n) return hipSuccess;
+    dim3 g(n), b(128);
+    switch (ts) {
+    case 0: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_FAST>), g, b, 0, s, descs, list, blob, out, status); break;
+    case 1: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_DEFAULT>), g, b, 0, s, descs, list, blob, out, status); break;
+    case 2: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_HIGH>), g, b, 0, s, descs, list, blob, out, status); break;
+    case 3: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_MHIGH>), g, b, 0, s, descs, list, blob, out, status); break;
+    case 4: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_M5>), g, b, 0, s, descs, list, blob, out, status); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 }  // namespace wvg

@@ -127,12 +127,19 @@ struct BitReader {
         skip(n);
         return v;
     }
-    // count leading one bits (stream order), capped at `cap` (cap <= 40)
-    WVF_HD int ones_run(int cap) {
+    // consume a run of one bits the way the reference's getbit loops do
+    // (WordsUtils.cs:321, 381, 391): up to `cap` ones, plus the terminating
+    // zero when fewer than `cap` were found.  cap <= 40.
+    WVF_HD int consume_ones(int cap) {
         need(cap + 1);
         uint64_t inv = ~win;
         int r = inv ? __builtin_ctzll(inv) : 64;
-        return r < cap ? r : cap;
+        if (r >= cap) {
+            skip(cap);
+            return cap;
+        }
+        skip(r + 1);
+        return r;
     }
 };
 
@@ -187,7 +194,8 @@ WVF_HD void update_error_limit(Entropy &w, uint32_t flags, int &exc) {
 
 // One residual of get_words (WordsUtils.cs:290-503).  `c` is entidx, `even`
 // is ((csamples & 1) == 0).  Returns DEC_* and the value in `out`.
-WVF_HD int get_word(Entropy &w, BitReader &bs, uint32_t flags, int c, bool even, int32_t &out) {
+template <class BR>
+WVF_HD int get_word(Entropy &w, BR &bs, uint32_t flags, int c, bool even, int32_t &out) {
     using namespace wvf;
     int exc = 0;
     const bool mono = (flags & MONO_DATA) != 0;
@@ -200,12 +208,8 @@ WVF_HD int get_word(Entropy &w, BitReader &bs, uint32_t flags, int c, bool even,
                 return DEC_OK;
             }
         } else {
-            int cbits = bs.ones_run(33);
-            if (cbits == 33) {
-                bs.skip(33);
-                return DEC_BITS_ERROR;
-            }
-            bs.skip(cbits + 1);
+            int cbits = bs.consume_ones(33);
+            if (cbits == 33) return DEC_BITS_ERROR;
             if (cbits < 2)
                 w.zeros_acc = cbits;
             else
@@ -225,20 +229,12 @@ WVF_HD int get_word(Entropy &w, BitReader &bs, uint32_t flags, int c, bool even,
         ones = 0;
     } else {
         // unary count with LIMIT_ONES escape (:361-409): leading ones, capped at 17
-        int u = bs.ones_run(17);
-        if (u == 17) {
-            bs.skip(17);
-            return DEC_BITS_ERROR;
-        }
-        bs.skip(u + 1);
+        int u = bs.consume_ones(17);
+        if (u == 17) return DEC_BITS_ERROR;
         ones = u;
         if (u == LIMIT_ONES) {
-            int cbits = bs.ones_run(33);
-            if (cbits == 33) {
-                bs.skip(33);
-                return DEC_BITS_ERROR;
-            }
-            bs.skip(cbits + 1);
+            int cbits = bs.consume_ones(33);
+            if (cbits == 33) return DEC_BITS_ERROR;
             if (cbits < 2)
                 ones = cbits;
             else
