@@ -11,7 +11,7 @@ import os
 import subprocess
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "build", "libwvgpu.so")
+LIB_PATH = os.environ.get("WVG_LIB") or os.path.join(_PKG, "build", "libwvgpu.so")  # WVG_LIB: experiment builds
 
 WVG_ST_CRC_CHECKED = 0x01
 WVG_ST_CRC_ERROR = 0x02

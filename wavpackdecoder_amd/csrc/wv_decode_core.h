@@ -152,7 +152,7 @@ struct Entropy {
     int32_t errlim[2];
     int64_t acc[2], dlt[2];
     int64_t zeros_acc;
-    bool h1, h0;
+    int32_t h1, h0;  // holding_one / holding_zero as 0/1 (ints keep them in SGPRs on the GPU)
 };
 
 // update_error_limit (WordsUtils.cs:195-261)
@@ -576,7 +576,7 @@ WVF_HD uint32_t decode_pcm_block(const BlockDesc &d, const uint8_t *blob, Store 
         w.dlt[c] = d.bitrate_delta[c];
     }
     w.zeros_acc = 0;
-    w.h0 = w.h1 = false;
+    w.h0 = w.h1 = 0;
 
     PassState ps[MAXP];
     for (int i = 0; i < nt; i++) {

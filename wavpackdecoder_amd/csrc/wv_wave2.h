@@ -33,6 +33,18 @@ constexpr int SLOT_DW = 256;    // one staging slot = 1 KiB
 constexpr int NSLOT = 4;
 constexpr uint32_t SPIN_LIMIT = 1u << 26;  // bounded waits: a bug ends the kernel, never hangs the GPU
 
+// Performance experiments (never in the shipped build): 1 = reconstruction
+// wave only drains the ring, 2 = parser wave publishes zeros without parsing.
+// 3 = as 1, plus parser counters written over the block's first output ints.
+#ifndef WV2_EXP
+#define WV2_EXP 0
+#endif
+#if WV2_EXP == 3
+#define WV2_PROF(x) x
+#else
+#define WV2_PROF(x)
+#endif
+
 struct Shared {
     uint32_t stream[NSLOT * SLOT_DW];
     int32_t res[RES_RING];
@@ -49,10 +61,11 @@ __device__ __forceinline__ void lds_store_rel(uint32_t *p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-// put a wave-uniform value into one lane of a VGPR (v_cmp + v_cndmask; the
-// v_writelane_b32 encoding on gfx950 cannot take both operands from SGPRs)
+// v_writelane_b32 (lane select through M0): put a wave-uniform value into one
+// lane of a VGPR.  clang has no builtin for it; this binds the LLVM intrinsic.
+extern "C" __device__ int32_t wv2_writelane_i32(int32_t val, int32_t lane, int32_t old) __asm("llvm.amdgcn.writelane.i32");
 __device__ __forceinline__ int32_t writelane(int32_t val, int lane_sel, int32_t vreg) {
-    return ((int)(threadIdx.x & 63) == lane_sel) ? val : vreg;
+    return wv2_writelane_i32(val, lane_sel, vreg);
 }
 
 // ---------------------------------------------------------------------------
@@ -67,9 +80,10 @@ struct LdsReader {
     uint64_t win;
     int nb;
     uint32_t rd;      // next dword index (relative to A) to enter the window
-    uint32_t nextdw;  // == dword rd, prefetched from LDS
+    uint32_t nextv;   // dword rd as loaded from LDS (VGPR; read lane 0 only when it is needed)
     uint4 stage;      // chunk in flight (per lane 16 B)
     int lane;
+    WV2_PROF(uint32_t n_fast = 0; uint32_t n_zr = 0; uint32_t n_slow = 0; uint32_t n_refill = 0; uint64_t t_wait = 0;)
 
     // Branch-free on purpose: a divergent branch anywhere in the parser makes
     // the compiler move the (uniform) bit window into VGPRs.
@@ -106,7 +120,7 @@ struct LdsReader {
         win = (uint64_t)lds_dw(0) | ((uint64_t)lds_dw(1) << 32);
         nb = 64;
         rd = 2;
-        nextdw = lds_dw(2);
+        nextv = ring[2];
         while (skip >= 32) {
             win >>= 32;
             nb -= 32;
@@ -119,7 +133,7 @@ struct LdsReader {
         }
     }
     __device__ __forceinline__ void refill32() {
-        win |= (uint64_t)nextdw << nb;
+        win |= (uint64_t)uni(nextv) << nb;
         nb += 32;
         rd++;
         if ((rd & (SLOT_DW - 1)) == 0) {  // entering chunk c = rd / 256
@@ -127,7 +141,7 @@ struct LdsReader {
             put_chunk(c + 1, stage);
             stage = load_chunk(c + 2);
         }
-        nextdw = lds_dw(rd);
+        nextv = ring[rd & (NSLOT * SLOT_DW - 1)];  // waited for at the next refill, not here
     }
     // 32-bit refills keep the window invariant: bits at and above nb are 0,
     // so a refill is only legal while nb <= 32; every caller needs <= 32 bits.
@@ -179,7 +193,187 @@ struct LdsReader {
 // boolean is turned into an integer (that lowers to v_cndmask and drags the
 // whole loop onto the VALU).
 // ---------------------------------------------------------------------------
-template <bool MONO>
+
+// One residual of a lossless block, common case only (WordsUtils.cs:355-503
+// with no hybrid terms): not in zero-run mode (the caller checks), fewer than
+// 16 unary ones, a non-negative median, and the whole word inside the bit
+// window (nb >= 32 on entry; the bound checked is unary + bitcount + 1).
+// Returns false with no state changed when the word is not of that form; the
+// caller then runs the general get_word.
+//
+// Hand-scheduled scalar code: this is the serial critical path of a block
+// (one wave issues one instruction per ~4 cycles, a taken branch costs ~19),
+// and the compiler's version spent ~2.5x the instructions on register
+// shuffles and structurised control flow.  The bit window is copied to VCC so
+// its low dword can be named (vcc_lo).  Arithmetic is exact modulo 2^32,
+// which is all the output keeps: maxcode is median_k >> 4 (high - low in
+// get_word), and low/mid wrap like the int64 values truncated by the (int)
+// cast at WordsUtils.cs:499-503.
+//   case 0:  low = 0,              mk = m0;  m0 -= ((m0+126)>>7)*2
+//   case 1:  low = A0,             mk = m1;  m0 += ((m0+128)>>7)*5, m1 -= ((m1+62)>>6)*2
+//   case 2:  low = A0+A1,          mk = m2;  m0, m1 += ..., m2 -= ((m2+30)>>5)*2
+//   case n:  low = A0+A1+(n-2)*A2, mk = m2;  m0, m1, m2 += ...       (Ak = (mk>>4)+1)
+//   read_code: n1 = bitcount-1, extras = 2^bitcount - mc - 1 (WordsUtils.cs:546-570)
+#define WV2_BOUND(MK)                                   \
+    "s_lshr_b32 %[mc], " MK ", 4\n"                      \
+    "s_or_b32 %[t0], %[mc], 1\n"                          \
+    "s_flbit_i32_b32 %[t0], %[t0]\n"                      \
+    "s_sub_u32 %[n1], 31, %[t0]\n"                        \
+    "s_add_u32 %[t0], %[n1], 2\n"                         \
+    "s_cmp_gt_u32 %[t0], %[avail]\n"                      \
+    "s_cbranch_scc1 L_done_%=\n"
+#define WV2_INC(M, ADD, SH)                               \
+    "s_add_i32 %[t0], " M ", " ADD "\n"                   \
+    "s_ashr_i32 %[t0], %[t0], " SH "\n"                   \
+    "s_mul_i32 %[t0], %[t0], 5\n"                         \
+    "s_add_i32 " M ", " M ", %[t0]\n"
+#define WV2_DEC(M, ADD, SH1)                              \
+    "s_add_i32 %[t0], " M ", " ADD "\n"                   \
+    "s_ashr_i32 %[t0], %[t0], " SH1 "\n"                  \
+    "s_and_b32 %[t0], %[t0], -2\n"                        \
+    "s_sub_i32 " M ", " M ", %[t0]\n"
+
+template <int C>
+__device__ __forceinline__ bool fast_word(Entropy &w, LdsReader &rd, int32_t &out) {
+    uint32_t ok, o, t0, u, ones, c1, nh0, nh1, mc, n1, low, avail, ex, v;
+    uint32_t nb = (uint32_t)rd.nb;
+    int32_t m0 = w.med[C][0], m1 = w.med[C][1], m2 = w.med[C][2], h0 = w.h0, h1 = w.h1;
+    asm volatile(
+        "s_mov_b32 %[ok], 0\n"
+        "s_mov_b64 vcc, %[win]\n"
+        "s_cmp_lg_u32 %[h0], 0\n"
+        "s_cbranch_scc1 L_h0_%=\n"
+        // unary run (WordsUtils.cs:361-409 without the escape)
+        "s_orn2_b32 %[t0], 0x10000, vcc_lo\n"
+        "s_ff1_i32_b32 %[u], %[t0]\n"
+        "s_cmp_gt_u32 %[u], 15\n"
+        "s_cbranch_scc1 L_done_%=\n"
+        "s_add_u32 %[c1], %[u], 1\n"
+        "s_lshr_b32 %[ones], %[u], 1\n"
+        "s_add_u32 %[ones], %[ones], %[h1]\n"
+        "s_and_b32 %[nh1], %[u], 1\n"
+        "s_xor_b32 %[nh0], %[nh1], 1\n"
+        "s_sub_u32 %[avail], %[nb], %[c1]\n"
+        "s_cmp_lg_u32 %[ones], 0\n"
+        "s_cbranch_scc1 L_ge1_%=\n"
+        "L_c0_%=:\n"
+        "s_cmp_lt_i32 %[m0], 0\n"
+        "s_cbranch_scc1 L_done_%=\n"
+        WV2_BOUND("%[m0]")
+        "s_mov_b32 %[low], 0\n"
+        WV2_DEC("%[m0]", "126", "6")
+        "L_tail_%=:\n"
+        "s_mov_b32 %[h0], %[nh0]\n"
+        "s_mov_b32 %[h1], %[nh1]\n"
+        "s_lshr_b64 vcc, vcc, %[c1]\n"
+        "s_sub_u32 %[nb], %[nb], %[c1]\n"
+        "s_lshl_b32 %[ex], 2, %[n1]\n"
+        "s_not_b32 %[t0], %[mc]\n"
+        "s_add_u32 %[ex], %[ex], %[t0]\n"
+        "s_bfm_b32 %[t0], %[n1], 0\n"
+        "s_and_b32 %[v], vcc_lo, %[t0]\n"
+        "s_cmp_lt_u32 %[v], %[ex]\n"
+        "s_cbranch_scc1 L_small_%=\n"
+        "s_lshr_b32 %[t0], vcc_lo, %[n1]\n"
+        "s_and_b32 %[t0], %[t0], 1\n"
+        "s_lshl_b32 %[v], %[v], 1\n"
+        "s_sub_u32 %[v], %[v], %[ex]\n"
+        "s_add_u32 %[v], %[v], %[t0]\n"
+        "s_add_u32 %[n1], %[n1], 1\n"
+        "L_small_%=:\n"
+        "s_add_u32 %[v], %[v], %[low]\n"
+        "s_lshr_b32 %[t0], vcc_lo, %[n1]\n"
+        "s_bfe_i32 %[t0], %[t0], 0x10000\n"
+        "s_xor_b32 %[o], %[v], %[t0]\n"
+        "s_add_u32 %[n1], %[n1], 1\n"
+        "s_lshr_b64 %[win], vcc, %[n1]\n"
+        "s_sub_u32 %[nb], %[nb], %[n1]\n"
+        "s_mov_b32 %[ok], 1\n"
+        "s_branch L_done_%=\n"
+        // holding_zero set: this word's unary count is 0, h1 unchanged
+        "L_h0_%=:\n"
+        "s_mov_b32 %[c1], 0\n"
+        "s_mov_b32 %[nh0], 0\n"
+        "s_mov_b32 %[nh1], %[h1]\n"
+        "s_mov_b32 %[avail], %[nb]\n"
+        "s_branch L_c0_%=\n"
+        "L_ge1_%=:\n"
+        "s_cmp_eq_u32 %[ones], 1\n"
+        "s_cbranch_scc0 L_ge2_%=\n"
+        "s_cmp_lt_i32 %[m1], 0\n"
+        "s_cbranch_scc1 L_done_%=\n"
+        WV2_BOUND("%[m1]")
+        "s_ashr_i32 %[low], %[m0], 4\n"
+        "s_add_u32 %[low], %[low], 1\n"
+        WV2_INC("%[m0]", "128", "7")
+        WV2_DEC("%[m1]", "62", "5")
+        "s_branch L_tail_%=\n"
+        "L_ge2_%=:\n"
+        "s_cmp_lt_i32 %[m2], 0\n"
+        "s_cbranch_scc1 L_done_%=\n"
+        WV2_BOUND("%[m2]")
+        "s_ashr_i32 %[low], %[m0], 4\n"
+        "s_ashr_i32 %[t0], %[m1], 4\n"
+        "s_add_u32 %[low], %[low], %[t0]\n"
+        "s_add_u32 %[low], %[low], 2\n"
+        WV2_INC("%[m0]", "128", "7")
+        WV2_INC("%[m1]", "64", "6")
+        "s_cmp_eq_u32 %[ones], 2\n"
+        "s_cbranch_scc0 L_ge3_%=\n"
+        WV2_DEC("%[m2]", "30", "4")
+        "s_branch L_tail_%=\n"
+        "L_ge3_%=:\n"
+        "s_add_u32 %[t0], %[mc], 1\n"
+        "s_sub_u32 %[u], %[ones], 2\n"
+        "s_mul_i32 %[t0], %[t0], %[u]\n"
+        "s_add_u32 %[low], %[low], %[t0]\n"
+        WV2_INC("%[m2]", "32", "5")
+        "s_branch L_tail_%=\n"
+        "L_done_%=:\n"
+        : [ok] "=&s"(ok), [o] "=&s"(o), [t0] "=&s"(t0), [u] "=&s"(u), [ones] "=&s"(ones), [c1] "=&s"(c1),
+          [nh0] "=&s"(nh0), [nh1] "=&s"(nh1), [mc] "=&s"(mc), [n1] "=&s"(n1), [low] "=&s"(low),
+          [avail] "=&s"(avail), [ex] "=&s"(ex), [v] "=&s"(v), [win] "+s"(rd.win), [nb] "+s"(nb),
+          [m0] "+s"(m0), [m1] "+s"(m1), [m2] "+s"(m2), [h0] "+s"(h0), [h1] "+s"(h1)
+        :
+        : "vcc", "scc");
+    w.med[C][0] = m0;
+    w.med[C][1] = m1;
+    w.med[C][2] = m2;
+    w.h0 = h0;
+    w.h1 = h1;
+    rd.nb = (int)nb;
+    out = (int32_t)o;
+    return ok != 0;
+}
+#undef WV2_BOUND
+#undef WV2_INC
+#undef WV2_DEC
+
+// one residual: the fast path for lossless blocks, the zero-run countdown,
+// else the general get_word (wv_decode_core.h)
+template <int C, bool LOSSLESS>
+__device__ __forceinline__ int parse_word(Entropy &w, LdsReader &rd, uint32_t flags, int32_t &v) {
+    if (LOSSLESS) {
+        const uint32_t m00 = (uint32_t)(w.med[0][0] | w.med[1][0]);
+        const bool zr = __builtin_expect(m00 <= 1u, 0) && (w.h0 | w.h1) == 0;
+        if (__builtin_expect(!zr, 1)) {
+            if (__builtin_expect(rd.nb < 32, 0)) rd.refill32();
+            if (__builtin_expect(fast_word<C>(w, rd, v), 1)) {
+                WV2_PROF(rd.n_fast++;)
+                return DEC_OK;
+            }
+        } else if (w.zeros_acc > 1) {  // inside a zero run (WordsUtils.cs:306-311; slow_level is dead here)
+            w.zeros_acc--;
+            v = 0;
+            WV2_PROF(rd.n_zr++;)
+            return DEC_OK;
+        }
+    }
+    WV2_PROF(rd.n_slow++;)
+    return get_word(w, rd, flags, C, C == 0, v);
+}
+
+template <bool MONO, bool LOSSLESS>
 __device__ __forceinline__ void parse_loop(const BlockDesc &d, LdsReader &rd, Entropy &w, Shared &sh, int lane) {
     const uint32_t flags = d.flags;
     const uint32_t total = MONO ? d.nframes : 2u * d.nframes;
@@ -188,35 +382,42 @@ __device__ __forceinline__ void parse_loop(const BlockDesc &d, LdsReader &rd, En
     uint32_t err = 0;
     uint32_t consumed = 0;
     while (k < total) {
-        int32_t v;
-        int rc = get_word(w, rd, flags, 0, true, v);
-        if (rc != DEC_OK) {
-            err = (uint32_t)rc;
-            break;
-        }
-        resv = writelane(v, (int)(k & 63), resv);
-        k++;
-        if (!MONO) {
-            rc = get_word(w, rd, flags, 1, false, v);
-            if (rc != DEC_OK) {
+        const uint32_t kend = min(total, (k & ~63u) + 64u);  // next batch boundary
+        while (k < kend) {
+            int32_t v = 0;
+            int rc = WV2_EXP == 2 ? DEC_OK : parse_word<0, LOSSLESS>(w, rd, flags, v);
+            if (__builtin_expect(rc != DEC_OK, 0)) {
                 err = (uint32_t)rc;
                 break;
             }
             resv = writelane(v, (int)(k & 63), resv);
             k++;
+            if (!MONO) {
+                rc = WV2_EXP == 2 ? DEC_OK : parse_word<1, LOSSLESS>(w, rd, flags, v);
+                if (__builtin_expect(rc != DEC_OK, 0)) {
+                    err = (uint32_t)rc;
+                    break;
+                }
+                resv = writelane(v, (int)(k & 63), resv);
+                k++;
+            }
         }
-        if ((k & 63) == 0 || k == total) {
+        if (err) break;
+        {
             // wait for ring space, publish the batch
             uint32_t base = (k - 1) & ~63u;
             uint32_t spins = 0;
+            WV2_PROF(uint64_t tw0 = clock64();)
             while (base + 64 - consumed > (uint32_t)RES_RING) {
                 __builtin_amdgcn_s_sleep(2);
                 consumed = uni(lds_load_acq(&sh.consumed));
+                if (uni(lds_load_acq(&sh.stop))) return;  // the block was muted
                 if (++spins > SPIN_LIMIT) {
                     err = 3;
                     break;
                 }
             }
+            WV2_PROF(rd.t_wait += clock64() - tw0;)
             if (err) break;
             sh.res[(base % RES_RING) + lane] = resv;
             lds_store_rel(&sh.produced, k);
@@ -240,7 +441,8 @@ __device__ __forceinline__ void parse_loop(const BlockDesc &d, LdsReader &rd, En
     }
 }
 
-__device__ __forceinline__ void parser(const BlockDesc &d, const uint8_t *blob, Shared &sh, int lane) {
+__device__ __forceinline__ void parser(const BlockDesc &d, const uint8_t *blob, Shared &sh, int lane, int32_t *dbg) {
+    WV2_PROF(const uint64_t t_start = clock64();)
     LdsReader rd;
     rd.init(blob, d.bits_off, d.bits_len, sh.stream, lane);
     Entropy w;
@@ -254,11 +456,28 @@ __device__ __forceinline__ void parser(const BlockDesc &d, const uint8_t *blob, 
         w.dlt[c] = d.bitrate_delta[c];
     }
     w.zeros_acc = 0;
-    w.h0 = w.h1 = false;
-    if (d.flags & wvf::MONO_DATA)
-        parse_loop<true>(d, rd, w, sh, lane);
-    else
-        parse_loop<false>(d, rd, w, sh, lane);
+    w.h0 = w.h1 = 0;
+    const bool mono = (d.flags & wvf::MONO_DATA) != 0, lossless = (d.flags & wvf::HYBRID_FLAG) == 0;
+    if (mono) {
+        if (lossless) parse_loop<true, true>(d, rd, w, sh, lane);
+        else parse_loop<true, false>(d, rd, w, sh, lane);
+    } else {
+        if (lossless) parse_loop<false, true>(d, rd, w, sh, lane);
+        else parse_loop<false, false>(d, rd, w, sh, lane);
+    }
+#if WV2_EXP == 3
+    const uint64_t t_total = clock64() - t_start;
+    uint32_t vals[8] = {rd.n_fast, rd.n_zr, rd.n_slow, rd.n_refill, (uint32_t)t_total, (uint32_t)(t_total >> 32),
+                        (uint32_t)rd.t_wait, (uint32_t)(rd.t_wait >> 32)};
+    if (lane < 8) {
+        uint32_t x = vals[0];
+#pragma unroll
+        for (int i = 1; i < 8; i++) x = lane == i ? vals[i] : x;
+        dbg[lane] = (int32_t)x;
+    }
+#else
+    (void)dbg;
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -550,7 +769,7 @@ __device__ __forceinline__ void recon_impl(const BlockDesc &d, Shared &sh, int32
     }
 
         for (uint32_t g = 0; g < BF / 8; g++) {
-            if (t0 + g * 8 >= tvalid) break;
+            if (WV2_EXP == 1 || WV2_EXP == 3 || t0 + g * 8 >= tvalid) break;
             do {
                 WV2_FRAME(0) WV2_FRAME(1) WV2_FRAME(2) WV2_FRAME(3) WV2_FRAME(4) WV2_FRAME(5) WV2_FRAME(6) WV2_FRAME(7)
             } while (0);
@@ -560,7 +779,7 @@ __device__ __forceinline__ void recon_impl(const BlockDesc &d, Shared &sh, int32
         // store the batch: 64 ints per instruction, one per lane
         const uint32_t nv = (mute_at >= 0 ? (uint32_t)mute_at : tvalid) - t0;
         const uint64_t base = (uint64_t)t0 * OCH;
-        if ((uint32_t)lane < nv * OCH) out[base + lane] = o0;
+        if (WV2_EXP != 3 && (uint32_t)lane < nv * OCH) out[base + lane] = o0;
         if (LAYOUT == 2 && (uint32_t)lane + 64 < nv * OCH) out[base + 64 + lane] = o1;
         const bool bits_err = tvalid < tend;
         if (mute_at >= 0 || bits_err) {
@@ -610,7 +829,7 @@ __device__ __forceinline__ void block_2wave(const BlockDesc *descs, const uint32
     }
     __syncthreads();
     if (wave == 0)
-        parser(d, blob, sh, lane);
+        parser(d, blob, sh, lane, out + d.out_off);
     else
         recon<Ts...>(d, sh, out, &status[bi], lane);
 }
