@@ -27,7 +27,20 @@ def main():
         b.decode()
         b.sync()
         ms = b.time(10)
-        if os.environ.get("WVG_PROF"):
+        if os.environ.get("WVG_PROF") == "4":
+            import numpy as np
+            o = b.download().view("uint32").astype("uint64")
+            per = o.size // n
+            blk = o[: per * n].reshape(n, per)
+            tp = blk[:, 4] | (blk[:, 5] << 32)
+            tr = blk[:, 8] | (blk[:, 9] << 32)
+            trw = blk[:, 10] | (blk[:, 11] << 32)
+            for name, arr in (("parser", tp), ("recon", tr)):
+                idx = np.argsort(arr)[::-1][:6]
+                print(f"  {name}: median={np.median(arr):.0f} max={arr.max()} slowest="
+                      + ", ".join(f"{i}:{arr[i]}(fast={blk[i,0]},zr={blk[i,1]},slow={blk[i,2]},rwait={trw[i]})" for i in idx),
+                      flush=True)
+        elif os.environ.get("WVG_PROF"):
             c = b.download()[:8].view("uint32").astype("uint64")
             words = 2 * b.frames // n
             t = int(c[4] | (c[5] << 32))

@@ -35,11 +35,12 @@ constexpr uint32_t SPIN_LIMIT = 1u << 26;  // bounded waits: a bug ends the kern
 
 // Performance experiments (never in the shipped build): 1 = reconstruction
 // wave only drains the ring, 2 = parser wave publishes zeros without parsing.
-// 3 = as 1, plus parser counters written over the block's first output ints.
+// 3 = as 1, plus parser counters written over the block's first output ints;
+// 4 = full decode, parser counters in ints 0-7 and recon cycles in ints 8-11.
 #ifndef WV2_EXP
 #define WV2_EXP 0
 #endif
-#if WV2_EXP == 3
+#if WV2_EXP == 3 || WV2_EXP == 4
 #define WV2_PROF(x) x
 #else
 #define WV2_PROF(x)
@@ -59,6 +60,13 @@ __device__ __forceinline__ uint32_t lds_load_acq(uint32_t *p) {
 }
 __device__ __forceinline__ void lds_store_rel(uint32_t *p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Publish a counter after this wave's LDS writes: DS operations of one wave
+// complete in order, so waiting for the LDS queue is enough; a release store
+// would also wait for every outstanding global load/store (vmcnt(0)).
+__device__ __forceinline__ void lds_publish(uint32_t *p, uint32_t v) {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), vmcnt/expcnt untouched
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 // v_writelane_b32 (lane select through M0): put a wave-uniform value into one
@@ -420,7 +428,7 @@ __device__ __forceinline__ void parse_loop(const BlockDesc &d, LdsReader &rd, En
             WV2_PROF(rd.t_wait += clock64() - tw0;)
             if (err) break;
             sh.res[(base % RES_RING) + lane] = resv;
-            lds_store_rel(&sh.produced, k);
+            lds_publish(&sh.produced, k);
             if (uni(lds_load_acq(&sh.stop))) return;
         }
     }
@@ -465,7 +473,7 @@ __device__ __forceinline__ void parser(const BlockDesc &d, const uint8_t *blob, 
         if (lossless) parse_loop<false, true>(d, rd, w, sh, lane);
         else parse_loop<false, false>(d, rd, w, sh, lane);
     }
-#if WV2_EXP == 3
+#if WV2_EXP == 3 || WV2_EXP == 4
     const uint64_t t_total = clock64() - t_start;
     uint32_t vals[8] = {rd.n_fast, rd.n_zr, rd.n_slow, rd.n_refill, (uint32_t)t_total, (uint32_t)(t_total >> 32),
                         (uint32_t)rd.t_wait, (uint32_t)(rd.t_wait >> 32)};
@@ -481,159 +489,171 @@ __device__ __forceinline__ void parser(const BlockDesc &d, const uint8_t *blob, 
 }
 
 // ---------------------------------------------------------------------------
-// reconstruction wave: pass state for a compile-time term list
+// reconstruction wave, on the vector ALU.
+//
+// The parser wave is scalar-issue bound and shares its SIMD's scalar issue
+// slot with any other wave there, so the reconstruction runs on the VALU:
+// even lanes carry channel A (left / mono), odd lanes channel B (right).
+// Passes with positive terms (17, 18, 1..8) run both channels in one
+// instruction; the cross-channel negative terms (-1, -2, -3) exchange values
+// between lane pairs with a DPP quad permute.  All lane pairs compute the same
+// values, so a wave-wide ballot of a per-frame test is that frame's verdict.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ int32_t swap_pair(int32_t x) {  // lane 2i <-> 2i+1
+    return __builtin_amdgcn_update_dpp(x, x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+}
+__device__ __forceinline__ int32_t iabs(int32_t x) { return x < 0 ? (int32_t)(0u - (uint32_t)x) : x; }
+
+// weight update of positive terms (UnpackUtils.cs:747-748): w +- delta when
+// both sample and input are non-zero; negative terms clamp to +-1024
+// (:808-818), and |w| <= 1024 holds for them throughout (restore_weight
+// range, clamped updates), so the clamp is a plain med3.
+__device__ __forceinline__ int32_t vupd(int32_t w, int32_t s, int32_t x, int32_t delta) {
+    int32_t dd = (s ^ x) < 0 ? -delta : delta;
+    dd = s != 0 ? dd : 0;
+    dd = x != 0 ? dd : 0;
+    return wvf::add32(w, dd);
+}
+__device__ __forceinline__ int32_t vupdc(int32_t w, int32_t s, int32_t x, int32_t delta) {
+    return max(-1024, min(1024, vupd(w, s, x, delta)));
+}
+
 template <int T>
-struct PState {
-    int32_t wA, wB;
-    int32_t a[(T >= 17) ? 2 : 8];  // s0,s1 (17,18), ring (1..8, and mono negative), s0 (stereo negative)
-    int32_t b[(T >= 17) ? 2 : 8];
+struct VPass {
+    static constexpr int NH = (T >= 17) ? 2 : ((T >= 1) ? 8 : ((T < 0) ? 8 : 1));
+    int32_t w;       // weight of this lane's channel
+    int32_t h[NH];   // 17/18: s0,s1; 1..8 (and mono negative): ring; stereo negative: h[0]
     int32_t delta;
 
-    __device__ __forceinline__ void init(const BlockDesc &d, int p) {
-        wA = d.weight_A[p];
-        wB = d.weight_B[p];
+    __device__ __forceinline__ void init(const BlockDesc &d, int p, bool isB) {
+        w = isB ? d.weight_B[p] : d.weight_A[p];
         delta = d.delta[p];
-        if (T <= 8) {
-            constexpr int TT = (T >= 1) ? T : ((T & 7) == 0 ? 8 : (T & 7));  // ring length in use
 #pragma unroll
-            for (int i = 0; i < 8; i++) a[i] = b[i] = 0;
-            if (T >= 1 || true) {
-#pragma unroll
-                for (int i = 0; i < 8; i++) {
-                    if (i < TT) {
-                        a[(8 - TT + i) & 7] = d.samples_A[p][i];
-                        b[(8 - TT + i) & 7] = d.samples_B[p][i];
-                    }
-                }
-            }
-            if (T < 0) {  // stereo negative terms use slot 0 only
-                a[0] = d.samples_A[p][0];
-                b[0] = d.samples_B[p][0];
-            }
+        for (int i = 0; i < NH; i++) h[i] = 0;
+        if (T >= 17) {
+            h[0] = isB ? d.samples_B[p][0] : d.samples_A[p][0];
+            h[1] = isB ? d.samples_B[p][1] : d.samples_A[p][1];
         } else {
-            a[0] = d.samples_A[p][0];
-            a[1] = d.samples_A[p][1];
-            b[0] = d.samples_B[p][0];
-            b[1] = d.samples_B[p][1];
+            // ring: slot (U - TT) & 7 is read at phase U; TT = T (1..8) or T & 7 (mono negative)
+            constexpr int TT = (T >= 1) ? T : ((T & 7) == 0 ? 8 : (T & 7));
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+                if (i < TT) h[(8 - TT + i) & 7] = isB ? d.samples_B[p][i] : d.samples_A[p][i];
         }
     }
-    __device__ __forceinline__ void trunc() {
-        wA = (int16_t)wA;
-        wB = (int16_t)wB;
+    __device__ __forceinline__ void init_stereo_neg(const BlockDesc &d, int p, bool isB) {
+        w = isB ? d.weight_B[p] : d.weight_A[p];
+        delta = d.delta[p];
+#pragma unroll
+        for (int i = 0; i < NH; i++) h[i] = 0;
+        h[0] = isB ? d.samples_B[p][0] : d.samples_A[p][0];
     }
-    // stereo frame at ring phase U (= block frame & 7)
+    __device__ __forceinline__ void trunc() { w = (int16_t)w; }
+
+    // one frame of this pass; x is the lane's channel value in and out
     template <int U>
-    __device__ __forceinline__ void stereo(int32_t &L, int32_t &R) {
+    __device__ __forceinline__ void stereo(int32_t &x, bool isB) {
         using namespace wvf;
         if constexpr (T == 17 || T == 18) {
-            int32_t sa = T == 17 ? sub32(mul32(2, a[0]), a[1]) : (sub32(mul32(3, a[0]), a[1]) >> 1);
-            int32_t oa = add32(apply_weight(wA, sa), L);
-            upd_w(wA, sa, L, delta);
-            a[1] = a[0];
-            a[0] = oa;
-            L = oa;
-            int32_t sb = T == 17 ? sub32(mul32(2, b[0]), b[1]) : (sub32(mul32(3, b[0]), b[1]) >> 1);
-            int32_t ob = add32(apply_weight(wB, sb), R);
-            upd_w(wB, sb, R, delta);
-            b[1] = b[0];
-            b[0] = ob;
-            R = ob;
+            const int32_t sa = T == 17 ? sub32(mul32(2, h[0]), h[1]) : (sub32(mul32(3, h[0]), h[1]) >> 1);
+            const int32_t o = add32(apply_weight(w, sa), x);
+            w = vupd(w, sa, x, delta);
+            h[1] = h[0];
+            h[0] = o;
+            x = o;
         } else if constexpr (T >= 1 && T <= 8) {
-            int32_t sa = a[(U - T) & 7];
-            int32_t oa = add32(apply_weight(wA, sa), L);
-            upd_w(wA, sa, L, delta);
-            a[U & 7] = oa;
-            L = oa;
-            int32_t sb = b[(U - T) & 7];
-            int32_t ob = add32(apply_weight(wB, sb), R);
-            upd_w(wB, sb, R, delta);
-            b[U & 7] = ob;
-            R = ob;
-        } else if constexpr (T == -1) {
-            int32_t sa = add32(L, apply_weight(wA, a[0]));
-            upd_wc(wA, a[0], L, delta);
-            int32_t o = add32(R, apply_weight(wB, sa));
-            upd_wc(wB, sa, R, delta);
-            L = sa;
-            R = o;
-            a[0] = o;
-        } else if constexpr (T == -2) {
-            int32_t sb = add32(R, apply_weight(wB, b[0]));
-            upd_wc(wB, b[0], R, delta);
-            int32_t o = add32(L, apply_weight(wA, sb));
-            upd_wc(wA, sb, L, delta);
-            R = sb;
-            L = o;
-            b[0] = o;
-        } else if constexpr (T == -3) {
-            int32_t sa = add32(L, apply_weight(wA, a[0]));
-            upd_wc(wA, a[0], L, delta);
-            int32_t sb = add32(R, apply_weight(wB, b[0]));
-            upd_wc(wB, b[0], R, delta);
-            b[0] = sa;
-            a[0] = sb;
-            L = sa;
-            R = sb;
+            const int32_t sa = h[(U - T) & 7];
+            const int32_t o = add32(apply_weight(w, sa), x);
+            w = vupd(w, sa, x, delta);
+            h[U & 7] = o;
+            x = o;
+        } else if constexpr (T == -1) {  // A first, then B from A's result; A keeps B's output
+            const int32_t s1 = add32(x, apply_weight(w, h[0]));
+            const int32_t w1 = vupdc(w, h[0], x, delta);
+            const int32_t y = swap_pair(s1);
+            const int32_t s2 = add32(x, apply_weight(w, y));
+            const int32_t w2 = vupdc(w, y, x, delta);
+            const int32_t s2x = swap_pair(s2);
+            x = isB ? s2 : s1;
+            w = isB ? w2 : w1;
+            h[0] = isB ? h[0] : s2x;
+        } else if constexpr (T == -2) {  // B first, then A; B keeps A's output
+            const int32_t s1 = add32(x, apply_weight(w, h[0]));
+            const int32_t w1 = vupdc(w, h[0], x, delta);
+            const int32_t y = swap_pair(s1);
+            const int32_t s2 = add32(x, apply_weight(w, y));
+            const int32_t w2 = vupdc(w, y, x, delta);
+            const int32_t s2x = swap_pair(s2);
+            x = isB ? s1 : s2;
+            w = isB ? w1 : w2;
+            h[0] = isB ? s2x : h[0];
+        } else if constexpr (T == -3) {  // both, then exchange histories
+            const int32_t sv = add32(x, apply_weight(w, h[0]));
+            w = vupdc(w, h[0], x, delta);
+            h[0] = swap_pair(sv);
+            x = sv;
         }
     }
     template <int U>
-    __device__ __forceinline__ void mono(int32_t &X) {
+    __device__ __forceinline__ void mono(int32_t &x) {
         using namespace wvf;
         if constexpr (T == 17 || T == 18) {
-            int32_t sa = T == 17 ? sub32(mul32(2, a[0]), a[1]) : (sub32(mul32(3, a[0]), a[1]) >> 1);
-            int32_t o = add32(apply_weight(wA, sa), X);
-            upd_w(wA, sa, X, delta);
-            a[1] = a[0];
-            a[0] = o;
-            X = o;
+            const int32_t sa = T == 17 ? sub32(mul32(2, h[0]), h[1]) : (sub32(mul32(3, h[0]), h[1]) >> 1);
+            const int32_t o = add32(apply_weight(w, sa), x);
+            w = vupd(w, sa, x, delta);
+            h[1] = h[0];
+            h[0] = o;
+            x = o;
         } else {
-            constexpr int TT = (T >= 1 && T <= 8) ? T : (T & 7);  // mono negative terms: default case
-            int32_t sa = a[(U - (TT == 0 ? 8 : TT)) & 7];
-            int32_t o = add32(apply_weight(wA, sa), X);
-            upd_w(wA, sa, X, delta);
-            a[U & 7] = o;
-            X = o;
+            constexpr int TT = (T >= 1 && T <= 8) ? T : ((T & 7) == 0 ? 8 : (T & 7));
+            const int32_t sa = h[(U - TT) & 7];
+            const int32_t o = add32(apply_weight(w, sa), x);
+            w = vupd(w, sa, x, delta);
+            h[U & 7] = o;
+            x = o;
         }
     }
 };
 
 template <int... Ts>
-struct Chain;
+struct VChain;
 template <>
-struct Chain<> {
-    __device__ __forceinline__ void init(const BlockDesc &, int) {}
+struct VChain<> {
+    __device__ __forceinline__ void init(const BlockDesc &, int, bool, bool) {}
     __device__ __forceinline__ void trunc() {}
     template <int U>
-    __device__ __forceinline__ void stereo(int32_t &, int32_t &) {}
+    __device__ __forceinline__ void stereo(int32_t &, bool) {}
     template <int U>
     __device__ __forceinline__ void mono(int32_t &) {}
 };
 template <int T, int... Ts>
-struct Chain<T, Ts...> {
-    PState<T> p;
-    Chain<Ts...> rest;
-    __device__ __forceinline__ void init(const BlockDesc &d, int i) {
-        p.init(d, i);
-        rest.init(d, i + 1);
+struct VChain<T, Ts...> {
+    VPass<T> p;
+    VChain<Ts...> rest;
+    __device__ __forceinline__ void init(const BlockDesc &d, int i, bool isB, bool mono) {
+        if (T < 0 && !mono)
+            p.init_stereo_neg(d, i, isB);
+        else
+            p.init(d, i, isB);
+        rest.init(d, i + 1, isB, mono);
     }
     __device__ __forceinline__ void trunc() {
         p.trunc();
         rest.trunc();
     }
     template <int U>
-    __device__ __forceinline__ void stereo(int32_t &L, int32_t &R) {
-        p.template stereo<U>(L, R);
-        rest.template stereo<U>(L, R);
+    __device__ __forceinline__ void stereo(int32_t &x, bool isB) {
+        p.template stereo<U>(x, isB);
+        rest.template stereo<U>(x, isB);
     }
     template <int U>
-    __device__ __forceinline__ void mono(int32_t &X) {
-        p.template mono<U>(X);
-        rest.template mono<U>(X);
+    __device__ __forceinline__ void mono(int32_t &x) {
+        p.template mono<U>(x);
+        rest.template mono<U>(x);
     }
 };
 
-__device__ __forceinline__ int32_t iabs(int32_t x) { return x < 0 ? (int32_t)(0u - (uint32_t)x) : x; }
+__device__ __forceinline__ bool any_lane(bool c) { return __builtin_amdgcn_ballot_w64(c) != 0; }
 
 // Output of the mute path: the whole chunk becomes fixup(0) and every later
 // chunk 0 (UnpackUtils.cs:527-543, 649-664).  All lanes store.
@@ -650,6 +670,100 @@ __device__ __forceinline__ void mute_fill(uint32_t first_chunk, uint32_t chunk, 
     }
 }
 
+// Chunk-seam bookkeeping of the reconstruction (uniform, SALU).
+struct Seams {
+    uint32_t chunk_start, chunk_end, seam8, bsp, chunk, nfr;
+    bool crc_stop;
+};
+
+// One residual batch (32 stereo / 64 mono frames from t0).  LEAN: full batch,
+// no chunk-seam event inside, so no per-frame seam or validity tests.  The
+// steps per frame are those of decode_pcm_block in wv_decode_core.h.
+template <int LAYOUT, bool LEAN, bool JOINT, bool IDENT, class CH>
+__device__ __forceinline__ void recon_batch(CH &ch, const Fixup &fx, const int32_t *res, uint32_t rbase, int32_t &o0,
+                                            int32_t &o1, int32_t &crc, int32_t ml, uint32_t t0, uint32_t tvalid,
+                                            Seams &sm, int &mute_at, int lane) {
+    using namespace wvf;
+    constexpr bool MONO = LAYOUT != 0;
+    constexpr uint32_t BF = MONO ? 64 : 32;
+    const bool isB = !MONO && (lane & 1);
+    const int pair = lane >> 1;
+    for (uint32_t g = 0; g < BF / 8; g++) {
+        if (!LEAN && t0 + g * 8 >= tvalid) break;
+        int32_t xr[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            xr[u] = MONO ? res[(rbase + g * 8 + u) % RES_RING] : res[(rbase + 2 * (g * 8 + u) + (lane & 1)) % RES_RING];
+#define WV2_VFRAME(U)                                                                          \
+    {                                                                                          \
+        const uint32_t j = g * 8 + (U);                                                        \
+        const uint32_t t = t0 + j;                                                             \
+        if (LEAN || t < tvalid) {                                                              \
+            int32_t x = xr[U];                                                                 \
+            int32_t fl;                                                                        \
+            if (MONO) {                                                                        \
+                ch.template mono<U>(x);                                                        \
+                if (LEAN) {                                                                    \
+                    if (__builtin_expect(any_lane(iabs(x) > ml), 0)) {                         \
+                        mute_at = (int)t;                                                      \
+                        break;                                                                 \
+                    }                                                                          \
+                    crc = add32(mul32(crc, 3), x);                                             \
+                } else {                                                                       \
+                    if (!sm.crc_stop && any_lane(iabs(x) > ml)) {                              \
+                        const uint32_t q = sm.bsp + (t - sm.chunk_start);                      \
+                        if (q != sm.chunk_end - sm.chunk_start) {                              \
+                            mute_at = (int)t;                                                  \
+                            break;                                                             \
+                        }                                                                      \
+                        sm.crc_stop = true;                                                    \
+                    }                                                                          \
+                    if (!sm.crc_stop) crc = add32(mul32(crc, 3), x);                           \
+                }                                                                              \
+                fl = x;                                                                        \
+            } else {                                                                           \
+                ch.template stereo<U>(x, isB);                                                 \
+                const int32_t y = swap_pair(x);                                                \
+                int32_t Lv = isB ? y : x, Rv = isB ? x : y;                                    \
+                if (JOINT) {                                                                   \
+                    Rv = sub32(Rv, Lv >> 1);                                                   \
+                    Lv = add32(Lv, Rv);                                                        \
+                }                                                                              \
+                if (__builtin_expect(any_lane(max(iabs(Lv), iabs(Rv)) > ml), 0)) {             \
+                    mute_at = (int)t;                                                          \
+                    break;                                                                     \
+                }                                                                              \
+                crc = add32(mul32(crc, 9), add32(mul32(Lv, 3), Rv));                           \
+                fl = isB ? Rv : Lv;                                                            \
+            }                                                                                  \
+            if (!LEAN && (t == sm.seam8 || t == sm.chunk_end - 1)) ch.trunc();                 \
+            if (!IDENT) fl = fixup_tail(fx, fl);                                               \
+            if (LAYOUT == 1) {                                                                 \
+                o0 = lane == (int)j ? fl : o0;                                                 \
+            } else if (LAYOUT == 2) {                                                          \
+                if (j < 32) o0 = pair == (int)j ? fl : o0;                                     \
+                else o1 = pair == (int)j - 32 ? fl : o1;                                       \
+            } else {                                                                           \
+                o0 = pair == (int)j ? fl : o0;                                                 \
+            }                                                                                  \
+            if (!LEAN && t == sm.chunk_end - 1) {                                              \
+                sm.chunk_start = t + 1;                                                        \
+                sm.chunk_end = sm.chunk_start + sm.chunk < sm.nfr ? sm.chunk_start + sm.chunk : sm.nfr; \
+                sm.seam8 = (!MONO && sm.chunk_end - sm.chunk_start >= 16) ? sm.chunk_start + 7 : 0xFFFFFFFFu; \
+                sm.bsp = 0;                                                                    \
+                sm.crc_stop = false;                                                           \
+            }                                                                                  \
+        }                                                                                      \
+    }
+        do {
+            WV2_VFRAME(0) WV2_VFRAME(1) WV2_VFRAME(2) WV2_VFRAME(3) WV2_VFRAME(4) WV2_VFRAME(5) WV2_VFRAME(6)
+            WV2_VFRAME(7)
+        } while (0);
+#undef WV2_VFRAME
+        if (mute_at >= 0) break;
+    }
+}
+
 // LAYOUT 0: stereo; 1: mono (MONO_FLAG); 2: FALSE_STEREO (mono decode, 2 ints/frame)
 template <int LAYOUT, int... Ts>
 __device__ __forceinline__ void recon_impl(const BlockDesc &d, Shared &sh, int32_t *out_base, uint32_t *status_out,
@@ -663,29 +777,34 @@ __device__ __forceinline__ void recon_impl(const BlockDesc &d, Shared &sh, int32
     const bool joint = (flags & JOINT_STEREO) != 0;
     const int32_t ml = d.mute_limit;
     const uint32_t nfr = d.nframes;
-    const uint32_t chunk = d.chunk;
     int32_t *out = out_base + d.out_off;
 
-    Chain<Ts...> ch;
-    ch.init(d, 0);
+    VChain<Ts...> ch;
+    ch.init(d, 0, !MONO && (lane & 1), MONO);
     Fixup fx;
     fixup_init(fx, d);
+    const bool ident = fx.mode == 3 && fx.shift == 0 && !fx.lossy;  // fixup is the identity
 
     uint32_t status = 0;
-    int32_t crc = -1;
+    int32_t crc = -1;  // identical in every lane
     bool crc_garbage = false;
-    uint32_t chunk_start = 0;
-    uint32_t chunk_end = d.first_chunk < nfr ? d.first_chunk : nfr;
-    uint32_t seam8 = (!MONO && chunk_end - chunk_start >= 16) ? chunk_start + 7 : 0xFFFFFFFFu;
-    uint32_t bsp = d.first_bsp;
-    bool crc_stop = false;
+    Seams sm;
+    sm.chunk = d.chunk;
+    sm.nfr = nfr;
+    sm.chunk_start = 0;
+    sm.chunk_end = d.first_chunk < nfr ? d.first_chunk : nfr;
+    sm.seam8 = (!MONO && sm.chunk_end >= 16) ? 7 : 0xFFFFFFFFu;
+    sm.bsp = d.first_bsp;
+    sm.crc_stop = false;
     uint32_t produced = 0;
+    WV2_PROF(const uint64_t r_start = clock64(); uint64_t r_wait = 0;)
 
     for (uint32_t t0 = 0; t0 < nfr; t0 += BF) {
         uint32_t tend = t0 + BF < nfr ? t0 + BF : nfr;
         uint32_t need = tend * WPF;
         uint32_t spins = 0;
         uint32_t perr = 0;
+        WV2_PROF(const uint64_t rw0 = clock64();)
         while (produced < need) {
             produced = uni(lds_load_acq(&sh.produced));
             if (produced >= need) break;
@@ -700,82 +819,37 @@ __device__ __forceinline__ void recon_impl(const BlockDesc &d, Shared &sh, int32
                 break;
             }
         }
+        WV2_PROF(r_wait += clock64() - rw0;)
         if (perr == DEC_EXCEPTION || perr == 3) {
             status |= ST_EXCEPTION;
             lds_store_rel(&sh.stop, 1);
             break;
         }
-        uint32_t tvalid = produced < need ? produced / WPF : tend;  // a bits error cuts the batch short
-        int32_t v = sh.res[((t0 * WPF) % RES_RING) + lane];
+        const uint32_t tvalid = produced < need ? produced / WPF : tend;  // a bits error cuts the batch short
         int32_t o0 = 0, o1 = 0;  // staged outputs (o1: false-stereo second half)
         int mute_at = -1;
-
-#define WV2_FRAME(U)                                                                          \
-    {                                                                                         \
-        const uint32_t j = g * 8 + (U);                                                       \
-        const uint32_t t = t0 + j;                                                            \
-        if (t < tvalid) {                                                                     \
-            int32_t L, R = 0;                                                                 \
-            if (MONO) {                                                                       \
-                L = __builtin_amdgcn_readlane(v, (int)j);                                     \
-                ch.template mono<U>(L);                                                       \
-                if (!crc_stop && iabs(L) > ml) {                                              \
-                    uint32_t q = bsp + (t - chunk_start);                                     \
-                    if (q != chunk_end - chunk_start) {                                       \
-                        mute_at = (int)t;                                                     \
-                        break;                                                                \
-                    }                                                                         \
-                    crc_stop = true;                                                          \
-                }                                                                             \
-                if (!crc_stop) crc = add32(mul32(crc, 3), L);                                 \
-            } else {                                                                          \
-                L = __builtin_amdgcn_readlane(v, (int)(2 * j));                               \
-                R = __builtin_amdgcn_readlane(v, (int)(2 * j + 1));                           \
-                ch.template stereo<U>(L, R);                                                  \
-                if (joint) {                                                                  \
-                    R = sub32(R, L >> 1);                                                     \
-                    L = add32(L, R);                                                          \
-                }                                                                             \
-                if (iabs(L) > ml || iabs(R) > ml) {                                           \
-                    mute_at = (int)t;                                                         \
-                    break;                                                                    \
-                }                                                                             \
-                crc = add32(mul32(add32(mul32(crc, 3), L), 3), R);                            \
-            }                                                                                 \
-            if (t == seam8 || t == chunk_end - 1) ch.trunc();                                 \
-            const int32_t fl = fixup_tail(fx, L);                                             \
-            if (LAYOUT == 1) {                                                                \
-                o0 = writelane(fl, (int)j, o0);                                               \
-            } else if (LAYOUT == 2) {                                                         \
-                if (j < 32) {                                                                 \
-                    o0 = writelane(fl, (int)(2 * j), o0);                                     \
-                    o0 = writelane(fl, (int)(2 * j + 1), o0);                                 \
-                } else {                                                                      \
-                    o1 = writelane(fl, (int)(2 * j - 64), o1);                                \
-                    o1 = writelane(fl, (int)(2 * j - 63), o1);                                \
-                }                                                                             \
-            } else {                                                                          \
-                o0 = writelane(fl, (int)(2 * j), o0);                                         \
-                o0 = writelane(fixup_tail(fx, R), (int)(2 * j + 1), o0);                      \
-            }                                                                                 \
-            if (t == chunk_end - 1) {                                                         \
-                chunk_start = t + 1;                                                          \
-                chunk_end = chunk_start + chunk < nfr ? chunk_start + chunk : nfr;            \
-                seam8 = (!MONO && chunk_end - chunk_start >= 16) ? chunk_start + 7 : 0xFFFFFFFFu; \
-                bsp = 0;                                                                      \
-                crc_stop = false;                                                             \
-            }                                                                                 \
-        }                                                                                     \
-    }
-
-        for (uint32_t g = 0; g < BF / 8; g++) {
-            if (WV2_EXP == 1 || WV2_EXP == 3 || t0 + g * 8 >= tvalid) break;
-            do {
-                WV2_FRAME(0) WV2_FRAME(1) WV2_FRAME(2) WV2_FRAME(3) WV2_FRAME(4) WV2_FRAME(5) WV2_FRAME(6) WV2_FRAME(7)
-            } while (0);
-            if (mute_at >= 0) break;
+        const uint32_t rbase = t0 * WPF;
+        // A full batch with no chunk-seam event inside takes the lean path.
+        const uint32_t tlast = t0 + BF - 1;
+        const bool seam_in = (sm.seam8 >= t0 && sm.seam8 <= tlast) ||
+                             (sm.chunk_end - 1 >= t0 && sm.chunk_end - 1 <= tlast);
+        const bool quirk_in =
+            MONO && (sm.crc_stop || (sm.bsp > 0 && sm.chunk_end - sm.bsp >= t0 && sm.chunk_end - sm.bsp <= tlast));
+        if (WV2_EXP == 1 || WV2_EXP == 3) {
+        } else if (tvalid == t0 + BF && !seam_in && !quirk_in) {
+            if (joint) {
+                if (ident) recon_batch<LAYOUT, true, true, true>(ch, fx, sh.res, rbase, o0, o1, crc, ml, t0, tvalid, sm, mute_at, lane);
+                else recon_batch<LAYOUT, true, true, false>(ch, fx, sh.res, rbase, o0, o1, crc, ml, t0, tvalid, sm, mute_at, lane);
+            } else {
+                if (ident) recon_batch<LAYOUT, true, false, true>(ch, fx, sh.res, rbase, o0, o1, crc, ml, t0, tvalid, sm, mute_at, lane);
+                else recon_batch<LAYOUT, true, false, false>(ch, fx, sh.res, rbase, o0, o1, crc, ml, t0, tvalid, sm, mute_at, lane);
+            }
+        } else {
+            if (joint) recon_batch<LAYOUT, false, true, false>(ch, fx, sh.res, rbase, o0, o1, crc, ml, t0, tvalid, sm, mute_at, lane);
+            else recon_batch<LAYOUT, false, false, false>(ch, fx, sh.res, rbase, o0, o1, crc, ml, t0, tvalid, sm, mute_at, lane);
         }
-#undef WV2_FRAME
+        // the batch's residuals have been read: release the ring space
+        lds_publish(&sh.consumed, tend * WPF);
         // store the batch: 64 ints per instruction, one per lane
         const uint32_t nv = (mute_at >= 0 ? (uint32_t)mute_at : tvalid) - t0;
         const uint64_t base = (uint64_t)t0 * OCH;
@@ -786,21 +860,29 @@ __device__ __forceinline__ void recon_impl(const BlockDesc &d, Shared &sh, int32
             if (bits_err && mute_at < 0) {
                 status |= ST_BITS_ERROR;
                 crc_garbage = true;
-                if (MONO && chunk_start == 0 && bsp > 0) status |= ST_NONDET;
+                if (MONO && sm.chunk_start == 0 && sm.bsp > 0) status |= ST_NONDET;
             }
             status |= ST_MUTED;
             lds_store_rel(&sh.stop, 1);
             const int32_t z0 = fixup_tail(fx, 0);
-            mute_fill<OCH>(d.first_chunk, chunk, nfr, z0, z0, out, chunk_start, lane);
+            mute_fill<OCH>(d.first_chunk, sm.chunk, nfr, z0, z0, out, sm.chunk_start, lane);
             break;
         }
-        lds_store_rel(&sh.consumed, tend * WPF);
     }
     if (!(status & ST_EXCEPTION) && nfr == d.block_samples) {
         status |= ST_CRC_CHECKED;
-        if (crc_garbage || crc != d.crc) status |= ST_CRC_ERROR;
+        if (crc_garbage || (int32_t)uni((uint32_t)crc) != d.crc) status |= ST_CRC_ERROR;
     }
     if (lane == 0) *status_out = d.fstatus | status;
+#if WV2_EXP == 4
+    const uint64_t r_total = clock64() - r_start;
+    if (lane == 0) {
+        out[8] = (int32_t)(uint32_t)r_total;
+        out[9] = (int32_t)(uint32_t)(r_total >> 32);
+        out[10] = (int32_t)(uint32_t)r_wait;
+        out[11] = (int32_t)(uint32_t)(r_wait >> 32);
+    }
+#endif
 }
 
 template <int... Ts>
