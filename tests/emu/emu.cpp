@@ -17,6 +17,19 @@ struct HostStore {
     int32_t *out;
     uint64_t base;
     void put(uint64_t i, int32_t v) { out[base + i] = v; }
+
+// FileInfo fields of the host framing, for the WavpackGet* getters' tests.
+int emu_file_info(const uint8_t *file, size_t len, int64_t *vals, int nvals) {
+    FramingOutput fo;
+    FileInfo info;
+    frame_file(file, len, 0, 0, 0, 4096, fo, info);
+    int64_t v[] = {info.open_ok, info.total_samples, info.sample_rate, info.num_channels, info.bits_per_sample,
+                   info.bytes_per_sample, info.reduced_channels, info.mode, info.version, info.is_float,
+                   info.out_frames, info.out_nch, (int64_t)fo.descs.size(), (int64_t)info.dsd_multiplier};
+    int n = (int)(sizeof(v) / sizeof(v[0]));
+    for (int i = 0; i < n && i < nvals; i++) vals[i] = v[i];
+    return n;
+}
 };
 
 extern "C" {
@@ -58,6 +71,9 @@ int64_t emu_decode(const uint8_t *file, size_t len, int chunk, int32_t *out, int
                 }
             }
         }
+        // a block decoded from state the device cannot see (malformed files only):
+        // the reference decodes garbage and its CRC check fails (as wv_api.cpp)
+        if ((st & ST_UNSUPPORTED) && d.nframes == d.block_samples) st |= ST_CRC_CHECKED | ST_CRC_ERROR;
         *status_or |= st;
         if (st & ST_CRC_ERROR) (*crc_errors)++;
         if (st & ST_EXCEPTION) {
@@ -69,5 +85,18 @@ int64_t emu_decode(const uint8_t *file, size_t len, int chunk, int32_t *out, int
         for (int64_t i = 0; i < fl.second; i++) out[fl.first + i] = 0x55;
     if (exception) return -3;
     return info.out_frames;
+}
+
+// FileInfo fields of the host framing, for the WavpackGet* getters' tests.
+int emu_file_info(const uint8_t *file, size_t len, int64_t *vals, int nvals) {
+    FramingOutput fo;
+    FileInfo info;
+    frame_file(file, len, 0, 0, 0, 4096, fo, info);
+    int64_t v[] = {info.open_ok, info.total_samples, info.sample_rate, info.num_channels, info.bits_per_sample,
+                   info.bytes_per_sample, info.reduced_channels, info.mode, info.version, info.is_float,
+                   info.out_frames, info.out_nch, (int64_t)fo.descs.size(), (int64_t)info.dsd_multiplier};
+    int n = (int)(sizeof(v) / sizeof(v[0]));
+    for (int i = 0; i < n && i < nvals; i++) vals[i] = v[i];
+    return n;
 }
 }

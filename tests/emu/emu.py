@@ -1,0 +1,50 @@
+"""TEST-ONLY ctypes binding of tests/emu/libwvemu.so (host build of the device decode core)."""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_L = None
+
+INFO_FIELDS = ("open_ok", "total_samples", "sample_rate", "num_channels", "bits_per_sample", "bytes_per_sample",
+               "reduced_channels", "mode", "version", "is_float", "out_frames", "out_nch", "num_blocks",
+               "dsd_multiplier")
+
+
+def lib():
+    global _L
+    if _L is None:
+        L = ctypes.CDLL(os.path.join(_HERE, "libwvemu.so"))
+        L.emu_decode.restype = ctypes.c_int64
+        L.emu_decode.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64,
+                                 ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int),
+                                 ctypes.POINTER(ctypes.c_uint32)]
+        L.emu_file_info.restype = ctypes.c_int
+        L.emu_file_info.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int]
+        _L = L
+    return _L
+
+
+def decode(data: bytes, chunk: int = 4096):
+    """-> (frames or -2/-3, samples int32 flat, crc_errors, status_or)"""
+    cap = max(len(data) * 16, 1 << 16)
+    while True:
+        out = np.zeros(cap, dtype=np.int32)
+        crc = ctypes.c_int64(0)
+        nch = ctypes.c_int(0)
+        st = ctypes.c_uint32(0)
+        n = lib().emu_decode(data, len(data), chunk, out.ctypes.data, cap, ctypes.byref(crc), ctypes.byref(nch),
+                             ctypes.byref(st))
+        if n == -4:
+            cap *= 4
+            continue
+        if n < 0:
+            return int(n), np.zeros(0, np.int32), crc.value, st.value
+        return int(n), out[: n * nch.value].copy(), crc.value, st.value
+
+
+def file_info(data: bytes) -> dict:
+    vals = np.zeros(len(INFO_FIELDS), dtype=np.int64)
+    lib().emu_file_info(data, len(data), vals.ctypes.data, len(INFO_FIELDS))
+    return dict(zip(INFO_FIELDS, (int(v) for v in vals)))

@@ -96,3 +96,33 @@ def test_c2_full_size_roundtrip(gpu_batch_cls):
     assert res[0].crc_errors == 0
     assert res[0].frames == pcm.shape[0] == 1024 * 22050
     np.testing.assert_array_equal(out, pcm.reshape(-1))
+
+
+def test_golden_fixtures(gpu_batch_cls):
+    """The committed fixtures (tests/golden) decode to the manifest's SHA-256, all in one batch."""
+    import hashlib
+
+    from tests import golden
+    fx = list(golden.load())
+    out, res, infos = _gpu_decode([d for _, d, _ in fx], 4096, gpu_batch_cls)
+    for (name, data, m), r, info in zip(fx, res, infos):
+        assert r.frames == m["frames"] and r.crc_errors == m["crc_errors"], name
+        got = out[info.out_offset: info.out_offset + m["frames"] * m["nch"]]
+        assert hashlib.sha256(got.astype("<i4").tobytes()).hexdigest() == m["sha256_int32le"], name
+
+
+def test_edge_inputs(gpu_batch_cls):
+    """Empty and non-WavPack inputs open with an error (WavPackUtils.cs:36-120); a batch that
+    mixes them with a real file still decodes the real one; ragged block sizes and a 1-frame
+    tail block decode exactly."""
+    from synth import wvsynth as S
+    x = S.audio_like(4097, 2, 16, seed=31)
+    real = S.encode_pcm(x, S.EncParams(terms=S.TERMS_DEFAULT, block_samples=4096))  # 4096 + 1-frame tail
+    ragged = S.encode_pcm(x, S.EncParams(terms=S.TERMS_FAST, block_samples=1237))
+    files = [b"", b"RIFF" + b"\0" * 60, real, ragged]
+    out, res, infos = _gpu_decode(files, 4096, gpu_batch_cls)
+    assert not infos[0].open_ok and not infos[1].open_ok
+    for k in (2, 3):
+        info = infos[k]
+        assert res[k].frames == 4097 and res[k].crc_errors == 0
+        np.testing.assert_array_equal(out[info.out_offset: info.out_offset + 4097 * 2], x.reshape(-1))

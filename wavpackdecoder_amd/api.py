@@ -227,23 +227,35 @@ def WavpackLossy(wpc) -> bool:
 
 
 def WavpackGetSampleRate(wpc) -> int:
-    return int(wpc._info.sample_rate)
+    """WavPackUtils.cs:379-385 (DSD: the 1-bit rate, multiplier x 8 x stored rate)."""
+    i = wpc._info
+    if i.sample_rate != 0:
+        return int(i.dsd_multiplier * i.sample_rate * 8) if i.dsd_multiplier > 0 else int(i.sample_rate)
+    return 44100
 
 
 def WavpackGetNumChannels(wpc) -> int:
-    return int(wpc._info.num_channels)
+    """WavPackUtils.cs:390-396."""
+    return int(wpc._info.num_channels) or 2
 
 
 def WavpackGetBitsPerSample(wpc) -> int:
-    return int(wpc._info.bits_per_sample)
+    """WavPackUtils.cs:407-415."""
+    i = wpc._info
+    if i.bits_per_sample != 0:
+        return int(i.bits_per_sample) // 8 if i.dsd_multiplier > 0 else int(i.bits_per_sample)
+    return 16
 
 
 def WavpackGetBytesPerSample(wpc) -> int:
-    return int(wpc._info.bytes_per_sample)
+    """WavPackUtils.cs:422-428."""
+    return int(wpc._info.bytes_per_sample) or 2
 
 
 def WavpackGetReducedChannels(wpc) -> int:
-    return int(wpc._info.reduced_channels) or int(wpc._info.num_channels) or 2
+    """WavPackUtils.cs:436-442."""
+    i = wpc._info
+    return int(i.reduced_channels) or int(i.num_channels) or 2
 
 
 def WavpackGetMode(wpc) -> int:
