@@ -99,6 +99,21 @@ def algorithmic_bytes(data: bytes, nch: int = 2) -> int:
     return tot
 
 
+def pmc_traffic(kernel_substr: str = "wv_pcm_2wave<17, 17>"):
+    """Per-launch HBM bytes of the bench kernel from the newest profiles/<tag>_pmc.json
+    (rocprofv3 FETCH_SIZE / WRITE_SIZE passes, scripts/profile.sh + scripts/pmc_to_profile.py)."""
+    import glob
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json"))):
+        with open(path) as f:
+            d = json.load(f)
+        if kernel_substr in d.get("kernel", ""):
+            best = (path, d)
+    if best is None:
+        return None, None
+    return float(best[1]["traffic_bytes_per_launch"]), os.path.relpath(best[0], ROOT)
+
+
 def cpu_baseline(data: bytes, threads: int, reps: int):
     """Oracle (C port of the reference path) on host threads; ctypes drops the GIL."""
     from concurrent.futures import ThreadPoolExecutor
@@ -180,7 +195,18 @@ def main():
     frames_total = _sum(pg, float(frames_rank))
     value = frames_total * args.steps / dt / 1e6
 
+    # PCIe-inclusive rate (host bytes in -> host int32 out), reported beside `value`, never as it
+    host_out = np.empty(max(b.out_ints, 1), dtype=np.int32)
+    t_e2e = time.perf_counter()
+    b.upload()
+    b.decode()
+    b.sync()
+    b._check(b._L.wvg_batch_download(b._b, host_out.ctypes.data, host_out.size))
+    t_e2e = time.perf_counter() - t_e2e
+    e2e = frames_rank / t_e2e / 1e6
+
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic()
     line = None
     if rank == 0:
         cpu = None
@@ -208,9 +234,14 @@ def main():
                        "frames_per_gpu": int(frames_rank), "compressed_bytes_per_gpu": len(data),
                        "parallelism": f"file-shard x{ws}, no collectives"},
             "hbm_gbs": round(achieved, 2),
+            "pcie_inclusive": {"value": round(e2e, 2), "unit": "Msamples/s", "ms": round(t_e2e * 1e3, 3),
+                               "what": "upload of the compressed batch + decode + download of int32 PCM, rank 0"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
-                         "kernel_ms": round(kernel_ms, 4), "alg_bytes_per_launch": alg_bytes},
+                         "frac": round(achieved / HBM_PEAK_GBS, 6),
+                         "traffic": None if traffic is None else int(traffic),
+                         "traffic_unit": "bytes/launch (PMC FETCH_SIZE x2 + WRITE_SIZE)", "traffic_source": traffic_src,
+                         "kernel_ms": round(kernel_ms, 4), "alg_bytes_per_launch": alg_bytes,
+                         "binding_limit": "serial entropy decode per block (scalar issue of one wave), not HBM"},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

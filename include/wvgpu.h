@@ -128,6 +128,10 @@ int wvg_batch_time(wvg_batch *b, int iters, float *ms);
 int wvg_decode_file(wvg_ctx *ctx, const uint8_t *file, size_t len, int chunk_frames, int32_t *out, int64_t cap_ints,
                     wvg_file_info *info, wvg_file_result *res);
 
+/* WavpackOpenFileInput (WavPackUtils.cs:36-120) without a device: host framing
+ * only, fills what the getters report.  WVG_ERR_OPEN when the file does not open. */
+int wvg_probe_file(const uint8_t *file, size_t len, uint32_t open_flags, int chunk_frames, wvg_file_info *info);
+
 /* WavpackFormatSamples (WavPackUtils.cs:288-341) on the host: int32 -> LE PCM bytes. */
 int wvg_format_samples(const int32_t *src, int64_t samcnt, int bps, uint8_t *pcm, int64_t pcm_len, int offset,
                        int dsd);

@@ -99,32 +99,33 @@ def test_dsd_mode0_false_stereo_exception():
 
 
 def test_file_info_matches_oracle_getters():
-    """WavpackOpenFileInput's fields (WavPackUtils.cs:36-120) from the host framing, through the
-    product's getter mirror (wavpackdecoder_amd/api.py, WavPackUtils.cs:346-499)."""
-    import types
-
+    """WavpackOpenFileInput + getters (WavPackUtils.cs:36-120, 346-499) through the product
+    API (wvg_probe_file is host-only framing, so this runs without a GPU) vs the oracle."""
     from wavpackdecoder_amd import api
     L = O.lib()
     for name, data, _ in PCM[:8] + DSD:
         ctx = L.wvo_open(data, len(data), 0)
         try:
-            info = E.file_info(data)
-            assert info["open_ok"] == 1
-            wpc = types.SimpleNamespace(_info=types.SimpleNamespace(**info))
-            assert api.WavpackGetNumSamples(wpc) == L.wvo_get_num_samples(ctx, 0)
-            assert api.WavpackGetNumSamples(wpc, True) == L.wvo_get_num_samples(ctx, 1)
-            assert api.WavpackGetSampleRate(wpc) == L.wvo_get_sample_rate(ctx)
-            assert api.WavpackGetNumChannels(wpc) == L.wvo_get_num_channels(ctx)
-            assert api.WavpackGetBitsPerSample(wpc) == L.wvo_get_bits_per_sample(ctx)
-            assert api.WavpackGetBytesPerSample(wpc) == L.wvo_get_bytes_per_sample(ctx)
-            assert api.WavpackGetReducedChannels(wpc) == L.wvo_get_reduced_channels(ctx)
-            assert api.WavpackGetMode(wpc) == L.wvo_get_mode(ctx)
-            assert api.WavpackGetVersion(wpc) == L.wvo_get_version(ctx)
-            assert api.WavpackGetIsFloat(wpc) == bool(L.wvo_get_is_float(ctx))
+            wpc = api.WavpackOpenFileInput(data)
+            assert api.WavpackGetErrorMessage(wpc) is None, name
+            assert api.WavpackGetNumSamples(wpc) == L.wvo_get_num_samples(ctx, 0), name
+            assert api.WavpackGetNumSamples(wpc, True) == L.wvo_get_num_samples(ctx, 1), name
+            assert api.WavpackGetSampleRate(wpc) == L.wvo_get_sample_rate(ctx), name
+            assert api.WavpackGetNumChannels(wpc) == L.wvo_get_num_channels(ctx), name
+            assert api.WavpackGetBitsPerSample(wpc) == L.wvo_get_bits_per_sample(ctx), name
+            assert api.WavpackGetBytesPerSample(wpc) == L.wvo_get_bytes_per_sample(ctx), name
+            assert api.WavpackGetReducedChannels(wpc) == L.wvo_get_reduced_channels(ctx), name
+            assert api.WavpackGetMode(wpc) == L.wvo_get_mode(ctx), name
+            assert api.WavpackGetVersion(wpc) == L.wvo_get_version(ctx), name
+            assert api.WavpackGetIsFloat(wpc) == bool(L.wvo_get_is_float(ctx)), name
+            assert api.WavpackGetIsFive(wpc) == bool(L.wvo_get_is_five(ctx)), name
+            assert api.WavpackGetFileFormat(wpc) == L.wvo_get_file_format(ctx), name
         finally:
             L.wvo_close(ctx)
 
 
 def test_not_wavpack():
+    from wavpackdecoder_amd import api
     assert E.file_info(b"RIFF" + b"\0" * 200)["open_ok"] == 0
+    assert api.WavpackGetErrorMessage(api.WavpackOpenFileInput(b"RIFF" + b"\0" * 200))
     assert O.decode_file(b"RIFF" + b"\0" * 200).status == -2

@@ -2,8 +2,9 @@
 reference's WavPackUtils.WavpackUnpackSamples hot path).
 
 Layout:
-  csrc/wv_decode.hip      HIP kernels for gfx950 (PCM + DSD block decode)
-  csrc/wv_decode_core.h   per-block decode (host+device source)
+  csrc/wv_wave2.h         two-wave PCM kernel: scalar parser wave + VALU reconstruction wave
+  csrc/wv_decode.hip      HIP kernels for gfx950 (instantiations, lane-per-block PCM/DSD kernels)
+  csrc/wv_decode_core.h   per-block decode (host+device source; lane kernels, tests/emu)
   csrc/wv_framing.cpp     host framing: .wv bytes -> block descriptors
   csrc/wv_api.cpp         C-ABI (include/wvgpu.h) -> build/libwvgpu.so
   api.py                  mirror of the reference's WavPackUtils API

@@ -86,6 +86,7 @@ def lib():
         "wvg_batch_time": (i32, [vp, i32, ctypes.POINTER(ctypes.c_float)]),
         "wvg_decode_file": (i32, [vp, ctypes.c_char_p, ctypes.c_size_t, i32, vp, i64, ctypes.POINTER(WvgFileInfo),
                                   ctypes.POINTER(WvgFileResult)]),
+        "wvg_probe_file": (i32, [ctypes.c_char_p, ctypes.c_size_t, u32, i32, ctypes.POINTER(WvgFileInfo)]),
         "wvg_format_samples": (i32, [vp, i64, i32, vp, i64, i32, i32]),
     }
     for name, (res, args) in sig.items():
@@ -100,4 +101,4 @@ EXPORTED = ("wvg_open", "wvg_close", "wvg_last_error", "wvg_batch_new", "wvg_bat
             "wvg_batch_upload", "wvg_batch_decode", "wvg_batch_sync", "wvg_batch_out_ints", "wvg_batch_device_out",
             "wvg_batch_num_blocks", "wvg_batch_bytes_in", "wvg_batch_frames", "wvg_batch_download",
             "wvg_batch_file_result", "wvg_batch_block_status", "wvg_batch_time", "wvg_decode_file",
-            "wvg_format_samples")
+            "wvg_probe_file", "wvg_format_samples")

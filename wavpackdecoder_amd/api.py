@@ -172,9 +172,7 @@ def WavpackOpenFileInput(reader, flags: int = 0) -> WavpackContext:
     data = bytes(data)
     wpc = WavpackContext(data, flags)
     L = _L.lib()
-    b = L.wvg_batch_new(_context(), SAMPLE_BUFFER_SIZE)
-    rc = L.wvg_batch_add_file(b, data, len(data), int(flags), ctypes.byref(wpc._info))
-    L.wvg_batch_free(b)
+    rc = L.wvg_probe_file(data, len(data), int(flags), SAMPLE_BUFFER_SIZE, ctypes.byref(wpc._info))  # host only
     if rc < 0 or not wpc._info.open_ok:
         wpc.error_message = wpc._info.error.decode() or "not compatible with this version of WavPack file!"
     return wpc
@@ -226,36 +224,26 @@ def WavpackLossy(wpc) -> bool:
     return bool(wpc._info.lossy)
 
 
+# wvg_file_info carries the getters' results (wv_api.cpp fill_info applies
+# WavPackUtils.cs:379-442: DSD rate x multiplier x 8, bits / 8, defaults).
 def WavpackGetSampleRate(wpc) -> int:
-    """WavPackUtils.cs:379-385 (DSD: the 1-bit rate, multiplier x 8 x stored rate)."""
-    i = wpc._info
-    if i.sample_rate != 0:
-        return int(i.dsd_multiplier * i.sample_rate * 8) if i.dsd_multiplier > 0 else int(i.sample_rate)
-    return 44100
+    return int(wpc._info.sample_rate)
 
 
 def WavpackGetNumChannels(wpc) -> int:
-    """WavPackUtils.cs:390-396."""
-    return int(wpc._info.num_channels) or 2
+    return int(wpc._info.num_channels)
 
 
 def WavpackGetBitsPerSample(wpc) -> int:
-    """WavPackUtils.cs:407-415."""
-    i = wpc._info
-    if i.bits_per_sample != 0:
-        return int(i.bits_per_sample) // 8 if i.dsd_multiplier > 0 else int(i.bits_per_sample)
-    return 16
+    return int(wpc._info.bits_per_sample)
 
 
 def WavpackGetBytesPerSample(wpc) -> int:
-    """WavPackUtils.cs:422-428."""
-    return int(wpc._info.bytes_per_sample) or 2
+    return int(wpc._info.bytes_per_sample)
 
 
 def WavpackGetReducedChannels(wpc) -> int:
-    """WavPackUtils.cs:436-442."""
-    i = wpc._info
-    return int(i.reduced_channels) or int(i.num_channels) or 2
+    return int(wpc._info.reduced_channels)
 
 
 def WavpackGetMode(wpc) -> int:

@@ -129,15 +129,8 @@ void wvg_batch_free(wvg_batch *b) {
     delete b;
 }
 
-int wvg_batch_add_file(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open_flags, wvg_file_info *info) {
-    if (!b || (!file && len)) return WVG_ERR_ARG;
-    if (b->uploaded) free_dev(b);
-    size_t base = (b->blob.size() + 15) & ~(size_t)15;
-    b->blob.resize(base + len);
-    if (len) memcpy(b->blob.data() + base, file, len);
-    FileInfo fi;
-    frame_file(b->blob.data() + base, len, base, (uint64_t)b->out_ints, open_flags, b->chunk, b->fo, fi);
-    wvg_file_info wi;
+// FileInfo -> the getters' view (WavPackUtils.cs:346-499 applied here, once)
+static void fill_info(const FileInfo &fi, wvg_file_info &wi) {
     memset(&wi, 0, sizeof(wi));
     wi.open_ok = fi.open_ok;
     strncpy(wi.error, fi.error.c_str(), sizeof(wi.error) - 1);
@@ -155,6 +148,28 @@ int wvg_batch_add_file(wvg_batch *b, const uint8_t *file, size_t len, uint32_t o
     wi.sample_rate = fi.sample_rate ? (fi.dsd_multiplier > 0 ? (int64_t)fi.dsd_multiplier * fi.sample_rate * 8 : fi.sample_rate) : 44100;
     wi.total_samples = fi.total_samples;
     wi.out_frames = fi.out_frames;
+    wi.out_offset = 0;
+}
+
+int wvg_probe_file(const uint8_t *file, size_t len, uint32_t open_flags, int chunk_frames, wvg_file_info *info) {
+    if ((!file && len) || !info) return WVG_ERR_ARG;
+    FramingOutput fo;
+    FileInfo fi;
+    frame_file(file, len, 0, 0, open_flags, chunk_frames > 0 ? chunk_frames : 4096, fo, fi);
+    fill_info(fi, *info);
+    return fi.open_ok ? WVG_OK : WVG_ERR_OPEN;
+}
+
+int wvg_batch_add_file(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open_flags, wvg_file_info *info) {
+    if (!b || (!file && len)) return WVG_ERR_ARG;
+    if (b->uploaded) free_dev(b);
+    size_t base = (b->blob.size() + 15) & ~(size_t)15;
+    b->blob.resize(base + len);
+    if (len) memcpy(b->blob.data() + base, file, len);
+    FileInfo fi;
+    frame_file(b->blob.data() + base, len, base, (uint64_t)b->out_ints, open_flags, b->chunk, b->fo, fi);
+    wvg_file_info wi;
+    fill_info(fi, wi);
     wi.out_offset = b->out_ints;
     wi.header_off = fi.header_off;
     wi.header_len = fi.header_len;
@@ -298,23 +313,27 @@ int wvg_batch_file_result(wvg_batch *b, int file, wvg_file_result *res) {
 }
 
 int wvg_batch_time(wvg_batch *b, int iters, float *ms) {
+    // mean device time of one decode launch: an event pair around each launch on
+    // the decode stream, so launch gaps between iterations are not counted
     if (!b || !b->uploaded || iters <= 0) return WVG_ERR_ARG;
     wvg_ctx *c = b->ctx;
-    hipEvent_t e0, e1;
-    HIPCHK(c, hipEventCreate(&e0));
-    HIPCHK(c, hipEventCreate(&e1));
-    HIPCHK(c, hipEventRecord(e0, c->stream));
+    std::vector<hipEvent_t> ev((size_t)iters * 2);
+    for (auto &e : ev) HIPCHK(c, hipEventCreate(&e));
     for (int i = 0; i < iters; i++) {
+        HIPCHK(c, hipEventRecord(ev[2 * i], c->stream));
         int rc = wvg_batch_decode(b, nullptr);
         if (rc) return rc;
+        HIPCHK(c, hipEventRecord(ev[2 * i + 1], c->stream));
     }
-    HIPCHK(c, hipEventRecord(e1, c->stream));
-    HIPCHK(c, hipEventSynchronize(e1));
-    float t = 0;
-    HIPCHK(c, hipEventElapsedTime(&t, e0, e1));
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
-    *ms = t / (float)iters;
+    HIPCHK(c, hipEventSynchronize(ev.back()));
+    double tot = 0;
+    for (int i = 0; i < iters; i++) {
+        float t = 0;
+        HIPCHK(c, hipEventElapsedTime(&t, ev[2 * i], ev[2 * i + 1]));
+        tot += t;
+    }
+    for (auto &e : ev) hipEventDestroy(e);
+    *ms = (float)(tot / iters);
     return WVG_OK;
 }
 
