@@ -195,6 +195,106 @@ struct LdsReader {
 };
 
 // ---------------------------------------------------------------------------
+// Scalar-memory bit reader with the BitReader interface used by get_word:
+// the payload is read dword by dword with s_load (constant address space, so
+// the loads are scalar and go through the scalar cache), two dwords ahead of
+// the window; bytes at or past the end read as 0xFF (BitsUtils.cs:125-139).
+// No LDS staging, no VALU, no cross-lane moves on the refill path.
+// ---------------------------------------------------------------------------
+typedef const __attribute__((address_space(4))) uint32_t *cdw_ptr;
+
+struct SmemReader {
+    cdw_ptr base;   // dword-aligned start of the payload
+    uint32_t E;     // real bytes from base
+    uint64_t win;
+    int nb;
+    uint32_t rd;    // index of the next dword to enter the window (== n0)
+    uint32_t n0, n1;
+    WV2_PROF(uint32_t n_fast = 0; uint32_t n_zr = 0; uint32_t n_slow = 0; uint32_t n_refill = 0; uint64_t t_wait = 0;)
+
+    __device__ __forceinline__ uint32_t ld(uint32_t i) const {
+        const uint32_t b = 4u * i;
+        if (__builtin_expect(b + 4u <= E, 1)) return base[i];
+        if (b >= E) return 0xFFFFFFFFu;
+        return base[i] | (0xFFFFFFFFu << (8u * (E - b)));  // partial last dword (the blob is padded)
+    }
+    __device__ __forceinline__ void init(const uint8_t *blob, uint64_t off, uint64_t len) {
+        const uint64_t a = off & ~(uint64_t)3;
+        base = (cdw_ptr)(blob + a);
+        E = (uint32_t)(len + (off - a));
+        win = (uint64_t)ld(0) | ((uint64_t)ld(1) << 32);
+        nb = 64;
+        rd = 2;
+        n0 = ld(2);
+        n1 = ld(3);
+        const int skip = (int)(off - a) * 8;
+        if (skip) {
+            win >>= skip;
+            nb -= skip;
+        }
+    }
+    __device__ __forceinline__ void refill32() {
+        win |= (uint64_t)n0 << nb;
+        nb += 32;
+        rd++;
+        n0 = n1;
+        n1 = ld(rd + 1);
+    }
+    __device__ __forceinline__ void need(int n) {
+        if (nb < n) refill32();
+    }
+    __device__ __forceinline__ void skip(int n) {
+        win >>= n;
+        nb -= n;
+    }
+    __device__ __forceinline__ int getbit() {
+        need(1);
+        int b = (int)(win & 1);
+        skip(1);
+        return b;
+    }
+    __device__ __forceinline__ uint32_t getbits(int n) {
+        if (n <= 0) return 0;
+        need(n);
+        uint32_t v = (uint32_t)(win & ((1ull << n) - 1));
+        skip(n);
+        return v;
+    }
+    __device__ __forceinline__ int consume_ones(int cap) {
+        int total = 0;
+        for (;;) {
+            if (nb <= 32) refill32();
+            uint64_t inv = ~win;
+            int r = inv ? __builtin_ctzll(inv) : 64;
+            if (total + r >= cap) {
+                skip(cap - total);
+                return cap;
+            }
+            if (r < nb) {
+                skip(r + 1);
+                return total + r;
+            }
+            total += nb;
+            win = 0;
+            nb = 0;
+        }
+    }
+};
+
+#ifndef WV2_READER
+#define WV2_READER SmemReader
+#endif
+typedef WV2_READER Reader;
+
+__device__ __forceinline__ void init_reader(SmemReader &rd, const uint8_t *blob, const BlockDesc &d, Shared &, int) {
+    rd.init(blob, d.bits_off, d.bits_len);
+}
+__device__ __forceinline__ void init_reader(LdsReader &rd, const uint8_t *blob, const BlockDesc &d, Shared &sh,
+                                            int lane) {
+    rd.init(blob, d.bits_off, d.bits_len, sh.stream, lane);
+}
+
+// ---------------------------------------------------------------------------
 // parser wave.  Everything here must stay wave-uniform (SGPRs, scalar
 // branches): channel indices are compile-time constants so the entropy state
 // is never indexed at run time (that would put it in scratch), and no uniform
@@ -242,7 +342,7 @@ struct LdsReader {
     "s_sub_i32 " M ", " M ", %[t0]\n"
 
 template <int C>
-__device__ __forceinline__ bool fast_word(Entropy &w, LdsReader &rd, int32_t &out) {
+__device__ __forceinline__ bool fast_word(Entropy &w, Reader &rd, int32_t &out) {
     uint32_t ok, o, t0, u, ones, c1, nh0, nh1, mc, n1, low, avail, ex, v;
     uint32_t nb = (uint32_t)rd.nb;
     int32_t m0 = w.med[C][0], m1 = w.med[C][1], m2 = w.med[C][2], h0 = w.h0, h1 = w.h1;
@@ -357,10 +457,237 @@ __device__ __forceinline__ bool fast_word(Entropy &w, LdsReader &rd, int32_t &ou
 #undef WV2_INC
 #undef WV2_DEC
 
+// ---------------------------------------------------------------------------
+// The lossless inner loop as one scalar sequence: words k..kend-1 (stereo:
+// alternating channel contexts 0/1 starting at channel 0), each the common
+// case of fast_word, with the bit window held in VCC (so its halves can be
+// named) and the SmemReader refill (two dwords prefetched with s_load) done
+// in place.  Exits early (reason 1) before touching any state of a word that
+// is not of the common form, or when a refill would read near the payload
+// end; the caller then runs the general get_word for that word.  Leaves no
+// scalar load outstanding.
+// ---------------------------------------------------------------------------
+#define WV2_W_BOUND(MK, SUF)                                  \
+    "s_lshr_b32 %[mc], " MK ", 4\n"                            \
+    "s_or_b32 %[t0], %[mc], 1\n"                                \
+    "s_flbit_i32_b32 %[t0], %[t0]\n"                            \
+    "s_sub_u32 %[n1], 31, %[t0]\n"                              \
+    "s_add_u32 %[t0], %[n1], 2\n"                               \
+    "s_cmp_gt_u32 %[t0], %[avail]\n"                            \
+    "s_cbranch_scc1 LX_%=\n"
+#define WV2_W_INC(M, ADD, SH)                                   \
+    "s_add_i32 %[t0], " M ", " ADD "\n"                         \
+    "s_ashr_i32 %[t0], %[t0], " SH "\n"                         \
+    "s_mul_i32 %[t0], %[t0], 5\n"                               \
+    "s_add_i32 " M ", " M ", %[t0]\n"
+#define WV2_W_DEC(M, ADD, SH1)                                  \
+    "s_add_i32 %[t0], " M ", " ADD "\n"                         \
+    "s_ashr_i32 %[t0], %[t0], " SH1 "\n"                        \
+    "s_and_b32 %[t0], %[t0], -2\n"                              \
+    "s_sub_i32 " M ", " M ", %[t0]\n"
+// one word of channel context C (medians M0..M2); falls through to the next word
+#define WV2_WORD(C, M0, M1, M2)                                                  \
+    "LW" C "_%=:\n"                                                              \
+    "s_or_b32 %[t0], %[m00], %[m10]\n" /* zero-run mode possible: general path */ \
+    "s_cmp_lt_u32 %[t0], 2\n"                                                    \
+    "s_cbranch_scc1 LX_%=\n"                                                     \
+    "s_cmp_lt_u32 %[nb], 32\n"                                                   \
+    "s_cbranch_scc1 LR" C "_%=\n"                                                \
+    "LRD" C "_%=:\n"                                                             \
+    "s_cmp_lg_u32 %[h0], 0\n"                                                    \
+    "s_cbranch_scc1 LH" C "_%=\n"                                                \
+    "s_orn2_b32 %[t0], 0x10000, vcc_lo\n"                                        \
+    "s_ff1_i32_b32 %[u], %[t0]\n"                                                \
+    "s_cmp_gt_u32 %[u], 15\n"                                                    \
+    "s_cbranch_scc1 LX_%=\n"                                                     \
+    "s_add_u32 %[c1], %[u], 1\n"                                                 \
+    "s_lshr_b32 %[ones], %[u], 1\n"                                              \
+    "s_add_u32 %[ones], %[ones], %[h1]\n"                                        \
+    "s_and_b32 %[nh1], %[u], 1\n"                                                \
+    "s_xor_b32 %[nh0], %[nh1], 1\n"                                              \
+    "s_sub_u32 %[avail], %[nb], %[c1]\n"                                         \
+    "s_cmp_lg_u32 %[ones], 0\n"                                                  \
+    "s_cbranch_scc1 LG1" C "_%=\n"                                               \
+    "LC0" C "_%=:\n"                                                             \
+    "s_cmp_lt_i32 " M0 ", 0\n"                                                   \
+    "s_cbranch_scc1 LX_%=\n"                                                     \
+    WV2_W_BOUND(M0, C)                                                           \
+    "s_mov_b32 %[low], 0\n"                                                      \
+    WV2_W_DEC(M0, "126", "6")                                                    \
+    "LT" C "_%=:\n"                                                              \
+    "s_mov_b32 %[h0], %[nh0]\n"                                                  \
+    "s_mov_b32 %[h1], %[nh1]\n"                                                  \
+    "s_lshr_b64 vcc, vcc, %[c1]\n"                                               \
+    "s_sub_u32 %[nb], %[nb], %[c1]\n"                                            \
+    "s_lshl_b32 %[ex], 2, %[n1]\n"                                               \
+    "s_not_b32 %[t0], %[mc]\n"                                                   \
+    "s_add_u32 %[ex], %[ex], %[t0]\n"                                            \
+    "s_bfm_b32 %[t0], %[n1], 0\n"                                                \
+    "s_and_b32 %[v], vcc_lo, %[t0]\n"                                            \
+    "s_cmp_lt_u32 %[v], %[ex]\n"                                                 \
+    "s_cbranch_scc1 LS" C "_%=\n"                                                \
+    "s_lshr_b32 %[t0], vcc_lo, %[n1]\n"                                          \
+    "s_and_b32 %[t0], %[t0], 1\n"                                                \
+    "s_lshl_b32 %[v], %[v], 1\n"                                                 \
+    "s_sub_u32 %[v], %[v], %[ex]\n"                                              \
+    "s_add_u32 %[v], %[v], %[t0]\n"                                              \
+    "s_add_u32 %[n1], %[n1], 1\n"                                                \
+    "LS" C "_%=:\n"                                                              \
+    "s_add_u32 %[v], %[v], %[low]\n"                                             \
+    "s_lshr_b32 %[t0], vcc_lo, %[n1]\n"                                          \
+    "s_bfe_i32 %[t0], %[t0], 0x10000\n"                                          \
+    "s_xor_b32 %[v], %[v], %[t0]\n"                                              \
+    "s_add_u32 %[n1], %[n1], 1\n"                                                \
+    "s_lshr_b64 vcc, vcc, %[n1]\n"                                               \
+    "s_sub_u32 %[nb], %[nb], %[n1]\n"                                            \
+    "s_and_b32 %[t0], %[k], 63\n"                                                \
+    "s_mov_b32 m0, %[t0]\n"                                                      \
+    "v_writelane_b32 %[resv], %[v], m0\n"                                        \
+    "s_add_u32 %[k], %[k], 1\n"                                                  \
+    "s_branch LN" C "_%=\n"                                                      \
+    /* out of line: refill from the prefetched dwords */                          \
+    "LR" C "_%=:\n"                                                              \
+    "s_lshl_b32 %[t0], %[rd], 2\n"                                               \
+    "s_add_u32 %[t0], %[t0], 12\n"                                               \
+    "s_cmp_gt_u32 %[t0], %[E]\n"                                                 \
+    "s_cbranch_scc1 LX_%=\n"                                                     \
+    "s_waitcnt lgkmcnt(0)\n"                                                     \
+    "s_lshl_b32 %[v], %[n0], %[nb]\n"                                            \
+    "s_or_b32 vcc_lo, vcc_lo, %[v]\n"                                            \
+    "s_lshr_b32 %[v], %[n0], 1\n"                                                \
+    "s_sub_u32 %[u], 31, %[nb]\n"                                                \
+    "s_lshr_b32 %[v], %[v], %[u]\n"                                              \
+    "s_or_b32 vcc_hi, vcc_hi, %[v]\n"                                            \
+    "s_add_u32 %[nb], %[nb], 32\n"                                               \
+    "s_add_u32 %[rd], %[rd], 1\n"                                                \
+    "s_mov_b32 %[n0], %[n1s]\n"                                                  \
+    "s_sub_u32 %[t0], %[t0], 4\n"                                                \
+    "s_load_dword %[n1s], %[base], %[t0]\n"                                      \
+    "s_branch LRD" C "_%=\n"                                                     \
+    /* holding_zero: unary count 0, h1 unchanged */                               \
+    "LH" C "_%=:\n"                                                              \
+    "s_mov_b32 %[c1], 0\n"                                                       \
+    "s_mov_b32 %[nh0], 0\n"                                                      \
+    "s_mov_b32 %[nh1], %[h1]\n"                                                  \
+    "s_mov_b32 %[avail], %[nb]\n"                                                \
+    "s_branch LC0" C "_%=\n"                                                     \
+    "LG1" C "_%=:\n"                                                             \
+    "s_cmp_eq_u32 %[ones], 1\n"                                                  \
+    "s_cbranch_scc0 LG2" C "_%=\n"                                               \
+    "s_cmp_lt_i32 " M1 ", 0\n"                                                   \
+    "s_cbranch_scc1 LX_%=\n"                                                     \
+    WV2_W_BOUND(M1, C)                                                           \
+    "s_ashr_i32 %[low], " M0 ", 4\n"                                             \
+    "s_add_u32 %[low], %[low], 1\n"                                              \
+    WV2_W_INC(M0, "128", "7")                                                    \
+    WV2_W_DEC(M1, "62", "5")                                                     \
+    "s_branch LT" C "_%=\n"                                                      \
+    "LG2" C "_%=:\n"                                                             \
+    "s_cmp_lt_i32 " M2 ", 0\n"                                                   \
+    "s_cbranch_scc1 LX_%=\n"                                                     \
+    WV2_W_BOUND(M2, C)                                                           \
+    "s_ashr_i32 %[low], " M0 ", 4\n"                                             \
+    "s_ashr_i32 %[t0], " M1 ", 4\n"                                              \
+    "s_add_u32 %[low], %[low], %[t0]\n"                                          \
+    "s_add_u32 %[low], %[low], 2\n"                                              \
+    WV2_W_INC(M0, "128", "7")                                                    \
+    WV2_W_INC(M1, "64", "6")                                                     \
+    "s_cmp_eq_u32 %[ones], 2\n"                                                  \
+    "s_cbranch_scc0 LG3" C "_%=\n"                                               \
+    WV2_W_DEC(M2, "30", "4")                                                     \
+    "s_branch LT" C "_%=\n"                                                      \
+    "LG3" C "_%=:\n"                                                             \
+    "s_add_u32 %[t0], %[mc], 1\n"                                                \
+    "s_sub_u32 %[u], %[ones], 2\n"                                               \
+    "s_mul_i32 %[t0], %[t0], %[u]\n"                                             \
+    "s_add_u32 %[low], %[low], %[t0]\n"                                          \
+    WV2_W_INC(M2, "32", "5")                                                     \
+    "s_branch LT" C "_%=\n"                                                      \
+    "LN" C "_%=:\n"
+
+// returns true when k reached kend, false when the word at k needs get_word
+template <bool MONO>
+__device__ __forceinline__ bool lossless_run(Entropy &w, SmemReader &rd, uint32_t &k, uint32_t kend, int32_t &resv) {
+    uint32_t reason, t0, u, ones, c1, nh0, nh1, mc, n1, low, avail, ex, v;
+    uint32_t nb = (uint32_t)rd.nb, rdi = rd.rd, n0 = rd.n0, n1s = rd.n1;
+    int32_t m00 = w.med[0][0], m01 = w.med[0][1], m02 = w.med[0][2];
+    int32_t m10 = w.med[1][0], m11 = w.med[1][1], m12 = w.med[1][2];
+    int32_t h0 = w.h0, h1 = w.h1;
+    uint32_t kk = k;
+    uint64_t win = rd.win;
+    if (MONO) {
+        asm volatile(
+            "s_mov_b64 vcc, %[win]\n"
+            "LL_%=:\n"
+            "s_cmp_ge_u32 %[k], %[kend]\n"
+            "s_cbranch_scc1 LD_%=\n"
+            WV2_WORD("a", "%[m00]", "%[m01]", "%[m02]")
+            "s_branch LL_%=\n"
+            "LX_%=:\n"
+            "s_mov_b32 %[reason], 1\n"
+            "s_branch LE_%=\n"
+            "LD_%=:\n"
+            "s_mov_b32 %[reason], 0\n"
+            "LE_%=:\n"
+            "s_waitcnt lgkmcnt(0)\n"
+            "s_mov_b64 %[win], vcc\n"
+            : [reason] "=&s"(reason), [t0] "=&s"(t0), [u] "=&s"(u), [ones] "=&s"(ones), [c1] "=&s"(c1),
+              [nh0] "=&s"(nh0), [nh1] "=&s"(nh1), [mc] "=&s"(mc), [n1] "=&s"(n1), [low] "=&s"(low),
+              [avail] "=&s"(avail), [ex] "=&s"(ex), [v] "=&s"(v), [win] "+s"(win), [nb] "+s"(nb), [rd] "+s"(rdi),
+              [n0] "+s"(n0), [n1s] "+s"(n1s), [m00] "+s"(m00), [m01] "+s"(m01), [m02] "+s"(m02), [m10] "+s"(m10),
+              [h0] "+s"(h0), [h1] "+s"(h1), [k] "+s"(kk), [resv] "+v"(resv)
+            : [kend] "s"(kend), [E] "s"(rd.E), [base] "s"(rd.base)
+            : "vcc", "scc", "m0");
+    } else {
+        asm volatile(
+            "s_mov_b64 vcc, %[win]\n"
+            "LL_%=:\n"
+            "s_cmp_ge_u32 %[k], %[kend]\n"
+            "s_cbranch_scc1 LD_%=\n"
+            WV2_WORD("a", "%[m00]", "%[m01]", "%[m02]")
+            WV2_WORD("b", "%[m10]", "%[m11]", "%[m12]")
+            "s_branch LL_%=\n"
+            "LX_%=:\n"
+            "s_mov_b32 %[reason], 1\n"
+            "s_branch LE_%=\n"
+            "LD_%=:\n"
+            "s_mov_b32 %[reason], 0\n"
+            "LE_%=:\n"
+            "s_waitcnt lgkmcnt(0)\n"
+            "s_mov_b64 %[win], vcc\n"
+            : [reason] "=&s"(reason), [t0] "=&s"(t0), [u] "=&s"(u), [ones] "=&s"(ones), [c1] "=&s"(c1),
+              [nh0] "=&s"(nh0), [nh1] "=&s"(nh1), [mc] "=&s"(mc), [n1] "=&s"(n1), [low] "=&s"(low),
+              [avail] "=&s"(avail), [ex] "=&s"(ex), [v] "=&s"(v), [win] "+s"(win), [nb] "+s"(nb), [rd] "+s"(rdi),
+              [n0] "+s"(n0), [n1s] "+s"(n1s), [m00] "+s"(m00), [m01] "+s"(m01), [m02] "+s"(m02), [m10] "+s"(m10),
+              [m11] "+s"(m11), [m12] "+s"(m12), [h0] "+s"(h0), [h1] "+s"(h1), [k] "+s"(kk), [resv] "+v"(resv)
+            : [kend] "s"(kend), [E] "s"(rd.E), [base] "s"(rd.base)
+            : "vcc", "scc", "m0");
+    }
+    rd.win = win;
+    rd.nb = (int)nb;
+    rd.rd = rdi;
+    rd.n0 = n0;
+    rd.n1 = n1s;
+    w.med[0][0] = m00;
+    w.med[0][1] = m01;
+    w.med[0][2] = m02;
+    w.med[1][0] = m10;
+    w.med[1][1] = m11;
+    w.med[1][2] = m12;
+    w.h0 = h0;
+    w.h1 = h1;
+    k = kk;
+    return reason == 0;
+}
+#undef WV2_W_BOUND
+#undef WV2_W_INC
+#undef WV2_W_DEC
+#undef WV2_WORD
+
 // one residual: the fast path for lossless blocks, the zero-run countdown,
 // else the general get_word (wv_decode_core.h)
 template <int C, bool LOSSLESS>
-__device__ __forceinline__ int parse_word(Entropy &w, LdsReader &rd, uint32_t flags, int32_t &v) {
+__device__ __forceinline__ int parse_word(Entropy &w, Reader &rd, uint32_t flags, int32_t &v) {
     if (LOSSLESS) {
         const uint32_t m00 = (uint32_t)(w.med[0][0] | w.med[1][0]);
         const bool zr = __builtin_expect(m00 <= 1u, 0) && (w.h0 | w.h1) == 0;
@@ -382,7 +709,7 @@ __device__ __forceinline__ int parse_word(Entropy &w, LdsReader &rd, uint32_t fl
 }
 
 template <bool MONO, bool LOSSLESS>
-__device__ __forceinline__ void parse_loop(const BlockDesc &d, LdsReader &rd, Entropy &w, Shared &sh, int lane) {
+__device__ __forceinline__ void parse_loop(const BlockDesc &d, Reader &rd, Entropy &w, Shared &sh, int lane) {
     const uint32_t flags = d.flags;
     const uint32_t total = MONO ? d.nframes : 2u * d.nframes;
     int32_t resv = 0;
@@ -392,23 +719,23 @@ __device__ __forceinline__ void parse_loop(const BlockDesc &d, LdsReader &rd, En
     while (k < total) {
         const uint32_t kend = min(total, (k & ~63u) + 64u);  // next batch boundary
         while (k < kend) {
+            if (LOSSLESS && WV2_EXP != 2 && (MONO || (k & 1) == 0)) {
+                if (lossless_run<MONO>(w, rd, k, kend, resv)) break;
+            }
+            // the word at k (and, in stereo, its pair) through the general path
             int32_t v = 0;
-            int rc = WV2_EXP == 2 ? DEC_OK : parse_word<0, LOSSLESS>(w, rd, flags, v);
+            int rc = DEC_OK;
+            if (MONO || (k & 1) == 0) {
+                rc = WV2_EXP == 2 ? DEC_OK : parse_word<0, LOSSLESS>(w, rd, flags, v);
+            } else {
+                rc = WV2_EXP == 2 ? DEC_OK : parse_word<1, LOSSLESS>(w, rd, flags, v);
+            }
             if (__builtin_expect(rc != DEC_OK, 0)) {
                 err = (uint32_t)rc;
                 break;
             }
             resv = writelane(v, (int)(k & 63), resv);
             k++;
-            if (!MONO) {
-                rc = WV2_EXP == 2 ? DEC_OK : parse_word<1, LOSSLESS>(w, rd, flags, v);
-                if (__builtin_expect(rc != DEC_OK, 0)) {
-                    err = (uint32_t)rc;
-                    break;
-                }
-                resv = writelane(v, (int)(k & 63), resv);
-                k++;
-            }
         }
         if (err) break;
         {
@@ -451,8 +778,8 @@ __device__ __forceinline__ void parse_loop(const BlockDesc &d, LdsReader &rd, En
 
 __device__ __forceinline__ void parser(const BlockDesc &d, const uint8_t *blob, Shared &sh, int lane, int32_t *dbg) {
     WV2_PROF(const uint64_t t_start = clock64();)
-    LdsReader rd;
-    rd.init(blob, d.bits_off, d.bits_len, sh.stream, lane);
+    Reader rd;
+    init_reader(rd, blob, d, sh, lane);
     Entropy w;
 #pragma unroll
     for (int c = 0; c < 2; c++) {
