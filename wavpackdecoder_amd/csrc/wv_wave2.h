@@ -467,14 +467,14 @@ __device__ __forceinline__ bool fast_word(Entropy &w, Reader &rd, int32_t &out) 
 // end; the caller then runs the general get_word for that word.  Leaves no
 // scalar load outstanding.
 // ---------------------------------------------------------------------------
-#define WV2_W_BOUND(MK, SUF)                                  \
+#define WV2_W_BOUND(MK)                                       \
     "s_lshr_b32 %[mc], " MK ", 4\n"                            \
     "s_or_b32 %[t0], %[mc], 1\n"                                \
     "s_flbit_i32_b32 %[t0], %[t0]\n"                            \
     "s_sub_u32 %[n1], 31, %[t0]\n"                              \
     "s_add_u32 %[t0], %[n1], 2\n"                               \
     "s_cmp_gt_u32 %[t0], %[avail]\n"                            \
-    "s_cbranch_scc1 LX_%=\n"
+    "s_cbranch_scc1 LB" C "_%=\n"
 #define WV2_W_INC(M, ADD, SH)                                   \
     "s_add_i32 %[t0], " M ", " ADD "\n"                         \
     "s_ashr_i32 %[t0], %[t0], " SH "\n"                         \
@@ -485,12 +485,39 @@ __device__ __forceinline__ bool fast_word(Entropy &w, Reader &rd, int32_t &out) 
     "s_ashr_i32 %[t0], %[t0], " SH1 "\n"                        \
     "s_and_b32 %[t0], %[t0], -2\n"                              \
     "s_sub_i32 " M ", " M ", %[t0]\n"
-// one word of channel context C (medians M0..M2); falls through to the next word
+// read_code + sign + window advance + residual into lane M0 (WordsUtils.cs:494-503, 546-570)
+#define WV2_TAIL(C, SFX)                                                                 \
+    "s_lshr_b64 vcc, vcc, %[c1]\n"                                               \
+    "s_sub_u32 %[nb], %[nb], %[c1]\n"                                            \
+    "s_lshl_b32 %[ex], 2, %[n1]\n"                                               \
+    "s_not_b32 %[t0], %[mc]\n"                                                   \
+    "s_add_u32 %[ex], %[ex], %[t0]\n"                                            \
+    "s_bfm_b32 %[t0], %[n1], 0\n"                                                \
+    "s_and_b32 %[v], vcc_lo, %[t0]\n"                                            \
+    "s_cmp_lt_u32 %[v], %[ex]\n"                                                 \
+    "s_cbranch_scc1 LS" C SFX "_%=\n"                                            \
+    "s_lshr_b32 %[t0], vcc_lo, %[n1]\n"                                          \
+    "s_and_b32 %[t0], %[t0], 1\n"                                                \
+    "s_lshl_b32 %[v], %[v], 1\n"                                                 \
+    "s_sub_u32 %[v], %[v], %[ex]\n"                                              \
+    "s_add_u32 %[v], %[v], %[t0]\n"                                              \
+    "s_add_u32 %[n1], %[n1], 1\n"                                                \
+    "LS" C SFX "_%=:\n"                                                          \
+    "s_add_u32 %[v], %[v], %[low]\n"                                             \
+    "s_lshr_b32 %[t0], vcc_lo, %[n1]\n"                                          \
+    "s_bfe_i32 %[t0], %[t0], 0x10000\n"                                          \
+    "s_xor_b32 %[v], %[v], %[t0]\n"                                              \
+    "s_add_u32 %[n1], %[n1], 1\n"                                                \
+    "s_lshr_b64 vcc, vcc, %[n1]\n"                                               \
+    "s_sub_u32 %[nb], %[nb], %[n1]\n"                                            \
+    "v_writelane_b32 %[resv], %[v], m0\n"                                        \
+    "s_add_u32 m0, m0, 1\n"
+
+// Hot code of one word of channel context C (medians M0..M2); falls through to
+// the next word.  Register roles: VCC = bit window, M0 = lane of this word in
+// the residual batch, h0/h1 committed early (a bail restores them: h0 was 0
+// on the unary path, 1 on the holding path; h1 = ones - (u >> 1)).
 #define WV2_WORD(C, M0, M1, M2)                                                  \
-    "LW" C "_%=:\n"                                                              \
-    "s_or_b32 %[t0], %[m00], %[m10]\n" /* zero-run mode possible: general path */ \
-    "s_cmp_lt_u32 %[t0], 2\n"                                                    \
-    "s_cbranch_scc1 LX_%=\n"                                                     \
     "s_cmp_lt_u32 %[nb], 32\n"                                                   \
     "s_cbranch_scc1 LR" C "_%=\n"                                                \
     "LRD" C "_%=:\n"                                                             \
@@ -503,49 +530,25 @@ __device__ __forceinline__ bool fast_word(Entropy &w, Reader &rd, int32_t &out) 
     "s_add_u32 %[c1], %[u], 1\n"                                                 \
     "s_lshr_b32 %[ones], %[u], 1\n"                                              \
     "s_add_u32 %[ones], %[ones], %[h1]\n"                                        \
-    "s_and_b32 %[nh1], %[u], 1\n"                                                \
-    "s_xor_b32 %[nh0], %[nh1], 1\n"                                              \
+    "s_and_b32 %[h1], %[u], 1\n"                                                 \
+    "s_xor_b32 %[h0], %[h1], 1\n"                                                \
     "s_sub_u32 %[avail], %[nb], %[c1]\n"                                         \
     "s_cmp_lg_u32 %[ones], 0\n"                                                  \
     "s_cbranch_scc1 LG1" C "_%=\n"                                               \
     "LC0" C "_%=:\n"                                                             \
     "s_cmp_lt_i32 " M0 ", 0\n"                                                   \
-    "s_cbranch_scc1 LX_%=\n"                                                     \
-    WV2_W_BOUND(M0, C)                                                           \
+    "s_cbranch_scc1 LB" C "_%=\n"                                                \
+    WV2_W_BOUND(M0)                                                              \
     "s_mov_b32 %[low], 0\n"                                                      \
     WV2_W_DEC(M0, "126", "6")                                                    \
+    "s_cmp_lt_u32 " M0 ", 2\n" /* zero-run mode may start: finish, then exit */  \
+    "s_cbranch_scc1 LZ" C "_%=\n"                                                \
     "LT" C "_%=:\n"                                                              \
-    "s_mov_b32 %[h0], %[nh0]\n"                                                  \
-    "s_mov_b32 %[h1], %[nh1]\n"                                                  \
-    "s_lshr_b64 vcc, vcc, %[c1]\n"                                               \
-    "s_sub_u32 %[nb], %[nb], %[c1]\n"                                            \
-    "s_lshl_b32 %[ex], 2, %[n1]\n"                                               \
-    "s_not_b32 %[t0], %[mc]\n"                                                   \
-    "s_add_u32 %[ex], %[ex], %[t0]\n"                                            \
-    "s_bfm_b32 %[t0], %[n1], 0\n"                                                \
-    "s_and_b32 %[v], vcc_lo, %[t0]\n"                                            \
-    "s_cmp_lt_u32 %[v], %[ex]\n"                                                 \
-    "s_cbranch_scc1 LS" C "_%=\n"                                                \
-    "s_lshr_b32 %[t0], vcc_lo, %[n1]\n"                                          \
-    "s_and_b32 %[t0], %[t0], 1\n"                                                \
-    "s_lshl_b32 %[v], %[v], 1\n"                                                 \
-    "s_sub_u32 %[v], %[v], %[ex]\n"                                              \
-    "s_add_u32 %[v], %[v], %[t0]\n"                                              \
-    "s_add_u32 %[n1], %[n1], 1\n"                                                \
-    "LS" C "_%=:\n"                                                              \
-    "s_add_u32 %[v], %[v], %[low]\n"                                             \
-    "s_lshr_b32 %[t0], vcc_lo, %[n1]\n"                                          \
-    "s_bfe_i32 %[t0], %[t0], 0x10000\n"                                          \
-    "s_xor_b32 %[v], %[v], %[t0]\n"                                              \
-    "s_add_u32 %[n1], %[n1], 1\n"                                                \
-    "s_lshr_b64 vcc, vcc, %[n1]\n"                                               \
-    "s_sub_u32 %[nb], %[nb], %[n1]\n"                                            \
-    "s_and_b32 %[t0], %[k], 63\n"                                                \
-    "s_mov_b32 m0, %[t0]\n"                                                      \
-    "v_writelane_b32 %[resv], %[v], m0\n"                                        \
-    "s_add_u32 %[k], %[k], 1\n"                                                  \
-    "s_branch LN" C "_%=\n"                                                      \
-    /* out of line: refill from the prefetched dwords */                          \
+    WV2_TAIL(C, "h")
+
+// Cold blocks of that word, placed after the loop.
+#define WV2_WORD_COLD(C, M0, M1, M2, NEXT)                                       \
+    /* refill from the prefetched dwords (or exit near the payload end) */        \
     "LR" C "_%=:\n"                                                              \
     "s_lshl_b32 %[t0], %[rd], 2\n"                                               \
     "s_add_u32 %[t0], %[t0], 12\n"                                               \
@@ -567,16 +570,17 @@ __device__ __forceinline__ bool fast_word(Entropy &w, Reader &rd, int32_t &out) 
     /* holding_zero: unary count 0, h1 unchanged */                               \
     "LH" C "_%=:\n"                                                              \
     "s_mov_b32 %[c1], 0\n"                                                       \
-    "s_mov_b32 %[nh0], 0\n"                                                      \
-    "s_mov_b32 %[nh1], %[h1]\n"                                                  \
+    "s_mov_b32 %[h0], 0\n"                                                       \
+    "s_mov_b32 %[ones], 0\n"                                                     \
+    "s_mov_b32 %[u], 0\n"                                                        \
     "s_mov_b32 %[avail], %[nb]\n"                                                \
     "s_branch LC0" C "_%=\n"                                                     \
     "LG1" C "_%=:\n"                                                             \
     "s_cmp_eq_u32 %[ones], 1\n"                                                  \
     "s_cbranch_scc0 LG2" C "_%=\n"                                               \
     "s_cmp_lt_i32 " M1 ", 0\n"                                                   \
-    "s_cbranch_scc1 LX_%=\n"                                                     \
-    WV2_W_BOUND(M1, C)                                                           \
+    "s_cbranch_scc1 LB" C "_%=\n"                                                \
+    WV2_W_BOUND(M1)                                                              \
     "s_ashr_i32 %[low], " M0 ", 4\n"                                             \
     "s_add_u32 %[low], %[low], 1\n"                                              \
     WV2_W_INC(M0, "128", "7")                                                    \
@@ -584,8 +588,8 @@ __device__ __forceinline__ bool fast_word(Entropy &w, Reader &rd, int32_t &out) 
     "s_branch LT" C "_%=\n"                                                      \
     "LG2" C "_%=:\n"                                                             \
     "s_cmp_lt_i32 " M2 ", 0\n"                                                   \
-    "s_cbranch_scc1 LX_%=\n"                                                     \
-    WV2_W_BOUND(M2, C)                                                           \
+    "s_cbranch_scc1 LB" C "_%=\n"                                                \
+    WV2_W_BOUND(M2)                                                              \
     "s_ashr_i32 %[low], " M0 ", 4\n"                                             \
     "s_ashr_i32 %[t0], " M1 ", 4\n"                                              \
     "s_add_u32 %[low], %[low], %[t0]\n"                                          \
@@ -598,70 +602,103 @@ __device__ __forceinline__ bool fast_word(Entropy &w, Reader &rd, int32_t &out) 
     "s_branch LT" C "_%=\n"                                                      \
     "LG3" C "_%=:\n"                                                             \
     "s_add_u32 %[t0], %[mc], 1\n"                                                \
-    "s_sub_u32 %[u], %[ones], 2\n"                                               \
-    "s_mul_i32 %[t0], %[t0], %[u]\n"                                             \
+    "s_sub_u32 %[v], %[ones], 2\n"                                               \
+    "s_mul_i32 %[t0], %[t0], %[v]\n"                                             \
     "s_add_u32 %[low], %[low], %[t0]\n"                                          \
     WV2_W_INC(M2, "32", "5")                                                     \
     "s_branch LT" C "_%=\n"                                                      \
-    "LN" C "_%=:\n"
+    /* bail before the word commits anything but h0/h1: restore them */         \
+    "LB" C "_%=:\n"                                                              \
+    "s_cmp_eq_u32 %[c1], 0\n"                                                    \
+    "s_cbranch_scc1 LBH" C "_%=\n"                                               \
+    "s_lshr_b32 %[t0], %[u], 1\n"                                                \
+    "s_sub_u32 %[h1], %[ones], %[t0]\n"                                          \
+    "s_mov_b32 %[h0], 0\n"                                                       \
+    "s_branch LX_%=\n"                                                           \
+    "LBH" C "_%=:\n"                                                             \
+    "s_mov_b32 %[h0], 1\n"                                                       \
+    "s_branch LX_%=\n"                                                           \
+    /* this channel's median[0] dropped below 2: finish the word, then exit */  \
+    "LZ" C "_%=:\n"                                                              \
+    WV2_TAIL(C, "z")                                                             \
+    "s_branch LE_%=\n"
 
 // returns true when k reached kend, false when the word at k needs get_word
 template <bool MONO>
 __device__ __forceinline__ bool lossless_run(Entropy &w, SmemReader &rd, uint32_t &k, uint32_t kend, int32_t &resv) {
-    uint32_t reason, t0, u, ones, c1, nh0, nh1, mc, n1, low, avail, ex, v;
+    // zero-run mode possible at the first word: general path
+    if ((uint32_t)(w.med[0][0] | w.med[1][0]) < 2u) return false;
+    uint32_t t0, u, ones, c1, mc, n1, low, avail, ex, v, keep;
     uint32_t nb = (uint32_t)rd.nb, rdi = rd.rd, n0 = rd.n0, n1s = rd.n1;
     int32_t m00 = w.med[0][0], m01 = w.med[0][1], m02 = w.med[0][2];
     int32_t m10 = w.med[1][0], m11 = w.med[1][1], m12 = w.med[1][2];
     int32_t h0 = w.h0, h1 = w.h1;
-    uint32_t kk = k;
+    const uint32_t kbase = k & ~63u;
+    uint32_t lane = k - kbase;             // word index inside the batch (M0 in the loop)
+    const uint32_t lend = kend - kbase;    // <= 64
     uint64_t win = rd.win;
     if (MONO) {
         asm volatile(
+            "s_mov_b32 %[keep], m0\n"
+            "s_mov_b32 m0, %[lane]\n"
             "s_mov_b64 vcc, %[win]\n"
             "LL_%=:\n"
-            "s_cmp_ge_u32 %[k], %[kend]\n"
-            "s_cbranch_scc1 LD_%=\n"
+            "s_cmp_ge_u32 m0, %[lend]\n"
+            "s_cbranch_scc1 LE_%=\n"
+#define C "a"
             WV2_WORD("a", "%[m00]", "%[m01]", "%[m02]")
+#undef C
             "s_branch LL_%=\n"
+#define C "a"
+            WV2_WORD_COLD("a", "%[m00]", "%[m01]", "%[m02]", "")
+#undef C
             "LX_%=:\n"
-            "s_mov_b32 %[reason], 1\n"
-            "s_branch LE_%=\n"
-            "LD_%=:\n"
-            "s_mov_b32 %[reason], 0\n"
             "LE_%=:\n"
             "s_waitcnt lgkmcnt(0)\n"
             "s_mov_b64 %[win], vcc\n"
-            : [reason] "=&s"(reason), [t0] "=&s"(t0), [u] "=&s"(u), [ones] "=&s"(ones), [c1] "=&s"(c1),
-              [nh0] "=&s"(nh0), [nh1] "=&s"(nh1), [mc] "=&s"(mc), [n1] "=&s"(n1), [low] "=&s"(low),
-              [avail] "=&s"(avail), [ex] "=&s"(ex), [v] "=&s"(v), [win] "+s"(win), [nb] "+s"(nb), [rd] "+s"(rdi),
-              [n0] "+s"(n0), [n1s] "+s"(n1s), [m00] "+s"(m00), [m01] "+s"(m01), [m02] "+s"(m02), [m10] "+s"(m10),
-              [h0] "+s"(h0), [h1] "+s"(h1), [k] "+s"(kk), [resv] "+v"(resv)
-            : [kend] "s"(kend), [E] "s"(rd.E), [base] "s"(rd.base)
-            : "vcc", "scc", "m0");
+            "s_mov_b32 %[lane], m0\n"
+            "s_mov_b32 m0, %[keep]\n"
+            : [t0] "=&s"(t0), [u] "=&s"(u), [ones] "=&s"(ones), [c1] "=&s"(c1), [mc] "=&s"(mc), [n1] "=&s"(n1),
+              [low] "=&s"(low), [avail] "=&s"(avail), [ex] "=&s"(ex), [v] "=&s"(v), [keep] "=&s"(keep),
+              [win] "+s"(win), [nb] "+s"(nb), [rd] "+s"(rdi), [n0] "+s"(n0), [n1s] "+s"(n1s), [m00] "+s"(m00),
+              [m01] "+s"(m01), [m02] "+s"(m02), [m10] "+s"(m10), [h0] "+s"(h0), [h1] "+s"(h1), [lane] "+s"(lane),
+              [resv] "+v"(resv)
+            : [lend] "s"(lend), [E] "s"(rd.E), [base] "s"(rd.base)
+            : "vcc", "scc");
     } else {
         asm volatile(
+            "s_mov_b32 %[keep], m0\n"
+            "s_mov_b32 m0, %[lane]\n"
             "s_mov_b64 vcc, %[win]\n"
             "LL_%=:\n"
-            "s_cmp_ge_u32 %[k], %[kend]\n"
-            "s_cbranch_scc1 LD_%=\n"
+            "s_cmp_ge_u32 m0, %[lend]\n"
+            "s_cbranch_scc1 LE_%=\n"
+#define C "a"
             WV2_WORD("a", "%[m00]", "%[m01]", "%[m02]")
+#undef C
+#define C "b"
             WV2_WORD("b", "%[m10]", "%[m11]", "%[m12]")
+#undef C
             "s_branch LL_%=\n"
+#define C "a"
+            WV2_WORD_COLD("a", "%[m00]", "%[m01]", "%[m02]", "")
+#undef C
+#define C "b"
+            WV2_WORD_COLD("b", "%[m10]", "%[m11]", "%[m12]", "")
+#undef C
             "LX_%=:\n"
-            "s_mov_b32 %[reason], 1\n"
-            "s_branch LE_%=\n"
-            "LD_%=:\n"
-            "s_mov_b32 %[reason], 0\n"
             "LE_%=:\n"
             "s_waitcnt lgkmcnt(0)\n"
             "s_mov_b64 %[win], vcc\n"
-            : [reason] "=&s"(reason), [t0] "=&s"(t0), [u] "=&s"(u), [ones] "=&s"(ones), [c1] "=&s"(c1),
-              [nh0] "=&s"(nh0), [nh1] "=&s"(nh1), [mc] "=&s"(mc), [n1] "=&s"(n1), [low] "=&s"(low),
-              [avail] "=&s"(avail), [ex] "=&s"(ex), [v] "=&s"(v), [win] "+s"(win), [nb] "+s"(nb), [rd] "+s"(rdi),
-              [n0] "+s"(n0), [n1s] "+s"(n1s), [m00] "+s"(m00), [m01] "+s"(m01), [m02] "+s"(m02), [m10] "+s"(m10),
-              [m11] "+s"(m11), [m12] "+s"(m12), [h0] "+s"(h0), [h1] "+s"(h1), [k] "+s"(kk), [resv] "+v"(resv)
-            : [kend] "s"(kend), [E] "s"(rd.E), [base] "s"(rd.base)
-            : "vcc", "scc", "m0");
+            "s_mov_b32 %[lane], m0\n"
+            "s_mov_b32 m0, %[keep]\n"
+            : [t0] "=&s"(t0), [u] "=&s"(u), [ones] "=&s"(ones), [c1] "=&s"(c1), [mc] "=&s"(mc), [n1] "=&s"(n1),
+              [low] "=&s"(low), [avail] "=&s"(avail), [ex] "=&s"(ex), [v] "=&s"(v), [keep] "=&s"(keep),
+              [win] "+s"(win), [nb] "+s"(nb), [rd] "+s"(rdi), [n0] "+s"(n0), [n1s] "+s"(n1s), [m00] "+s"(m00),
+              [m01] "+s"(m01), [m02] "+s"(m02), [m10] "+s"(m10), [m11] "+s"(m11), [m12] "+s"(m12), [h0] "+s"(h0),
+              [h1] "+s"(h1), [lane] "+s"(lane), [resv] "+v"(resv)
+            : [lend] "s"(lend), [E] "s"(rd.E), [base] "s"(rd.base)
+            : "vcc", "scc");
     }
     rd.win = win;
     rd.nb = (int)nb;
@@ -676,13 +713,15 @@ __device__ __forceinline__ bool lossless_run(Entropy &w, SmemReader &rd, uint32_
     w.med[1][2] = m12;
     w.h0 = h0;
     w.h1 = h1;
-    k = kk;
-    return reason == 0;
+    k = kbase + lane;
+    return k >= kend;
 }
 #undef WV2_W_BOUND
 #undef WV2_W_INC
 #undef WV2_W_DEC
 #undef WV2_WORD
+#undef WV2_WORD_COLD
+#undef WV2_TAIL
 
 // one residual: the fast path for lossless blocks, the zero-run countdown,
 // else the general get_word (wv_decode_core.h)
