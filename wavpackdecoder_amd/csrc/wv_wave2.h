@@ -40,6 +40,18 @@ constexpr uint32_t SPIN_LIMIT = 1u << 26;  // bounded waits: a bug ends the kern
 #ifndef WV2_EXP
 #define WV2_EXP 0
 #endif
+#ifndef WV2_NARROW
+#define WV2_NARROW 1  // 0: lossless_run only (experiment builds)
+#endif
+// The reconstruction wave keeps the parser's payload ahead of it in the CU's
+// scalar cache: a scalar load per 64-byte line up to WV2_PF_AHEAD bytes past
+// the position the parser last published (0: off, experiment builds).
+#ifndef WV2_PF
+#define WV2_PF 1
+#endif
+#ifndef WV2_PF_AHEAD
+#define WV2_PF_AHEAD 1024u
+#endif
 #if WV2_EXP == 3 || WV2_EXP == 4
 #define WV2_PROF(x) x
 #else
@@ -53,6 +65,7 @@ struct Shared {
     uint32_t consumed;  // words released (recon -> parser)
     uint32_t err;       // parser outcome: 0 running/ok, DEC_BITS_ERROR, DEC_EXCEPTION, 3 timeout
     uint32_t stop;      // recon asks the parser to stop (block muted)
+    uint32_t pos;       // parser's read position (dword index), a prefetch hint
 };
 
 __device__ __forceinline__ uint32_t lds_load_acq(uint32_t *p) {
@@ -723,6 +736,282 @@ __device__ __forceinline__ bool lossless_run(Entropy &w, SmemReader &rd, uint32_
 #undef WV2_WORD_COLD
 #undef WV2_TAIL
 
+// ---------------------------------------------------------------------------
+// Narrow lossless run: the words of lossless_run for a batch whose entropy
+// state bounds every word, so that the per-word tests of lossless_run leave
+// the hot path (WordsUtils.cs:304-503 otherwise unchanged):
+//   * max(med[0][0], med[1][0]) >= 256 at batch start.  median[0] falls by
+//     m -= 2*((m+126)>>7) >= m - (m+126)/64 per word, so after <= 64 words
+//     m + 126 >= (63/64)^64 * 382 > 139: neither zero-run test (:304) can
+//     become true inside the batch -> no zero-run check per word;
+//   * every median < 2^21 (stereo: <= 32 updates per channel) or < 2^19
+//     (mono: <= 64) at batch start.  m += 5*((m+128)>>7) gives
+//     m + 128 <= (133/128)^n (m0 + 128): every median stays in [0, 2^23)
+//     (decrements never cross 0), so maxcode = m >> 4 < 2^19, n1 <= 18, and a
+//     word with <= 7 unary ones (c1 <= 8 bits) needs c1 + n1 + 2 <= 28 bits:
+//     it fits the >= 32 bits the window holds at word start, all in its low
+//     dword -> no negative-median test, no window bound test.  Words with
+//     8..15 unary ones (ones_count >= 4, out of line) test the bound; 16
+//     (the escape, :386) leaves the run.
+// The unary count and the holding_one/holding_zero pairing (:354-428) are
+// branch-free (holding_zero reads no unary bits: u := 0, c1 := 0); ones == 0
+// is inline, ones >= 1 out of line with its own copy of the read_code tail.
+// The window refills from a 64-bit prefetch (s_load_dwordx2, one dword ahead
+// of the window), and the run leaves (state intact) before a prefetch could
+// read past the payload end.  Register roles as in lossless_run: VCC = bit
+// window, M0 = lane of the word in the residual batch.
+// ---------------------------------------------------------------------------
+#define NW_DEC(M, ADD, SH1) /* m -= ((m + ADD) >> (SH1 + 1)) * 2 */ \
+    "s_add_i32 %[t0], " M ", " ADD "\n"                             \
+    "s_ashr_i32 %[t0], %[t0], " SH1 "\n"                            \
+    "s_and_b32 %[t0], %[t0], -2\n"                                  \
+    "s_sub_i32 " M ", " M ", %[t0]\n"
+#define NW_INC(M, ADD, SH) /* m += ((m + ADD) >> SH) * 5 */         \
+    "s_add_i32 %[t0], " M ", " ADD "\n"                             \
+    "s_ashr_i32 %[t0], %[t0], " SH "\n"                             \
+    "s_mul_i32 %[t0], %[t0], 5\n"                                   \
+    "s_add_i32 " M ", " M ", %[t0]\n"
+// read_code(maxcode = mc) + sign + window advance + residual into lane M0
+// (WordsUtils.cs:477-503, 546-570).  z = clz(mc|1), n1 = 31 - z = bitcount-1
+// (mc|1 makes maxcode 0 read no code bits), extras = 2^(n1+1) - 1 - mc.
+#define NW_TAIL(I, S, LOWOP)                                        \
+    "s_or_b32 %[t0], %[mc], 1\n"                                    \
+    "s_flbit_i32_b32 %[z], %[t0]\n"                                 \
+    "s_lshr_b32 %[t], vcc_lo, %[c1]\n"                              \
+    "s_lshr_b32 %[ex], -1, %[z]\n"                                  \
+    "s_sub_u32 %[ex], %[ex], %[mc]\n"                               \
+    "s_lshr_b32 %[t0], 0x7fffffff, %[z]\n"                          \
+    "s_and_b32 %[v], %[t], %[t0]\n"                                 \
+    "s_sub_u32 %[n1], 31, %[z]\n"                                   \
+    "s_cmp_lt_u32 %[v], %[ex]\n"                                    \
+    "s_cbranch_scc1 NS" I S "_%=\n"                                 \
+    "s_lshl_b32 %[v], %[v], 1\n"                                    \
+    "s_sub_u32 %[v], %[v], %[ex]\n"                                 \
+    "s_bitcmp1_b32 %[t], %[n1]\n"                                   \
+    "s_addc_u32 %[v], %[v], 0\n"                                    \
+    "s_add_u32 %[n1], %[n1], 1\n"                                   \
+    "NS" I S "_%=:\n"                                               \
+    LOWOP                                                           \
+    "s_bitcmp1_b32 %[t], %[n1]\n"                                   \
+    "s_cselect_b32 %[t0], -1, 0\n"                                  \
+    "s_xor_b32 %[v], %[v], %[t0]\n"                                 \
+    "s_add_u32 %[n1], %[n1], %[c1]\n"                               \
+    "s_add_u32 %[n1], %[n1], 1\n"                                   \
+    "s_lshr_b64 vcc, vcc, %[n1]\n"                                  \
+    "s_sub_u32 %[nb], %[nb], %[n1]\n"                               \
+    "v_writelane_b32 %[resv], %[v], m0\n"                           \
+    "s_add_u32 m0, m0, 1\n"
+// hot part of word I (channel medians MA): refill test, unary + holding
+// flags, ones == 0 inline; falls through to the next word
+#define NW_WORD(I, MA)                                              \
+    "NW" I "_%=:\n"                                                 \
+    "s_cmp_lt_u32 %[nb], 32\n"                                      \
+    "s_cbranch_scc1 NR" I "_%=\n"                                   \
+    "NA" I "_%=:\n"                                                 \
+    "s_orn2_b32 %[t0], 0x10000, vcc_lo\n"                           \
+    "s_ff1_i32_b32 %[u], %[t0]\n"                                   \
+    "s_cmp_lg_u32 %[h0], 0\n"                                       \
+    "s_cselect_b32 %[u], 0, %[u]\n"                                 \
+    "s_lshr_b32 %[ones], %[u], 1\n"                                 \
+    "s_add_u32 %[ones], %[ones], %[h1]\n"                           \
+    "s_and_b32 %[h1], %[u], 1\n"                                    \
+    "s_add_u32 %[c1], %[u], 1\n"                                    \
+    "s_sub_u32 %[c1], %[c1], %[h0]\n"                               \
+    "s_xor_b32 %[t0], %[h1], 1\n"                                   \
+    "s_sub_u32 %[h0], %[t0], %[h0]\n"                               \
+    "s_cmp_lg_u32 %[ones], 0\n"                                     \
+    "s_cbranch_scc1 NG" I "_%=\n"                                   \
+    "s_lshr_b32 %[mc], " MA ", 4\n"                                 \
+    NW_DEC(MA, "126", "6")                                          \
+    NW_TAIL(I, "a", "")
+// cold parts of word I, placed after the loop; NEXT = label of the next word
+#define NW_COLD(I, NEXT, MA, MB, MC)                                \
+    "NR" I "_%=:\n" /* refill 32 bits, prefetch the next dword */   \
+    "s_cmp_gt_u32 %[off], %[elim]\n"                                \
+    "s_cbranch_scc1 NX_%=\n"                                        \
+    "s_waitcnt lgkmcnt(0)\n"                                        \
+    "s_lshl_b64 %[tq], %[q], %[nb]\n"                               \
+    "s_or_b64 vcc, vcc, %[tq]\n"                                    \
+    "s_add_u32 %[nb], %[nb], 32\n"                                  \
+    "s_load_dwordx2 %[q], %[base], %[off]\n"                        \
+    "s_add_u32 %[off], %[off], 4\n"                                 \
+    "s_branch NA" I "_%=\n"                                         \
+    "NG" I "_%=:\n" /* ones == 1 */                                 \
+    "s_cmp_eq_u32 %[ones], 1\n"                                     \
+    "s_cbranch_scc0 NH" I "_%=\n"                                   \
+    "s_lshr_b32 %[low], " MA ", 4\n"                                \
+    "s_add_u32 %[low], %[low], 1\n"                                 \
+    "s_lshr_b32 %[mc], " MB ", 4\n"                                 \
+    NW_INC(MA, "128", "7")                                          \
+    NW_DEC(MB, "62", "5")                                           \
+    NW_TAIL(I, "b", "s_add_u32 %[v], %[v], %[low]\n")               \
+    "s_branch " NEXT "_%=\n"                                        \
+    "NH" I "_%=:\n" /* ones >= 2 */                                 \
+    "s_lshr_b32 %[mc], " MC ", 4\n"                                 \
+    "s_cmp_gt_u32 %[u], 7\n"                                        \
+    "s_cbranch_scc1 NK" I "_%=\n"                                   \
+    "NJ" I "_%=:\n"                                                 \
+    "s_lshr_b32 %[low], " MA ", 4\n"                                \
+    "s_lshr_b32 %[t0], " MB ", 4\n"                                 \
+    "s_add_u32 %[low], %[low], %[t0]\n"                             \
+    "s_add_u32 %[low], %[low], 2\n"                                 \
+    NW_INC(MA, "128", "7")                                          \
+    NW_INC(MB, "64", "6")                                           \
+    "s_cmp_eq_u32 %[ones], 2\n"                                     \
+    "s_cbranch_scc0 NM" I "_%=\n"                                   \
+    NW_DEC(MC, "30", "4")                                           \
+    NW_TAIL(I, "c", "s_add_u32 %[v], %[v], %[low]\n")               \
+    "s_branch " NEXT "_%=\n"                                        \
+    "NM" I "_%=:\n" /* ones >= 3 */                                 \
+    "s_add_u32 %[t0], %[mc], 1\n"                                   \
+    "s_sub_u32 %[v], %[ones], 2\n"                                  \
+    "s_mul_i32 %[t0], %[t0], %[v]\n"                                \
+    "s_add_u32 %[low], %[low], %[t0]\n"                             \
+    NW_INC(MC, "32", "5")                                           \
+    NW_TAIL(I, "d", "s_add_u32 %[v], %[v], %[low]\n")               \
+    "s_branch " NEXT "_%=\n"                                        \
+    "NK" I "_%=:\n" /* 8..16 unary ones: escape, or test the bound */ \
+    "s_cmp_gt_u32 %[u], 15\n"                                       \
+    "s_cbranch_scc1 NB" I "_%=\n"                                   \
+    "s_or_b32 %[t0], %[mc], 1\n"                                    \
+    "s_flbit_i32_b32 %[t0], %[t0]\n"                                \
+    "s_cmp_lt_u32 %[c1], %[t0]\n" /* c1 + n1 + 2 <= 32 */           \
+    "s_cbranch_scc1 NJ" I "_%=\n"                                   \
+    "NB" I "_%=:\n" /* leave before the word commits: restore h0/h1 */ \
+    "s_lshr_b32 %[t0], %[u], 1\n"                                   \
+    "s_sub_u32 %[h1], %[ones], %[t0]\n"                             \
+    "s_mov_b32 %[h0], 0\n"                                          \
+    "s_branch NX_%=\n"
+
+#define NW_CHECK(L) /* batch end? */                                \
+    L "_%=:\n"                                                      \
+    "s_cmp_ge_u32 m0, %[lend]\n"                                    \
+    "s_cbranch_scc1 NE_%=\n"
+
+// true when the narrow run may start at this batch position (see above)
+template <bool MONO>
+__device__ __forceinline__ bool narrow_ok(const Entropy &w, const SmemReader &rd) {
+    const int32_t mx = max(w.med[0][0], w.med[1][0]);
+    const uint32_t all = (uint32_t)(w.med[0][0] | w.med[0][1] | w.med[0][2] | w.med[1][0] | w.med[1][1] | w.med[1][2]);
+    return mx >= 256 && all < (MONO ? (1u << 19) : (1u << 21)) && rd.E >= 16u;
+}
+
+// returns true when k reached kend, false when the word at k needs get_word
+template <bool MONO>
+__device__ __forceinline__ bool lossless_run_narrow(Entropy &w, SmemReader &rd, uint32_t &k, uint32_t kend,
+                                                    int32_t &resv) {
+    uint32_t t0, t, u, ones, c1, mc, z, n1, low, ex, v, keep;
+    uint64_t tq;
+    uint32_t nb = (uint32_t)rd.nb;
+    uint32_t off = 4u * (rd.rd + 1u);                      // byte offset of the next prefetch
+    uint64_t q = (uint64_t)rd.n0 | ((uint64_t)rd.n1 << 32);  // dwords rd, rd+1
+    const uint32_t elim = rd.E - 8u;
+    int32_t m00 = w.med[0][0], m01 = w.med[0][1], m02 = w.med[0][2];
+    int32_t m10 = w.med[1][0], m11 = w.med[1][1], m12 = w.med[1][2];
+    int32_t h0 = w.h0, h1 = w.h1;
+    const uint32_t kbase = k & ~63u;
+    uint32_t lane = k - kbase;
+    const uint32_t lend = kend - kbase;
+    uint64_t win = rd.win;
+    if (MONO) {
+        asm volatile(
+            "s_mov_b32 %[keep], m0\n"
+            "s_mov_b32 m0, %[lane]\n"
+            "s_mov_b64 vcc, %[win]\n"
+            NW_CHECK("NL")
+            NW_WORD("0", "%[m00]")
+            NW_CHECK("NC0")
+            NW_WORD("1", "%[m00]")
+            NW_CHECK("NC1")
+            NW_WORD("2", "%[m00]")
+            NW_CHECK("NC2")
+            NW_WORD("3", "%[m00]")
+            "NC3_%=:\n"
+            "s_branch NL_%=\n"
+            NW_COLD("0", "NC0", "%[m00]", "%[m01]", "%[m02]")
+            NW_COLD("1", "NC1", "%[m00]", "%[m01]", "%[m02]")
+            NW_COLD("2", "NC2", "%[m00]", "%[m01]", "%[m02]")
+            NW_COLD("3", "NC3", "%[m00]", "%[m01]", "%[m02]")
+            "NX_%=:\n"
+            "NE_%=:\n"
+            "s_waitcnt lgkmcnt(0)\n"
+            "s_mov_b64 %[win], vcc\n"
+            "s_mov_b32 %[lane], m0\n"
+            "s_mov_b32 m0, %[keep]\n"
+            : [t0] "=&s"(t0), [t] "=&s"(t), [u] "=&s"(u), [ones] "=&s"(ones), [c1] "=&s"(c1), [mc] "=&s"(mc),
+              [z] "=&s"(z), [n1] "=&s"(n1), [low] "=&s"(low), [ex] "=&s"(ex), [v] "=&s"(v), [keep] "=&s"(keep),
+              [tq] "=&s"(tq), [win] "+s"(win), [nb] "+s"(nb), [off] "+s"(off), [q] "+s"(q), [m00] "+s"(m00),
+              [m01] "+s"(m01), [m02] "+s"(m02), [h0] "+s"(h0), [h1] "+s"(h1), [lane] "+s"(lane), [resv] "+v"(resv)
+            : [lend] "s"(lend), [elim] "s"(elim), [base] "s"(rd.base)
+            : "vcc", "scc");
+    } else {
+        asm volatile(
+            "s_mov_b32 %[keep], m0\n"
+            "s_mov_b32 m0, %[lane]\n"
+            "s_mov_b64 vcc, %[win]\n"
+            "s_cmp_ge_u32 m0, %[lend]\n"
+            "s_cbranch_scc1 NE_%=\n"
+            "NL_%=:\n"
+            NW_WORD("0", "%[m00]")
+            NW_WORD("1", "%[m10]")
+            NW_CHECK("NC1")
+            NW_WORD("2", "%[m00]")
+            NW_WORD("3", "%[m10]")
+            NW_CHECK("NC3")
+            NW_WORD("4", "%[m00]")
+            NW_WORD("5", "%[m10]")
+            NW_CHECK("NC5")
+            NW_WORD("6", "%[m00]")
+            NW_WORD("7", "%[m10]")
+            "NC7_%=:\n"
+            "s_cmp_lt_u32 m0, %[lend]\n"
+            "s_cbranch_scc1 NL_%=\n"
+            "s_branch NE_%=\n"
+            NW_COLD("0", "NW1", "%[m00]", "%[m01]", "%[m02]")
+            NW_COLD("1", "NC1", "%[m10]", "%[m11]", "%[m12]")
+            NW_COLD("2", "NW3", "%[m00]", "%[m01]", "%[m02]")
+            NW_COLD("3", "NC3", "%[m10]", "%[m11]", "%[m12]")
+            NW_COLD("4", "NW5", "%[m00]", "%[m01]", "%[m02]")
+            NW_COLD("5", "NC5", "%[m10]", "%[m11]", "%[m12]")
+            NW_COLD("6", "NW7", "%[m00]", "%[m01]", "%[m02]")
+            NW_COLD("7", "NC7", "%[m10]", "%[m11]", "%[m12]")
+            "NX_%=:\n"
+            "NE_%=:\n"
+            "s_waitcnt lgkmcnt(0)\n"
+            "s_mov_b64 %[win], vcc\n"
+            "s_mov_b32 %[lane], m0\n"
+            "s_mov_b32 m0, %[keep]\n"
+            : [t0] "=&s"(t0), [t] "=&s"(t), [u] "=&s"(u), [ones] "=&s"(ones), [c1] "=&s"(c1), [mc] "=&s"(mc),
+              [z] "=&s"(z), [n1] "=&s"(n1), [low] "=&s"(low), [ex] "=&s"(ex), [v] "=&s"(v), [keep] "=&s"(keep),
+              [tq] "=&s"(tq), [win] "+s"(win), [nb] "+s"(nb), [off] "+s"(off), [q] "+s"(q), [m00] "+s"(m00),
+              [m01] "+s"(m01), [m02] "+s"(m02), [m10] "+s"(m10), [m11] "+s"(m11), [m12] "+s"(m12), [h0] "+s"(h0),
+              [h1] "+s"(h1), [lane] "+s"(lane), [resv] "+v"(resv)
+            : [lend] "s"(lend), [elim] "s"(elim), [base] "s"(rd.base)
+            : "vcc", "scc");
+    }
+    rd.win = win;
+    rd.nb = (int)nb;
+    rd.rd = off / 4u - 1u;
+    rd.n0 = (uint32_t)q;
+    rd.n1 = (uint32_t)(q >> 32);
+    w.med[0][0] = m00;
+    w.med[0][1] = m01;
+    w.med[0][2] = m02;
+    w.med[1][0] = m10;
+    w.med[1][1] = m11;
+    w.med[1][2] = m12;
+    w.h0 = h0;
+    w.h1 = h1;
+    k = kbase + lane;
+    return k >= kend;
+}
+#undef NW_DEC
+#undef NW_INC
+#undef NW_TAIL
+#undef NW_WORD
+#undef NW_COLD
+#undef NW_CHECK
+
 // one residual: the fast path for lossless blocks, the zero-run countdown,
 // else the general get_word (wv_decode_core.h)
 template <int C, bool LOSSLESS>
@@ -758,8 +1047,25 @@ __device__ __forceinline__ void parse_loop(const BlockDesc &d, Reader &rd, Entro
     while (k < total) {
         const uint32_t kend = min(total, (k & ~63u) + 64u);  // next batch boundary
         while (k < kend) {
+            // inside a zero run (WordsUtils.cs:304-317): the next zeros_acc - 1
+            // words are 0 and change nothing but zeros_acc (slow_level is dead
+            // in lossless blocks) -> a whole stretch of the batch at once
+            if (LOSSLESS && WV2_EXP != 2 && __builtin_expect(w.zeros_acc > 1, 0) &&
+                (uint32_t)(w.med[0][0] | w.med[1][0]) <= 1u && (w.h0 | w.h1) == 0) {
+                const uint32_t n = (uint32_t)min((int64_t)(kend - k), w.zeros_acc - 1);
+                const uint32_t lo = k & 63u;
+                resv = ((uint32_t)lane - lo < n) ? 0 : resv;
+                w.zeros_acc -= n;
+                k += n;
+                WV2_PROF(rd.n_zr += n;)
+                continue;
+            }
             if (LOSSLESS && WV2_EXP != 2 && (MONO || (k & 1) == 0)) {
-                if (lossless_run<MONO>(w, rd, k, kend, resv)) break;
+                if (WV2_NARROW && narrow_ok<MONO>(w, rd)) {
+                    if (lossless_run_narrow<MONO>(w, rd, k, kend, resv)) break;
+                } else if (lossless_run<MONO>(w, rd, k, kend, resv)) {
+                    break;
+                }
             }
             // the word at k (and, in stereo, its pair) through the general path
             int32_t v = 0;
@@ -794,6 +1100,7 @@ __device__ __forceinline__ void parse_loop(const BlockDesc &d, Reader &rd, Entro
             WV2_PROF(rd.t_wait += clock64() - tw0;)
             if (err) break;
             sh.res[(base % RES_RING) + lane] = resv;
+            if (WV2_PF) __hip_atomic_store(&sh.pos, rd.rd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             lds_publish(&sh.produced, k);
             if (uni(lds_load_acq(&sh.stop))) return;
         }
@@ -1130,9 +1437,32 @@ __device__ __forceinline__ void recon_batch(CH &ch, const Fixup &fx, const int32
     }
 }
 
+// Reconstruction-wave side of the payload prefetch: touch every 64-byte line
+// from pf up to WV2_PF_AHEAD bytes past the parser's published position
+// (at most 4 lines per call), so the parser's s_loads hit the CU's scalar
+// cache.  Byte offsets are relative to the dword-aligned payload base and
+// stay <= pf_end (the last whole dword of the payload).
+__device__ __forceinline__ void scalar_prefetch(uint32_t &pf, cdw_ptr base, uint32_t pf_end, Shared &sh) {
+    const uint32_t pos = uni(__hip_atomic_load(&sh.pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) * 4u;
+    uint32_t tgt = pos + WV2_PF_AHEAD;
+    if (tgt > pf_end) tgt = pf_end;
+    if (pf > tgt) return;
+    const uint32_t o0 = pf, o1 = min(pf + 64u, tgt), o2 = min(pf + 128u, tgt), o3 = min(pf + 192u, tgt);
+    uint32_t d0, d1, d2, d3;
+    asm volatile(
+        "s_load_dword %[d0], %[b], %[o0]\n"
+        "s_load_dword %[d1], %[b], %[o1]\n"
+        "s_load_dword %[d2], %[b], %[o2]\n"
+        "s_load_dword %[d3], %[b], %[o3]\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        : [d0] "=&s"(d0), [d1] "=&s"(d1), [d2] "=&s"(d2), [d3] "=&s"(d3)
+        : [b] "s"(base), [o0] "s"(o0), [o1] "s"(o1), [o2] "s"(o2), [o3] "s"(o3));
+    pf = (o3 + 64u) & ~63u;
+}
+
 // LAYOUT 0: stereo; 1: mono (MONO_FLAG); 2: FALSE_STEREO (mono decode, 2 ints/frame)
 template <int LAYOUT, int... Ts>
-__device__ __forceinline__ void recon_impl(const BlockDesc &d, Shared &sh, int32_t *out_base, uint32_t *status_out,
+__device__ __forceinline__ void recon_impl(const BlockDesc &d, const uint8_t *blob, Shared &sh, int32_t *out_base, uint32_t *status_out,
                                            int lane) {
     using namespace wvf;
     constexpr bool MONO = LAYOUT != 0;  // mono decode path (MONO_DATA)
@@ -1163,6 +1493,10 @@ __device__ __forceinline__ void recon_impl(const BlockDesc &d, Shared &sh, int32
     sm.bsp = d.first_bsp;
     sm.crc_stop = false;
     uint32_t produced = 0;
+    // scalar-cache prefetch of the parser's payload (SmemReader layout: dword-aligned base)
+    const cdw_ptr pf_base = (cdw_ptr)(blob + (d.bits_off & ~(uint64_t)3));
+    const uint32_t pf_end = d.bits_len + (uint32_t)(d.bits_off & 3) >= 4u ? d.bits_len + (uint32_t)(d.bits_off & 3) - 4u : 0u;
+    uint32_t pf = 0;
     WV2_PROF(const uint64_t r_start = clock64(); uint64_t r_wait = 0;)
 
     for (uint32_t t0 = 0; t0 < nfr; t0 += BF) {
@@ -1186,6 +1520,7 @@ __device__ __forceinline__ void recon_impl(const BlockDesc &d, Shared &sh, int32
             }
         }
         WV2_PROF(r_wait += clock64() - rw0;)
+        if (WV2_PF) scalar_prefetch(pf, pf_base, pf_end, sh);
         if (perr == DEC_EXCEPTION || perr == 3) {
             status |= ST_EXCEPTION;
             lds_store_rel(&sh.stop, 1);
@@ -1252,14 +1587,14 @@ __device__ __forceinline__ void recon_impl(const BlockDesc &d, Shared &sh, int32
 }
 
 template <int... Ts>
-__device__ __forceinline__ void recon(const BlockDesc &d, Shared &sh, int32_t *out, uint32_t *status_out, int lane) {
+__device__ __forceinline__ void recon(const BlockDesc &d, const uint8_t *blob, Shared &sh, int32_t *out, uint32_t *status_out, int lane) {
     const uint32_t f = d.flags;
     if (f & wvf::FALSE_STEREO)
-        recon_impl<2, Ts...>(d, sh, out, status_out, lane);
+        recon_impl<2, Ts...>(d, blob, sh, out, status_out, lane);
     else if (f & wvf::MONO_FLAG)
-        recon_impl<1, Ts...>(d, sh, out, status_out, lane);
+        recon_impl<1, Ts...>(d, blob, sh, out, status_out, lane);
     else
-        recon_impl<0, Ts...>(d, sh, out, status_out, lane);
+        recon_impl<0, Ts...>(d, blob, sh, out, status_out, lane);
 }
 
 template <int... Ts>
@@ -1274,12 +1609,31 @@ __device__ __forceinline__ void block_2wave(const BlockDesc *descs, const uint32
         sh.consumed = 0;
         sh.err = 0;
         sh.stop = 0;
+        sh.pos = 0;
     }
     __syncthreads();
+#if WV2_EXP == 5
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    const uint64_t t_beg = __builtin_amdgcn_s_memrealtime();
+#endif
     if (wave == 0)
         parser(d, blob, sh, lane, out + d.out_off);
     else
-        recon<Ts...>(d, sh, out, &status[bi], lane);
+        recon<Ts...>(d, blob, sh, out, &status[bi], lane);
+#if WV2_EXP == 5
+    // placement + timeline probe: ints 12-15 (parser) / 16-19 (recon) of the block's output
+    const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+    __syncthreads();
+    if (lane == 0) {
+        int32_t *o = out + d.out_off + 12 + wave * 4;
+        o[0] = (int32_t)hw;
+        o[1] = (int32_t)xcc;
+        o[2] = (int32_t)(uint32_t)t_beg;
+        o[3] = (int32_t)(uint32_t)t_end;
+    }
+#endif
 }
 
 }  // namespace w2
