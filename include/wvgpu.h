@@ -136,6 +136,23 @@ int wvg_probe_file(const uint8_t *file, size_t len, uint32_t open_flags, int chu
 int wvg_format_samples(const int32_t *src, int64_t samcnt, int bps, uint8_t *pcm, int64_t pcm_len, int offset,
                        int dsd);
 
+/* WavpackFormatSamples over a decoded batch, on the device (epilogue kernel on
+ * `stream` after wvg_batch_decode): every file's int32 output becomes its
+ * little-endian PCM image at info.bytes_per_sample, 1-byte samples +128 unless
+ * `dsd` (the reference's dsd argument; WvDemo.cs:125 passes false).  The image
+ * stays in HBM; file i starts at byte wvg_batch_pcm_offset(b, i). */
+int wvg_batch_format(wvg_batch *b, int dsd, void *stream);
+int64_t wvg_batch_pcm_bytes(const wvg_batch *b);
+int64_t wvg_batch_pcm_offset(const wvg_batch *b, int file);  /* -1: the file did not open */
+uint8_t *wvg_batch_device_pcm(wvg_batch *b);                 /* device pointer to the PCM image */
+int wvg_batch_download_pcm(wvg_batch *b, uint8_t *host, int64_t cap);
+
+/* WvDemo.Main (WvDemo.cs:15-168) for one file of a formatted batch built with
+ * chunk_frames 4096: the .wav bytes it writes (stored RIFF header or the
+ * synthesized RIFF/fmt/data headers, the PCM, the stored trailer) and its exit
+ * code.  out == NULL queries the length only. */
+int wvg_batch_wav(wvg_batch *b, int file, uint8_t *out, int64_t cap, int64_t *wav_len, int32_t *exit_code);
+
 #ifdef __cplusplus
 }
 #endif

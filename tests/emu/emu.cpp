@@ -17,19 +17,6 @@ struct HostStore {
     int32_t *out;
     uint64_t base;
     void put(uint64_t i, int32_t v) { out[base + i] = v; }
-
-// FileInfo fields of the host framing, for the WavpackGet* getters' tests.
-int emu_file_info(const uint8_t *file, size_t len, int64_t *vals, int nvals) {
-    FramingOutput fo;
-    FileInfo info;
-    frame_file(file, len, 0, 0, 0, 4096, fo, info);
-    int64_t v[] = {info.open_ok, info.total_samples, info.sample_rate, info.num_channels, info.bits_per_sample,
-                   info.bytes_per_sample, info.reduced_channels, info.mode, info.version, info.is_float,
-                   info.out_frames, info.out_nch, (int64_t)fo.descs.size(), (int64_t)info.dsd_multiplier};
-    int n = (int)(sizeof(v) / sizeof(v[0]));
-    for (int i = 0; i < n && i < nvals; i++) vals[i] = v[i];
-    return n;
-}
 };
 
 extern "C" {

@@ -111,6 +111,66 @@ def test_golden_fixtures(gpu_batch_cls):
         assert hashlib.sha256(got.astype("<i4").tobytes()).hexdigest() == m["sha256_int32le"], name
 
 
+def _oracle_format(ints, bps, dsd):
+    import ctypes
+    L = O.lib()
+    L.wvo_format_samples.restype = ctypes.c_int
+    L.wvo_format_samples.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64,
+                                     ctypes.c_int, ctypes.c_int]
+    src = np.ascontiguousarray(ints, dtype=np.int32)
+    buf = np.zeros(max(src.size * bps, 1), dtype=np.uint8)
+    assert L.wvo_format_samples(src.ctypes.data, src.size, bps, buf.ctypes.data, buf.size, 0, dsd) == 1
+    return buf[: src.size * bps]
+
+
+@pytest.mark.parametrize("dsd", [0, 1])
+def test_format_epilogue_matches_oracle(gpu_batch_cls, dsd):
+    """The device WavpackFormatSamples epilogue (WavPackUtils.cs:288-341) over a whole
+    batch equals the oracle's restatement applied to the same int32 output, for every
+    mode (1/2/3/4 bytes per sample) and both values of the dsd argument."""
+    cases = V.pcm_cases() + V.dsd_cases()
+    b = gpu_batch_cls(4096)
+    idx = [b.add_file(d) for _, d, _ in cases]
+    b.decode()
+    b.format(dsd=bool(dsd))
+    pcm = b.download_pcm()
+    out = b.download()
+    offs = [b.pcm_offset(i) for i in idx]
+    infos = list(b.infos)
+    b.close()
+    seen = set()
+    for (name, _, _), off, info in zip(cases, offs, infos):
+        n = info.out_frames * info.reduced_channels
+        bps = info.bytes_per_sample
+        seen.add(bps)
+        ints = out[info.out_offset: info.out_offset + n]
+        np.testing.assert_array_equal(pcm[off: off + n * bps], _oracle_format(ints, bps, dsd), err_msg=name)
+    assert seen == {1, 2, 3, 4}
+
+
+def test_wvdemo_wav_matches_oracle():
+    """WvDemo.Main (WvDemo.cs:15-168) through the GPU path: the same .wav bytes and exit
+    code as the oracle's WvDemo, for every mode, config 1 (20 s, stored RIFF header,
+    long enough to pass the loop_samples quirk), short files (the DivideByZero exit
+    after the first call) and corrupted streams (CRC errors, C# exceptions)."""
+    from synth import corpora
+    from synth import wvsynth as S
+    from wavpackdecoder_amd.api import wv_demo
+    files = [(n, d) for n, d, c in V.pcm_cases() + V.dsd_cases() if c == 4096]
+    files.append(("config1", corpora.c1()[1]))
+    x = S.audio_like(450000, 2, 16, seed=21)
+    files.append(("synth_wav_hdr", S.encode_pcm(x, S.EncParams(terms=S.TERMS_FAST, block_samples=44100))))
+    base = S.encode_pcm(S.audio_like(20000, 2, 16, seed=11), S.EncParams(terms=S.TERMS_DEFAULT, block_samples=4000))
+    files += [(f"corrupt#{k}", V.corrupt(base, k)) for k in range(10)]
+    files += [("empty", b""), ("not_wavpack", b"RIFF" + b"\0" * 60)]
+    for name, data in files:
+        rc_ref, wav_ref = O.demo(data)
+        rc, wav = wv_demo(data)
+        assert rc == rc_ref, name
+        assert len(wav) == len(wav_ref), name
+        assert wav == wav_ref, name
+
+
 def test_edge_inputs(gpu_batch_cls):
     """Empty and non-WavPack inputs open with an error (WavPackUtils.cs:36-120); a batch that
     mixes them with a real file still decodes the real one; ragged block sizes and a 1-frame

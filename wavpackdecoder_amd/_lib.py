@@ -88,6 +88,12 @@ def lib():
                                   ctypes.POINTER(WvgFileResult)]),
         "wvg_probe_file": (i32, [ctypes.c_char_p, ctypes.c_size_t, u32, i32, ctypes.POINTER(WvgFileInfo)]),
         "wvg_format_samples": (i32, [vp, i64, i32, vp, i64, i32, i32]),
+        "wvg_batch_format": (i32, [vp, i32, vp]),
+        "wvg_batch_pcm_bytes": (i64, [vp]),
+        "wvg_batch_pcm_offset": (i64, [vp, i32]),
+        "wvg_batch_device_pcm": (vp, [vp]),
+        "wvg_batch_download_pcm": (i32, [vp, vp, i64]),
+        "wvg_batch_wav": (i32, [vp, i32, vp, i64, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -101,4 +107,5 @@ EXPORTED = ("wvg_open", "wvg_close", "wvg_last_error", "wvg_batch_new", "wvg_bat
             "wvg_batch_upload", "wvg_batch_decode", "wvg_batch_sync", "wvg_batch_out_ints", "wvg_batch_device_out",
             "wvg_batch_num_blocks", "wvg_batch_bytes_in", "wvg_batch_frames", "wvg_batch_download",
             "wvg_batch_file_result", "wvg_batch_block_status", "wvg_batch_time", "wvg_decode_file",
-            "wvg_probe_file", "wvg_format_samples")
+            "wvg_probe_file", "wvg_format_samples", "wvg_batch_format", "wvg_batch_pcm_bytes", "wvg_batch_pcm_offset",
+            "wvg_batch_device_pcm", "wvg_batch_download_pcm", "wvg_batch_wav")

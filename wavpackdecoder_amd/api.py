@@ -116,6 +116,27 @@ class DecodeBatch:
             raise RuntimeError("block status unavailable (download first)")
         return st[:k]
 
+    def format(self, dsd: bool = False, stream=None):
+        """WavpackFormatSamples (WavPackUtils.cs:288-341) over the decoded batch, on the device."""
+        self._check(self._L.wvg_batch_format(self._b, int(bool(dsd)), stream))
+
+    def pcm_offset(self, i: int) -> int:
+        return int(self._L.wvg_batch_pcm_offset(self._b, int(i)))
+
+    def download_pcm(self) -> np.ndarray:
+        n = int(self._L.wvg_batch_pcm_bytes(self._b))
+        out = np.empty(max(n, 1), dtype=np.uint8)
+        self._check(self._L.wvg_batch_download_pcm(self._b, out.ctypes.data, out.size))
+        return out[:n]
+
+    def wav(self, i: int):
+        """WvDemo.Main for file i (WvDemo.cs:15-168): (exit_code, .wav bytes)."""
+        n, rc = ctypes.c_int64(), ctypes.c_int32()
+        self._check(self._L.wvg_batch_wav(self._b, int(i), None, 0, ctypes.byref(n), ctypes.byref(rc)))
+        buf = np.empty(max(n.value, 1), dtype=np.uint8)
+        self._check(self._L.wvg_batch_wav(self._b, int(i), buf.ctypes.data, buf.size, ctypes.byref(n), ctypes.byref(rc)))
+        return int(rc.value), buf[: n.value].tobytes()
+
     def result(self, i: int) -> _L.WvgFileResult:
         r = _L.WvgFileResult()
         self._check(self._L.wvg_batch_file_result(self._b, int(i), ctypes.byref(r)))
@@ -203,6 +224,24 @@ def WavpackFormatSamples(src: np.ndarray, samcnt: int, bps: int, pcm_buffer: byt
     view = (ctypes.c_uint8 * len(pcm_buffer)).from_buffer(pcm_buffer)
     return bool(L.wvg_format_samples(s.ctypes.data, int(samcnt), int(bps), ctypes.addressof(view), len(pcm_buffer),
                                      int(offset), int(bool(dsd))))
+
+
+def wv_demo(data: bytes):
+    """WvDemo.Main (WvDemo.cs:15-168) on the GPU path: (exit_code, .wav bytes).
+
+    Decode (WavpackUnpackSamples calls of SAMPLE_BUFFER_SIZE frames), the
+    WavpackFormatSamples epilogue on the device, then the header / PCM /
+    trailer layout WvDemo writes."""
+    b = DecodeBatch(SAMPLE_BUFFER_SIZE)
+    try:
+        idx = b.add_file(bytes(data))
+        if idx < 0:
+            return 1, b""
+        b.decode()
+        b.format(dsd=False)
+        return b.wav(idx)
+    finally:
+        b.close()
 
 
 def WavpackGetNumSamples(wpc, native: bool = False) -> int:

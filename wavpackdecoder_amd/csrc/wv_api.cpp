@@ -14,11 +14,13 @@
 namespace wvg {
 hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint32_t n_pcm, const uint32_t *dsd_list,
                          uint32_t n_dsd, const uint8_t *blob, const uint8_t *tables, int32_t *ptables, int32_t *out,
-                         uint32_t *status, uint32_t *mute_chunk, hipStream_t s);
+                         uint32_t *status, uint32_t *aux, hipStream_t s);
 int term_set_of(const BlockDesc &d);
 hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, uint32_t n, const uint8_t *blob,
-                        int32_t *out, uint32_t *status, hipStream_t s);
+                        int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s);
+hipError_t launch_format(const FormatSeg *segs, uint32_t nseg, const int32_t *in, uint8_t *out, int dsd, hipStream_t s);
 constexpr int kMaxTermSets = 8;
+constexpr uint32_t kFormatSeg = 65536;  // values per format work item
 }
 
 using namespace wvg;
@@ -41,14 +43,19 @@ struct wvg_batch {
     std::vector<uint32_t> ts_list[kMaxTermSets];        // two-wave kernels per term set
     uint32_t *d_ts[kMaxTermSets] = {nullptr};
     int force_lane = 0;                                 // WVG_FORCE_LANE=1: everything on the lane kernel
-    std::vector<uint32_t> h_status;
+    std::vector<uint32_t> h_status, h_aux;
     int64_t bytes_in = 0, frames = 0;
+    // format epilogue: per-file byte image of WavpackFormatSamples
+    std::vector<int64_t> pcm_off;                       // per file, -1 when it did not open
+    int64_t pcm_bytes = 0;
+    std::vector<FormatSeg> segs;
     // device
-    uint8_t *d_blob = nullptr, *d_tables = nullptr;
+    uint8_t *d_blob = nullptr, *d_tables = nullptr, *d_pcm = nullptr;
     BlockDesc *d_descs = nullptr;
+    FormatSeg *d_segs = nullptr;
     int32_t *d_out = nullptr, *d_ptables = nullptr;
-    uint32_t *d_status = nullptr, *d_mute = nullptr, *d_pcm = nullptr, *d_dsd = nullptr;
-    bool uploaded = false, downloaded = false;
+    uint32_t *d_status = nullptr, *d_mute = nullptr, *d_pcml = nullptr, *d_dsd = nullptr;
+    bool uploaded = false, downloaded = false, formatted = false;
 };
 
 static int hip_fail(wvg_ctx *c, hipError_t e, const char *what) {
@@ -104,22 +111,25 @@ wvg_batch *wvg_batch_new(wvg_ctx *c, int chunk_frames) {
 static void free_dev(wvg_batch *b) {
     hipFree(b->d_blob);
     hipFree(b->d_tables);
+    hipFree(b->d_pcm);
     hipFree(b->d_descs);
+    hipFree(b->d_segs);
     hipFree(b->d_out);
     hipFree(b->d_ptables);
     hipFree(b->d_status);
     hipFree(b->d_mute);
-    hipFree(b->d_pcm);
+    hipFree(b->d_pcml);
     hipFree(b->d_dsd);
     for (int t = 0; t < kMaxTermSets; t++) {
         hipFree(b->d_ts[t]);
         b->d_ts[t] = nullptr;
     }
-    b->d_blob = b->d_tables = nullptr;
+    b->d_blob = b->d_tables = b->d_pcm = nullptr;
     b->d_descs = nullptr;
+    b->d_segs = nullptr;
     b->d_out = b->d_ptables = nullptr;
-    b->d_status = b->d_mute = b->d_pcm = b->d_dsd = nullptr;
-    b->uploaded = false;
+    b->d_status = b->d_mute = b->d_pcml = b->d_dsd = nullptr;
+    b->uploaded = b->formatted = false;
 }
 
 void wvg_batch_free(wvg_batch *b) {
@@ -178,8 +188,24 @@ int wvg_batch_add_file(wvg_batch *b, const uint8_t *file, size_t len, uint32_t o
     b->finfo.push_back(fi);
     b->infos.push_back(wi);
     if (info) *info = wi;
-    if (!fi.open_ok) return WVG_ERR_OPEN;
-    b->out_ints += fi.out_frames * fi.out_nch;
+    if (!fi.open_ok) {
+        b->pcm_off.push_back(-1);
+        return WVG_ERR_OPEN;
+    }
+    // the file's WavpackFormatSamples image: frames x reduced channels x bytes per sample, 16-B aligned
+    const int64_t nvals = fi.out_frames * fi.out_nch;
+    b->pcm_bytes = (b->pcm_bytes + 15) & ~(int64_t)15;
+    b->pcm_off.push_back(b->pcm_bytes);
+    for (int64_t s = 0; s < nvals; s += kFormatSeg) {
+        FormatSeg g;
+        g.in_off = (uint64_t)(b->out_ints + s);
+        g.out_off = (uint64_t)(b->pcm_bytes + s * wi.bytes_per_sample);
+        g.n = (uint32_t)(nvals - s < (int64_t)kFormatSeg ? nvals - s : kFormatSeg);
+        g.bps = (uint32_t)wi.bytes_per_sample;
+        b->segs.push_back(g);
+    }
+    b->pcm_bytes += nvals * wi.bytes_per_sample;
+    b->out_ints += nvals;
     for (int64_t k = fi.first_desc; k < fi.first_desc + fi.num_desc; k++) {
         const BlockDesc &d = b->fo.descs[(size_t)k];
         int ts = (d.kind == KIND_PCM && !b->force_lane) ? term_set_of(d) : -1;
@@ -219,9 +245,9 @@ int wvg_batch_upload(wvg_batch *b) {
     HIPCHK(c, hipMemcpyAsync(b->d_status, st.data(), sizeof(uint32_t) * st.size(), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemsetAsync(b->d_mute, 0, sizeof(uint32_t) * (nd ? nd : 1), c->stream));
     size_t np = b->pcm_list.size(), ns = b->dsd_list.size();
-    HIPCHK(c, hipMalloc(&b->d_pcm, sizeof(uint32_t) * (np ? np : 1)));
+    HIPCHK(c, hipMalloc(&b->d_pcml, sizeof(uint32_t) * (np ? np : 1)));
     HIPCHK(c, hipMalloc(&b->d_dsd, sizeof(uint32_t) * (ns ? ns : 1)));
-    if (np) HIPCHK(c, hipMemcpyAsync(b->d_pcm, b->pcm_list.data(), sizeof(uint32_t) * np, hipMemcpyHostToDevice, c->stream));
+    if (np) HIPCHK(c, hipMemcpyAsync(b->d_pcml, b->pcm_list.data(), sizeof(uint32_t) * np, hipMemcpyHostToDevice, c->stream));
     if (ns) HIPCHK(c, hipMemcpyAsync(b->d_dsd, b->dsd_list.data(), sizeof(uint32_t) * ns, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMalloc(&b->d_ptables, sizeof(int32_t) * 256 * (ns ? ns : 1)));
     for (int t = 0; t < kMaxTermSets; t++) {
@@ -243,10 +269,11 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
     for (int t = 0; t < kMaxTermSets; t++)
         if (!b->ts_list[t].empty())
             HIPCHK(c, launch_2wave(t, b->d_descs, b->d_ts[t], (uint32_t)b->ts_list[t].size(), b->d_blob, b->d_out,
-                                   b->d_status, s));
-    HIPCHK(c, launch_decode(b->d_descs, b->d_pcm, (uint32_t)b->pcm_list.size(), b->d_dsd, (uint32_t)b->dsd_list.size(),
+                                   b->d_status, b->d_mute, s));
+    HIPCHK(c, launch_decode(b->d_descs, b->d_pcml, (uint32_t)b->pcm_list.size(), b->d_dsd, (uint32_t)b->dsd_list.size(),
                             b->d_blob, b->d_tables, b->d_ptables, b->d_out, b->d_status, b->d_mute, s));
     b->downloaded = false;
+    b->formatted = false;
     return WVG_OK;
 }
 
@@ -263,6 +290,19 @@ int64_t wvg_batch_num_blocks(const wvg_batch *b) { return b ? (int64_t)b->fo.des
 int64_t wvg_batch_bytes_in(const wvg_batch *b) { return b ? b->bytes_in : 0; }
 int64_t wvg_batch_frames(const wvg_batch *b) { return b ? b->frames : 0; }
 
+static int download_status(wvg_batch *b) {
+    wvg_ctx *c = b->ctx;
+    size_t nd = b->fo.descs.size();
+    b->h_status.assign(nd, 0);
+    b->h_aux.assign(nd, 0);
+    if (nd) {
+        HIPCHK(c, hipMemcpy(b->h_status.data(), b->d_status, sizeof(uint32_t) * nd, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(b->h_aux.data(), b->d_mute, sizeof(uint32_t) * nd, hipMemcpyDeviceToHost));
+    }
+    b->downloaded = true;
+    return WVG_OK;
+}
+
 int wvg_batch_download(wvg_batch *b, int32_t *host_out, int64_t cap_ints) {
     if (!b || !b->uploaded) return WVG_ERR_ARG;
     wvg_ctx *c = b->ctx;
@@ -272,11 +312,7 @@ int wvg_batch_download(wvg_batch *b, int32_t *host_out, int64_t cap_ints) {
         if (b->out_ints)
             HIPCHK(c, hipMemcpy(host_out, b->d_out, sizeof(int32_t) * (size_t)b->out_ints, hipMemcpyDeviceToHost));
     }
-    size_t nd = b->fo.descs.size();
-    b->h_status.assign(nd, 0);
-    if (nd) HIPCHK(c, hipMemcpy(b->h_status.data(), b->d_status, sizeof(uint32_t) * nd, hipMemcpyDeviceToHost));
-    b->downloaded = true;
-    return WVG_OK;
+    return download_status(b);
 }
 
 int wvg_batch_block_status(wvg_batch *b, uint32_t *out, int64_t cap) {
@@ -285,6 +321,13 @@ int wvg_batch_block_status(wvg_batch *b, uint32_t *out, int64_t cap) {
     if (cap < n) return WVG_ERR_SPACE;
     if (n) memcpy(out, b->h_status.data(), sizeof(uint32_t) * (size_t)n);
     return (int)n;
+}
+
+// the file's first block that raised the reference's exception (-1: none)
+static int64_t first_exception_block(const wvg_batch *b, const FileInfo &fi) {
+    for (int64_t k = fi.first_desc; k < fi.first_desc + fi.num_desc; k++)
+        if (b->h_status[(size_t)k] & ST_EXCEPTION) return k;
+    return -1;
 }
 
 int wvg_batch_file_result(wvg_batch *b, int file, wvg_file_result *res) {
@@ -391,6 +434,144 @@ int wvg_format_samples(const int32_t *src, int64_t samcnt, int bps, uint8_t *pcm
         break;
     }
     return 1;
+}
+
+// ---------------------------------------------------------------------------
+// WavpackFormatSamples epilogue + the WvDemo .wav image
+// ---------------------------------------------------------------------------
+int wvg_batch_format(wvg_batch *b, int dsd, void *stream) {
+    if (!b || !b->uploaded) return WVG_ERR_ARG;
+    wvg_ctx *c = b->ctx;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    if (!b->d_pcm) {
+        HIPCHK(c, hipMalloc(&b->d_pcm, (size_t)(b->pcm_bytes ? b->pcm_bytes : 1)));
+        HIPCHK(c, hipMemsetAsync(b->d_pcm, 0, (size_t)(b->pcm_bytes ? b->pcm_bytes : 1), s));
+        HIPCHK(c, hipMalloc(&b->d_segs, sizeof(FormatSeg) * (b->segs.empty() ? 1 : b->segs.size())));
+        if (!b->segs.empty())
+            HIPCHK(c, hipMemcpyAsync(b->d_segs, b->segs.data(), sizeof(FormatSeg) * b->segs.size(),
+                                     hipMemcpyHostToDevice, s));
+    }
+    HIPCHK(c, launch_format(b->d_segs, (uint32_t)b->segs.size(), b->d_out, b->d_pcm, dsd ? 1 : 0, s));
+    b->formatted = true;
+    return WVG_OK;
+}
+
+int64_t wvg_batch_pcm_bytes(const wvg_batch *b) { return b ? b->pcm_bytes : 0; }
+
+int64_t wvg_batch_pcm_offset(const wvg_batch *b, int file) {
+    if (!b || file < 0 || file >= (int)b->pcm_off.size()) return WVG_ERR_ARG;
+    return b->pcm_off[(size_t)file];
+}
+
+uint8_t *wvg_batch_device_pcm(wvg_batch *b) { return b ? b->d_pcm : nullptr; }
+
+int wvg_batch_download_pcm(wvg_batch *b, uint8_t *host, int64_t cap) {
+    if (!b || !b->formatted || (!host && b->pcm_bytes)) return WVG_ERR_ARG;
+    if (cap < b->pcm_bytes) return WVG_ERR_SPACE;
+    wvg_ctx *c = b->ctx;
+    HIPCHK(c, hipDeviceSynchronize());
+    if (b->pcm_bytes) HIPCHK(c, hipMemcpy(host, b->d_pcm, (size_t)b->pcm_bytes, hipMemcpyDeviceToHost));
+    return WVG_OK;
+}
+
+static void put_le32(uint8_t *p, uint32_t v) {
+    p[0] = (uint8_t)v;
+    p[1] = (uint8_t)(v >> 8);
+    p[2] = (uint8_t)(v >> 16);
+    p[3] = (uint8_t)(v >> 24);
+}
+
+// WvDemo.Main (WvDemo.cs:15-168) for file `file` of a formatted batch whose
+// chunk is the demo's 4096 (Defines.SAMPLE_BUFFER_SIZE): the bytes it writes
+// to the .wav and its exit code.
+int wvg_batch_wav(wvg_batch *b, int file, uint8_t *out, int64_t cap, int64_t *wav_len, int32_t *exit_code) {
+    if (!b || !b->formatted || file < 0 || file >= (int)b->finfo.size() || !wav_len || !exit_code) return WVG_ERR_ARG;
+    wvg_ctx *c = b->ctx;
+    const FileInfo &fi = b->finfo[(size_t)file];
+    const wvg_file_info &wi = b->infos[(size_t)file];
+    *wav_len = 0;
+    *exit_code = 1;
+    if (!fi.open_ok) return WVG_OK;  // WvDemo.cs:41-46: error message, no .wav
+    HIPCHK(c, hipDeviceSynchronize());
+    if (!b->downloaded) {
+        int rc = download_status(b);
+        if (rc) return rc;
+    }
+    wvg_file_result r;
+    wvg_batch_file_result(b, file, &r);
+    const int nch = wi.reduced_channels, bps = wi.bytes_per_sample;
+    const int64_t block_align = (int64_t)bps * nch;
+    const int64_t total_native = fi.total_samples * (wi.dsd_multiplier > 0 ? 8 : 1);  // WavpackGetNumSamples(wpc, true)
+    const int64_t loop_samples = total_native / 100 / 4096 * 4096;                    // WvDemo.cs:112
+    // frames written: whole calls before the one that threw (WvDemo.cs:144 catch)
+    int64_t limit = fi.out_frames;
+    bool exc = fi.exception != 0;
+    const int64_t kx = first_exception_block(b, fi);
+    if (kx >= 0) {
+        const BlockDesc &d = b->fo.descs[(size_t)kx];
+        const int64_t start = ((int64_t)d.out_off - wi.out_offset) / (nch ? nch : 1);  // block's first output frame
+        const int64_t t = b->h_aux[(size_t)kx];
+        int64_t call;
+        if (t < (int64_t)d.first_chunk) call = start - (int64_t)d.first_bsp / (nch ? nch : 1);
+        else call = start + d.first_chunk + (t - d.first_chunk) / d.chunk * d.chunk;
+        limit = call < limit ? call : limit;
+        exc = true;
+    }
+    int64_t frames;
+    bool trailer = false;
+    int32_t rc = 1;
+    if (fi.first_call_frames < 0) {
+        frames = 0;  // the first call threw
+    } else if (loop_samples == 0) {
+        // `total % loop_samples` divides by zero after the first call's write (WvDemo.cs:130)
+        frames = limit < fi.first_call_frames ? limit : fi.first_call_frames;
+    } else {
+        frames = limit;
+        if (!exc) {
+            trailer = true;
+            rc = ((fi.total_samples != -1 && fi.out_frames != fi.total_samples) || r.crc_errors > 0) ? 1 : 0;
+        }
+    }
+    // header: the stored RIFF header unless float, else RiffChunkHeader + "fmt " + WaveHeader + "data"
+    // (WvDemo.cs:74-105, ChunkHeader.cs:29-45, RiffChunkHeader.cs:66-87, WaveHeader.cs:109-142)
+    uint8_t synth[44];
+    const uint8_t *hdr = nullptr;
+    int64_t hlen = 0;
+    if (fi.header_off >= 0 && !wi.is_float) {
+        hdr = b->blob.data() + (size_t)fi.header_off;
+        hlen = fi.header_len;
+    } else {
+        memcpy(synth, "RIFF", 4);
+        put_le32(synth + 4, (uint32_t)(total_native * block_align + 2 * 8 + 16) + 4);
+        memcpy(synth + 8, "WAVE", 4);
+        memcpy(synth + 12, "fmt ", 4);
+        put_le32(synth + 16, 16);
+        synth[20] = 1;
+        synth[21] = 0;
+        synth[22] = (uint8_t)nch;
+        synth[23] = (uint8_t)(nch >> 8);
+        put_le32(synth + 24, (uint32_t)wi.sample_rate);
+        put_le32(synth + 28, (uint32_t)(wi.sample_rate * block_align));
+        synth[32] = (uint8_t)block_align;
+        synth[33] = (uint8_t)(block_align >> 8);
+        synth[34] = (uint8_t)wi.bits_per_sample;
+        synth[35] = (uint8_t)(wi.bits_per_sample >> 8);
+        memcpy(synth + 36, "data", 4);
+        put_le32(synth + 40, (uint32_t)(total_native * block_align));
+        hdr = synth;
+        hlen = 44;
+    }
+    const int64_t pcm = frames * block_align;
+    const int64_t tlen = trailer && fi.trailer_off >= 0 ? fi.trailer_len : 0;
+    const int64_t total = hlen + pcm + tlen;
+    *wav_len = total;
+    *exit_code = rc;
+    if (!out) return WVG_OK;  // size query
+    if (cap < total) return WVG_ERR_SPACE;
+    memcpy(out, hdr, (size_t)hlen);
+    if (pcm) HIPCHK(c, hipMemcpy(out + hlen, b->d_pcm + b->pcm_off[(size_t)file], (size_t)pcm, hipMemcpyDeviceToHost));
+    if (tlen) memcpy(out + hlen + pcm, b->blob.data() + (size_t)fi.trailer_off, (size_t)tlen);
+    return WVG_OK;
 }
 
 }  // extern "C"

@@ -1,15 +1,24 @@
 // wv_decode.hip -- HIP kernels (gfx950) for the WavPack block decode.
 //
 // Kernel map:
+//   wv_pcm_2wave<terms> : one workgroup (parser wave + reconstruction wave) per
+//                         PCM block whose decorrelation term list has a
+//                         specialised instantiation (wv_wave2.h).
 //   wv_decode_pcm_lane  : one lane per PCM block; runs decode_pcm_block
 //                         (get_words -> decorr passes -> joint/CRC/mute ->
 //                         fixup -> int32 store) fused, sample-major.
 //   wv_decode_dsd_lane  : one lane per DSD block (DsdUtils modes 0/1/3).
 //   wv_dsd_fill         : post-pass writing the 0x55 mute fills of DSD blocks in
 //                         call-buffer coordinates (DsdUtils.cs:104-117, quirk B-9).
+//   wv_format_pcm       : WavpackFormatSamples (WavPackUtils.cs:288-341) over the
+//                         decoded batch, int32 -> little-endian PCM bytes.
 // No MFMA: there is no contraction in this path; the work is serial integer
 // bit-parsing per block, so the design goal is many independent blocks in
 // flight with the whole per-sample pipeline in registers.
+//
+// Per-block aux word (aux[]): DSD blocks record the first muted chunk, PCM
+// blocks the block frame of the residual whose decode raised the reference's
+// C# exception (with ST_EXCEPTION).
 #include <hip/hip_runtime.h>
 
 #include "wv_decode_core.h"
@@ -26,13 +35,14 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_pcm_lane(const BlockD
                                                                     const uint32_t *__restrict__ list, uint32_t n,
                                                                     const uint8_t *__restrict__ blob,
                                                                     int32_t *__restrict__ out,
-                                                                    uint32_t *__restrict__ status) {
+                                                                    uint32_t *__restrict__ status,
+                                                                    uint32_t *__restrict__ aux) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint32_t bi = list[i];
     const BlockDesc &d = descs[bi];
     DevStore st{out + d.out_off};
-    status[bi] = d.fstatus | decode_pcm_block(d, blob, st);
+    status[bi] = d.fstatus | decode_pcm_block(d, blob, st, &aux[bi]);
 }
 
 extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_lane(const BlockDesc *__restrict__ descs,
@@ -76,6 +86,32 @@ extern "C" __global__ void __launch_bounds__(64) wv_dsd_fill(const BlockDesc *__
     }
 }
 
+// WavpackFormatSamples (WavPackUtils.cs:288-341): one workgroup per segment of
+// a file's int32 output; bytes_per_sample 1 (+128, or the raw byte with
+// dsd), 2, 3 or 4, little-endian.  Memory-bound epilogue: 4 B read + bps B
+// written per value.
+extern "C" __global__ void __launch_bounds__(256) wv_format_pcm(const FormatSeg *__restrict__ segs,
+                                                                const int32_t *__restrict__ in,
+                                                                uint8_t *__restrict__ out, int dsd) {
+    const FormatSeg s = segs[blockIdx.x];
+    const int32_t *src = in + s.in_off;
+    uint8_t *dst = out + s.out_off;
+    for (uint32_t i = threadIdx.x; i < s.n; i += 256) {
+        const int32_t t = src[i];
+        switch (s.bps) {
+        case 1: dst[i] = dsd ? (uint8_t)t : (uint8_t)(0xFF & (t + 128)); break;
+        case 2: reinterpret_cast<uint16_t *>(dst)[i] = (uint16_t)t; break;
+        case 3:
+            dst[3 * (uint64_t)i] = (uint8_t)t;
+            dst[3 * (uint64_t)i + 1] = (uint8_t)(t >> 8);
+            dst[3 * (uint64_t)i + 2] = (uint8_t)(t >> 16);
+            break;
+        case 4: reinterpret_cast<int32_t *>(dst)[i] = t; break;
+        default: break;  // the reference writes nothing for other widths
+        }
+    }
+}
+
 }  // namespace wvg
 
 // ---------------------------------------------------------------------------
@@ -88,8 +124,8 @@ template <int... Ts>
 __global__ void __launch_bounds__(128) wv_pcm_2wave(const BlockDesc *__restrict__ descs,
                                                     const uint32_t *__restrict__ list,
                                                     const uint8_t *__restrict__ blob, int32_t *__restrict__ out,
-                                                    uint32_t *__restrict__ status) {
-    w2::block_2wave<Ts...>(descs, list, blob, out, status);
+                                                    uint32_t *__restrict__ status, uint32_t *__restrict__ aux) {
+    w2::block_2wave<Ts...>(descs, list, blob, out, status, aux);
 }
 
 #define WVG_TS_FAST 17, 17
@@ -128,15 +164,15 @@ int term_set_of(const BlockDesc &d) {
 }
 
 hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, uint32_t n, const uint8_t *blob,
-                        int32_t *out, uint32_t *status, hipStream_t s) {
+                        int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s) {
     if (!n) return hipSuccess;
     dim3 g(n), b(128);
     switch (ts) {
-    case 0: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_FAST>), g, b, 0, s, descs, list, blob, out, status); break;
-    case 1: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_DEFAULT>), g, b, 0, s, descs, list, blob, out, status); break;
-    case 2: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_HIGH>), g, b, 0, s, descs, list, blob, out, status); break;
-    case 3: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_MHIGH>), g, b, 0, s, descs, list, blob, out, status); break;
-    case 4: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_M5>), g, b, 0, s, descs, list, blob, out, status); break;
+    case 0: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_FAST>), g, b, 0, s, descs, list, blob, out, status, aux); break;
+    case 1: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_DEFAULT>), g, b, 0, s, descs, list, blob, out, status, aux); break;
+    case 2: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_HIGH>), g, b, 0, s, descs, list, blob, out, status, aux); break;
+    case 3: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_MHIGH>), g, b, 0, s, descs, list, blob, out, status, aux); break;
+    case 4: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_M5>), g, b, 0, s, descs, list, blob, out, status, aux); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -151,17 +187,23 @@ namespace wvg {
 
 hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint32_t n_pcm, const uint32_t *dsd_list,
                          uint32_t n_dsd, const uint8_t *blob, const uint8_t *tables, int32_t *ptables, int32_t *out,
-                         uint32_t *status, uint32_t *mute_chunk, hipStream_t s) {
+                         uint32_t *status, uint32_t *aux, hipStream_t s) {
     if (n_pcm) {
         hipLaunchKernelGGL(wv_decode_pcm_lane, dim3((n_pcm + 63) / 64), dim3(64), 0, s, descs, pcm_list, n_pcm, blob,
-                           out, status);
+                           out, status, aux);
     }
     if (n_dsd) {
         hipLaunchKernelGGL(wv_decode_dsd_lane, dim3((n_dsd + 63) / 64), dim3(64), 0, s, descs, dsd_list, n_dsd, blob,
-                           tables, ptables, out, status, mute_chunk);
+                           tables, ptables, out, status, aux);
         hipLaunchKernelGGL(wv_dsd_fill, dim3((n_dsd + 63) / 64), dim3(64), 0, s, descs, dsd_list, n_dsd, status,
-                           mute_chunk, out);
+                           aux, out);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_format(const FormatSeg *segs, uint32_t nseg, const int32_t *in, uint8_t *out, int dsd, hipStream_t s) {
+    if (!nseg) return hipSuccess;
+    hipLaunchKernelGGL(wv_format_pcm, dim3(nseg), dim3(256), 0, s, segs, in, out, dsd);
     return hipGetLastError();
 }
 

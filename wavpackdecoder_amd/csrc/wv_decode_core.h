@@ -546,7 +546,7 @@ WVF_HD int32_t fixup_wvx(const Fixup &f, BitReader &xb, int32_t x, int32_t &crc_
 // one PCM block
 // ---------------------------------------------------------------------------
 template <class Store>
-WVF_HD uint32_t decode_pcm_block(const BlockDesc &d, const uint8_t *blob, Store &out) {
+WVF_HD uint32_t decode_pcm_block(const BlockDesc &d, const uint8_t *blob, Store &out, uint32_t *exc_frame = nullptr) {
     using namespace wvf;
     const uint32_t flags = d.flags;
     const bool mono = (flags & MONO_DATA) != 0;       // decode path (UnpackUtils.cs:549)
@@ -625,7 +625,10 @@ WVF_HD uint32_t decode_pcm_block(const BlockDesc &d, const uint8_t *blob, Store 
             int rc = get_word(w, bs, flags, 0, true, L);
             if (rc == DEC_OK && !mono) rc = get_word(w, bs, flags, 1, false, R);
             if (rc != DEC_OK) {
-                if (rc == DEC_EXCEPTION) return status | ST_EXCEPTION;
+                if (rc == DEC_EXCEPTION) {
+                    if (exc_frame) *exc_frame = t;  // block frame of the word that threw
+                    return status | ST_EXCEPTION;
+                }
                 // get_words stopped short: the reference decorrelates stale buffer
                 // contents; the chunk is muted and the CRC is garbage (-> error)
                 status |= ST_BITS_ERROR;

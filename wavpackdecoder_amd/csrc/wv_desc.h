@@ -80,4 +80,13 @@ struct alignas(16) BlockDesc {
     int32_t dsd_pad[1];
 };
 
+// One piece (<= 64K values) of one file's int32 output for the format
+// epilogue (WavpackFormatSamples, WavPackUtils.cs:288-341).
+struct FormatSeg {
+    uint64_t in_off;   // first int32 of the piece in the batch output
+    uint64_t out_off;  // its first byte in the batch PCM image
+    uint32_t n;        // values
+    uint32_t bps;      // bytes per sample of the file (WavpackGetBytesPerSample)
+};
+
 }  // namespace wvg

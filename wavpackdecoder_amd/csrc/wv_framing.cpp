@@ -902,6 +902,7 @@ void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t ou
                 samples -= n;
                 if (F.sample_index == F.total_samples) break;
             }
+            if (info.first_call_frames < 0) info.first_call_frames = unpacked;
             if (unpacked == 0) break;
             out_frames += unpacked;
             if (info.exception) break;

@@ -33,6 +33,7 @@ struct FileInfo {
     // output of the chunked caller
     int32_t out_nch = 0;        // ints per frame
     int64_t out_frames = 0;     // frames all calls return
+    int64_t first_call_frames = -1;  // frames the first call returns (-1: it threw)
     int64_t header_off = -1, header_len = 0, trailer_off = -1, trailer_len = 0;  // RIFF/ALT header+trailer
     // blocks of this file inside the batch descriptor array
     int64_t first_desc = 0, num_desc = 0;

@@ -1463,7 +1463,7 @@ __device__ __forceinline__ void scalar_prefetch(uint32_t &pf, cdw_ptr base, uint
 // LAYOUT 0: stereo; 1: mono (MONO_FLAG); 2: FALSE_STEREO (mono decode, 2 ints/frame)
 template <int LAYOUT, int... Ts>
 __device__ __forceinline__ void recon_impl(const BlockDesc &d, const uint8_t *blob, Shared &sh, int32_t *out_base, uint32_t *status_out,
-                                           int lane) {
+                                           uint32_t *exc_out, int lane) {
     using namespace wvf;
     constexpr bool MONO = LAYOUT != 0;  // mono decode path (MONO_DATA)
     constexpr int WPF = MONO ? 1 : 2;   // residual words per frame
@@ -1523,6 +1523,7 @@ __device__ __forceinline__ void recon_impl(const BlockDesc &d, const uint8_t *bl
         if (WV2_PF) scalar_prefetch(pf, pf_base, pf_end, sh);
         if (perr == DEC_EXCEPTION || perr == 3) {
             status |= ST_EXCEPTION;
+            if (lane == 0) *exc_out = produced / WPF;  // block frame of the word that threw
             lds_store_rel(&sh.stop, 1);
             break;
         }
@@ -1587,19 +1588,20 @@ __device__ __forceinline__ void recon_impl(const BlockDesc &d, const uint8_t *bl
 }
 
 template <int... Ts>
-__device__ __forceinline__ void recon(const BlockDesc &d, const uint8_t *blob, Shared &sh, int32_t *out, uint32_t *status_out, int lane) {
+__device__ __forceinline__ void recon(const BlockDesc &d, const uint8_t *blob, Shared &sh, int32_t *out, uint32_t *status_out,
+                                      uint32_t *exc_out, int lane) {
     const uint32_t f = d.flags;
     if (f & wvf::FALSE_STEREO)
-        recon_impl<2, Ts...>(d, blob, sh, out, status_out, lane);
+        recon_impl<2, Ts...>(d, blob, sh, out, status_out, exc_out, lane);
     else if (f & wvf::MONO_FLAG)
-        recon_impl<1, Ts...>(d, blob, sh, out, status_out, lane);
+        recon_impl<1, Ts...>(d, blob, sh, out, status_out, exc_out, lane);
     else
-        recon_impl<0, Ts...>(d, blob, sh, out, status_out, lane);
+        recon_impl<0, Ts...>(d, blob, sh, out, status_out, exc_out, lane);
 }
 
 template <int... Ts>
 __device__ __forceinline__ void block_2wave(const BlockDesc *descs, const uint32_t *list, const uint8_t *blob, int32_t *out,
-                            uint32_t *status) {
+                            uint32_t *status, uint32_t *aux) {
     __shared__ Shared sh;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint32_t bi = list[blockIdx.x];
@@ -1621,7 +1623,7 @@ __device__ __forceinline__ void block_2wave(const BlockDesc *descs, const uint32
     if (wave == 0)
         parser(d, blob, sh, lane, out + d.out_off);
     else
-        recon<Ts...>(d, blob, sh, out, &status[bi], lane);
+        recon<Ts...>(d, blob, sh, out, &status[bi], &aux[bi], lane);
 #if WV2_EXP == 5
     // placement + timeline probe: ints 12-15 (parser) / 16-19 (recon) of the block's output
     const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
