@@ -239,7 +239,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": None if traffic is None else int(traffic),
-                         "traffic_unit": "bytes/launch (PMC FETCH_SIZE x2 + WRITE_SIZE)", "traffic_source": traffic_src,
+                         "traffic_unit": "bytes/launch (PMC FETCH_SIZE + WRITE_SIZE, scale calibrated in the profile)", "traffic_source": traffic_src,
                          "kernel_ms": round(kernel_ms, 4), "alg_bytes_per_launch": alg_bytes,
                          "binding_limit": "serial entropy decode per block (scalar issue of one wave), not HBM"},
             "cpu_baseline": cpu,

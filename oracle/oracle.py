@@ -108,6 +108,30 @@ def decode_file(data: bytes, chunk: int = 4096, max_frames: int | None = None) -
         return DecodeResult(out[: n * nch.value].copy(), int(n), nch.value, crc.value, lossy.value, 0)
 
 
+def decode_file_from(data: bytes, start: int, chunk: int = 4096):
+    """WavpackOpenFileInput + SetSample(start) (WavPackUtils.cs:509-594) + the
+    WvDemo loop from there -> (DecodeResult, seek_rc): seek_rc 1 positioned,
+    0 SetSample returned false, -1 an exception escaped it."""
+    L = lib()
+    f = L.wvo_decode_file_from
+    f.restype = ctypes.c_int64
+    f.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
+                  ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+    max_frames = max(len(data) * 8, 1 << 16)
+    while True:
+        cap = max_frames * 2
+        out = np.zeros(cap, dtype=np.int32)
+        crc, nch, src = ctypes.c_int64(0), ctypes.c_int(0), ctypes.c_int(0)
+        n = f(data, len(data), int(start), out.ctypes.data, cap, chunk, ctypes.byref(crc), ctypes.byref(nch),
+              ctypes.byref(src))
+        if n >= 0 and n * max(nch.value, 1) > cap:
+            max_frames = int(n) + 16
+            continue
+        if n < 0:
+            return DecodeResult(np.zeros(0, np.int32), 0, nch.value, crc.value, 0, int(n)), src.value
+        return DecodeResult(out[: n * nch.value].copy(), int(n), nch.value, crc.value, 0, 0), src.value
+
+
 def demo(data: bytes):
     """WvDemo.Main equivalent -> (exit_code, wav_bytes)."""
     L = lib()

@@ -2086,7 +2086,15 @@ static void ctx_init(wvo_ctx *wpc)
     wpc->stream.wvbits.buf_len = BITSTREAM_BUFFER_SIZE;
 }
 
+static wvo_ctx *open_at(const uint8_t *file, size_t len, uint32_t flags, int64_t pos);
+
 wvo_ctx *wvo_open(const uint8_t *file, size_t len, uint32_t flags) /* WavPackUtils.cs:36-120 */
+{
+    return open_at(file, len, flags, 0);
+}
+
+/* WavpackOpenFileInput on a BinaryReader positioned at `pos` (seek re-opens at a block) */
+static wvo_ctx *open_at(const uint8_t *file, size_t len, uint32_t flags, int64_t pos)
 {
     wvo_ctx *wpc = (wvo_ctx *)malloc(sizeof(wvo_ctx));
     jmp_buf jb, *saved = g_jmp;
@@ -2094,7 +2102,7 @@ wvo_ctx *wvo_open(const uint8_t *file, size_t len, uint32_t flags) /* WavPackUti
     WavpackStream *wps = &wpc->stream;
     wpc->infile.data = file;
     wpc->infile.len = (int64_t)len;
-    wpc->infile.pos = 0;
+    wpc->infile.pos = pos;
     wpc->total_samples = -1;
     wpc->norm_offset = 0;
     wpc->open_flags = 0;
@@ -2229,6 +2237,137 @@ int64_t wvo_unpack_samples(wvo_ctx *wpc, int32_t *buffer, int64_t blen, int64_t 
     }
     g_jmp = saved;
     return samples_unpacked;
+}
+
+/* WavpackContext.stream = c.stream: the context adopts the stream of a context
+ * opened at a block (its arrays move; the old stream's arrays are released) */
+static void adopt_stream(wvo_ctx *wpc, wvo_ctx *c)
+{
+    WavpackStream *wps = &wpc->stream;
+    if (wps->wvbits.valid) free(wps->wvbits.buf);
+    if (wps->wvcbits.valid) free(wps->wvcbits.buf);
+    if (wps->wvxbits.valid) free(wps->wvxbits.buf);
+    dsd_release(wpc, &wps->dsd);
+    memcpy(wps, &c->stream, sizeof(*wps));
+    memset(&c->stream, 0, sizeof(c->stream));
+    wvo_close(c);
+}
+
+int wvo_set_sample(wvo_ctx *wpc, int64_t targetSample) /* SetSample -> seek, WavPackUtils.cs:509-594 */
+{
+    WavpackStream *wps = &wpc->stream;
+    jmp_buf jb, *saved = g_jmp;
+    g_jmp = &jb;
+    if (setjmp(jb)) { /* only IOException is caught inside seek (:590); anything else escapes */
+        g_jmp = saved;
+        wpc->exception = g_exc;
+        return -1;
+    }
+    if (targetSample >= wpc->total_samples) {
+        g_jmp = saved;
+        return 0;
+    }
+    if (targetSample < 0) targetSample = 0;
+    int steps = 25;      /* maximum steps to position */
+    const int min = 5;   /* min count of block for seek forward by just read header */
+    while (steps-- > 0) {
+        int64_t seek_pos = wps->wphdr.stream_position;
+        if (targetSample <= (int64_t)wps->wphdr.block_samples)
+            seek_pos = 0;
+        else if (targetSample < wps->wphdr.block_index ||
+                 targetSample > wps->wphdr.block_index + (int64_t)wps->wphdr.block_samples) {
+            int64_t distance = targetSample - wps->wphdr.block_index;
+            distance += distance > 0 ? (-1 * (int64_t)wps->wphdr.block_samples + 1)
+                                     : (-2 * (int64_t)wps->wphdr.block_samples + 1);
+            if (wps->wphdr.block_samples == 0) cs_throw(WVO_EXC_DIVZERO);
+            int64_t blocks = distance / (int64_t)wps->wphdr.block_samples;
+            if (blocks >= 0 && blocks <= min)
+                seek_pos = -1;
+            else
+                seek_pos += blocks * wps->wphdr.average_block_size;
+            if (seek_pos >= wpc->infile.len) seek_pos = -1;
+        }
+        if (seek_pos != -1) {
+            if (seek_pos < 0) { /* Stream.Seek before the beginning: IOException, caught (:590) */
+                g_jmp = saved;
+                return 0;
+            }
+            wpc->infile.pos = seek_pos;
+        }
+        read_next_header(&wpc->infile, &wps->wphdr);
+        if (wps->wphdr.error) continue;
+        if (steps == 0 || (targetSample >= wps->wphdr.block_index &&
+                           targetSample < wps->wphdr.block_index + (int64_t)wps->wphdr.block_samples)) {
+            int64_t index = targetSample - wps->wphdr.block_index;
+            wvo_ctx *c = open_at(wpc->infile.data, (size_t)wpc->infile.len, 0, wps->wphdr.stream_position);
+            wpc->infile.pos = c->infile.pos; /* one shared BinaryReader */
+            if (c->exception) {
+                int e = c->exception;
+                wvo_close(c);
+                cs_throw(e);
+            }
+            adopt_stream(wpc, c);
+            int32_t temp_buf[SAMPLE_BUFFER_SIZE];
+            while (index > 0) {
+                int64_t toUnpack = SAMPLE_BUFFER_SIZE / wvo_get_reduced_channels(wpc);
+                if (index < toUnpack) toUnpack = index;
+                g_jmp = saved;
+                toUnpack = wvo_unpack_samples(wpc, temp_buf, SAMPLE_BUFFER_SIZE, toUnpack);
+                g_jmp = &jb;
+                if (toUnpack < 0) { /* the exception escapes SetSample */
+                    g_jmp = saved;
+                    return -1;
+                }
+                if (toUnpack == 0) { /* the C# loop never ends */
+                    wpc->exception = WVO_EXC_HANG;
+                    g_jmp = saved;
+                    return -1;
+                }
+                index -= toUnpack;
+            }
+            g_jmp = saved;
+            return 1;
+        }
+        if (seek_pos == -1) {
+            wpc->infile.pos = wps->wphdr.stream_position + wps->wphdr.ckSize;
+            steps--; /* "do not account forward seek by headers" (:586) */
+        }
+    }
+    g_jmp = saved;
+    return 0;
+}
+
+int64_t wvo_decode_file_from(const uint8_t *file, size_t len, int64_t start, int32_t *out, int64_t out_cap, int chunk,
+                             int64_t *crc_errors, int *nch, int *seek_rc)
+{
+    wvo_ctx *wpc = wvo_open(file, len, 0);
+    if (wpc->error_message && wpc->error_message[0]) {
+        wvo_close(wpc);
+        return -2;
+    }
+    int ch = wvo_get_reduced_channels(wpc);
+    *seek_rc = wvo_set_sample(wpc, start);
+    if (*seek_rc < 0) {
+        wvo_close(wpc);
+        return -3;
+    }
+    int32_t *tmp = (int32_t *)malloc(sizeof(int32_t) * (size_t)chunk * (size_t)ch);
+    int64_t total = 0, got, rv = 0;
+    while (1) {
+        got = wvo_unpack_samples(wpc, tmp, (int64_t)chunk * ch, chunk);
+        if (got < 0) { rv = -3; break; }
+        if (got > 0) {
+            int64_t n = got * ch;
+            if ((total * ch + n) <= out_cap) memcpy(out + total * ch, tmp, sizeof(int32_t) * (size_t)n);
+            total += got;
+        }
+        if (got == 0) break;
+    }
+    if (crc_errors) *crc_errors = wvo_get_num_errors(wpc);
+    if (nch) *nch = ch;
+    free(tmp);
+    wvo_close(wpc);
+    return rv < 0 ? rv : total;
 }
 
 int wvo_format_samples(const int32_t *src, int64_t samcnt, int bps, uint8_t *pcm, int64_t pcm_len, int offset,

@@ -68,7 +68,18 @@ int wvo_exception(wvo_ctx *ctx); /* 0 none, else WVO_EXC_* */
 const uint8_t *wvo_get_header(wvo_ctx *ctx, int *len);
 const uint8_t *wvo_get_trailer(wvo_ctx *ctx, int *len);
 
-enum { WVO_EXC_NONE = 0, WVO_EXC_INDEX = 1, WVO_EXC_DIVZERO = 2, WVO_EXC_IO = 3, WVO_EXC_STACK = 4 };
+enum { WVO_EXC_NONE = 0, WVO_EXC_INDEX = 1, WVO_EXC_DIVZERO = 2, WVO_EXC_IO = 3, WVO_EXC_STACK = 4, WVO_EXC_HANG = 5 };
+
+/* WavPackUtils.SetSample -> seek (WavPackUtils.cs:509-594): 1 positioned (the C#
+ * `true`), 0 not (`false`), -1 an exception escaped (or the discard loop would
+ * never end: WVO_EXC_HANG). */
+int wvo_set_sample(wvo_ctx *ctx, int64_t sample);
+
+/* open + SetSample(start) + WavpackUnpackSamples loop of `chunk` frames per call
+ * (like wvo_decode_file); *seek_rc receives wvo_set_sample's result.
+ * Returns frames after the seek, -2 open error, -3 exception. */
+int64_t wvo_decode_file_from(const uint8_t *file, size_t len, int64_t start, int32_t *out, int64_t out_cap, int chunk,
+                             int64_t *crc_errors, int *nch, int *seek_rc);
 
 /* Convenience used by tests/bench: open + loop WavpackUnpackSamples with
  * `chunk` frames per call exactly like WvDemo.cs:110-135 (chunk 4096), all

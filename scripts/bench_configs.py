@@ -1,0 +1,99 @@
+#!/usr/bin/env python3
+"""Device-resident decode rate of the BASELINE.json configurations other than the
+headline one (bench.py runs config 2).  Not part of the driver contract: the
+numbers go into DESIGN.md.
+
+  C1  WvDemo file (20 s 16-bit stereo, default terms): decode + the
+      WavpackFormatSamples epilogue, one file
+  C3  4,096 x 44,100-frame 24-bit stereo high-mode blocks (16 terms)
+  C4  1,024 x 22,050-frame float32 hybrid (FloatUtils.float_values path)
+  C5  mixed corpus sample (NFILES files of the 100k corpus; mono/stereo,
+      16/24-bit, DSD modes 0/1/3)
+
+Each line: kernel ms (hipEvents, mean of K decodes with input resident in HBM),
+Mframes/s, CRC errors, and a lossless round-trip check where one exists.
+usage: python scripts/bench_configs.py [c1 c3 c4 c5] [--c3-blocks N] [--c5-files N]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from synth import corpora  # noqa: E402
+from wavpackdecoder_amd.api import DecodeBatch  # noqa: E402
+
+
+def run(name, files, pcm=None, iters=5, fmt=False):
+    t0 = time.perf_counter()
+    b = DecodeBatch(4096)
+    for f in files:
+        b.add_file(f)
+    t_frame = time.perf_counter() - t0
+    b.upload()
+    b.decode()
+    b.sync()
+    ms = b.time(iters)
+    out = b.download()
+    crc = sum(b.result(i).crc_errors for i in range(len(files)) if b.infos[i].open_ok)
+    ok = None
+    if pcm is not None:
+        ok = bool(np.array_equal(out, pcm.reshape(-1)))
+    fmt_ms = None
+    if fmt:
+        t = time.perf_counter()
+        for _ in range(iters):
+            b.format()
+        b.sync()
+        fmt_ms = (time.perf_counter() - t) / iters * 1e3
+    line = {"config": name, "files": len(files), "blocks": b.num_blocks, "frames": b.frames,
+            "compressed_bytes": b.bytes_in, "kernel_ms": round(ms, 3),
+            "Mframes_per_s": round(b.frames / ms / 1e3, 1), "crc_errors": int(crc),
+            "lossless_roundtrip": ok, "host_framing_s": round(t_frame, 3)}
+    if fmt_ms is not None:
+        line["format_epilogue_ms_wall"] = round(fmt_ms, 3)
+    print(json.dumps(line), flush=True)
+    b.close()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("configs", nargs="*", default=["c1", "c3", "c4", "c5"])
+    ap.add_argument("--c3-blocks", type=int, default=1024)
+    ap.add_argument("--c3-copies", type=int, default=4)
+    ap.add_argument("--c5-files", type=int, default=4000)
+    a = ap.parse_args()
+    from wavpackdecoder_amd import _lib
+    import wavpackdecoder_amd.api as api
+    api._ctx = _lib.lib().wvg_open(0)
+    for c in a.configs:
+        if c == "c1":
+            pcm, data = corpora.c1()
+            run("C1 WvDemo file 20 s 16-bit stereo default", [data], pcm, fmt=True)
+        elif c == "c3":
+            # generating 4,096 distinct 44,100-frame blocks takes ~3 min on one core, so the
+            # batch is C3_COPIES files of c3_blocks distinct blocks each (every block is still
+            # decoded independently; the copies only share content)
+            pcm, data = corpora.c3(nblocks=a.c3_blocks, return_pcm=True)
+            run(f"C3 {a.c3_copies} x {a.c3_blocks} x 44100 24-bit stereo high (16 terms)", [data] * a.c3_copies,
+                np.concatenate([pcm.reshape(-1)] * a.c3_copies))
+            del pcm, data
+        elif c == "c4":
+            run("C4 1024 x 22050 float32 hybrid+bitrate", [corpora.c4()])
+        elif c == "c5":
+            run(f"C5 mixed corpus, files 0..{a.c5_files - 1}", corpora.c5(a.c5_files))
+        elif c.startswith("dsd"):  # dsd0 / dsd1 / dsd3: 64 stereo files of one 22,050-frame block in one mode
+            from synth import wvsynth as S
+            mode = int(c[3:])
+            files = [S.encode_dsd(S.dsd_random_like(22050, 2, seed=i, density=0.5),
+                                  S.DsdParams(nch=2, mode=mode, block_samples=22050)) for i in range(64)]
+            run(f"DSD mode {mode}: 64 files x 22050 frames stereo", files)
+
+
+if __name__ == "__main__":
+    main()

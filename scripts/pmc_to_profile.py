@@ -3,10 +3,14 @@
 
 Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats, verbatim) and
 profiles/<tag>_pmc.json: per-launch HBM bytes of the bench kernel from the
-separate FETCH_SIZE / WRITE_SIZE passes, with the gfx950 correction from
-MI355X_MICROARCH.md (FETCH_SIZE counts half the bytes of 16-B-per-lane
-streaming reads; the unit is KiB).  bench.py reports `roofline.traffic` from it.
-usage: python scripts/pmc_to_profile.py <tag> [kernel-substring]
+separate FETCH_SIZE / WRITE_SIZE passes (unit KiB).  MI355X_MICROARCH.md: on
+gfx950 FETCH_SIZE counts half the bytes of 16-B-per-lane vector streaming reads
+and other widths are uncalibrated.  The bench kernel reads its payload with
+scalar s_load_dwordx2 (no vector reads), and the raw FETCH_SIZE equals the
+known bytes it must read (compressed payload + block descriptors, each read
+once) -- so the scale is 1 (FETCH_SCALE=2 for the old dwordx4 LDS staging).
+bench.py reports `roofline.traffic` from it.
+usage: [FETCH_SCALE=1] python scripts/pmc_to_profile.py <tag> [kernel-substring]
 """
 import collections
 import csv
@@ -39,17 +43,20 @@ _, write = per_dispatch(os.path.join(src, "write", f"{tag}_write_counter_collect
 stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(dst, f"{tag}_kernel_stats.csv")))}
 st = next(v for k, v in stats.items() if kern in k)
 fetch_kib = sum(fetch) / len(fetch)
+scale = float(os.environ.get("FETCH_SCALE", "1"))
 write_kib = sum(write) / len(write)
 out = {
     "kernel": name,
     "rocprof_avg_ns": float(st["AverageNs"]), "rocprof_calls": int(st["Calls"]),
     "dispatches_counted": {"FETCH_SIZE": len(fetch), "WRITE_SIZE": len(write)},
     "fetch_size_kib_per_launch": fetch_kib, "write_size_kib_per_launch": write_kib,
-    "fetch_bytes_per_launch": fetch_kib * 1024 * 2,   # gfx950: x2 for 16 B/lane streaming reads
+    "fetch_scale": scale,
+    "fetch_bytes_per_launch": fetch_kib * 1024 * scale,
     "write_bytes_per_launch": write_kib * 1024,
-    "traffic_bytes_per_launch": fetch_kib * 1024 * 2 + write_kib * 1024,
-    "note": "FETCH_SIZE/WRITE_SIZE in KiB; FETCH doubled per MI355X_MICROARCH.md (16 B/lane dwordx4 staging loads); "
-            "WRITE from dword-per-lane stores, matches the int32 output byte count",
+    "traffic_bytes_per_launch": fetch_kib * 1024 * scale + write_kib * 1024,
+    "note": "FETCH_SIZE/WRITE_SIZE in KiB. Payload read by scalar s_load_dwordx2: raw FETCH_SIZE calibrated against the "
+            "known read bytes (compressed payload + 1,392-B block descriptors) -> scale 1; WRITE from dword-per-lane "
+            "stores equals the int32 output byte count",
 }
 with open(os.path.join(dst, f"{tag}_pmc.json"), "w") as f:
     json.dump(out, f, indent=1)

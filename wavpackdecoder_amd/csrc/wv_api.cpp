@@ -3,6 +3,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -14,7 +15,7 @@
 namespace wvg {
 hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint32_t n_pcm, const uint32_t *dsd_list,
                          uint32_t n_dsd, const uint8_t *blob, const uint8_t *tables, int32_t *ptables, int32_t *out,
-                         uint32_t *status, uint32_t *aux, hipStream_t s);
+                         uint32_t *status, uint32_t *aux, hipStream_t s_pcm, hipStream_t s_dsd);
 int term_set_of(const BlockDesc &d);
 hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, uint32_t n, const uint8_t *blob,
                         int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s);
@@ -25,9 +26,16 @@ constexpr uint32_t kFormatSeg = 65536;  // values per format work item
 
 using namespace wvg;
 
+// The kernels of one decode (a two-wave launch per term set, the PCM lane
+// kernel, the DSD kernels) are independent: they fork from the caller's stream
+// onto side streams and join back, so small groups run concurrently.
+constexpr int kSide = kMaxTermSets + 2;
+
 struct wvg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t side[kSide] = {nullptr};
+    hipEvent_t fork = nullptr, join[kSide] = {nullptr};
     std::string err;
 };
 
@@ -83,8 +91,13 @@ wvg_ctx *wvg_open(int device) {
         return nullptr;
     }
     c->device = device;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-        delete c;
+    bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
+              hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess;
+    for (int i = 0; ok && i < kSide; i++)
+        ok = hipStreamCreateWithFlags(&c->side[i], hipStreamNonBlocking) == hipSuccess &&
+             hipEventCreateWithFlags(&c->join[i], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        wvg_close(c);
         return nullptr;
     }
     return c;
@@ -92,6 +105,11 @@ wvg_ctx *wvg_open(int device) {
 
 void wvg_close(wvg_ctx *c) {
     if (!c) return;
+    for (int i = 0; i < kSide; i++) {
+        if (c->side[i]) hipStreamDestroy(c->side[i]);
+        if (c->join[i]) hipEventDestroy(c->join[i]);
+    }
+    if (c->fork) hipEventDestroy(c->fork);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -244,6 +262,15 @@ int wvg_batch_upload(wvg_batch *b) {
     for (size_t k = 0; k < nd; k++) st[k] = b->fo.descs[k].fstatus;
     HIPCHK(c, hipMemcpyAsync(b->d_status, st.data(), sizeof(uint32_t) * st.size(), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemsetAsync(b->d_mute, 0, sizeof(uint32_t) * (nd ? nd : 1), c->stream));
+    // lane kernels run 64 blocks per wave in lock-step: group blocks of one DSD
+    // mode and of similar length into the same waves (order is free: every
+    // block writes its own output range; DSD fills follow on the same stream)
+    auto by_kind_len = [&](uint32_t x, uint32_t y) {
+        const BlockDesc &p = b->fo.descs[x], &q = b->fo.descs[y];
+        return p.kind != q.kind ? p.kind < q.kind : (p.nframes != q.nframes ? p.nframes > q.nframes : x < y);
+    };
+    std::sort(b->pcm_list.begin(), b->pcm_list.end(), by_kind_len);
+    std::sort(b->dsd_list.begin(), b->dsd_list.end(), by_kind_len);
     size_t np = b->pcm_list.size(), ns = b->dsd_list.size();
     HIPCHK(c, hipMalloc(&b->d_pcml, sizeof(uint32_t) * (np ? np : 1)));
     HIPCHK(c, hipMalloc(&b->d_dsd, sizeof(uint32_t) * (ns ? ns : 1)));
@@ -266,12 +293,30 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
     if (!b || !b->uploaded) return WVG_ERR_ARG;
     wvg_ctx *c = b->ctx;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    // one stream slot per non-empty launch group: term sets 0..7, PCM lane, DSD
+    int used[kSide], n = 0;
+    for (int t = 0; t < kMaxTermSets; t++)
+        if (!b->ts_list[t].empty()) used[n++] = t;
+    if (!b->pcm_list.empty()) used[n++] = kMaxTermSets;
+    if (!b->dsd_list.empty()) used[n++] = kMaxTermSets + 1;
+    auto slot = [&](int g) -> hipStream_t { return n > 1 ? c->side[g] : s; };
+    if (n > 1) {
+        HIPCHK(c, hipEventRecord(c->fork, s));
+        for (int i = 0; i < n; i++) HIPCHK(c, hipStreamWaitEvent(c->side[used[i]], c->fork, 0));
+    }
     for (int t = 0; t < kMaxTermSets; t++)
         if (!b->ts_list[t].empty())
             HIPCHK(c, launch_2wave(t, b->d_descs, b->d_ts[t], (uint32_t)b->ts_list[t].size(), b->d_blob, b->d_out,
-                                   b->d_status, b->d_mute, s));
+                                   b->d_status, b->d_mute, slot(t)));
     HIPCHK(c, launch_decode(b->d_descs, b->d_pcml, (uint32_t)b->pcm_list.size(), b->d_dsd, (uint32_t)b->dsd_list.size(),
-                            b->d_blob, b->d_tables, b->d_ptables, b->d_out, b->d_status, b->d_mute, s));
+                            b->d_blob, b->d_tables, b->d_ptables, b->d_out, b->d_status, b->d_mute,
+                            slot(kMaxTermSets), slot(kMaxTermSets + 1)));
+    if (n > 1) {
+        for (int i = 0; i < n; i++) {
+            HIPCHK(c, hipEventRecord(c->join[used[i]], c->side[used[i]]));
+            HIPCHK(c, hipStreamWaitEvent(s, c->join[used[i]], 0));
+        }
+    }
     b->downloaded = false;
     b->formatted = false;
     return WVG_OK;

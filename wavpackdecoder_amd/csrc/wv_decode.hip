@@ -53,12 +53,16 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_lane(const BlockD
                                                                     int32_t *__restrict__ out,
                                                                     uint32_t *__restrict__ status,
                                                                     uint32_t *__restrict__ mute_chunk) {
+    // mode 3's adaptive ptable (DsdUtils.cs:409-421) is read and written once per
+    // decoded bit on the serial path: keep it in LDS (1 KiB per lane), not in HBM
+    __shared__ int32_t pt_lds[64 * 256];
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    (void)ptables;
     uint32_t bi = list[i];
     const BlockDesc &d = descs[bi];
     DevStore st{out + d.out_off};
-    DsdResult r = decode_dsd_block(d, blob, tables, ptables + (size_t)i * 256, st);
+    DsdResult r = decode_dsd_block(d, blob, tables, pt_lds + threadIdx.x * 256, st);
     status[bi] = d.fstatus | r.status;
     mute_chunk[bi] = r.mute_chunk;
 }
@@ -185,17 +189,19 @@ hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, ui
 // ---------------------------------------------------------------------------
 namespace wvg {
 
+// generic PCM blocks (lane kernel) on s_pcm; DSD blocks (decode, then the mute
+// fills that depend on it) on s_dsd
 hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint32_t n_pcm, const uint32_t *dsd_list,
                          uint32_t n_dsd, const uint8_t *blob, const uint8_t *tables, int32_t *ptables, int32_t *out,
-                         uint32_t *status, uint32_t *aux, hipStream_t s) {
+                         uint32_t *status, uint32_t *aux, hipStream_t s_pcm, hipStream_t s_dsd) {
     if (n_pcm) {
-        hipLaunchKernelGGL(wv_decode_pcm_lane, dim3((n_pcm + 63) / 64), dim3(64), 0, s, descs, pcm_list, n_pcm, blob,
-                           out, status, aux);
+        hipLaunchKernelGGL(wv_decode_pcm_lane, dim3((n_pcm + 63) / 64), dim3(64), 0, s_pcm, descs, pcm_list, n_pcm,
+                           blob, out, status, aux);
     }
     if (n_dsd) {
-        hipLaunchKernelGGL(wv_decode_dsd_lane, dim3((n_dsd + 63) / 64), dim3(64), 0, s, descs, dsd_list, n_dsd, blob,
-                           tables, ptables, out, status, aux);
-        hipLaunchKernelGGL(wv_dsd_fill, dim3((n_dsd + 63) / 64), dim3(64), 0, s, descs, dsd_list, n_dsd, status,
+        hipLaunchKernelGGL(wv_decode_dsd_lane, dim3((n_dsd + 63) / 64), dim3(64), 0, s_dsd, descs, dsd_list, n_dsd,
+                           blob, tables, ptables, out, status, aux);
+        hipLaunchKernelGGL(wv_dsd_fill, dim3((n_dsd + 63) / 64), dim3(64), 0, s_dsd, descs, dsd_list, n_dsd, status,
                            aux, out);
     }
     return hipGetLastError();
