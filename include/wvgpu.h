@@ -73,6 +73,8 @@ typedef struct {
     int64_t header_off, header_len;   /* RIFF/ALT header bytes inside the file (WavpackGetHeader), -1 none */
     int64_t trailer_off, trailer_len; /* WavpackGetTrailer */
     char error[96];
+    int32_t seek_result;        /* wvg_batch_add_file_at: SetSample's result (1 true, 0 false, -1 it threw) */
+    int32_t reserved;
 } wvg_file_info;
 
 typedef struct {
@@ -99,6 +101,15 @@ void wvg_batch_free(wvg_batch *b);
  * The bytes are copied into the batch.  Returns the file index (>= 0) or
  * WVG_ERR_OPEN (info->error set; the file contributes no output). */
 int wvg_batch_add_file(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open_flags, wvg_file_info *info);
+
+/* The same, for a caller that calls WavPackUtils.SetSample(wpc, start_sample)
+ * (WavPackUtils.cs:509-594: the block search, then decode-and-discard up to the
+ * sample in calls of 4096 / reduced-channels frames) right after opening: the
+ * file's output is what the following WavpackUnpackSamples calls return.
+ * info->seek_result holds SetSample's result; when it is 0 the output starts
+ * at the beginning, as the reference's context does. */
+int wvg_batch_add_file_at(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open_flags, int64_t start_sample,
+                          wvg_file_info *info);
 
 /* Copy blob + descriptors to the device and zero the output. */
 int wvg_batch_upload(wvg_batch *b);

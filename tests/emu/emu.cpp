@@ -15,17 +15,22 @@ using namespace wvg;
 
 struct HostStore {
     int32_t *out;
-    uint64_t base;
-    void put(uint64_t i, int32_t v) { out[base + i] = v; }
+    uint64_t base;  // may be a wrapped negative offset (a seek's discarded frames precede it)
+    uint64_t skip;
+    void put(uint64_t i, int32_t v) {
+        if (i >= skip) out[base + i] = v;
+    }
 };
 
 extern "C" {
 // Returns frames (or -2 open error, -3 exception); fills out (cap ints).
-int64_t emu_decode(const uint8_t *file, size_t len, int chunk, int32_t *out, int64_t cap, int64_t *crc_errors,
-                   int *nch, uint32_t *status_or) {
+// seek_to >= 0: as a caller that calls SetSample(seek_to) first (*seek_rc: its result).
+int64_t emu_decode_from(const uint8_t *file, size_t len, int64_t seek_to, int chunk, int32_t *out, int64_t cap,
+                        int64_t *crc_errors, int *nch, uint32_t *status_or, int *seek_rc) {
     FramingOutput fo;
     FileInfo info;
-    frame_file(file, len, 0, 0, 0, chunk, fo, info);
+    frame_file(file, len, 0, 0, 0, chunk, fo, info, seek_to);
+    *seek_rc = info.seek_result;
     *crc_errors = 0;
     *status_or = 0;
     *nch = info.out_nch;
@@ -38,7 +43,7 @@ int64_t emu_decode(const uint8_t *file, size_t len, int chunk, int32_t *out, int
     std::vector<std::pair<int64_t, int64_t>> fills;
     for (auto &d : fo.descs) {
         uint32_t st = d.fstatus;
-        HostStore hs{out, d.out_off};
+        HostStore hs{out, d.out_off, (uint64_t)d.pre_end * d.out_nch};
         if (d.kind == KIND_PCM) {
             st |= decode_pcm_block(d, file, hs);
         } else if (d.kind != KIND_SKIP) {
@@ -49,12 +54,12 @@ int64_t emu_decode(const uint8_t *file, size_t len, int chunk, int32_t *out, int
                 uint32_t f = 0, cl = d.first_chunk;
                 for (uint32_t ci = 0; f < d.nframes; ci++) {
                     uint32_t n = cl < d.nframes - f ? cl : d.nframes - f;
-                    if (ci >= r.mute_chunk) {
+                    if (ci >= r.mute_chunk && f >= d.pre_end) {
                         int64_t start = (int64_t)d.out_off + (int64_t)f * d.out_nch - (ci == 0 ? d.first_bsp : 0);
                         fills.push_back({start, (int64_t)n * d.call_nch});
                     }
                     f += n;
-                    cl = d.chunk;
+                    cl = next_call_len(d, f);
                 }
             }
         }
@@ -72,6 +77,12 @@ int64_t emu_decode(const uint8_t *file, size_t len, int chunk, int32_t *out, int
         for (int64_t i = 0; i < fl.second; i++) out[fl.first + i] = 0x55;
     if (exception) return -3;
     return info.out_frames;
+}
+
+int64_t emu_decode(const uint8_t *file, size_t len, int chunk, int32_t *out, int64_t cap, int64_t *crc_errors,
+                   int *nch, uint32_t *status_or) {
+    int seek_rc = 0;
+    return emu_decode_from(file, len, -1, chunk, out, cap, crc_errors, nch, status_or, &seek_rc);
 }
 
 // FileInfo fields of the host framing, for the WavpackGet* getters' tests.

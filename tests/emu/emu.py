@@ -44,6 +44,28 @@ def decode(data: bytes, chunk: int = 4096):
         return int(n), out[: n * nch.value].copy(), crc.value, st.value
 
 
+def decode_from(data: bytes, start: int, chunk: int = 4096):
+    """SetSample(start) then the chunked loop -> (frames or -2/-3, samples, crc_errors, status_or, seek_rc)"""
+    L = lib()
+    f = L.emu_decode_from
+    f.restype = ctypes.c_int64
+    f.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64,
+                  ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint32),
+                  ctypes.POINTER(ctypes.c_int)]
+    cap = max(len(data) * 16, 1 << 16)
+    while True:
+        out = np.zeros(cap, dtype=np.int32)
+        crc, nch, st, src = ctypes.c_int64(0), ctypes.c_int(0), ctypes.c_uint32(0), ctypes.c_int(0)
+        n = f(data, len(data), int(start), chunk, out.ctypes.data, cap, ctypes.byref(crc), ctypes.byref(nch),
+              ctypes.byref(st), ctypes.byref(src))
+        if n == -4:
+            cap *= 4
+            continue
+        if n < 0:
+            return int(n), np.zeros(0, np.int32), crc.value, st.value, src.value
+        return int(n), out[: n * nch.value].copy(), crc.value, st.value, src.value
+
+
 def file_info(data: bytes) -> dict:
     vals = np.zeros(len(INFO_FIELDS), dtype=np.int64)
     lib().emu_file_info(data, len(data), vals.ctypes.data, len(INFO_FIELDS))

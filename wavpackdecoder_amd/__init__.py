@@ -15,6 +15,6 @@ from .api import (  # noqa: F401
     WavpackGetBytesPerSample, WavpackGetErrorMessage, WavpackGetFileFormat, WavpackGetHeader, WavpackGetIsFive,
     WavpackGetIsFloat, WavpackGetMode, WavpackGetNumChannels, WavpackGetNumErrors, WavpackGetNumSamples,
     WavpackGetReducedChannels, WavpackGetSampleIndex, WavpackGetSampleRate, WavpackGetTrailer, WavpackGetVersion,
-    WavpackLossy, WavpackOpenFileInput, WavpackUnpackSamples, wv_demo,
+    WavpackLossy, WavpackOpenFileInput, WavpackUnpackSamples, wv_demo, SetSample, SetTime,
 )
 from ._lib import build, lib  # noqa: F401

@@ -32,6 +32,7 @@ class WvgFileInfo(ctypes.Structure):
         ("sample_rate", ctypes.c_int64), ("total_samples", ctypes.c_int64), ("out_frames", ctypes.c_int64),
         ("out_offset", ctypes.c_int64), ("header_off", ctypes.c_int64), ("header_len", ctypes.c_int64),
         ("trailer_off", ctypes.c_int64), ("trailer_len", ctypes.c_int64), ("error", ctypes.c_char * 96),
+        ("seek_result", ctypes.c_int32), ("reserved", ctypes.c_int32),
     ]
 
 
@@ -72,6 +73,7 @@ def lib():
         "wvg_batch_new": (vp, [vp, i32]),
         "wvg_batch_free": (None, [vp]),
         "wvg_batch_add_file": (i32, [vp, ctypes.c_char_p, ctypes.c_size_t, u32, ctypes.POINTER(WvgFileInfo)]),
+        "wvg_batch_add_file_at": (i32, [vp, ctypes.c_char_p, ctypes.c_size_t, u32, i64, ctypes.POINTER(WvgFileInfo)]),
         "wvg_batch_upload": (i32, [vp]),
         "wvg_batch_decode": (i32, [vp, vp]),
         "wvg_batch_sync": (i32, [vp]),
@@ -104,6 +106,7 @@ def lib():
 
 
 EXPORTED = ("wvg_open", "wvg_close", "wvg_last_error", "wvg_batch_new", "wvg_batch_free", "wvg_batch_add_file",
+            "wvg_batch_add_file_at",
             "wvg_batch_upload", "wvg_batch_decode", "wvg_batch_sync", "wvg_batch_out_ints", "wvg_batch_device_out",
             "wvg_batch_num_blocks", "wvg_batch_bytes_in", "wvg_batch_frames", "wvg_batch_download",
             "wvg_batch_file_result", "wvg_batch_block_status", "wvg_batch_time", "wvg_decode_file",

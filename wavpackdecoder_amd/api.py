@@ -60,9 +60,15 @@ class DecodeBatch:
         self._uploaded = False
         self._data: list = []
 
-    def add_file(self, data: bytes, open_flags: int = 0):
+    def add_file(self, data: bytes, open_flags: int = 0, start_sample: int | None = None):
+        """Frame one file; with start_sample, as a caller that calls SetSample(start_sample)
+        right after WavpackOpenFileInput (WavPackUtils.cs:509-594)."""
         info = _L.WvgFileInfo()
-        idx = self._L.wvg_batch_add_file(self._b, data, len(data), int(open_flags), ctypes.byref(info))
+        if start_sample is None:
+            idx = self._L.wvg_batch_add_file(self._b, data, len(data), int(open_flags), ctypes.byref(info))
+        else:
+            idx = self._L.wvg_batch_add_file_at(self._b, data, len(data), int(open_flags), int(start_sample),
+                                                ctypes.byref(info))
         self.infos.append(info)
         self._uploaded = False
         return idx
@@ -169,11 +175,12 @@ class WavpackContext:
         self._result = None
         self._pos = 0  # frames already handed out
         self._chunk = None
+        self._seek = None  # SetSample target, applied when the file is decoded
         self.error_message = None
 
     def _decode(self, chunk: int):
         b = DecodeBatch(chunk)
-        idx = b.add_file(self._data, self._flags)
+        idx = b.add_file(self._data, self._flags, self._seek)
         if idx < 0:
             raise RuntimeError("file cannot be opened: " + self._info.error.decode())
         b.decode()
@@ -212,6 +219,38 @@ def WavpackUnpackSamples(wpc: WavpackContext, buffer: np.ndarray, samples: int) 
     buffer[: n * nch] = wpc._decoded[wpc._pos:wpc._pos + n].reshape(-1)
     wpc._pos += n
     return n
+
+
+def SetSample(wpc: WavpackContext, sample: int) -> bool:
+    """WavPackUtils.cs:509-594.  The decode happens on the next WavpackUnpackSamples
+    call, from the block the reference's search lands on; the result is the C#
+    return value.  (After samples were already handed out, the block search of
+    the reference starts from the current block; for well-formed files it ends
+    on the same block, which is what this mirror decodes from.)"""
+    if wpc.error_message:
+        return False
+    # the block search runs in the host framing (no device work until the decode)
+    b = DecodeBatch(SAMPLE_BUFFER_SIZE)
+    try:
+        idx = b.add_file(wpc._data, wpc._flags, int(sample))
+        if idx < 0:
+            return False
+        info = b.infos[idx]
+    finally:
+        b.close()
+    if info.seek_result < 0:
+        raise WavpackException("the reference's SetSample raises an exception on this file")
+    if info.seek_result == 1:
+        wpc._seek = int(sample)
+        wpc._decoded = None
+        wpc._pos = 0
+        wpc._result = None
+    return info.seek_result == 1
+
+
+def SetTime(wpc: WavpackContext, milliseconds: int) -> bool:
+    """WavPackUtils.cs:504-507: SetSample(ms / 1000 * sample_rate) (integer division first)."""
+    return SetSample(wpc, int(milliseconds) // 1000 * int(wpc._info.sample_rate))
 
 
 def WavpackFormatSamples(src: np.ndarray, samcnt: int, bps: int, pcm_buffer: bytearray, offset: int = 0,

@@ -177,6 +177,7 @@ static void fill_info(const FileInfo &fi, wvg_file_info &wi) {
     wi.total_samples = fi.total_samples;
     wi.out_frames = fi.out_frames;
     wi.out_offset = 0;
+    wi.seek_result = fi.seek_result;
 }
 
 int wvg_probe_file(const uint8_t *file, size_t len, uint32_t open_flags, int chunk_frames, wvg_file_info *info) {
@@ -188,14 +189,15 @@ int wvg_probe_file(const uint8_t *file, size_t len, uint32_t open_flags, int chu
     return fi.open_ok ? WVG_OK : WVG_ERR_OPEN;
 }
 
-int wvg_batch_add_file(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open_flags, wvg_file_info *info) {
+static int add_file(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open_flags, int64_t seek_to,
+                    wvg_file_info *info) {
     if (!b || (!file && len)) return WVG_ERR_ARG;
     if (b->uploaded) free_dev(b);
     size_t base = (b->blob.size() + 15) & ~(size_t)15;
     b->blob.resize(base + len);
     if (len) memcpy(b->blob.data() + base, file, len);
     FileInfo fi;
-    frame_file(b->blob.data() + base, len, base, (uint64_t)b->out_ints, open_flags, b->chunk, b->fo, fi);
+    frame_file(b->blob.data() + base, len, base, (uint64_t)b->out_ints, open_flags, b->chunk, b->fo, fi, seek_to);
     wvg_file_info wi;
     fill_info(fi, wi);
     wi.out_offset = b->out_ints;
@@ -235,6 +237,16 @@ int wvg_batch_add_file(wvg_batch *b, const uint8_t *file, size_t len, uint32_t o
     // compressed bytes of the file's decoded blocks (whole file is a fine proxy)
     b->bytes_in += (int64_t)len;
     return (int)b->infos.size() - 1;
+}
+
+int wvg_batch_add_file(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open_flags, wvg_file_info *info) {
+    return add_file(b, file, len, open_flags, -1, info);
+}
+
+int wvg_batch_add_file_at(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open_flags, int64_t start_sample,
+                          wvg_file_info *info) {
+    if (start_sample < 0) return WVG_ERR_ARG;
+    return add_file(b, file, len, open_flags, start_sample, info);
 }
 
 int wvg_batch_upload(wvg_batch *b) {

@@ -26,9 +26,14 @@
 
 namespace wvg {
 
+// output of one block: value i (frame * ints per frame + channel) at out[i];
+// the first `skip` values belong to a seek's discard calls and are dropped
 struct DevStore {
     int32_t *out;
-    __device__ __forceinline__ void put(uint64_t i, int32_t v) { out[i] = v; }
+    uint64_t skip;
+    __device__ __forceinline__ void put(uint64_t i, int32_t v) {
+        if (i >= skip) out[i] = v;
+    }
 };
 
 extern "C" __global__ void __launch_bounds__(64) wv_decode_pcm_lane(const BlockDesc *__restrict__ descs,
@@ -41,7 +46,7 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_pcm_lane(const BlockD
     if (i >= n) return;
     uint32_t bi = list[i];
     const BlockDesc &d = descs[bi];
-    DevStore st{out + d.out_off};
+    DevStore st{out + d.out_off, (uint64_t)d.pre_end * d.out_nch};
     status[bi] = d.fstatus | decode_pcm_block(d, blob, st, &aux[bi]);
 }
 
@@ -61,7 +66,7 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_lane(const BlockD
     (void)ptables;
     uint32_t bi = list[i];
     const BlockDesc &d = descs[bi];
-    DevStore st{out + d.out_off};
+    DevStore st{out + d.out_off, (uint64_t)d.pre_end * d.out_nch};
     DsdResult r = decode_dsd_block(d, blob, tables, pt_lds + threadIdx.x * 256, st);
     status[bi] = d.fstatus | r.status;
     mute_chunk[bi] = r.mute_chunk;
@@ -81,12 +86,12 @@ extern "C" __global__ void __launch_bounds__(64) wv_dsd_fill(const BlockDesc *__
     uint32_t f = 0, cl = d.first_chunk, mc = mute_chunk[bi];
     for (uint32_t ci = 0; f < d.nframes; ci++) {
         uint32_t len = cl < d.nframes - f ? cl : d.nframes - f;
-        if (ci >= mc) {
+        if (ci >= mc && f >= d.pre_end) {  // a seek's discard calls fill a buffer that is dropped
             int64_t start = (int64_t)d.out_off + (int64_t)f * d.out_nch - (ci == 0 ? (int64_t)d.first_bsp : 0);
             for (int64_t k = 0; k < (int64_t)len * d.call_nch; k++) out[start + k] = 0x55;
         }
         f += len;
-        cl = d.chunk;
+        cl = next_call_len(d, f);
     }
 }
 

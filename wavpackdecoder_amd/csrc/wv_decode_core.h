@@ -609,7 +609,7 @@ WVF_HD uint32_t decode_pcm_block(const BlockDesc &d, const uint8_t *blob, Store 
             for (uint32_t j = 0; j < n; j++)
                 for (int c = 0; c < och; c++) out.put((uint64_t)(f + j) * och + c, 0);
             f += n;
-            chunk_len = d.chunk;
+            chunk_len = next_call_len(d, f);
             bsp = 0;
             first = false;
             continue;
@@ -719,7 +719,7 @@ WVF_HD uint32_t decode_pcm_block(const BlockDesc &d, const uint8_t *blob, Store 
             }
         }
         f += n;
-        chunk_len = d.chunk;
+        chunk_len = next_call_len(d, f);
         bsp = 0;
         first = false;
     }
@@ -897,7 +897,7 @@ WVF_HD DsdResult decode_dsd_block(const BlockDesc &d, const uint8_t *blob, const
             res.mute_chunk = ci;
         }
         f += n;
-        chunk_len = d.chunk;
+        chunk_len = next_call_len(d, f);
         ci++;
     }
     if (d.nframes == d.block_samples) {

@@ -77,8 +77,24 @@ struct alignas(16) BlockDesc {
     uint64_t dsd_table_off; // offset into the batch's DSD table area (fast mode)
     int32_t dsd_rate_i;
     int32_t dsd_filters[2][7];  // filter1..5, factor (high mode), per channel
-    int32_t dsd_pad[1];
+    // --- seek (WavPackUtils.cs:521-594): after SetSample the block is decoded from
+    // its start by discard calls of pre_chunk frames up to frame pre_end, whose
+    // output is dropped; frame pre_end lands at out_off (which then lies
+    // pre_end * out_nch ints before the file's output, as a wrapped offset)
+    uint32_t pre_end;       // 0: no discard phase
+    uint32_t pre_chunk;     // SAMPLE_BUFFER_SIZE / reduced channels (WavPackUtils.cs:576)
+    int32_t pad_[3];
 };
+static_assert(sizeof(BlockDesc) % 16 == 0, "BlockDesc is loaded with 16-B alignment");
+
+// frames in the call that starts at block frame `start` (the caller's chunk
+// schedule seen from inside one block, discard calls of a seek included)
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline uint32_t next_call_len(const BlockDesc &d, uint32_t start) {
+    return start < d.pre_end ? (d.pre_end - start < d.pre_chunk ? d.pre_end - start : d.pre_chunk) : d.chunk;
+}
 
 // One piece (<= 64K values) of one file's int32 output for the format
 // epilogue (WavpackFormatSamples, WavPackUtils.cs:288-341).

@@ -4,6 +4,7 @@
 
 #include <string.h>
 
+#include <memory>
 #include <stdexcept>
 
 #include "wv_format.h"
@@ -659,7 +660,10 @@ class Framer {
         d.int32_ones = int32_ones;
         d.int32_dups = int32_dups;
         d.int32_max_width = int32_max_width;
-        if (!inited_this_block) status |= ST_UNSUPPORTED;
+        // a header whose block was not unpack_init'ed decodes with the stream state
+        // left from earlier metadata (sticky state, B-8): fine while that state is
+        // unconsumed (the fresh/known flags below), unsupported once consumed
+        (void)inited_this_block;
         if (flags & DSD_FLAG) {
             if (!dsd.fresh) status |= ST_UNSUPPORTED;
             d.kind = dsd.mode == 0 ? KIND_DSD_RAW : dsd.mode == 1 ? KIND_DSD_FAST : KIND_DSD_HIGH;
@@ -742,6 +746,131 @@ class Framer {
     }
 };
 
+// ---- WavpackOpenFileInput (WavPackUtils.cs:36-120) from the reader's current
+// position; false (and the error message) when the reference reports an error
+bool open_input(Framer &F, uint32_t open_flags, std::string &err) {
+    while (F.wphdr.block_samples == 0) {
+        F.read_next_header();
+        if (F.wphdr.error) {
+            err = "not compatible with this version of WavPack file!";
+            return false;
+        }
+        if (F.wphdr.block_samples > 0 && F.wphdr.total_samples != 0xFFFFFFFFLL) F.total_samples = F.wphdr.total_samples;
+        if (!F.unpack_init()) {
+            err = F.error_message;
+            return false;
+        }
+    }
+    F.cfg_flags = (F.cfg_flags & ~0xffLL) | (F.wphdr.flags & 0xff);
+    F.bytes_per_sample = (int)((F.wphdr.flags & BYTES_STORED) + 1);
+    F.float_norm_exp_cfg = F.float_norm_exp;
+    F.bits_per_sample = (int)(F.bytes_per_sample * 8 - ((F.wphdr.flags & SHIFT_MASK) >> SHIFT_LSB));
+    if (F.cfg_flags & FLOAT_DATA) {
+        F.bytes_per_sample = 3;
+        F.bits_per_sample = 24;
+    }
+    if (F.sample_rate == 0) {
+        static const int64_t rates[15] = {6000,  8000,  9600,  11025, 12000, 16000, 22050, 24000,
+                                          32000, 44100, 48000, 64000, 88200, 96000, 192000};
+        if (F.wphdr.block_samples == 0 || (F.wphdr.flags & SRATE_MASK) == SRATE_MASK)
+            F.sample_rate = 44100;
+        else
+            F.sample_rate = rates[(F.wphdr.flags & SRATE_MASK) >> SRATE_LSB];
+    }
+    if (F.num_channels == 0) {
+        F.num_channels = (F.wphdr.flags & MONO_FLAG) ? 1 : 2;
+        F.channel_mask = 0x5 - F.num_channels;
+    }
+    if ((open_flags & 0x8) && !(F.wphdr.flags & FINAL_BLOCK)) F.reduced_channels = (F.wphdr.flags & MONO_FLAG) ? 1 : 2;
+    if (!(open_flags & 0x8) && F.num_channels > 2) {
+        err = "only two channels supported!";
+        return false;
+    }
+    if (F.wphdr.flags & DSD_FLAG) {
+        F.bytes_per_sample = 1;
+        F.bits_per_sample = 8;
+    }
+    return true;
+}
+
+// `wpc.stream = c.stream` (WavPackUtils.cs:572): the WavpackStream part of the
+// state moves; the context part (config, totals, header/trailer, lossy_blocks,
+// crc_errors) stays the caller's
+void take_stream(Framer &F, const Framer &c) {
+    F.wphdr = c.wphdr;
+    F.wvbits = c.wvbits;
+    F.wvcbits = c.wvcbits;
+    F.wvxbits = c.wvxbits;
+    F.wvx_fresh = c.wvx_fresh;
+    F.wvx_skip_bits = c.wvx_skip_bits;
+    F.crc_mvx = c.crc_mvx;
+    F.w = c.w;
+    F.num_terms = c.num_terms;
+    for (int i = 0; i < 16; i++) F.passes[i] = c.passes[i];
+    F.int32_sent_bits = c.int32_sent_bits;
+    F.int32_zeros = c.int32_zeros;
+    F.int32_ones = c.int32_ones;
+    F.int32_dups = c.int32_dups;
+    F.float_flags = c.float_flags;
+    F.float_shift = c.float_shift;
+    F.float_max_exp = c.float_max_exp;
+    F.float_norm_exp = c.float_norm_exp;
+    F.int32_max_width = c.int32_max_width;
+    F.sample_index = c.sample_index;
+    F.dsd = c.dsd;
+    F.inited_this_block = c.inited_this_block;
+}
+
+// SetSample -> seek (WavPackUtils.cs:509-594), restated over the header walk:
+// 1 positioned at the block holding `target` (`index` frames into it, still to
+// be decoded and discarded), 0 the C# `false` (context untouched), exceptions
+// other than IOException escape (CsException)
+int seek(Framer &F, int64_t target, int64_t &index) {
+    if (target >= F.total_samples) return 0;
+    if (target < 0) target = 0;
+    int steps = 25;
+    const int min = 5;
+    while (steps-- > 0) {
+        Hdr &h = F.wphdr;
+        int64_t seek_pos = h.stream_position;
+        if (target <= (int64_t)h.block_samples)
+            seek_pos = 0;
+        else if (target < h.block_index || target > h.block_index + (int64_t)h.block_samples) {
+            int64_t distance = target - h.block_index;
+            distance += distance > 0 ? (-1 * (int64_t)h.block_samples + 1) : (-2 * (int64_t)h.block_samples + 1);
+            if (h.block_samples == 0) throw CsException();  // DivideByZeroException
+            int64_t blocks = distance / (int64_t)h.block_samples;
+            if (blocks >= 0 && blocks <= min)
+                seek_pos = -1;
+            else
+                seek_pos += blocks * h.average_block_size;
+            if (seek_pos >= F.in.len) seek_pos = -1;
+        }
+        if (seek_pos != -1) {
+            if (seek_pos < 0) return 0;  // Stream.Seek before the start: IOException, caught (:590)
+            F.in.pos = seek_pos;
+        }
+        F.read_next_header();
+        if (F.wphdr.error) continue;
+        if (steps == 0 || (target >= F.wphdr.block_index && target < F.wphdr.block_index + (int64_t)F.wphdr.block_samples)) {
+            index = target - F.wphdr.block_index;
+            std::unique_ptr<Framer> c(new Framer());
+            c->in = F.in;
+            c->in.pos = F.wphdr.stream_position;
+            std::string err;
+            open_input(*c, 0, err);  // the reference does not look at c's error
+            F.in.pos = c->in.pos;    // one BinaryReader
+            take_stream(F, *c);
+            return 1;
+        }
+        if (seek_pos == -1) {
+            F.in.pos = F.wphdr.stream_position + F.wphdr.ckSize;
+            steps--;
+        }
+    }
+    return 0;
+}
+
 }  // namespace
 
 int compute_mode(const FileInfo &info) {  // WavPackUtils.cs:133-167 (fields captured at open)
@@ -749,54 +878,18 @@ int compute_mode(const FileInfo &info) {  // WavPackUtils.cs:133-167 (fields cap
 }
 
 void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t out_base_ints, uint32_t open_flags,
-                int chunk, FramingOutput &out, FileInfo &info) {
-    Framer F;
+                int chunk, FramingOutput &out, FileInfo &info, int64_t seek_to) {
+    std::unique_ptr<Framer> FP(new Framer());
+    Framer &F = *FP;
     F.in.d = file;
     F.in.len = (int64_t)len;
     info = FileInfo();
     info.first_desc = (int64_t)out.descs.size();
     try {
-        // ---- WavpackOpenFileInput (WavPackUtils.cs:36-120)
-        while (F.wphdr.block_samples == 0) {
-            F.read_next_header();
-            if (F.wphdr.error) {
-                info.error = "not compatible with this version of WavPack file!";
-                return;
-            }
-            if (F.wphdr.block_samples > 0 && F.wphdr.total_samples != 0xFFFFFFFFLL) F.total_samples = F.wphdr.total_samples;
-            if (!F.unpack_init()) {
-                info.error = F.error_message;
-                return;
-            }
-        }
-        F.cfg_flags = (F.cfg_flags & ~0xffLL) | (F.wphdr.flags & 0xff);
-        F.bytes_per_sample = (int)((F.wphdr.flags & BYTES_STORED) + 1);
-        F.float_norm_exp_cfg = F.float_norm_exp;
-        F.bits_per_sample = (int)(F.bytes_per_sample * 8 - ((F.wphdr.flags & SHIFT_MASK) >> SHIFT_LSB));
-        if (F.cfg_flags & FLOAT_DATA) {
-            F.bytes_per_sample = 3;
-            F.bits_per_sample = 24;
-        }
-        if (F.sample_rate == 0) {
-            static const int64_t rates[15] = {6000,  8000,  9600,  11025, 12000, 16000, 22050, 24000,
-                                              32000, 44100, 48000, 64000, 88200, 96000, 192000};
-            if (F.wphdr.block_samples == 0 || (F.wphdr.flags & SRATE_MASK) == SRATE_MASK)
-                F.sample_rate = 44100;
-            else
-                F.sample_rate = rates[(F.wphdr.flags & SRATE_MASK) >> SRATE_LSB];
-        }
-        if (F.num_channels == 0) {
-            F.num_channels = (F.wphdr.flags & MONO_FLAG) ? 1 : 2;
-            F.channel_mask = 0x5 - F.num_channels;
-        }
-        if ((open_flags & 0x8) && !(F.wphdr.flags & FINAL_BLOCK)) F.reduced_channels = (F.wphdr.flags & MONO_FLAG) ? 1 : 2;
-        if (!(open_flags & 0x8) && F.num_channels > 2) {
-            info.error = "only two channels supported!";
+        std::string err;
+        if (!open_input(F, open_flags, err)) {
+            info.error = err;
             return;
-        }
-        if (F.wphdr.flags & DSD_FLAG) {
-            F.bytes_per_sample = 1;
-            F.bits_per_sample = 8;
         }
     } catch (const CsException &) {
         info.error = "exception";
@@ -834,10 +927,29 @@ void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t ou
     int64_t out_frames = 0;
     BlockDesc *cur = nullptr;  // descriptor of the block being decoded
     int64_t cur_idx = -1;
+    // ---- SetSample(seek_to) (WavPackUtils.cs:509-594): its discard calls of
+    // SAMPLE_BUFFER_SIZE / reduced channels frames decode the start of the block
+    int64_t discard = 0;
+    const int64_t dchunk = nch > 0 ? 4096 / nch : 4096;
+    try {
+        if (seek_to >= 0) {
+            int64_t index = 0;
+            info.seek_result = seek(F, seek_to, index);
+            // (when the 25-step search gives up, `index` can exceed the block: the
+            // discard then runs on into the next blocks, as in the reference)
+            if (info.seek_result == 1 && index > 0) discard = index;
+        }
+    } catch (const CsException &) {
+        info.seek_result = -1;
+        info.exception = 1;
+        info.num_desc = 0;
+        return;
+    }
     // ---- the caller's loop (WvDemo.cs:117-135) over WavpackUnpackSamples (WavPackUtils.cs:200-282)
     try {
         for (;;) {
-            int64_t samples = chunk, unpacked = 0;
+            const bool disc_call = discard > 0;
+            int64_t samples = disc_call ? (discard < dchunk ? discard : dchunk) : chunk, unpacked = 0;
             int64_t buf_idx = 0;
             while (samples > 0) {
                 Hdr &h = F.wphdr;
@@ -859,7 +971,7 @@ void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t ou
                     unpacked += n;
                     samples -= n;
                     buf_idx += n * nch;
-                    if (buf_idx > (int64_t)chunk * nch) throw CsException();
+                    if (buf_idx > (int64_t)(disc_call ? 4096 : (int64_t)chunk * nch)) throw CsException();
                     continue;
                 }
                 int64_t n = hh.block_index + hh.block_samples - F.sample_index;
@@ -879,6 +991,14 @@ void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t ou
                     d.out_nch = (uint32_t)nch;
                     d.call_nch = (F.reduced_channels == 1 || F.num_channels == 1 || (hh.flags & MONO_FLAG)) ? 1 : 2;
                     d.nframes = 0;
+                    if (disc_call) {
+                        // a block met by the seek's discard calls: its first `rem` frames
+                        // go to the dropped temp buffer
+                        const int64_t rem = discard - unpacked;
+                        d.pre_end = (uint32_t)rem;
+                        d.pre_chunk = (uint32_t)dchunk;
+                        d.out_off = out_base_ints + (uint64_t)(out_frames * nch) - (uint64_t)(rem * nch);
+                    }
                     if (bch != nch) {
                         d.kind = KIND_SKIP;
                         d.fstatus |= ST_UNSUPPORTED;
@@ -901,6 +1021,15 @@ void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t ou
                 unpacked += n;
                 samples -= n;
                 if (F.sample_index == F.total_samples) break;
+            }
+            if (disc_call) {
+                if (unpacked == 0) {  // `index -= 0` forever (WavPackUtils.cs:574-579)
+                    info.seek_result = -1;
+                    info.exception = 1;
+                    break;
+                }
+                discard -= unpacked;
+                continue;
             }
             if (info.first_call_frames < 0) info.first_call_frames = unpacked;
             if (unpacked == 0) break;

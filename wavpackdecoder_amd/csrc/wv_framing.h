@@ -34,6 +34,7 @@ struct FileInfo {
     int32_t out_nch = 0;        // ints per frame
     int64_t out_frames = 0;     // frames all calls return
     int64_t first_call_frames = -1;  // frames the first call returns (-1: it threw)
+    int32_t seek_result = 0;    // SetSample: 1 positioned, 0 false, -1 exception (0 when no seek was asked)
     int64_t header_off = -1, header_len = 0, trailer_off = -1, trailer_len = 0;  // RIFF/ALT header+trailer
     // blocks of this file inside the batch descriptor array
     int64_t first_desc = 0, num_desc = 0;
@@ -48,8 +49,10 @@ struct FramingOutput {
 // Frame one file.  `file` must stay valid until the batch is uploaded.
 // `blob_base` is the file's byte offset inside the device blob; descriptors are
 // appended to `out` with out_off relative to `out_base_ints`.
+// seek_to >= 0: the caller calls SetSample(seek_to) (WavPackUtils.cs:509-594)
+// right after opening, and its calls return the frames from there on.
 void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t out_base_ints, uint32_t open_flags,
-                int chunk, FramingOutput &out, FileInfo &info);
+                int chunk, FramingOutput &out, FileInfo &info, int64_t seek_to = -1);
 
 // WavpackGetMode (WavPackUtils.cs:133-167) from the framed context values
 int compute_mode(const FileInfo &info);

@@ -1330,22 +1330,22 @@ __device__ __forceinline__ bool any_lane(bool c) { return __builtin_amdgcn_ballo
 
 // Output of the mute path: the whole chunk becomes fixup(0) and every later
 // chunk 0 (UnpackUtils.cs:527-543, 649-664).  All lanes store.
+// Values before `skip` (a seek's discard calls) are not stored.
 template <int OCH>
-__device__ __forceinline__ void mute_fill(uint32_t first_chunk, uint32_t chunk, uint32_t nfr, int32_t z0, int32_t z1,
-                                          int32_t *out, uint32_t chunk_start, int lane) {
-    uint32_t chunk_end = chunk_start + (chunk_start == 0 ? first_chunk : chunk);
-    if (chunk_end > nfr) chunk_end = nfr;
+__device__ __forceinline__ void mute_fill(uint32_t chunk_end, uint32_t nfr, int32_t z0, int32_t z1, int32_t *out,
+                                          uint32_t chunk_start, uint64_t skip, int lane) {
     uint64_t a0 = (uint64_t)chunk_start * OCH, a1 = (uint64_t)chunk_end * OCH, a2 = (uint64_t)nfr * OCH;
     for (uint64_t i = a0 + lane; i < a2; i += 64) {
         int32_t v = 0;
         if (i < a1) v = (OCH == 1) ? z0 : (((i & 1) == 0) ? z0 : z1);
-        out[i] = v;
+        if (i >= skip) out[i] = v;
     }
 }
 
 // Chunk-seam bookkeeping of the reconstruction (uniform, SALU).
 struct Seams {
     uint32_t chunk_start, chunk_end, seam8, bsp, chunk, nfr;
+    uint32_t pre_end, pre_chunk;  // a seek's discard calls (next_call_len in wv_desc.h)
     bool crc_stop;
 };
 
@@ -1421,7 +1421,9 @@ __device__ __forceinline__ void recon_batch(CH &ch, const Fixup &fx, const int32
             }                                                                                  \
             if (!LEAN && t == sm.chunk_end - 1) {                                              \
                 sm.chunk_start = t + 1;                                                        \
-                sm.chunk_end = sm.chunk_start + sm.chunk < sm.nfr ? sm.chunk_start + sm.chunk : sm.nfr; \
+                const uint32_t len_ = sm.chunk_start < sm.pre_end                                       \
+                                          ? min(sm.pre_chunk, sm.pre_end - sm.chunk_start) : sm.chunk;         \
+                sm.chunk_end = sm.chunk_start + len_ < sm.nfr ? sm.chunk_start + len_ : sm.nfr;        \
                 sm.seam8 = (!MONO && sm.chunk_end - sm.chunk_start >= 16) ? sm.chunk_start + 7 : 0xFFFFFFFFu; \
                 sm.bsp = 0;                                                                    \
                 sm.crc_stop = false;                                                           \
@@ -1474,6 +1476,7 @@ __device__ __forceinline__ void recon_impl(const BlockDesc &d, const uint8_t *bl
     const int32_t ml = d.mute_limit;
     const uint32_t nfr = d.nframes;
     int32_t *out = out_base + d.out_off;
+    const uint64_t skip = (uint64_t)d.pre_end * OCH;  // a seek's discarded values (not stored)
 
     VChain<Ts...> ch;
     ch.init(d, 0, !MONO && (lane & 1), MONO);
@@ -1486,6 +1489,8 @@ __device__ __forceinline__ void recon_impl(const BlockDesc &d, const uint8_t *bl
     bool crc_garbage = false;
     Seams sm;
     sm.chunk = d.chunk;
+    sm.pre_end = d.pre_end;
+    sm.pre_chunk = d.pre_chunk;
     sm.nfr = nfr;
     sm.chunk_start = 0;
     sm.chunk_end = d.first_chunk < nfr ? d.first_chunk : nfr;
@@ -1555,8 +1560,8 @@ __device__ __forceinline__ void recon_impl(const BlockDesc &d, const uint8_t *bl
         // store the batch: 64 ints per instruction, one per lane
         const uint32_t nv = (mute_at >= 0 ? (uint32_t)mute_at : tvalid) - t0;
         const uint64_t base = (uint64_t)t0 * OCH;
-        if (WV2_EXP != 3 && (uint32_t)lane < nv * OCH) out[base + lane] = o0;
-        if (LAYOUT == 2 && (uint32_t)lane + 64 < nv * OCH) out[base + 64 + lane] = o1;
+        if (WV2_EXP != 3 && (uint32_t)lane < nv * OCH && base + lane >= skip) out[base + lane] = o0;
+        if (LAYOUT == 2 && (uint32_t)lane + 64 < nv * OCH && base + 64 + lane >= skip) out[base + 64 + lane] = o1;
         const bool bits_err = tvalid < tend;
         if (mute_at >= 0 || bits_err) {
             if (bits_err && mute_at < 0) {
@@ -1567,7 +1572,7 @@ __device__ __forceinline__ void recon_impl(const BlockDesc &d, const uint8_t *bl
             status |= ST_MUTED;
             lds_store_rel(&sh.stop, 1);
             const int32_t z0 = fixup_tail(fx, 0);
-            mute_fill<OCH>(d.first_chunk, sm.chunk, nfr, z0, z0, out, sm.chunk_start, lane);
+            mute_fill<OCH>(sm.chunk_end, nfr, z0, z0, out, sm.chunk_start, skip, lane);
             break;
         }
     }
