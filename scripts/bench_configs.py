@@ -57,8 +57,33 @@ def run(name, files, pcm=None, iters=5, fmt=False):
             "lossless_roundtrip": ok, "host_framing_s": round(t_frame, 3)}
     if fmt_ms is not None:
         line["format_epilogue_ms_wall"] = round(fmt_ms, 3)
+    if CPU_THREADS:
+        line["cpu_baseline_Mframes_per_s"] = round(cpu_rate(files), 1)
+        line["cpu_threads"] = CPU_THREADS
     print(json.dumps(line), flush=True)
     b.close()
+
+
+CPU_THREADS = 0
+
+
+def cpu_rate(files):
+    """The oracle (C restatement of the reference path, 4096-frame calls) over the
+    same files on CPU_THREADS host threads (multi-block files split at block
+    boundaries so every thread has work); test infrastructure used as the
+    CPU baseline only."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import bench
+    from oracle import oracle as O
+    parts = []
+    for f in files:
+        parts += bench.split_blocks(f, max(1, CPU_THREADS // max(len(files), 1)))
+    with ThreadPoolExecutor(max_workers=CPU_THREADS) as ex:
+        t0 = time.perf_counter()
+        res = list(ex.map(lambda p: O.decode_file(p, chunk=4096, max_frames=len(p) * 8), parts))
+        dt = time.perf_counter() - t0
+    return sum(r.frames for r in res) / dt / 1e6
 
 
 def main():
@@ -67,7 +92,10 @@ def main():
     ap.add_argument("--c3-blocks", type=int, default=1024)
     ap.add_argument("--c3-copies", type=int, default=4)
     ap.add_argument("--c5-files", type=int, default=4000)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="also time the oracle on this many host threads")
     a = ap.parse_args()
+    global CPU_THREADS
+    CPU_THREADS = a.cpu_threads
     from wavpackdecoder_amd import _lib
     import wavpackdecoder_amd.api as api
     api._ctx = _lib.lib().wvg_open(0)
