@@ -675,13 +675,26 @@ static int get_words(int64_t nsamples, int64_t flags, words_data *w, Bitstream *
         if (c[entidx].error_limit == 0) {
             mid = read_code(bs, high - low);
             mid = mid + low;
-        } else
+        } else {
+            /* The C# loop (WordsUtils.cs:486-492) never ends for some negative
+             * error limits: from any start high-low settles into {-2,-1,0} within
+             * ~70 steps; there -1 is a fixed point, 0 waits for a 0 bit (none past
+             * the payload's end) and nothing exits below -2.  Report it as the
+             * exception it stands for instead of looping; 2^24 steps exceed every
+             * bit of a < 1 MiB block, so no terminating loop is cut short. */
+            int64_t steps = 0;
             while (high - low > c[entidx].error_limit) {
+                if (++steps > 72) {
+                    int64_t d = high - low;
+                    if ((d >= -2 && d <= 0 && (c[entidx].error_limit <= -3 || d == -1)) || steps > (1 << 24))
+                        cs_throw(WVO_EXC_HANG);
+                }
                 if (getbit(bs))
                     mid = (high + (low = mid) + 1) >> 1;
                 else
                     mid = ((high = mid - 1) + low + 1) >> 1;
             }
+        }
 
         if (getbit(bs))
             I_AT(buffer, buffer_len, buffer_counter) = (int32_t)~mid;

@@ -29,7 +29,9 @@ int64_t emu_decode_from(const uint8_t *file, size_t len, int64_t seek_to, int ch
                         int64_t *crc_errors, int *nch, uint32_t *status_or, int *seek_rc) {
     FramingOutput fo;
     FileInfo info;
+    fo.defer_values = true;  // as the product path: the metadata values come from meta_apply
     frame_file(file, len, 0, 0, 0, chunk, fo, info, seek_to);
+    apply_meta_jobs(fo, file);
     *seek_rc = info.seek_result;
     *crc_errors = 0;
     *status_or = 0;
@@ -83,6 +85,23 @@ int64_t emu_decode(const uint8_t *file, size_t len, int chunk, int32_t *out, int
                    int *nch, uint32_t *status_or) {
     int seek_rc = 0;
     return emu_decode_from(file, len, -1, chunk, out, cap, crc_errors, nch, status_or, &seek_rc);
+}
+
+// Descriptors of one file (bytes, BlockDesc after BlockDesc), framed with the
+// metadata values on the host (defer = 0) or deferred and applied by meta_apply
+// (defer = 1); returns the descriptor count (or -4: cap too small).
+int64_t emu_frame_descs(const uint8_t *file, size_t len, int64_t seek_to, int chunk, int defer, void *out,
+                        int64_t cap_bytes, int64_t *njobs) {
+    FramingOutput fo;
+    FileInfo info;
+    fo.defer_values = defer != 0;
+    frame_file(file, len, 0, 0, 0, chunk, fo, info, seek_to);
+    *njobs = (int64_t)fo.jobs.size();
+    if (defer) apply_meta_jobs(fo, file);
+    int64_t nb = (int64_t)(fo.descs.size() * sizeof(BlockDesc));
+    if (nb > cap_bytes) return -4;
+    if (nb) memcpy(out, fo.descs.data(), (size_t)nb);
+    return (int64_t)fo.descs.size();
 }
 
 // FileInfo fields of the host framing, for the WavpackGet* getters' tests.

@@ -186,3 +186,28 @@ def test_edge_inputs(gpu_batch_cls):
         info = infos[k]
         assert res[k].frames == 4097 and res[k].crc_errors == 0
         np.testing.assert_array_equal(out[info.out_offset: info.out_offset + 4097 * 2], x.reshape(-1))
+
+
+def test_fuzzed_metadata_device_parse(gpu_batch_cls):
+    """Device-side metadata parse (wv_meta_parse) on files whose
+    metadata sub-blocks were fuzzed, all in one batch: the GPU output equals the
+    host-core build (tests/emu: the same framing with the deferred values applied
+    on the host), which test_meta_defer.py checks against the oracle.  Includes
+    hybrid streams whose negative error limit makes the C# bisection loop forever
+    (reported as an exception on both sides)."""
+    from tests.emu import emu as E
+    from tests.test_meta_defer import _bases, meta_fuzz
+    files = [meta_fuzz(d, 9000 + 100 * b + s) for b, d in enumerate(_bases()) for s in range(12)]
+    files.append(meta_fuzz(_bases()[3], 5312))  # the never-ending bisection
+    out, res, infos = _gpu_decode(files, 4096, gpu_batch_cls)
+    for k, (f, r, info) in enumerate(zip(files, res, infos)):
+        n, eout, crc, st = E.decode(f)
+        if n == -2:
+            assert not info.open_ok, k
+            continue
+        assert r is not None, k
+        if n == -3:
+            assert r.exception == 1, k
+            continue
+        assert r.exception == 0 and r.frames == n and r.crc_errors == crc, k
+        np.testing.assert_array_equal(out[info.out_offset: info.out_offset + len(eout)], eout, err_msg=str(k))

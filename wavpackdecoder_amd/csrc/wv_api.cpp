@@ -20,6 +20,8 @@ int term_set_of(const BlockDesc &d);
 hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, uint32_t n, const uint8_t *blob,
                         int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s);
 hipError_t launch_format(const FormatSeg *segs, uint32_t nseg, const int32_t *in, uint8_t *out, int dsd, hipStream_t s);
+hipError_t launch_meta(BlockDesc *descs, const MetaJob *jobs, uint32_t njobs, const MetaItem *items, const uint8_t *blob,
+                       hipStream_t s);
 constexpr int kMaxTermSets = 8;
 constexpr uint32_t kFormatSeg = 65536;  // values per format work item
 }
@@ -60,6 +62,8 @@ struct wvg_batch {
     // device
     uint8_t *d_blob = nullptr, *d_tables = nullptr, *d_pcm = nullptr;
     BlockDesc *d_descs = nullptr;
+    MetaItem *d_items = nullptr;  // deferred metadata values (wv_meta.h), applied once per upload
+    MetaJob *d_jobs = nullptr;
     FormatSeg *d_segs = nullptr;
     int32_t *d_out = nullptr, *d_ptables = nullptr;
     uint32_t *d_status = nullptr, *d_mute = nullptr, *d_pcml = nullptr, *d_dsd = nullptr;
@@ -123,6 +127,10 @@ wvg_batch *wvg_batch_new(wvg_ctx *c, int chunk_frames) {
     b->chunk = chunk_frames;
     const char *fl = getenv("WVG_FORCE_LANE");
     b->force_lane = fl && fl[0] == '1';
+    // the decorr/entropy values of each block are parsed on the device (wv_meta_parse);
+    // WVG_HOST_META=1 keeps them on the host framing (A/B comparisons)
+    const char *hm = getenv("WVG_HOST_META");
+    b->fo.defer_values = !(hm && hm[0] == '1');
     return b;
 }
 
@@ -131,6 +139,8 @@ static void free_dev(wvg_batch *b) {
     hipFree(b->d_tables);
     hipFree(b->d_pcm);
     hipFree(b->d_descs);
+    hipFree(b->d_items);
+    hipFree(b->d_jobs);
     hipFree(b->d_segs);
     hipFree(b->d_out);
     hipFree(b->d_ptables);
@@ -144,6 +154,8 @@ static void free_dev(wvg_batch *b) {
     }
     b->d_blob = b->d_tables = b->d_pcm = nullptr;
     b->d_descs = nullptr;
+    b->d_items = nullptr;
+    b->d_jobs = nullptr;
     b->d_segs = nullptr;
     b->d_out = b->d_ptables = nullptr;
     b->d_status = b->d_mute = b->d_pcml = b->d_dsd = nullptr;
@@ -261,6 +273,14 @@ int wvg_batch_upload(wvg_batch *b) {
     size_t nd = b->fo.descs.size();
     HIPCHK(c, hipMalloc(&b->d_descs, sizeof(BlockDesc) * (nd ? nd : 1)));
     if (nd) HIPCHK(c, hipMemcpyAsync(b->d_descs, b->fo.descs.data(), sizeof(BlockDesc) * nd, hipMemcpyHostToDevice, c->stream));
+    if (!b->fo.jobs.empty()) {  // device-side metadata parse: finishes the descriptors in place
+        const size_t ni = b->fo.items.size(), nj = b->fo.jobs.size();
+        HIPCHK(c, hipMalloc(&b->d_items, sizeof(MetaItem) * ni));
+        HIPCHK(c, hipMalloc(&b->d_jobs, sizeof(MetaJob) * nj));
+        HIPCHK(c, hipMemcpyAsync(b->d_items, b->fo.items.data(), sizeof(MetaItem) * ni, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(b->d_jobs, b->fo.jobs.data(), sizeof(MetaJob) * nj, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, launch_meta(b->d_descs, b->d_jobs, (uint32_t)nj, b->d_items, b->d_blob, c->stream));
+    }
     size_t nt = b->fo.tables.size() + 16;
     HIPCHK(c, hipMalloc(&b->d_tables, nt));
     if (!b->fo.tables.empty())

@@ -10,6 +10,9 @@
 //   wv_decode_dsd_lane  : one lane per DSD block (DsdUtils modes 0/1/3).
 //   wv_dsd_fill         : post-pass writing the 0x55 mute fills of DSD blocks in
 //                         call-buffer coordinates (DsdUtils.cs:104-117, quirk B-9).
+//   wv_meta_parse       : one lane per block finishing its descriptor with the
+//                         deferred metadata values (wv_meta.h),
+//                         once per upload, before any decode launch.
 //   wv_format_pcm       : WavpackFormatSamples (WavPackUtils.cs:288-341) over the
 //                         decoded batch, int32 -> little-endian PCM bytes.
 // No MFMA: there is no contraction in this path; the work is serial integer
@@ -22,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include "wv_decode_core.h"
+#include "wv_meta.h"
 #include "wv_wave2.h"
 
 namespace wvg {
@@ -93,6 +97,22 @@ extern "C" __global__ void __launch_bounds__(64) wv_dsd_fill(const BlockDesc *__
         f += len;
         cl = next_call_len(d, f);
     }
+}
+
+// read_decorr_weights / read_decorr_samples / read_entropy_vars /
+// read_hybrid_profile (UnpackUtils.cs:196-360, WordsUtils.cs:75-187) for the
+// reads the host framing deferred: job i applies its items, in stream order,
+// to descriptor jobs[i].desc.  A few dozen bytes per block: latency, not
+// bandwidth, so one lane per block and nothing staged.
+extern "C" __global__ void __launch_bounds__(64) wv_meta_parse(BlockDesc *__restrict__ descs,
+                                                               const MetaJob *__restrict__ jobs, uint32_t n,
+                                                               const MetaItem *__restrict__ items,
+                                                               const uint8_t *__restrict__ blob) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const MetaJob j = jobs[i];
+    BlockDesc &d = descs[j.desc];
+    for (uint32_t k = 0; k < j.count; k++) meta_apply(d, items[j.first + k], blob);
 }
 
 // WavpackFormatSamples (WavPackUtils.cs:288-341): one workgroup per segment of
@@ -209,6 +229,13 @@ hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint3
         hipLaunchKernelGGL(wv_dsd_fill, dim3((n_dsd + 63) / 64), dim3(64), 0, s_dsd, descs, dsd_list, n_dsd, status,
                            aux, out);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_meta(BlockDesc *descs, const MetaJob *jobs, uint32_t njobs, const MetaItem *items, const uint8_t *blob,
+                       hipStream_t s) {
+    if (!njobs) return hipSuccess;
+    hipLaunchKernelGGL(wv_meta_parse, dim3((njobs + 63) / 64), dim3(64), 0, s, descs, jobs, njobs, items, blob);
     return hipGetLastError();
 }
 

@@ -298,7 +298,18 @@ WVF_HD int get_word(Entropy &w, BR &bs, uint32_t flags, int c, bool even, int32_
         mid = code + low;
     } else {
         mid = (high + low + 1) >> 1;
+        // The C# loop (WordsUtils.cs:486-492) never ends for some negative error
+        // limits (high-low settles in {-2,-1,0}: -1 is a fixed point, 0 waits for a
+        // 0 bit, nothing exits below -2): report the exception instead of hanging
+        // the lane.  2^24 steps exceed the bits of any block, so no loop that
+        // terminates is cut short (the oracle applies the same rule).
+        uint32_t steps = 0;
         while (high - low > w.errlim[c]) {
+            if (++steps > 72u) {
+                const int64_t dd = high - low;
+                if ((dd >= -2 && dd <= 0 && (w.errlim[c] <= -3 || dd == -1)) || steps > (1u << 24))
+                    return DEC_EXCEPTION;
+            }
             if (bs.getbit())
                 mid = (high + (low = mid) + 1) >> 1;
             else

@@ -80,9 +80,8 @@ struct Reader {  // System.IO.BinaryReader over the file bytes
 
 struct Md {  // WavpackMetadata.cs:15-23
     int byte_length = 0;
-    const uint8_t *data = nullptr;  // read_buffer or `big`
+    const uint8_t *data = nullptr;  // read_buffer, or the file bytes for a large sub-block
     int data_len = 0;
-    std::vector<uint8_t> big;
     int64_t data_file_off = 0;  // where data[0] came from
     uint8_t id = 0;
     bool hasdata = false;
@@ -129,6 +128,10 @@ class Framer {
     int64_t sample_index = 0;
     DsdState dsd;
     bool inited_this_block = false;  // unpack_init ran for the current header
+    // deferred metadata values (wv_meta.h): reads whose values the device
+    // computes; until materialize() the host copies of those values are stale
+    bool defer = false;
+    std::vector<MetaItem> pending;  // file offsets, stream order
 
     Framer() {
         memset(read_buffer, 0, sizeof(read_buffer));
@@ -215,13 +218,16 @@ class Framer {
         if (bytes_to_read > 0) {
             m.data_file_off = in.pos;
             if (bytes_to_read > BITSTREAM_BUFFER_SIZE) {
-                m.big.assign((size_t)bytes_to_read, 0);
-                m.data = m.big.data();
-                m.data_len = bytes_to_read;
-                if (in.read(m.big.data(), bytes_to_read) != bytes_to_read) {
+                // C# allocates a fresh array and fills it from the stream; a short read
+                // fails the block, so the view of the file bytes is the same data
+                if (in.len - in.pos < bytes_to_read) {
+                    in.pos = in.len;
                     m.hasdata = false;
                     return false;
                 }
+                m.data = in.d + in.pos;
+                m.data_len = bytes_to_read;
+                in.pos += bytes_to_read;
             } else {
                 m.data = read_buffer;
                 m.data_len = BITSTREAM_BUFFER_SIZE;
@@ -242,6 +248,60 @@ class Framer {
         return true;
     }
 
+    // ---- deferred values ---------------------------------------------------
+    struct Vals {  // meta_apply's view of the host state
+        int32_t median[2][3], slow_level[2];
+        int64_t bitrate_acc[2], bitrate_delta[2];
+        int16_t weight_A[16], weight_B[16];
+        int32_t samples_A[16][8], samples_B[16][8];
+    };
+    // run the pending reads on the host state (before a reader that needs it)
+    void materialize() {
+        if (pending.empty()) return;
+        Vals v;
+        memcpy(v.median, w.med, sizeof(v.median));
+        memcpy(v.slow_level, w.slow, sizeof(v.slow_level));
+        memcpy(v.bitrate_acc, w.acc, sizeof(v.bitrate_acc));
+        memcpy(v.bitrate_delta, w.dlt, sizeof(v.bitrate_delta));
+        for (int i = 0; i < 16; i++) {
+            v.weight_A[i] = passes[i].wA;
+            v.weight_B[i] = passes[i].wB;
+            memcpy(v.samples_A[i], passes[i].sA, sizeof(v.samples_A[i]));
+            memcpy(v.samples_B[i], passes[i].sB, sizeof(v.samples_B[i]));
+        }
+        for (const MetaItem &it : pending) meta_apply(v, it, in.d);
+        memcpy(w.med, v.median, sizeof(v.median));
+        memcpy(w.slow, v.slow_level, sizeof(v.slow_level));
+        memcpy(w.acc, v.bitrate_acc, sizeof(v.bitrate_acc));
+        memcpy(w.dlt, v.bitrate_delta, sizeof(v.bitrate_delta));
+        for (int i = 0; i < 16; i++) {
+            passes[i].wA = v.weight_A[i];
+            passes[i].wB = v.weight_B[i];
+            memcpy(passes[i].sA, v.samples_A[i], sizeof(v.samples_A[i]));
+            memcpy(passes[i].sB, v.samples_B[i], sizeof(v.samples_B[i]));
+        }
+        pending.clear();
+    }
+    // an item whose fields a later read overwrites completely is dropped
+    void drop_pending(uint32_t k0, uint32_t k1) {
+        size_t o = 0;
+        for (size_t i = 0; i < pending.size(); i++)
+            if (pending[i].kind != k0 && pending[i].kind != k1) pending[o++] = pending[i];
+        pending.resize(o);
+    }
+    void defer_read(const Md &m, uint32_t kind, int32_t arg, int32_t counter0 = 0) {
+        MetaItem it;
+        it.off = (uint64_t)m.data_file_off;
+        it.kind = kind;
+        it.len = (uint32_t)m.byte_length;
+        it.num_terms = num_terms;
+        it.arg = arg;
+        it.counter0 = counter0;
+        it.mono = (wphdr.flags & MONO_DATA) ? 1u : 0u;
+        pending.push_back(it);
+        if (pending.size() > 12) materialize();  // an odd stream: keep the device jobs short
+    }
+
     // ---- readers ------------------------------------------------------------
     bool read_decorr_terms(Md &m) {  // UnpackUtils.cs:156-187
         int termcnt = m.byte_length;
@@ -255,6 +315,7 @@ class Framer {
         }
         for (int i = 0; i < 16; i++) passes[i] = tmp[i];
         num_terms = termcnt;
+        drop_pending(META_WEIGHTS, META_SAMPLES);  // every pass was just reset
         return true;
     }
     bool read_decorr_weights(Md &m) {  // UnpackUtils.cs:196-239
@@ -262,6 +323,12 @@ class Framer {
         bool mono = (wphdr.flags & MONO_DATA) != 0;
         if (!mono) termcnt /= 2;
         if (termcnt > num_terms) return false;
+        if (defer) {  // reads stay inside the sub-block and cannot fail
+            for (int k = 0; k < termcnt; k++) passes[num_terms - 1 - k].known_w = true;
+            if (termcnt > 0) defer_read(m, META_WEIGHTS, termcnt);
+            return true;
+        }
+        materialize();
         int16_t wa = 0, wb = 0;
         int counter = 0, it = num_terms;
         while (termcnt > 0) {
@@ -278,6 +345,21 @@ class Framer {
         return true;
     }
     bool read_decorr_samples(Md &m) {  // UnpackUtils.cs:250-360 (quirk B-7 kept)
+        if (defer) {
+            // deferred when every iteration reads inside the sub-block and the
+            // passes do not run out (else the C# reads stale buffer bytes or throws)
+            const bool mono = (wphdr.flags & MONO_DATA) != 0;
+            const int q = num_terms > 0 ? passes[num_terms - 1].term : 0;
+            const int c0 = (wphdr.version == 0x402 && (wphdr.flags & HYBRID_FLAG)) ? (mono ? 2 : 4) : 0;
+            const int step = meta_samples_step(q, mono), span = m.byte_length - c0;
+            bool ok = span <= 0 || (step > 0 && span % step == 0 && span / step <= num_terms);
+            if (ok) {
+                for (int i = 0; i < num_terms; i++) passes[i].known_s = true;
+                if (num_terms > 0) defer_read(m, META_SAMPLES, q, c0);
+                return true;
+            }
+        }
+        materialize();
         int16_t term = 0;
         int32_t tA[8] = {0}, tB[8] = {0};
         int idx = 0;
@@ -327,6 +409,13 @@ class Framer {
         return true;
     }
     bool read_entropy_vars(Md &m) {  // WordsUtils.cs:75-116
+        if (defer && ((wphdr.flags & MONO_DATA) ? m.byte_length >= 6 : m.byte_length == 12)) {
+            drop_pending(META_ENTROPY, META_HYBRID);  // `w = new words_data()`
+            w.known = true;
+            defer_read(m, META_ENTROPY, 0);
+            return true;
+        }
+        materialize();
         int b[12];
         for (int i = 0; i < 6; i++) b[i] = m.at(i);
         bool mono = (wphdr.flags & MONO_DATA) != 0;
@@ -347,6 +436,16 @@ class Framer {
     }
     bool read_hybrid_profile(Md &m) {  // WordsUtils.cs:124-187
         bool mono = (wphdr.flags & MONO_DATA) != 0;
+        if (defer) {  // deferred when it reads exactly the sub-block (no stale bytes, no failure)
+            const int w2 = mono ? 2 : 4;
+            int need = ((wphdr.flags & HYBRID_BITRATE) ? w2 : 0) + w2;
+            if (need < m.byte_length) need += w2;
+            if (need == m.byte_length) {
+                defer_read(m, META_HYBRID, (int32_t)wphdr.flags);
+                return true;
+            }
+        }
+        materialize();
         int bc = 0;
         auto u16 = [&](int o) { return m.at(o) + (m.at(o + 1) << 8); };
         if (wphdr.flags & HYBRID_BITRATE) {
@@ -721,6 +820,18 @@ class Framer {
                 memcpy(d.samples_A[i], p.sA, sizeof(p.sA));
                 memcpy(d.samples_B[i], p.sB, sizeof(p.sB));
             }
+            if (!pending.empty()) {  // the device finishes these values (wv_meta_parse)
+                MetaJob j;
+                j.desc = (uint32_t)out.descs.size();
+                j.first = (uint32_t)out.items.size();
+                j.count = (uint32_t)pending.size();
+                j.pad_ = 0;
+                for (MetaItem it : pending) {
+                    it.off += blob_base;
+                    out.items.push_back(it);
+                }
+                out.jobs.push_back(j);
+            }
             if (num_terms < 0 || num_terms > 16) status |= ST_UNSUPPORTED;
             // term 0 in a stereo block behaves differently in the first 8 frames
             // and in decorr_stereo_pass_cont (UnpackUtils.cs:1118-1121)
@@ -819,6 +930,7 @@ void take_stream(Framer &F, const Framer &c) {
     F.sample_index = c.sample_index;
     F.dsd = c.dsd;
     F.inited_this_block = c.inited_this_block;
+    F.pending = c.pending;
 }
 
 // SetSample -> seek (WavPackUtils.cs:509-594), restated over the header walk:
@@ -855,6 +967,7 @@ int seek(Framer &F, int64_t target, int64_t &index) {
         if (steps == 0 || (target >= F.wphdr.block_index && target < F.wphdr.block_index + (int64_t)F.wphdr.block_samples)) {
             index = target - F.wphdr.block_index;
             std::unique_ptr<Framer> c(new Framer());
+            c->defer = F.defer;
             c->in = F.in;
             c->in.pos = F.wphdr.stream_position;
             std::string err;
@@ -873,6 +986,11 @@ int seek(Framer &F, int64_t target, int64_t &index) {
 
 }  // namespace
 
+void apply_meta_jobs(FramingOutput &out, const uint8_t *blob) {
+    for (const MetaJob &j : out.jobs)
+        for (uint32_t k = 0; k < j.count; k++) meta_apply(out.descs[j.desc], out.items[j.first + k], blob);
+}
+
 int compute_mode(const FileInfo &info) {  // WavPackUtils.cs:133-167 (fields captured at open)
     return info.mode;
 }
@@ -881,6 +999,7 @@ void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t ou
                 int chunk, FramingOutput &out, FileInfo &info, int64_t seek_to) {
     std::unique_ptr<Framer> FP(new Framer());
     Framer &F = *FP;
+    F.defer = out.defer_values;
     F.in.d = file;
     F.in.len = (int64_t)len;
     info = FileInfo();

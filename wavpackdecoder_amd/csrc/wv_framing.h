@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "wv_desc.h"
+#include "wv_meta.h"
 
 namespace wvg {
 
@@ -44,7 +45,17 @@ struct FileInfo {
 struct FramingOutput {
     std::vector<BlockDesc> descs;
     std::vector<uint8_t> tables;  // DSD tables (see BlockDesc::dsd_table_off)
+    // defer_values: the decorr weight/sample and entropy/hybrid values are left
+    // to meta_apply (wv_meta.h) -- the device parse kernel, or apply_meta_jobs on
+    // the host; until then those descriptor fields hold the older stream values
+    bool defer_values = false;
+    std::vector<MetaItem> items;  // offsets into the batch blob
+    std::vector<MetaJob> jobs;
 };
+
+// Host application of the deferred metadata values (what wv_meta_parse does on
+// the device); `blob` is the buffer the item offsets point into.
+void apply_meta_jobs(FramingOutput &out, const uint8_t *blob);
 
 // Frame one file.  `file` must stay valid until the batch is uploaded.
 // `blob_base` is the file's byte offset inside the device blob; descriptors are
