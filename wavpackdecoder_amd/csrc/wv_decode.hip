@@ -76,6 +76,201 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_lane(const BlockD
     mute_chunk[bi] = r.mute_chunk;
 }
 
+// The same two decoders with one 64-lane wave per block instead of one lane:
+// every value derives from blockIdx.x, so the compiler keeps the decode
+// wave-uniform (SGPRs, scalar branches, no divergence between blocks sharing a
+// wave) and lane 0 alone stores.  Blocks spread over the SIMDs instead of 64 of
+// them sharing one wave's lock-step issue.
+struct DevStoreWave {
+    int32_t *out;
+    uint64_t skip;
+    bool lead;
+    __device__ __forceinline__ void put(uint64_t i, int32_t v) {
+        if (lead && i >= skip) out[i] = v;
+    }
+};
+
+extern "C" __global__ void __launch_bounds__(64) wv_decode_pcm_wave(const BlockDesc *__restrict__ descs,
+                                                                    const uint32_t *__restrict__ list,
+                                                                    const uint8_t *__restrict__ blob,
+                                                                    int32_t *__restrict__ out,
+                                                                    uint32_t *__restrict__ status,
+                                                                    uint32_t *__restrict__ aux) {
+    const uint32_t bi = list[blockIdx.x];
+    const BlockDesc &d = descs[bi];
+    const bool lead = threadIdx.x == 0;
+    DevStoreWave st{out + d.out_off, (uint64_t)d.pre_end * d.out_nch, lead};
+    uint32_t exc = aux[bi];
+    const uint32_t s = d.fstatus | decode_pcm_block(d, blob, st, &exc);
+    if (lead) {
+        status[bi] = s;
+        aux[bi] = exc;
+    }
+}
+
+// Payload bytes for a wave-uniform decoder: aligned dwords through the scalar
+// cache (one s_load per 4 bytes, the current dword kept in an SGPR) instead of
+// a vector byte load, and its full memory latency, per byte.
+struct ByteSrcWave {
+    const uint32_t *w;  // the dword holding the payload's first byte
+    uint32_t sh;        // the payload's first byte within it
+    uint32_t cur_i, cur;
+    // pointer arithmetic on the kernel argument (no integer round trip) keeps
+    // the global address space, so the loads stay scalar, not flat
+    __device__ __forceinline__ void init(const uint8_t *p) {
+        sh = (uint32_t)((uintptr_t)p & 3);
+        w = (const uint32_t *)(p - sh);
+        cur_i = 0;
+        cur = __builtin_amdgcn_readfirstlane(w[0]);
+    }
+    __device__ __forceinline__ uint32_t byte(uint32_t bp) {
+        const uint32_t a = bp + sh;
+        if ((a >> 2) != cur_i) {
+            cur_i = a >> 2;
+            cur = __builtin_amdgcn_readfirstlane(w[cur_i]);
+        }
+        return (cur >> ((a & 3) * 8)) & 0xFFu;
+    }
+};
+
+// DsdUtils.init_dsd_block_high + decode_high (DsdUtils.cs:343-493) for one
+// block, wave-uniform, with the channel count a compile-time constant so the
+// per-channel filter state (value, filter0..6, factor) lives in scalar
+// registers.  Same results and status bits as decode_dsd_block's KIND_DSD_HIGH
+// path (wv_decode_core.h), which the CPU tests check against the oracle.
+template <int WCH>
+__device__ __forceinline__ DsdResult dsd_high_wave(const BlockDesc &d, const uint8_t *blob, const uint8_t *tables,
+                                                   int32_t *ptable, DevStoreWave &out) {
+    using namespace wvf;
+    const uint32_t flags = d.flags;
+    const bool fstereo = (flags & FALSE_STEREO) != 0;
+    const uint32_t och = (flags & MONO_FLAG) ? 1u : 2u;
+    const uint32_t dlen = d.dsd_data_len;
+    ByteSrcWave src;
+    src.init(blob + d.bits_off);
+    uint32_t bp = 0;
+    int32_t crc = -1;
+    DsdResult res = {0, 0};
+    bool mute = false;
+    uint32_t low = 0, high = 0xFFFFFFFFu, value = 0;
+    for (int i = 0; i < 4; i++) value = (value << 8) | src.byte(bp++);
+    {  // the block's initial probability table, 4 entries per lane
+        const int32_t *pt0 = (const int32_t *)(tables + d.dsd_table_off);
+        for (uint32_t i = threadIdx.x; i < 256; i += 64) ptable[i] = pt0[i];
+        __syncthreads();
+    }
+    int32_t q0[WCH], q1[WCH], q2[WCH], q3[WCH], q4[WCH], q5[WCH], q6[WCH], q7[WCH], q8[WCH], bytei[WCH];
+#pragma unroll
+    for (int c = 0; c < WCH; c++) {
+        q0[c] = 0;
+        q1[c] = 0;
+        q2[c] = d.dsd_filters[c][0];
+        q3[c] = d.dsd_filters[c][1];
+        q4[c] = d.dsd_filters[c][2];
+        q5[c] = d.dsd_filters[c][3];
+        q6[c] = d.dsd_filters[c][4];
+        q7[c] = 0;
+        q8[c] = d.dsd_filters[c][5];
+        bytei[c] = 0;
+    }
+    uint32_t f = 0, chunk_len = d.first_chunk, ci = 0;
+    while (f < d.nframes) {
+        uint32_t n = chunk_len;
+        if (n > d.nframes - f) n = d.nframes - f;
+        if (!mute) {
+            for (uint32_t j = 0; j < n; j++) {
+#pragma unroll
+                for (int c = 0; c < WCH; c++) q0[c] = add32(sub32(q2[c], q6[c]), mul32(q7[c], q8[c]) >> 2);
+                for (int bit = 0; bit < 8; bit++) {
+#pragma unroll
+                    for (int c = 0; c < WCH; c++) {
+                        const int pp = (q0[c] >> 8) & 255;
+                        const int32_t pv = __builtin_amdgcn_readfirstlane(ptable[pp]);
+                        const uint32_t split = low + ((high - low) >> 8) * ((uint32_t)pv >> 16);
+                        // branch-free: selects instead of a taken branch per decision
+                        const bool zero = value <= split;
+                        high = zero ? split : high;
+                        low = zero ? low : split + 1;
+                        ptable[pp] = pv + (((zero ? 0x010000FE : 0x00010000) - pv) >> 8);
+                        q1[c] = zero ? -1 : 0;
+                        while (((high ^ low) & 0xFF000000u) == 0 && bp < dlen) {
+                            value = (value << 8) | src.byte(bp++);
+                            high = (high << 8) | 0xFF;
+                            low <<= 8;
+                        }
+                        q0[c] = add32(q0[c], mul32(q7[c], 8));
+                        bytei[c] = shl32(bytei[c], 1) | (q1[c] & 1);
+                        q8[c] = add32(q8[c], (((q0[c] ^ q1[c]) >> 31) | 1) & ((q0[c] ^ sub32(q0[c], mul32(q7[c], 16))) >> 31));
+                        q2[c] = add32(q2[c], sub32(q1[c] & (1 << 20), q2[c]) >> 6);
+                        q3[c] = add32(q3[c], sub32(q1[c] & (1 << 20), q3[c]) >> 4);
+                        q4[c] = add32(q4[c], sub32(q3[c], q4[c]) >> 4);
+                        q5[c] = add32(q5[c], sub32(q4[c], q5[c]) >> 4);
+                        q0[c] = sub32(q5[c], q6[c]) >> 4;
+                        q6[c] = add32(q6[c], q0[c]);
+                        q7[c] = add32(q7[c], sub32(q0[c], q7[c]) >> 3);
+                        q0[c] = add32(sub32(q2[c], q6[c]), mul32(q7[c], q8[c]) >> 2);
+                    }
+                }
+                int32_t v[2] = {0, 0};
+#pragma unroll
+                for (int c = 0; c < WCH; c++) {
+                    v[c] = bytei[c] & 0xFF;
+                    q8[c] = sub32(q8[c], add32(q8[c], 512) >> 10);
+                    crc = add32(crc, add32(shl32(crc, 1), v[c]));
+                }
+                const uint64_t o = (uint64_t)(f + j) * och;
+                if (WCH == 1 && !fstereo) {
+                    out.put(o, v[0]);
+                } else if (fstereo) {
+                    out.put(o, v[0]);
+                    out.put(o + 1, v[0]);
+                } else {
+                    out.put(o, v[0]);
+                    out.put(o + 1, v[1]);
+                }
+            }
+            // DsdUtils.cs:99-101: the final chunk checks the crc and mutes on mismatch
+            if (f + n == d.block_samples && crc != d.crc) mute = true;
+        }
+        if (mute && !(res.status & ST_DSD_MUTE)) {
+            res.status |= ST_DSD_MUTE;
+            res.mute_chunk = ci;
+        }
+        f += n;
+        chunk_len = next_call_len(d, f);
+        ci++;
+    }
+    if (d.nframes == d.block_samples) {
+        res.status |= ST_CRC_CHECKED;
+        if (crc != d.crc) res.status |= ST_CRC_ERROR;
+    }
+    return res;
+}
+
+extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_wave(const BlockDesc *__restrict__ descs,
+                                                                    const uint32_t *__restrict__ list,
+                                                                    const uint8_t *__restrict__ blob,
+                                                                    const uint8_t *__restrict__ tables,
+                                                                    int32_t *__restrict__ out,
+                                                                    uint32_t *__restrict__ status,
+                                                                    uint32_t *__restrict__ mute_chunk) {
+    __shared__ int32_t pt_lds[256];  // mode 3's adaptive ptable, one per block
+    const uint32_t bi = list[blockIdx.x];
+    const BlockDesc &d = descs[bi];
+    const bool lead = threadIdx.x == 0;
+    DevStoreWave st{out + d.out_off, (uint64_t)d.pre_end * d.out_nch, lead};
+    DsdResult r;
+    if (d.kind == KIND_DSD_HIGH)
+        r = (d.flags & wvf::MONO_DATA) ? dsd_high_wave<1>(d, blob, tables, pt_lds, st)
+                                       : dsd_high_wave<2>(d, blob, tables, pt_lds, st);
+    else
+        r = decode_dsd_block(d, blob, tables, pt_lds, st);
+    if (lead) {
+        status[bi] = d.fstatus | r.status;
+        mute_chunk[bi] = r.mute_chunk;
+    }
+}
+
 // one thread per DSD block; fills only for blocks that muted
 extern "C" __global__ void __launch_bounds__(64) wv_dsd_fill(const BlockDesc *__restrict__ descs,
                                                              const uint32_t *__restrict__ list, uint32_t n,
@@ -219,13 +414,26 @@ namespace wvg {
 hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint32_t n_pcm, const uint32_t *dsd_list,
                          uint32_t n_dsd, const uint8_t *blob, const uint8_t *tables, int32_t *ptables, int32_t *out,
                          uint32_t *status, uint32_t *aux, hipStream_t s_pcm, hipStream_t s_dsd) {
+    // WVG_LANE_KERNELS=1: the lane-per-block kernels (A/B comparisons)
+    static const bool lanes = [] {
+        const char *e = getenv("WVG_LANE_KERNELS");
+        return e && e[0] == '1';
+    }();
     if (n_pcm) {
-        hipLaunchKernelGGL(wv_decode_pcm_lane, dim3((n_pcm + 63) / 64), dim3(64), 0, s_pcm, descs, pcm_list, n_pcm,
-                           blob, out, status, aux);
+        if (lanes)
+            hipLaunchKernelGGL(wv_decode_pcm_lane, dim3((n_pcm + 63) / 64), dim3(64), 0, s_pcm, descs, pcm_list,
+                               n_pcm, blob, out, status, aux);
+        else
+            hipLaunchKernelGGL(wv_decode_pcm_wave, dim3(n_pcm), dim3(64), 0, s_pcm, descs, pcm_list, blob, out, status,
+                               aux);
     }
     if (n_dsd) {
-        hipLaunchKernelGGL(wv_decode_dsd_lane, dim3((n_dsd + 63) / 64), dim3(64), 0, s_dsd, descs, dsd_list, n_dsd,
-                           blob, tables, ptables, out, status, aux);
+        if (lanes)
+            hipLaunchKernelGGL(wv_decode_dsd_lane, dim3((n_dsd + 63) / 64), dim3(64), 0, s_dsd, descs, dsd_list, n_dsd,
+                               blob, tables, ptables, out, status, aux);
+        else
+            hipLaunchKernelGGL(wv_decode_dsd_wave, dim3(n_dsd), dim3(64), 0, s_dsd, descs, dsd_list, blob, tables, out,
+                               status, aux);
         hipLaunchKernelGGL(wv_dsd_fill, dim3((n_dsd + 63) / 64), dim3(64), 0, s_dsd, descs, dsd_list, n_dsd, status,
                            aux, out);
     }
