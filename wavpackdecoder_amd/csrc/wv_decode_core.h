@@ -296,6 +296,26 @@ WVF_HD int get_word(Entropy &w, BR &bs, uint32_t flags, int c, bool even, int32_
             }
         }
         mid = code + low;
+    } else if (w.errlim[c] >= 0 && low >= 0 && high >= low && high < ((int64_t)1 << 30)) {
+        // The bisection (WordsUtils.cs:486-492) in 32 bits: with a non-negative
+        // error limit high-low stays >= 0 and at least halves every step, so it
+        // ends within 30 steps and its bits come from one 32-bit look-ahead;
+        // branch-free selects instead of a data-dependent branch per bit.
+        const int32_t el = w.errlim[c];
+        uint32_t lo = (uint32_t)low, hi = (uint32_t)high, md = (hi + lo + 1) >> 1;
+        bs.need(32);
+        uint32_t look = (uint32_t)bs.win;
+        int used = 0;
+        while ((int32_t)(hi - lo) > el) {
+            const bool one = (look & 1u) != 0;
+            look >>= 1;
+            used++;
+            lo = one ? md : lo;
+            hi = one ? hi : md - 1;
+            md = (hi + lo + 1) >> 1;
+        }
+        bs.skip(used);
+        mid = (int64_t)md;
     } else {
         mid = (high + low + 1) >> 1;
         // The C# loop (WordsUtils.cs:486-492) never ends for some negative error
