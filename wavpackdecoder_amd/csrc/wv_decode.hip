@@ -247,6 +247,128 @@ __device__ __forceinline__ DsdResult dsd_high_wave(const BlockDesc &d, const uin
     return res;
 }
 
+// DsdUtils mode 1's tables (prob u8, summed u16, lookup u8, value_lookup i32;
+// 16-B aligned by the framing) read through the scalar cache: a data-dependent
+// table read costs a scalar-cache hit, not a vector load's memory latency
+struct DsdTablesWave {
+    w2::cdw_ptr t;
+    int bins;
+    __device__ __forceinline__ uint32_t u8(uint32_t i) const { return (t[i >> 2] >> ((i & 3) * 8)) & 0xFFu; }
+    __device__ __forceinline__ uint32_t prob(uint32_t i) const { return u8(i); }
+    __device__ __forceinline__ uint32_t summed(uint32_t i) const {
+        const uint32_t b = (uint32_t)bins * 256u + 2u * i;
+        return (t[b >> 2] >> ((b & 2) * 8)) & 0xFFFFu;
+    }
+    __device__ __forceinline__ uint32_t lookup(uint32_t i) const { return u8((uint32_t)bins * 768u + i); }
+    __device__ __forceinline__ int32_t vlook(uint32_t i) const { return (int32_t)t[(uint32_t)bins * 512u + i]; }
+};
+
+// DsdUtils modes 0 (raw bytes) and 1 (init_dsd_block_fast + decode_fast,
+// DsdUtils.cs:149-304), wave-uniform, channel count a template parameter.
+// Same results and status bits as decode_dsd_block (wv_decode_core.h).
+template <int WCH, bool FAST>
+__device__ __forceinline__ DsdResult dsd_simple_wave(const BlockDesc &d, const uint8_t *blob, const uint8_t *tables,
+                                                     DevStoreWave &out) {
+    using namespace wvf;
+    const bool fstereo = (d.flags & FALSE_STEREO) != 0;
+    const uint32_t och = (d.flags & MONO_FLAG) ? 1u : 2u;
+    const uint32_t dlen = d.dsd_data_len;
+    ByteSrcWave src;
+    src.init(blob + d.bits_off);
+    DsdTablesWave tb;
+    tb.t = (w2::cdw_ptr)(tables + d.dsd_table_off);
+    tb.bins = d.dsd_history_bins;
+    const uint32_t bmask = (uint32_t)d.dsd_history_bins - 1u;
+    uint32_t bp = 0;
+    int32_t crc = -1;
+    DsdResult res = {0, 0};
+    bool mute = false;
+    uint32_t low = 0, high = 0xFFFFFFFFu, value = 0;
+    uint32_t p0 = 0, p1 = 0;
+    if (FAST)
+        for (int i = 0; i < 4; i++) value = (value << 8) | src.byte(bp++);
+    uint32_t f = 0, chunk_len = d.first_chunk, ci = 0;
+    while (f < d.nframes) {
+        uint32_t n = chunk_len;
+        if (n > d.nframes - f) n = d.nframes - f;
+        bool chunk_ok = true;
+        if (!mute) {
+            for (uint32_t j = 0; j < n && chunk_ok; j++) {
+                int32_t v[2] = {0, 0};
+#pragma unroll
+                for (int c = 0; c < WCH; c++) {
+                    uint32_t code;
+                    if (!FAST) {
+                        code = bp < dlen ? src.byte(bp) : 0u;
+                        bp++;
+                    } else {
+                        const uint32_t pi = p0 * 256u;
+                        const uint32_t tot = tb.summed(pi + 255u);
+                        if (tot == 0) { chunk_ok = false; break; }
+                        uint32_t mult = (high - low) / tot;
+                        if (mult == 0) {
+                            if (dlen - bp >= 4)
+                                for (int i = 0; i < 4; i++) value = (value << 8) | src.byte(bp++);
+                            low = 0;
+                            high = 0xFFFFFFFFu;
+                            mult = high / tot;
+                            if (mult == 0) { chunk_ok = false; break; }
+                        }
+                        const uint32_t index = (value - low) / mult;
+                        if (index >= tot) { chunk_ok = false; break; }
+                        code = tb.lookup((uint32_t)tb.vlook(p0) + index);
+                        if (code > 0) low += tb.summed(pi + code - 1u) * mult;
+                        high = low + tb.prob(pi + code) * mult - 1u;
+                        if (WCH == 1) {
+                            p0 = code & bmask;
+                        } else {
+                            p0 = p1;
+                            p1 = code & bmask;
+                        }
+                        while (((high ^ low) & 0xFF000000u) == 0 && bp < dlen) {
+                            value = (value << 8) | src.byte(bp++);
+                            high = (high << 8) | 0xFF;
+                            low <<= 8;
+                        }
+                    }
+                    v[c] = (int32_t)code;
+                }
+                if (!chunk_ok) break;
+#pragma unroll
+                for (int c = 0; c < WCH; c++) crc = add32(crc, add32(shl32(crc, 1), v[c]));
+                const uint64_t o = (uint64_t)(f + j) * och;
+                if (WCH == 1 && !fstereo) {
+                    out.put(o, v[0]);
+                } else if (fstereo) {
+                    out.put(o, v[0]);
+                    out.put(o + 1, v[0]);
+                } else {
+                    out.put(o, v[0]);
+                    out.put(o + 1, v[1]);
+                }
+            }
+            if (!chunk_ok) {
+                mute = true;
+                res.status |= ST_NONDET;  // the rest of this chunk's region keeps stale caller data
+            }
+            // DsdUtils.cs:99-101: the final chunk checks the crc and mutes on mismatch
+            if (!mute && f + n == d.block_samples && crc != d.crc) mute = true;
+        }
+        if (mute && !(res.status & ST_DSD_MUTE)) {
+            res.status |= ST_DSD_MUTE;
+            res.mute_chunk = ci;
+        }
+        f += n;
+        chunk_len = next_call_len(d, f);
+        ci++;
+    }
+    if (d.nframes == d.block_samples) {
+        res.status |= ST_CRC_CHECKED;
+        if (crc != d.crc) res.status |= ST_CRC_ERROR;
+    }
+    return res;
+}
+
 extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_wave(const BlockDesc *__restrict__ descs,
                                                                     const uint32_t *__restrict__ list,
                                                                     const uint8_t *__restrict__ blob,
@@ -263,6 +385,12 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_wave(const BlockD
     if (d.kind == KIND_DSD_HIGH)
         r = (d.flags & wvf::MONO_DATA) ? dsd_high_wave<1>(d, blob, tables, pt_lds, st)
                                        : dsd_high_wave<2>(d, blob, tables, pt_lds, st);
+    else if (d.kind == KIND_DSD_FAST)
+        r = (d.flags & wvf::MONO_DATA) ? dsd_simple_wave<1, true>(d, blob, tables, st)
+                                       : dsd_simple_wave<2, true>(d, blob, tables, st);
+    else if (d.kind == KIND_DSD_RAW)
+        r = (d.flags & wvf::MONO_DATA) ? dsd_simple_wave<1, false>(d, blob, tables, st)
+                                       : dsd_simple_wave<2, false>(d, blob, tables, st);
     else
         r = decode_dsd_block(d, blob, tables, pt_lds, st);
     if (lead) {
