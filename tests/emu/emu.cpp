@@ -23,6 +23,34 @@ struct HostStore {
 };
 
 extern "C" {
+// Frames n files back to back into one batch the way wvg_batch_add_file does
+// and counts descriptor writes outside their file's reserved output range:
+// *bad_reserved with file_out_extent (the product rule), *bad_values when only
+// the reported values (out_frames x out_nch) were reserved.
+void emu_batch_ranges(const uint8_t *blob, const uint64_t *offs, const uint64_t *lens, int n, int chunk,
+                      int64_t *bad_reserved, int64_t *bad_values) {
+    FramingOutput fo;
+    fo.defer_values = true;
+    *bad_reserved = *bad_values = 0;
+    int64_t base = 0;
+    for (int i = 0; i < n; i++) {
+        FileInfo fi;
+        frame_file(blob + offs[i], (size_t)lens[i], offs[i], (uint64_t)base, 0, chunk, fo, fi);
+        if (!fi.open_ok) continue;
+        const int64_t ext = file_out_extent(fo, fi, (uint64_t)base);
+        const int64_t vals = fi.out_frames * fi.out_nch;
+        for (int64_t k = fi.first_desc; k < fi.first_desc + fi.num_desc; k++) {
+            const BlockDesc &d = fo.descs[(size_t)k];
+            if (d.kind == KIND_SKIP) continue;
+            const int64_t lo = (int64_t)d.out_off - base + (int64_t)d.pre_end * d.out_nch;
+            const int64_t hi = (int64_t)d.out_off - base + (int64_t)d.nframes * d.out_nch;
+            if (lo < 0 || hi > ext) (*bad_reserved)++;
+            if (lo < 0 || hi > vals) (*bad_values)++;
+        }
+        base += ext;
+    }
+}
+
 // Returns frames (or -2 open error, -3 exception); fills out (cap ints).
 // seek_to >= 0: as a caller that calls SetSample(seek_to) first (*seek_rc: its result).
 int64_t emu_decode_from(const uint8_t *file, size_t len, int64_t seek_to, int chunk, int32_t *out, int64_t cap,

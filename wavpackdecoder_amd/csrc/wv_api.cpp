@@ -237,15 +237,8 @@ static int add_file(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open
         b->segs.push_back(g);
     }
     b->pcm_bytes += nvals * wi.bytes_per_sample;
-    // the output range reserved for the file covers every descriptor's writes: a
-    // file that raised the reference's exception mid-call has descriptors that run
-    // past its reported frames, and they must not land in the next file's range
-    int64_t extent = nvals;
-    for (int64_t k = fi.first_desc; k < fi.first_desc + fi.num_desc; k++) {
-        const BlockDesc &d = b->fo.descs[(size_t)k];
-        const int64_t e = (int64_t)d.out_off - b->out_ints + (int64_t)d.nframes * (int64_t)d.out_nch;
-        if (e > extent) extent = e;
-    }
+    // the output range reserved for the file covers every descriptor's writes
+    const int64_t extent = file_out_extent(b->fo, fi, (uint64_t)b->out_ints);
     b->out_ints += extent;
     for (int64_t k = fi.first_desc; k < fi.first_desc + fi.num_desc; k++) {
         const BlockDesc &d = b->fo.descs[(size_t)k];

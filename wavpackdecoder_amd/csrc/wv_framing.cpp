@@ -991,6 +991,16 @@ void apply_meta_jobs(FramingOutput &out, const uint8_t *blob) {
         for (uint32_t k = 0; k < j.count; k++) meta_apply(out.descs[j.desc], out.items[j.first + k], blob);
 }
 
+int64_t file_out_extent(const FramingOutput &out, const FileInfo &info, uint64_t out_base_ints) {
+    int64_t extent = info.out_frames * info.out_nch;
+    for (int64_t k = info.first_desc; k < info.first_desc + info.num_desc; k++) {
+        const BlockDesc &d = out.descs[(size_t)k];
+        const int64_t e = (int64_t)(d.out_off - out_base_ints) + (int64_t)d.nframes * (int64_t)d.out_nch;
+        if (e > extent) extent = e;
+    }
+    return extent;
+}
+
 int compute_mode(const FileInfo &info) {  // WavPackUtils.cs:133-167 (fields captured at open)
     return info.mode;
 }

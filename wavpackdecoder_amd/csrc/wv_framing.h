@@ -65,6 +65,12 @@ void apply_meta_jobs(FramingOutput &out, const uint8_t *blob);
 void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t out_base_ints, uint32_t open_flags,
                 int chunk, FramingOutput &out, FileInfo &info, int64_t seek_to = -1);
 
+// Output ints a batch reserves for a framed file: its reported values
+// (out_frames x out_nch) or more when a descriptor writes past them -- a file
+// that raised the C# exception mid-call keeps the descriptor of that call,
+// whose writes must not reach the next file's range.
+int64_t file_out_extent(const FramingOutput &out, const FileInfo &info, uint64_t out_base_ints);
+
 // WavpackGetMode (WavPackUtils.cs:133-167) from the framed context values
 int compute_mode(const FileInfo &info);
 
