@@ -31,20 +31,28 @@
 namespace wvg {
 
 #if defined(__HIPCC__)
-__constant__ uint8_t c_exp2_table[256] = {WVF_EXP2_TABLE};
-__constant__ uint8_t c_log2_table[256] = {WVF_LOG2_TABLE};
+__constant__ __attribute__((aligned(16))) uint8_t c_exp2_table[256] = {WVF_EXP2_TABLE};
+__constant__ __attribute__((aligned(16))) uint8_t c_log2_table[256] = {WVF_LOG2_TABLE};
+// A byte table read as the dword holding the byte, through the constant address
+// space: with a wave-uniform index (the parser wave, the wave-per-block kernels)
+// that is a scalar-cache load instead of a vector byte load and its memory
+// latency on the serial path; a divergent index still compiles to a vector load.
+__device__ __forceinline__ int tab_byte(const uint8_t *t, int i) {
+    typedef const __attribute__((address_space(4))) uint32_t *cdw;
+    return (int)((((cdw)t)[(unsigned)i >> 2] >> (((unsigned)i & 3u) * 8u)) & 0xFFu);
+}
 #endif
 
 WVF_HD int tab_exp2(int i) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    return c_exp2_table[i];
+    return tab_byte(c_exp2_table, i);
 #else
     return wvf::host_exp2_table[i];
 #endif
 }
 WVF_HD int tab_log2(int i) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    return c_log2_table[i];
+    return tab_byte(c_log2_table, i);
 #else
     return wvf::host_log2_table[i];
 #endif
