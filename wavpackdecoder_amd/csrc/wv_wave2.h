@@ -1191,6 +1191,15 @@ __device__ __forceinline__ int32_t vupdc(int32_t w, int32_t s, int32_t x, int32_
     return max(-1024, min(1024, vupd(w, s, x, delta)));
 }
 
+// a wave-uniform value kept in a VGPR: the reconstruction wave holds 16 passes'
+// deltas, and as SGPRs they overflowed the scalar file (spilled to VGPR lanes
+// and reloaded with v_readlane inside the frame loop)
+__device__ __forceinline__ int32_t in_vgpr(int32_t s) {
+    int32_t v;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "s"(s));
+    return v;
+}
+
 template <int T>
 struct VPass {
     static constexpr int NH = (T >= 17) ? 2 : ((T >= 1) ? 8 : ((T < 0) ? 8 : 1));
@@ -1200,7 +1209,7 @@ struct VPass {
 
     __device__ __forceinline__ void init(const BlockDesc &d, int p, bool isB) {
         w = isB ? d.weight_B[p] : d.weight_A[p];
-        delta = d.delta[p];
+        delta = in_vgpr(d.delta[p]);
 #pragma unroll
         for (int i = 0; i < NH; i++) h[i] = 0;
         if (T >= 17) {
@@ -1216,7 +1225,7 @@ struct VPass {
     }
     __device__ __forceinline__ void init_stereo_neg(const BlockDesc &d, int p, bool isB) {
         w = isB ? d.weight_B[p] : d.weight_A[p];
-        delta = d.delta[p];
+        delta = in_vgpr(d.delta[p]);
 #pragma unroll
         for (int i = 0; i < NH; i++) h[i] = 0;
         h[0] = isB ? d.samples_B[p][0] : d.samples_A[p][0];
