@@ -4,10 +4,14 @@
 //   wv_pcm_2wave<terms> : one workgroup (parser wave + reconstruction wave) per
 //                         PCM block whose decorrelation term list has a
 //                         specialised instantiation (wv_wave2.h).
-//   wv_decode_pcm_lane  : one lane per PCM block; runs decode_pcm_block
+//   wv_decode_pcm_wave  : one wave-uniform decode per PCM block without a
+//                         specialised term set; runs decode_pcm_block
 //                         (get_words -> decorr passes -> joint/CRC/mute ->
 //                         fixup -> int32 store) fused, sample-major.
-//   wv_decode_dsd_lane  : one lane per DSD block (DsdUtils modes 0/1/3).
+//   wv_decode_dsd_wave  : one wave-uniform decode per DSD block (DsdUtils modes
+//                         0/1/3, each a scalar specialisation).
+//   wv_decode_*_lane    : the same decodes one lane per block (A/B runs only,
+//                         WVG_LANE_KERNELS=1).
 //   wv_dsd_fill         : post-pass writing the 0x55 mute fills of DSD blocks in
 //                         call-buffer coordinates (DsdUtils.cs:104-117, quirk B-9).
 //   wv_meta_parse       : one lane per block finishing its descriptor with the
