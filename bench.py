@@ -5,25 +5,32 @@ metric : Msamples/sec decoded (node) + HBM GB/s, batched 44.1 kHz/16-bit stereo 
 step   : one decode of the config-2 batch (1,024 independent WavPack blocks x
          22,050 frames, 16-bit stereo, fast terms {17,17}) already resident in
          HBM -> int32 PCM in HBM (the WavpackUnpackSamples output contract)
-N GPUs : one process per GPU (torch.distributed.run); each rank decodes its
-         own C2-sized shard of blocks (weak scaling, per-GPU file partition);
-         no data-path collective -- only a CPU (gloo) barrier and a max-reduce
-         of the timings.
+N GPUs : one process per GPU.  Under torch.distributed.run the ranks come from
+         the environment (WORLD_SIZE must equal --gpus); `python bench.py --gpus N`
+         alone spawns the N rank processes itself (the parent never touches a GPU).
+         --workload c2 (default, weak scaling): every rank decodes its own copy of
+         the C2 batch, so per-GPU work is identical at every N.
+         --workload c5 (strong scaling): a fixed slice of the mixed corpus (C5) is
+         file-partitioned across the ranks (LPT on estimated device cost).
+         No data-path collective: only a CPU (gloo) barrier and max/sum reduces.
 value  : frames decoded by all ranks / max-over-ranks wall time of the K steps.
 
 Also printed in the same JSON line:
   roofline     : algorithmic bytes per launch (compressed bytes in + int32
                  out) / mean device time per launch measured
                  with hipEvents on the decode stream, vs 8 TB/s HBM peak.
-  cpu_baseline : the oracle (C restatement of the reference algorithm,
-                 kind "port") decoding the same C2 file split across host
-                 threads, on rank 0 only.
+  cpu_baseline : the oracle (C restatement of the reference algorithm, kind
+                 "port") on rank 0 only: one decoder context per thread on the
+                 physical cores of one socket that this process may use
+                 (BASELINE.md:35-38), plus a single-thread figure.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,17 +40,49 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+METRIC = "Msamples/sec decoded (node) + HBM GB/s, batched 44.1kHz/16-bit stereo blocks"
 
 
-def _dist():
+# ---------------------------------------------------------------------------
+# process layout
+# ---------------------------------------------------------------------------
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n: int, argv: list[str]) -> int:
+    """`bench.py --gpus N` without a launcher: start N rank processes (children,
+    never an exec; this parent initialises nothing on the GPU) and return the
+    worst exit code.  Rank 0 prints the JSON line."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
+
+
+def _dist(gpus: int):
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws != gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={ws} but --gpus {gpus}")
     pg = None
     if ws > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=ws)  # CPU barrier + timing reduce only
+        dist.init_process_group("gloo", rank=rank, world_size=ws)  # CPU barrier + timing reduces only
         pg = dist
     return ws, rank, local, pg
 
@@ -53,24 +92,27 @@ def _barrier(pg):
         pg.barrier()
 
 
-def _max(pg, v: float) -> float:
+def _reduce(pg, v: float, op: str) -> float:
     if pg is None:
         return v
     import torch
     t = torch.tensor([v], dtype=torch.float64)
-    pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    pg.all_reduce(t, op=pg.ReduceOp.MAX if op == "max" else pg.ReduceOp.SUM)
     return float(t.item())
 
 
-def _sum(pg, v: float) -> float:
+def _gather(pg, v: float, ws: int) -> list[float]:
     if pg is None:
-        return v
+        return [v]
     import torch
-    t = torch.tensor([v], dtype=torch.float64)
-    pg.all_reduce(t, op=pg.ReduceOp.SUM)
-    return float(t.item())
+    out = [torch.zeros(1, dtype=torch.float64) for _ in range(ws)]
+    pg.all_gather(out, torch.tensor([v], dtype=torch.float64))
+    return [float(t.item()) for t in out]
 
 
+# ---------------------------------------------------------------------------
+# workload helpers
+# ---------------------------------------------------------------------------
 def split_blocks(data: bytes, parts: int):
     """Split a multi-block .wv file at block boundaries into `parts` files."""
     offs = []
@@ -88,12 +130,15 @@ def split_blocks(data: bytes, parts: int):
     return [data[offs[k]:offs[min(k + per, nb)]] for k in range(0, nb, per)]
 
 
-def algorithmic_bytes(data: bytes, nch: int = 2) -> int:
-    """sum(ckSize + 8) + sum(block_samples * nch * 4)."""
+def algorithmic_bytes(data: bytes) -> int:
+    """sum(ckSize + 8) + sum(block_samples * nch_out * 4) over the
+    decoded blocks (INITIAL blocks; nch_out from the MONO_FLAG)."""
     i, tot = 0, 0
     while i + 32 <= len(data) and data[i:i + 4] == b"wvpk":
         ck = int.from_bytes(data[i + 4:i + 8], "little")
         bs = int.from_bytes(data[i + 20:i + 24], "little")
+        flags = int.from_bytes(data[i + 24:i + 28], "little")
+        nch = 1 if flags & 4 else 2
         tot += ck + 8 + bs * nch * 4
         i += ck + 8
     return tot
@@ -114,8 +159,37 @@ def pmc_traffic(kernel_substr: str = "wv_pcm_2wave<17, 17>"):
     return float(best[1]["traffic_bytes_per_launch"]), os.path.relpath(best[0], ROOT)
 
 
-def cpu_baseline(data: bytes, threads: int, reps: int):
-    """Oracle (C port of the reference path) on host threads; ctypes drops the GIL."""
+# ---------------------------------------------------------------------------
+# CPU baseline (BASELINE.md:35-38)
+# ---------------------------------------------------------------------------
+def cpu_topology() -> dict:
+    """Physical cores per socket and sockets (lscpu), CPUs this process may run on
+    (sched_getaffinity) and the lease's worker-thread share (OMP_NUM_THREADS)."""
+    topo = {"model": None, "sockets": None, "cores_per_socket": None, "threads_per_core": None}
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=20).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "Model name":
+                topo["model"] = v
+            elif k == "Socket(s)":
+                topo["sockets"] = int(v)
+            elif k == "Core(s) per socket":
+                topo["cores_per_socket"] = int(v)
+            elif k == "Thread(s) per core":
+                topo["threads_per_core"] = int(v)
+    except (OSError, ValueError, subprocess.SubprocessError):
+        pass
+    topo["affinity_cpus"] = len(os.sched_getaffinity(0))
+    share = os.environ.get("OMP_NUM_THREADS")
+    topo["lease_threads"] = int(share) if share and share.isdigit() else None
+    return topo
+
+
+def cpu_decode_rate(data: bytes, threads: int, reps: int):
+    """Oracle (C port of the reference path) on `threads` host threads, one decoder
+    context per thread over its share of the blocks; ctypes drops the GIL."""
     from concurrent.futures import ThreadPoolExecutor
 
     from oracle import oracle as O
@@ -133,52 +207,96 @@ def cpu_baseline(data: bytes, threads: int, reps: int):
     return frames / t / 1e6, t, frames
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--blocks", type=int, default=1024)
-    ap.add_argument("--block-frames", type=int, default=22050)
-    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("WV_CPU_THREADS", "16")))
-    ap.add_argument("--cpu-reps", type=int, default=5)
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--check", action="store_true", help="verify the decoded PCM against the generator's")
-    args = ap.parse_args()
+def cpu_baseline(data: bytes, reps: int, force_threads: int | None):
+    topo = cpu_topology()
+    cps = topo["cores_per_socket"] or topo["affinity_cpus"]
+    usable = min(topo["affinity_cpus"], topo["lease_threads"] or topo["affinity_cpus"])
+    threads = force_threads or max(1, min(cps, usable))
+    capped = threads < cps
+    v, t, fr = cpu_decode_rate(data, threads, reps)
+    # single thread on a bounded sample (~1/8 of the batch's blocks)
+    sample = split_blocks(data, 8)[0]
+    v1, t1, fr1 = cpu_decode_rate(sample, 1, max(1, min(reps, 3)))
+    per_core = v1
+    socket_est = per_core * cps  # linear per-core scaling to one socket (an upper bound for the CPU)
+    return {
+        "value": round(v, 2), "unit": "Msamples/s", "cores": threads, "kind": "port",
+        "sample": (f"oracle (C restatement of the C# path, -O2) decoding the full C2 file ({fr} frames) split at "
+                   f"block boundaries over {threads} threads, 4096-frame calls, median of {reps} runs; single "
+                   f"thread on {fr1} frames"),
+        "single_thread": round(v1, 2),
+        "socket": {"model": topo["model"], "sockets": topo["sockets"], "cores_per_socket": cps,
+                   "threads_per_core": topo["threads_per_core"], "affinity_cpus": topo["affinity_cpus"],
+                   "lease_threads": topo["lease_threads"],
+                   "capped_by_lease": capped,
+                   "per_core_scaled_to_socket": round(socket_est, 2)},
+    }
 
-    ws, rank, local, pg = _dist()
+
+# ---------------------------------------------------------------------------
+# one rank
+# ---------------------------------------------------------------------------
+def run_selftest(args) -> None:
+    """--selftest-dist: the process layout and the host reductions alone (no GPU):
+    what tests/test_bench_spawn.py checks on CPU with gloo."""
+    ws, rank, local, pg = _dist(args.gpus)
+    _barrier(pg)
+    tot = _reduce(pg, float(rank + 1), "sum")
+    mx = _reduce(pg, float(rank), "max")
+    allv = _gather(pg, float(10 * rank + local), ws)
+    if rank == 0:
+        print(json.dumps({"n_gpus": ws, "sum": tot, "max": mx, "gathered": allv}), flush=True)
+    if pg is not None:
+        pg.destroy_process_group()
+
+
+def run_rank(args) -> None:
+    if args.selftest_dist:
+        return run_selftest(args)
+    ws, rank, local, pg = _dist(args.gpus)
 
     from synth import corpora
     from wavpackdecoder_amd import _lib
+    import wavpackdecoder_amd.api as api
     from wavpackdecoder_amd.api import DecodeBatch
 
-    # each rank: its own C2-sized shard (rank 0 = the canonical C2 batch)
-    pcm, data = corpora.c2(nblocks=args.blocks, block=args.block_frames, return_pcm=True) if rank == 0 else (None, None)
-    if rank != 0:
-        data = corpora.c2_shard(rank, nblocks=args.blocks, block=args.block_frames)
+    pcm = None
+    if args.workload == "c2":
+        # every rank decodes its own copy of the C2 batch (identical per-GPU work at every N)
+        pcm, data = corpora.c2(nblocks=args.blocks, block=args.block_frames, return_pcm=True)
+        files = [data]
+        workload = "C2: 1024-block batch, 16-bit stereo 'fast' {17,17}, joint stereo, 44.1 kHz"
+        scaling = "weak"
+    else:
+        from wavpackdecoder_amd import shard
+        costs = [corpora.c5_cost(i) for i in range(args.c5_files)]
+        mine = shard.partition([int(c) for c in costs], ws)[rank]
+        files = [corpora.c5_file(i) for i in mine]
+        workload = f"C5: files 0..{args.c5_files - 1} of the mixed corpus, LPT file partition over {ws} GPU(s)"
+        scaling = "strong"
 
     L = _lib.lib()
-    import wavpackdecoder_amd.api as api
     api._ctx = L.wvg_open(local)
     if not api._ctx:
         raise SystemExit("no GPU")
 
     b = DecodeBatch(4096)
-    fi = b.add_file(data)
-    assert fi == 0
+    for f in files:
+        b.add_file(f)
     b.upload()
     frames_rank = b.frames
-    alg_bytes = algorithmic_bytes(data)
+    alg_bytes = sum(algorithmic_bytes(f) for f in files)
 
     for _ in range(args.warmup):
         b.decode()
     b.sync()
-    if args.check:
+    crc = 0
+    if args.check or args.workload == "c5":
         out = b.download()
-        if pcm is not None:
+        if pcm is not None and args.check:
             assert np.array_equal(out, pcm.reshape(-1)), "decoded PCM differs from the generator's"
-        r = b.result(0)
-        assert r.crc_errors == 0
+        crc = sum(b.result(i).crc_errors for i in range(len(files)) if b.infos[i].open_ok)
+        assert crc == 0, "CRC errors in a synthetic corpus"
 
     # device time per launch (hipEvents on the decode stream)
     kernel_ms = b.time(max(args.steps, 1))
@@ -191,33 +309,41 @@ def main():
     b.sync()
     t1 = time.perf_counter()
     _barrier(pg)
-    dt = _max(pg, t1 - t0)
-    frames_total = _sum(pg, float(frames_rank))
+    dt = _reduce(pg, t1 - t0, "max")
+    frames_total = _reduce(pg, float(frames_rank), "sum")
+    kms_all = _gather(pg, kernel_ms, ws)
     value = frames_total * args.steps / dt / 1e6
 
-    # PCIe-inclusive rate (host bytes in -> host int32 out), reported beside `value`, never as it
-    host_out = np.empty(max(b.out_ints, 1), dtype=np.int32)
+    # PCIe-inclusive rate (host bytes in -> host int32 out, framing included),
+    # reported beside `value`, never as it
     t_e2e = time.perf_counter()
-    b.upload()
-    b.decode()
-    b.sync()
-    b._check(b._L.wvg_batch_download(b._b, host_out.ctypes.data, host_out.size))
+    be = DecodeBatch(4096)
+    for f in files:
+        be.add_file(f)
+    be.upload()
+    be.decode()
+    host_out = np.empty(max(be.out_ints, 1), dtype=np.int32)
+    be._check(be._L.wvg_batch_download(be._b, host_out.ctypes.data, host_out.size))
     t_e2e = time.perf_counter() - t_e2e
+    be.close()
     e2e = frames_rank / t_e2e / 1e6
 
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic()
-    line = None
+    traffic, traffic_src = pmc_traffic() if args.workload == "c2" else (None, None)
     if rank == 0:
         cpu = None
-        if not args.no_cpu:
-            v, t, fr = cpu_baseline(data, args.cpu_threads, args.cpu_reps)
-            cpu = {"value": round(v, 2), "unit": "Msamples/s", "cores": args.cpu_threads, "kind": "port",
-                   "sample": f"oracle (C restatement of the C# path) decoding the full C2 file ({fr} frames) split "
-                             f"at block boundaries over {args.cpu_threads} threads, 4096-frame calls, median of "
-                             f"{args.cpu_reps} runs"}
+        if not args.no_cpu and args.workload == "c2":
+            cpu = cpu_baseline(files[0], args.cpu_reps, args.cpu_threads)
+        vs = None
+        if cpu is not None:
+            vs = {"measured": round(value / cpu["value"], 2),
+                  "per_gpu_vs_measured": round(value / ws / cpu["value"], 2),
+                  "per_gpu_vs_socket_scaled": round(value / ws / cpu["socket"]["per_core_scaled_to_socket"], 2),
+                  "per_gpu_vs_single_thread": round(value / ws / cpu["single_thread"], 2),
+                  "note": "ratios against the CPU baseline measured in this run (BASELINE.md has no published "
+                          "number); socket_scaled = single-thread rate x physical cores of one socket"}
         line = {
-            "metric": "Msamples/sec decoded (node) + HBM GB/s, batched 44.1kHz/16-bit stereo blocks",
+            "metric": METRIC,
             "value": round(value, 2),
             "unit": "Msamples/s",
             "n_gpus": ws,
@@ -225,21 +351,27 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
+            "scaling": scaling,
+            "vs_baseline": vs["measured"] if vs else None,
+            "vs_cpu": vs,
             "dtype": "int32",
-            "data": "synthetic (repo encoder, seeds 0xC2+block)",
-            "config": {"workload": "C2: 1024-block batch, 16-bit stereo 'fast' {17,17}, joint stereo, 44.1 kHz",
-                       "blocks_per_gpu": args.blocks, "block_frames": args.block_frames, "chunk_frames": 4096,
-                       "frames_per_gpu": int(frames_rank), "compressed_bytes_per_gpu": len(data),
+            "data": "synthetic (repo encoder; C2 seeds 0xC2+block, C5 seeds per file index)",
+            "config": {"workload": workload,
+                       "files_per_gpu_rank0": len(files), "blocks_rank0": b.num_blocks,
+                       "block_frames": args.block_frames if args.workload == "c2" else None, "chunk_frames": 4096,
+                       "frames_rank0": int(frames_rank), "frames_total": int(frames_total),
+                       "compressed_bytes_rank0": sum(len(f) for f in files),
                        "parallelism": f"file-shard x{ws}, no collectives"},
+            "per_rank_kernel_ms": [round(x, 4) for x in kms_all],
             "hbm_gbs": round(achieved, 2),
             "pcie_inclusive": {"value": round(e2e, 2), "unit": "Msamples/s", "ms": round(t_e2e * 1e3, 3),
-                               "what": "upload of the compressed batch + decode + download of int32 PCM, rank 0"},
+                               "what": "host framing + upload of the compressed batch + decode + download of "
+                                       "int32 PCM, rank 0"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": None if traffic is None else int(traffic),
-                         "traffic_unit": "bytes/launch (PMC FETCH_SIZE + WRITE_SIZE, scale calibrated in the profile)", "traffic_source": traffic_src,
+                         "traffic_unit": "bytes/launch (PMC FETCH_SIZE + WRITE_SIZE, scale calibrated in the profile)",
+                         "traffic_source": traffic_src,
                          "kernel_ms": round(kernel_ms, 4), "alg_bytes_per_launch": alg_bytes,
                          "binding_limit": "serial entropy decode per block (scalar issue of one wave), not HBM"},
             "cpu_baseline": cpu,
@@ -248,6 +380,26 @@ def main():
     b.close()
     if pg is not None:
         pg.destroy_process_group()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", choices=("c2", "c5"), default="c2")
+    ap.add_argument("--blocks", type=int, default=1024)
+    ap.add_argument("--block-frames", type=int, default=22050)
+    ap.add_argument("--c5-files", type=int, default=4000)
+    ap.add_argument("--cpu-threads", type=int, default=None, help="override the socket/lease-derived thread count")
+    ap.add_argument("--cpu-reps", type=int, default=5)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--check", action="store_true", help="verify the decoded PCM against the generator's")
+    ap.add_argument("--selftest-dist", action="store_true", help=argparse.SUPPRESS)
+    args = ap.parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    run_rank(args)
 
 
 if __name__ == "__main__":

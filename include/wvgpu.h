@@ -38,6 +38,7 @@ extern "C" {
 #define WVG_ERR_ARG (-2)      /* bad argument / state */
 #define WVG_ERR_OPEN (-3)     /* WavpackOpenFileInput failed (info.error holds the message) */
 #define WVG_ERR_SPACE (-4)    /* caller buffer too small */
+#define WVG_ERR_TIMEOUT (-5)  /* a kernel's bounded wait ran out (a decoder bug, never a property of the stream) */
 
 /* per-block status bits (wvg_file_result.status_or) */
 #define WVG_ST_CRC_CHECKED 0x01u
@@ -48,6 +49,7 @@ extern "C" {
 #define WVG_ST_UNSUPPORTED 0x20u /* depends on decode state of an earlier block (never in well-formed files) */
 #define WVG_ST_DSD_MUTE 0x40u
 #define WVG_ST_NONDET 0x80u      /* reference output depends on stale caller-buffer contents */
+#define WVG_ST_TIMEOUT 0x100u    /* the parser/reconstruction handshake timed out: output invalid (not a reference outcome) */
 
 typedef struct wvg_ctx wvg_ctx;
 typedef struct wvg_batch wvg_batch;
@@ -75,6 +77,8 @@ typedef struct {
     char error[96];
     int32_t seek_result;        /* wvg_batch_add_file_at: SetSample's result (1 true, 0 false, -1 it threw) */
     int32_t reserved;
+    int64_t sample_index0;      /* WavpackGetSampleIndex when the first WavpackUnpackSamples call starts
+                                   (after SetSample: the target); it then advances by the frames returned */
 } wvg_file_info;
 
 typedef struct {
@@ -84,6 +88,8 @@ typedef struct {
     int32_t exception;          /* the reference would have thrown (WvDemo exits 1) */
     uint32_t status_or;         /* OR of the WVG_ST_* bits of all blocks */
     int32_t num_blocks;
+    int64_t exception_frame;    /* with exception: frames the calls before the throwing call returned
+                                   (the throwing call is the one that starts there); -1 otherwise */
 } wvg_file_result;
 
 /* Device + stream ownership.  device < 0 => current device. */
@@ -130,6 +136,11 @@ int wvg_batch_download(wvg_batch *b, int32_t *host_out, int64_t cap_ints);
 int wvg_batch_file_result(wvg_batch *b, int file, wvg_file_result *res);
 /* per-block status words (after download), one per decoded block in file order */
 int wvg_batch_block_status(wvg_batch *b, uint32_t *out, int64_t cap);
+/* The blocks of one file (after download): for block k, end_frame[k] = the number of
+ * frames the caller has received when the block's last frame is unpacked (that is
+ * when WavpackUnpackSamples runs check_crc_error, WavPackUtils.cs:273-275), and its
+ * status word.  Returns the block count, or < 0. */
+int wvg_batch_file_blocks(wvg_batch *b, int file, int64_t *end_frame, uint32_t *status, int64_t cap);
 
 /* Device-side timing of `iters` back-to-back decodes (hipEvents on the
  * batch stream).  *ms receives the average per decode. */

@@ -22,7 +22,7 @@ import numpy as np
 from . import wvsynth as S
 
 _CACHE = os.environ.get("WVSYNTH_CACHE", os.path.join(os.path.expanduser("~"), ".cache", "wvsynth"))
-_VERSION = "v1"
+_VERSION = "v2"
 
 
 def _cached(key: str, make):
@@ -65,8 +65,8 @@ def c3(nblocks: int = 4096, block: int = 44100, return_pcm: bool = False):
     def make():
         parts = [S.audio_like(block, 2, 24, seed=0xC3 + b, sigma=4096.0) for b in range(nblocks)]
         pcm = np.concatenate(parts, axis=0)
-        data = S.encode_pcm(pcm, S.EncParams(terms=S.TERMS_HIGH, bytes_per_sample=3, block_samples=block,
-                                             config_flags=0x800 | 0x1000))
+        data = S.encode_pcm_parallel(pcm, S.EncParams(terms=S.TERMS_HIGH, bytes_per_sample=3, block_samples=block,
+                                                      config_flags=0x800 | 0x1000))
         return {"pcm": pcm, "wv": np.frombuffer(data, dtype=np.uint8)}
     d = _cached(f"c3-{nblocks}-{block}", make)
     data = d["wv"].tobytes()
@@ -121,6 +121,35 @@ def c5_file(i: int) -> bytes:
     mode = (0, 1, 3)[int(rng.integers(0, 3))]
     dd = S.dsd_random_like(frames, 2, seed=i, density=float(rng.uniform(0.3, 0.7)))
     return S.encode_dsd(dd, S.DsdParams(nch=2, mode=mode, block_samples=B))
+
+
+# relative device cost per frame of a block of each C5 kind (one serial chain per
+# block; DESIGN.md §6 per-mode timings): used to balance a strong-scaling split
+C5_COST = {"stereo16": 1.0, "mono16": 0.6, "stereo24": 1.6, "mono24": 1.0, "dsd0": 1.0, "dsd1": 4.5, "dsd3": 12.5}
+
+
+def c5_meta(i: int):
+    """(kind, frames) of file i of the mixed corpus without encoding it (the same
+    draws as c5_file)."""
+    rng = np.random.default_rng(0xC5 * 1_000_003 + i)
+    u = rng.random()
+    nblk = int(rng.integers(1, 3))
+    B = int(rng.integers(4410, 22051))
+    frames = nblk * B - int(rng.integers(0, B // 2))
+    if u < 0.40:
+        return "stereo16", frames
+    if u < 0.60:
+        return "mono16", frames
+    if u < 0.85:
+        return "stereo24", frames
+    if u < 0.90:
+        return "mono24", frames
+    return "dsd%d" % (0, 1, 3)[int(rng.integers(0, 3))], frames
+
+
+def c5_cost(i: int) -> float:
+    kind, frames = c5_meta(i)
+    return C5_COST[kind] * frames
 
 
 def c5(nfiles: int, start: int = 0):

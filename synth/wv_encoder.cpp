@@ -58,6 +58,15 @@ struct wvenc_params {
     int32_t total_unknown;     // write total_samples = 0xFFFFFFFF
     int32_t extras;            // bit0: DUMMY sub-block, bit1: unknown optional sub-block, bit2: NEW_CONFIG
     int32_t mag_override;      // >= 0 forces the MAG field
+    // INT32_DATA beyond `zeros` (UnpackUtils.cs:367-382, 1263-1345) and the
+    // extra wvx stream (init_wvx_bitstream, UnpackUtils.cs:115-147)
+    int32_t int32_sent_bits;   // low bits carried in the wvx stream (or dropped: lossy)
+    int32_t int32_ones;        // trailing one bits removed
+    int32_t int32_dups;        // trailing duplicated bits removed
+    int32_t wvx;               // 0 none, 1 ID_WVX_BITSTREAM, 2 ID_WVX_NEW_BITSTREAM
+    int32_t wvx_max_width;     // NEW variant: the 5-bit int32_max_width field (0 = none)
+    int32_t wvx_short;         // drop this many bytes from the end of every wvx payload (over-read tests)
+    int64_t total_override;    // > 0: header total_samples (a file encoded in parallel parts, then concatenated)
 };
 
 struct wvenc_dsd_params {
@@ -596,6 +605,93 @@ std::vector<uint8_t> riff_header(int nch, int bps, int bits, int rate, int64_t f
 // -------------------------------------------------------------------------
 // PCM file encoder
 // -------------------------------------------------------------------------
+// The int32 fixup of fixup_samples (UnpackUtils.cs:1263-1345) seen from the
+// encoder: how a pre-shift value v maps to the word coded in the main stream
+// (and the low bits coded in the wvx stream).
+struct Int32Map {
+    int mode = 0;  // 0: plain shift, 1: zeros/ones/dups per value, 2: wvx
+    int S = 0, Z = 0, O = 0, D = 0, shift = 0, maxw = 0;
+    // inverse of the decoder's zeros/ones/dups (UnpackUtils.cs:1300-1305)
+    int32_t inv_zod(int32_t v) const {
+        if (Z) return sar32(v, Z);
+        if (O) return sub32(sar32(add32(v, 1), O), 1);
+        if (D) return sar32(v, D);
+        return v;
+    }
+    int32_t zod(int32_t x) const {
+        if (Z) return shl32(x, Z);
+        if (O) return sub32(shl32(add32(x, 1), O), 1);
+        if (D) return sub32(shl32(add32(x, x & 1), D), x & 1);
+        return x;
+    }
+};
+
+Int32Map int32_map(const wvenc_params &P, uint32_t flags) {
+    Int32Map m;
+    m.S = P.int32_sent_bits;
+    m.Z = P.int32_zeros;
+    m.O = P.int32_ones;
+    m.D = P.int32_dups;
+    m.shift = P.shift;
+    m.maxw = P.wvx == 2 ? P.wvx_max_width : 0;
+    if (!(flags & INT32_DATA)) return m;
+    if (P.wvx) {
+        m.mode = 2;
+    } else if (m.S == 0 && (m.Z + m.O + m.D) != 0) {
+        m.mode = 1;
+        while ((flags & HYBRID_FLAG) && (flags & BYTES_STORED) == 3 && m.shift < 8) {  // :1318-1330
+            if (m.Z > 0) m.Z--;
+            else if (m.O > 0) m.O--;
+            else if (m.D > 0) m.D--;
+            else break;
+            m.shift++;
+        }
+    } else {
+        m.shift += m.Z + m.S + m.O + m.D;  // :1344-1345
+    }
+    return m;
+}
+
+// The reference's wvx fixup (UnpackUtils.cs:1271-1314) replayed over the
+// finished wvx stream, with BitsUtils.getbits' semantics (:37-68): the value
+// getbits returns is the unmasked shift register, i.e. every bit up to the next
+// byte boundary past the bits read, and fixup masks it with the sent_bits mask,
+// not the bits_to_read one.  So with max_width the low bits of a value can
+// pick up the first bits of the next one; the replay gives the values (and
+// crc_x) the reference produces.  Without max_width they are exactly v.
+int32_t replay_wvx(const Int32Map &im, bool fresh_new, const std::vector<uint8_t> &xb, const std::vector<int32_t> &ys,
+                   const std::vector<int32_t> &vs, bool lossless) {
+    uint64_t p = fresh_new ? 5 : 0;  // bit position (the NEW variant's max_width field was read at init)
+    auto bit_at = [&](uint64_t q) -> uint32_t { return q / 8 < xb.size() ? (xb[q / 8] >> (q % 8)) & 1u : 0u; };
+    const uint32_t mask = (uint32_t)shl32(1, im.S) - 1u;
+    int32_t crc = -1;
+    for (size_t i = 0; i < ys.size(); i++) {
+        int32_t x = ys[i];
+        if (im.S > 0) {
+            int btr = im.S;
+            bool read = true;
+            if (im.maxw > 0) {
+                int32_t pv = x < 0 ? ~x : x;
+                int width = count_bits_u32((uint32_t)pv) + im.S;
+                read = width <= im.maxw || (btr -= width - im.maxw) > 0;
+            }
+            if (read) {
+                const int bc = btr + (int)((8 - ((p + btr) & 7)) & 7);  // bits in the register after the loop
+                uint32_t sr = 0;
+                for (int k = 0; k < bc && k < 32; k++) sr |= bit_at(p + k) << k;
+                p += btr;
+                const uint32_t data = sr & mask;
+                x = shl32((int32_t)((uint32_t)shl32(x, btr) | data), im.S - btr);
+            } else
+                x = shl32(x, im.S);
+        }
+        x = im.zod(x);
+        if (lossless && im.maxw == 0 && x != vs[i]) throw std::runtime_error("value not representable with this int32/wvx layout");
+        crc = add32(add32(mul32(crc, 9), mul32(x & 0xffff, 3)), (x >> 16) & 0xffff);
+    }
+    return crc;
+}
+
 struct PcmEncoder {
     const wvenc_params &P;
     std::vector<Pass> passes;  // decoder order
@@ -608,7 +704,6 @@ struct PcmEncoder {
     std::vector<uint8_t> encode(const int32_t *x, int64_t frames) {
         std::vector<uint8_t> file;
         const bool mono_block = P.nch == 1 || P.false_stereo;
-        const int wch = mono_block ? 1 : 2;  // channels actually coded
         const int n = P.num_terms;
         passes.assign(n, Pass());
         for (int d = 0; d < n; d++) {
@@ -618,7 +713,8 @@ struct PcmEncoder {
         }
         const int64_t B = P.block_samples;
         int64_t nblocks = frames == 0 ? 0 : (frames + B - 1) / B;
-        int zeros = P.int32_zeros;
+        const bool int32 = P.int32_zeros || P.int32_sent_bits || P.int32_ones || P.int32_dups || (P.wvx && !P.float_data);
+        if (P.wvx && mono_block && P.nch == 2) throw std::runtime_error("wvx with FALSE_STEREO reads stale values");
         for (int64_t bi = 0; bi < nblocks; bi++) {
             int64_t f0 = bi * B;
             int64_t nf = std::min<int64_t>(B, frames - f0);
@@ -648,7 +744,7 @@ struct PcmEncoder {
             if (P.hybrid && P.hybrid_bitrate) flags |= HYBRID_BITRATE;
             if (P.hybrid && P.hybrid_balance && !mono_block) flags |= HYBRID_BALANCE;
             if (P.float_data) flags |= FLOAT_DATA;
-            if (zeros) flags |= INT32_DATA;
+            if (int32) flags |= INT32_DATA;
             flags |= INITIAL_BLOCK | FINAL_BLOCK;
             flags |= ((uint32_t)P.shift << SHIFT_LSB) & SHIFT_MASK;
             flags |= (uint32_t)srate_index(P.sample_rate) << SRATE_LSB;
@@ -656,7 +752,7 @@ struct PcmEncoder {
             // ---- metadata reflecting the start state (quantized the way the
             // decoder will restore it)
             std::vector<uint8_t> md;
-            if (bi == 0 && P.write_riff) {
+            if (bi == 0 && P.write_riff && P.block_index_start == 0) {
                 int bps = P.float_data ? 4 : P.bytes_per_sample;
                 int bits = P.float_data ? 32 : P.bytes_per_sample * 8 - P.shift;
                 put_subblock(md, ID_RIFF_HEADER, riff_header(P.nch, bps, bits, P.sample_rate, frames));
@@ -796,7 +892,38 @@ struct PcmEncoder {
                                            (uint8_t)P.float_norm_exp};
                 put_subblock(md, ID_FLOAT_INFO, fi);
             }
-            if (zeros) put_subblock(md, ID_INT32_INFO, std::vector<uint8_t>{0, (uint8_t)zeros, 0, 0});
+            if (int32)
+                put_subblock(md, ID_INT32_INFO, std::vector<uint8_t>{(uint8_t)P.int32_sent_bits, (uint8_t)P.int32_zeros,
+                                                                     (uint8_t)P.int32_ones, (uint8_t)P.int32_dups});
+            const Int32Map im = int32_map(P, flags);
+            // the wvx stream (UnpackUtils.cs:115-147, 1271-1314): the NEW variant
+            // starts with max_width (int) or two 5-bit float fields
+            BitWriter xw;
+            int32_t crc_x = -1;
+            if (P.wvx == 2) {
+                if (P.float_data) {
+                    xw.put(0, 5);
+                    xw.put(0, 5);
+                } else
+                    xw.put((uint32_t)P.wvx_max_width & 0x1f, 5);
+            }
+            // one value through the decoder's wvx fixup, inverted: y is the decoded
+            // main-stream word, v the pre-shift value it must become
+            std::vector<int32_t> wvx_y, wvx_v;
+            auto wvx_value = [&](int32_t y, int32_t v) {
+                if (im.mode != 2) return;
+                wvx_y.push_back(y);
+                wvx_v.push_back(v);
+                if (im.S <= 0) return;
+                const int32_t u = im.inv_zod(v);
+                int btr = im.S;
+                if (im.maxw > 0) {
+                    int32_t pv = y < 0 ? ~y : y;
+                    int width = count_bits_u32((uint32_t)pv) + im.S;
+                    if (!(width <= im.maxw || (btr -= width - im.maxw) > 0)) return;
+                }
+                xw.put((uint32_t)sar32(u, im.S - btr) & (uint32_t)(shl32(1, btr) - 1), btr);
+            };
 
             // ---- samples: pre-fixup domain values
             WordEncoder we(flags);
@@ -807,10 +934,18 @@ struct PcmEncoder {
             for (int64_t f = 0; f < nf; f++) {
                 const int32_t *xf = x + (f0 + f) * P.nch;
                 int32_t L = xf[0], R = P.nch == 2 ? xf[1] : 0;
-                int sh = P.shift + zeros;
-                if (sh) {
-                    L = sar32(L, sh);
-                    R = sar32(R, sh);
+                int32_t vL = 0, vR = 0;  // pre-shift (post-zod) values: the crc_x input
+                if (im.mode == 2) {
+                    vL = sar32(L, im.shift);
+                    vR = sar32(R, im.shift);
+                    L = sar32(im.inv_zod(vL), im.S);
+                    R = sar32(im.inv_zod(vR), im.S);
+                } else if (im.mode == 1) {
+                    L = im.inv_zod(sar32(L, im.shift));
+                    R = im.inv_zod(sar32(R, im.shift));
+                } else if (im.shift) {
+                    L = sar32(L, im.shift);
+                    R = sar32(R, im.shift);
                 }
                 if (mono_block) {
                     int32_t t = L;
@@ -819,6 +954,7 @@ struct PcmEncoder {
                     int32_t y = r;
                     for (int d = 0; d < n; d++) y = pass_fwd_mono(passes[d], y);
                     crc = add32(mul32(crc, 3), y);
+                    wvx_value(y, vL);
                     uint32_t a = y < 0 ? (uint32_t)(-(int64_t)y) : (uint32_t)y;
                     if (a > maxabs) maxabs = a;
                 } else {
@@ -849,6 +985,8 @@ struct PcmEncoder {
                         yL = add32(yL, yR);
                     }
                     crc = add32(mul32(add32(mul32(crc, 3), yL), 3), yR);
+                    wvx_value(yL, vL);
+                    wvx_value(yR, vR);
                     uint32_t a = yL < 0 ? (uint32_t)(-(int64_t)yL) : (uint32_t)yL;
                     uint32_t b = yR < 0 ? (uint32_t)(-(int64_t)yR) : (uint32_t)yR;
                     if (a > maxabs) maxabs = a;
@@ -863,6 +1001,16 @@ struct PcmEncoder {
             ent = we.w;
             if (bits.empty()) bits.push_back(0);
             put_subblock(md, ID_WV_BITSTREAM, bits);
+            if (P.wvx) {
+                std::vector<uint8_t> xb = xw.finish();
+                if (im.mode == 2) crc_x = replay_wvx(im, P.wvx == 2, xb, wvx_y, wvx_v, !P.hybrid);
+                const int32_t cm = P.float_data ? 0x1234567 : crc_x;  // float: crc_x is never checked (:1418-1420)
+                std::vector<uint8_t> pl = {(uint8_t)cm, (uint8_t)(cm >> 8), (uint8_t)(cm >> 16), (uint8_t)(cm >> 24)};
+                pl.insert(pl.end(), xb.begin(), xb.end());
+                while (pl.size() < 6 || (pl.size() & 1)) pl.push_back(0);  // > 4 bytes, even (:121)
+                for (int k = 0; k < P.wvx_short && pl.size() > 6; k += 2) pl.resize(pl.size() - 2);
+                put_subblock(md, P.wvx == 2 ? ID_WVX_NEW_BITSTREAM : ID_WVX_BITSTREAM, pl);
+            }
             if (bi == nblocks - 1 && P.write_riff) put_subblock(md, ID_RIFF_TRAILER, std::vector<uint8_t>{'t', 'r'});
 
             int mag = P.mag_override >= 0 ? P.mag_override : count_bits_u32(maxabs);
@@ -871,7 +1019,8 @@ struct PcmEncoder {
 
             std::vector<uint8_t> blk(32);
             blk.insert(blk.end(), md.begin(), md.end());
-            write_header(blk, P.version, frames, P.block_index_start + f0, (uint32_t)nf, flags, crc, P.total_unknown);
+            write_header(blk, P.version, P.total_override > 0 ? P.total_override : frames, P.block_index_start + f0,
+                         (uint32_t)nf, flags, crc, P.total_unknown);
             file.insert(file.end(), blk.begin(), blk.end());
         }
         return file;

@@ -26,6 +26,8 @@ TERMS_FAST = [17, 17]
 TERMS_DEFAULT = [18, 18, 2, 3, -2]
 TERMS_HIGH = [18, 18, 2, 3, -2, 18, 2, 4, 7, 5, 3, 6, 8, -1, 18, 2]
 TERMS_MONO_HIGH = [18, 18, 2, 3, 18, 2, 4, 7, 5, 3, 6, 8, 18, 2, 17, 1]
+TERMS_HIGH10 = [18, 18, 18, -2, 2, 3, 5, -1, 17, 4]  # [ext] WavPack 4 'high' (10 terms)
+TERMS_X3 = [18, -3, 1, 17, 2, -1, 3, -3, 18, 1]      # 'extra'-style list: cross-channel -3 and term 1
 
 
 class _Params(ctypes.Structure):
@@ -36,7 +38,8 @@ class _Params(ctypes.Structure):
             "block_samples", "sample_rate", "version", "hybrid", "hybrid_bitrate", "hybrid_balance",
             "bitrate_x256", "float_data", "float_flags", "float_shift", "float_max_exp", "float_norm_exp",
             "int32_zeros", "write_riff", "config_flags", "write_history", "reset_state", "block_index_start",
-            "total_unknown", "extras", "mag_override")]
+            "total_unknown", "extras", "mag_override", "int32_sent_bits", "int32_ones", "int32_dups", "wvx",
+            "wvx_max_width", "wvx_short")] + [("total_override", ctypes.c_int64)]
 
 
 class _DsdParams(ctypes.Structure):
@@ -75,6 +78,13 @@ class EncParams:
     total_unknown: bool = False
     extras: int = 0
     mag_override: int = -1
+    int32_sent_bits: int = 0
+    int32_ones: int = 0
+    int32_dups: int = 0
+    wvx: int = 0            # 0 none, 1 ID_WVX_BITSTREAM, 2 ID_WVX_NEW_BITSTREAM (UnpackUtils.cs:115-147)
+    wvx_max_width: int = 0  # NEW variant's int32_max_width
+    wvx_short: int = 0      # bytes dropped from every wvx payload (the reference then over-reads and throws)
+    total_override: int = 0  # > 0: header total_samples (parts encoded in parallel, then concatenated)
 
     def to_c(self) -> _Params:
         p = _Params()
@@ -87,12 +97,44 @@ class EncParams:
             p.deltas[i] = deltas[i]
         for n in ("block_samples", "sample_rate", "version", "bitrate_x256", "float_flags", "float_shift",
                   "float_max_exp", "float_norm_exp", "int32_zeros", "config_flags", "block_index_start",
-                  "extras", "mag_override"):
+                  "extras", "mag_override", "int32_sent_bits", "int32_ones", "int32_dups", "wvx", "wvx_max_width",
+                  "wvx_short", "total_override"):
             setattr(p, n, int(getattr(self, n)))
         for n in ("hybrid", "hybrid_bitrate", "hybrid_balance", "float_data", "write_riff", "write_history",
                   "reset_state", "total_unknown"):
             setattr(p, n, int(bool(getattr(self, n))))
         return p
+
+
+def encode_pcm_parallel(samples: np.ndarray, params: EncParams, workers: int | None = None) -> bytes:
+    """encode_pcm over whole-block parts in worker processes, concatenated: the
+    same stream as one encode_pcm call whenever the blocks do not carry state
+    (reset_state) -- and in any case a valid stream whose parts start from a
+    fresh encoder state (the decoder re-reads every block's state)."""
+    import dataclasses
+    from concurrent.futures import ProcessPoolExecutor
+    x = np.ascontiguousarray(samples, dtype=np.int32).reshape(-1, params.nch)
+    frames = x.shape[0]
+    B = params.block_samples
+    nblocks = (frames + B - 1) // B
+    if workers is None:
+        workers = min(16, int(os.environ.get("OMP_NUM_THREADS", "8") or 8), os.cpu_count() or 1)
+    if workers <= 1 or nblocks < 2 * workers:
+        return encode_pcm(x, params)
+    per = (nblocks + workers - 1) // workers
+    jobs = []
+    for k in range(0, nblocks, per):
+        p = dataclasses.replace(params, block_index_start=params.block_index_start + k * B, total_override=frames,
+                                write_riff=params.write_riff and k == 0)
+        jobs.append((x[k * B:(k + per) * B], p))
+    with ProcessPoolExecutor(max_workers=workers) as ex:
+        parts = list(ex.map(_encode_job, jobs))
+    return b"".join(parts)
+
+
+def _encode_job(job):
+    x, p = job
+    return encode_pcm(x, p)
 
 
 def build() -> str:
@@ -213,6 +255,33 @@ def float_mantissas(x: np.ndarray, max_exp: int = 126) -> np.ndarray:
     clipped to 24 bits (FloatUtils.cs:32-56)."""
     v = np.rint(x.astype(np.float64) * float(2 ** (150 - max_exp)))
     return np.clip(v, -(2 ** 30), 2 ** 30).astype(np.int32)
+
+
+def int32_layout(y: np.ndarray, sent_bits: int = 0, zeros: int = 0, ones: int = 0, dups: int = 0,
+                 max_width: int = 0, seed: int = 0) -> np.ndarray:
+    """int32 samples that an INT32_DATA block with these int32 info fields (and a wvx
+    stream carrying `sent_bits` low bits, NEW variant when max_width > 0) represents
+    exactly (UnpackUtils.cs:1271-1314): y is the main-stream word, random low bits are
+    appended (truncated as max_width requires), then zeros/ones/dups are applied."""
+    rng = np.random.default_rng(seed)
+    v = y.astype(np.int64)
+    if sent_bits:
+        low = rng.integers(0, 1 << sent_bits, size=y.shape, dtype=np.int64)
+        if max_width:
+            pv = np.where(v < 0, ~v, v)
+            width = np.array([int(a).bit_length() for a in pv.reshape(-1)], dtype=np.int64).reshape(y.shape) + sent_bits
+            btr = np.where(width <= max_width, sent_bits, sent_bits - (width - max_width))
+            btr = np.clip(btr, 0, sent_bits)
+            low = (low >> (sent_bits - btr)) << (sent_bits - btr)
+        v = (v << sent_bits) | low
+    if zeros:
+        v = v << zeros
+    elif ones:
+        v = ((v + 1) << ones) - 1
+    elif dups:
+        v = ((v + (v & 1)) << dups) - (v & 1)
+    assert v.min() >= -(2 ** 31) and v.max() < 2 ** 31, "int32 range"
+    return v.astype(np.int32)
 
 
 def dsd_like(frames: int, nch: int = 2, seed: int = 0) -> np.ndarray:

@@ -39,7 +39,10 @@ DSD = V.dsd_cases()
 @pytest.mark.parametrize("name,data,chunk", PCM, ids=[c[0] for c in PCM])
 def test_pcm_modes(name, data, chunk):
     r, st = check(data, chunk)
-    assert r.status == 0 and r.crc_errors == 0
+    if name.endswith("_short"):  # truncated wvx stream: the reference over-reads it and throws (B-10)
+        assert r.status == -3
+    else:
+        assert r.status == 0 and r.crc_errors == 0
 
 
 @pytest.mark.parametrize("name,data,chunk", DSD, ids=[c[0] for c in DSD])

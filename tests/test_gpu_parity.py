@@ -7,6 +7,7 @@ import pytest
 
 from oracle import oracle as O
 from tests import vectors as V
+from wavpackdecoder_amd._lib import WVG_ST_TIMEOUT
 
 pytestmark = pytest.mark.gpu
 
@@ -35,6 +36,8 @@ def _check_one(data, chunk, batch_cls, name, force_lane=False):
     ref = O.decode_file(data, chunk=chunk)
     out, res, infos = _gpu_decode([data], chunk, batch_cls, force_lane)
     r, info = res[0], infos[0]
+    # a kernel timeout is never a reference outcome (result() raises DecoderTimeout too)
+    assert r is None or not (r.status_or & WVG_ST_TIMEOUT), name
     if ref.status == -2:
         assert not info.open_ok, name
         return
@@ -49,7 +52,7 @@ def _check_one(data, chunk, batch_cls, name, force_lane=False):
     np.testing.assert_array_equal(got, ref.samples, err_msg=name)
 
 
-@pytest.mark.parametrize("lane", [False, True], ids=["2wave", "lane"])
+@pytest.mark.parametrize("lane", [False, True], ids=["2wave", "generic"])
 @pytest.mark.parametrize("case", V.pcm_cases(), ids=lambda c: c[0])
 def test_pcm_modes(case, lane, gpu_batch_cls):
     name, data, chunk = case
@@ -68,10 +71,13 @@ def test_corrupted_streams(gpu_batch_cls):
     m = S.audio_like(20000, 1, 16, seed=12)
     base = S.encode_pcm(x, S.EncParams(terms=S.TERMS_DEFAULT, block_samples=4000))
     basem = S.encode_pcm(m, S.EncParams(nch=1, terms=S.TERMS_MONO_HIGH, block_samples=3001))
+    basex = V.int32_file(x, sent_bits=6, ones=2, wvx=2, max_width=21)
     for lane in (False, True):
         for k in range(10):
             _check_one(V.corrupt(base, k), 4096, gpu_batch_cls, f"stereo#{k}", lane)
             _check_one(V.corrupt(basem, 100 + k), 1000, gpu_batch_cls, f"mono#{k}", lane)
+    for k in range(10):
+        _check_one(V.corrupt(basex, 200 + k), 4096, gpu_batch_cls, f"int32_wvx#{k}")
 
 
 def test_batch_of_many_files_matches_per_file(gpu_batch_cls):
@@ -81,6 +87,9 @@ def test_batch_of_many_files_matches_per_file(gpu_batch_cls):
     out, res, infos = _gpu_decode(files, 4096, gpu_batch_cls)
     for (name, data, _), r, info in zip(cases, res, infos):
         ref = O.decode_file(data, chunk=4096)
+        if ref.status == -3:  # the reference throws in this file
+            assert r.exception == 1, name
+            continue
         assert r.frames == ref.frames and r.crc_errors == ref.crc_errors, name
         got = out[info.out_offset: info.out_offset + ref.frames * ref.nch]
         np.testing.assert_array_equal(got, ref.samples, err_msg=name)
@@ -96,6 +105,17 @@ def test_c2_full_size_roundtrip(gpu_batch_cls):
     assert res[0].crc_errors == 0
     assert res[0].frames == pcm.shape[0] == 1024 * 22050
     np.testing.assert_array_equal(out, pcm.reshape(-1))
+
+
+def test_c3_full_block_high24(gpu_batch_cls):
+    """C3's block shape at full size (44,100-frame 24-bit stereo blocks, 16-term 'high'
+    chain) against the oracle, plus the lossless round trip."""
+    from synth import wvsynth as S
+    x = S.audio_like(2 * 44100 + 777, 2, 24, seed=0xC3)
+    data = S.encode_pcm(x, S.EncParams(terms=S.TERMS_HIGH, bytes_per_sample=3, block_samples=44100))
+    _check_one(data, 4096, gpu_batch_cls, "c3_full_block")
+    out, res, infos = _gpu_decode([data], 4096, gpu_batch_cls)
+    np.testing.assert_array_equal(out[: x.size], x.reshape(-1))
 
 
 def test_golden_fixtures(gpu_batch_cls):

@@ -21,6 +21,8 @@ WVG_ST_EXCEPTION = 0x10
 WVG_ST_UNSUPPORTED = 0x20
 WVG_ST_DSD_MUTE = 0x40
 WVG_ST_NONDET = 0x80
+WVG_ST_TIMEOUT = 0x100
+WVG_ERR_TIMEOUT = -5
 
 
 class WvgFileInfo(ctypes.Structure):
@@ -32,7 +34,7 @@ class WvgFileInfo(ctypes.Structure):
         ("sample_rate", ctypes.c_int64), ("total_samples", ctypes.c_int64), ("out_frames", ctypes.c_int64),
         ("out_offset", ctypes.c_int64), ("header_off", ctypes.c_int64), ("header_len", ctypes.c_int64),
         ("trailer_off", ctypes.c_int64), ("trailer_len", ctypes.c_int64), ("error", ctypes.c_char * 96),
-        ("seek_result", ctypes.c_int32), ("reserved", ctypes.c_int32),
+        ("seek_result", ctypes.c_int32), ("reserved", ctypes.c_int32), ("sample_index0", ctypes.c_int64),
     ]
 
 
@@ -40,6 +42,7 @@ class WvgFileResult(ctypes.Structure):
     _fields_ = [
         ("frames", ctypes.c_int64), ("crc_errors", ctypes.c_int64), ("lossy", ctypes.c_int32),
         ("exception", ctypes.c_int32), ("status_or", ctypes.c_uint32), ("num_blocks", ctypes.c_int32),
+        ("exception_frame", ctypes.c_int64),
     ]
 
 
@@ -85,6 +88,7 @@ def lib():
         "wvg_batch_download": (i32, [vp, vp, i64]),
         "wvg_batch_file_result": (i32, [vp, i32, ctypes.POINTER(WvgFileResult)]),
         "wvg_batch_block_status": (i32, [vp, vp, i64]),
+        "wvg_batch_file_blocks": (i32, [vp, i32, vp, vp, i64]),
         "wvg_batch_time": (i32, [vp, i32, ctypes.POINTER(ctypes.c_float)]),
         "wvg_decode_file": (i32, [vp, ctypes.c_char_p, ctypes.c_size_t, i32, vp, i64, ctypes.POINTER(WvgFileInfo),
                                   ctypes.POINTER(WvgFileResult)]),
@@ -109,6 +113,6 @@ EXPORTED = ("wvg_open", "wvg_close", "wvg_last_error", "wvg_batch_new", "wvg_bat
             "wvg_batch_add_file_at",
             "wvg_batch_upload", "wvg_batch_decode", "wvg_batch_sync", "wvg_batch_out_ints", "wvg_batch_device_out",
             "wvg_batch_num_blocks", "wvg_batch_bytes_in", "wvg_batch_frames", "wvg_batch_download",
-            "wvg_batch_file_result", "wvg_batch_block_status", "wvg_batch_time", "wvg_decode_file",
+            "wvg_batch_file_result", "wvg_batch_block_status", "wvg_batch_file_blocks", "wvg_batch_time", "wvg_decode_file",
             "wvg_probe_file", "wvg_format_samples", "wvg_batch_format", "wvg_batch_pcm_bytes", "wvg_batch_pcm_offset",
             "wvg_batch_device_pcm", "wvg_batch_download_pcm", "wvg_batch_wav")

@@ -10,12 +10,17 @@ Reference (C#, Quake4/WavPackDecoder WavPackUtils.cs):
     GetTrailer / GetIsFive / GetVersion / GetIsFloat       :346-499
 
 Same names, same argument meaning and the same error behaviour (errors are
-reported through GetErrorMessage; a decode that the reference would abort
-with a C# exception raises WavpackException here).  Underneath, the whole
-file is decoded by the MI355X kernels on the first WavpackUnpackSamples call
-and served from the decoded buffer; the chunk schedule is the caller's
-request size (the reference's seams are a function of it), 4096 frames by
-default like WvDemo.
+reported through GetErrorMessage; a call that the reference would abort with a
+C# exception raises WavpackException here, after every earlier call has
+returned its frames).  Underneath, the whole file is decoded by the MI355X
+kernels on the first WavpackUnpackSamples call and served from the decoded
+buffer; the chunk schedule is the caller's request size (the reference's
+seams are a function of it).  GetSampleIndex / GetNumErrors follow the calls
+made so far (WavPackUtils.cs:273-275, 355-366).  A caller that changes its
+request size mid-stream gets the samples of a decode scheduled at the first
+request size: identical for every well-formed stream (seams only matter for
+the (short) weight store of pathological weights and for the mute granularity
+of corrupted streams), and reported through `schedule_changed`.
 
 For throughput use DecodeBatch: many files, one upload, one decode.
 """
@@ -33,6 +38,11 @@ OPEN_2CH_MAX = 0x8         # Defines.cs:26
 
 class WavpackException(RuntimeError):
     """The reference would have raised a C# exception (WvDemo.cs:144 catch)."""
+
+
+class DecoderTimeout(RuntimeError):
+    """A decode kernel's bounded wait ran out (WVG_ST_TIMEOUT): a decoder fault, never a
+    property of the stream and never reported as a reference exception."""
 
 
 _ctx = None
@@ -122,6 +132,16 @@ class DecodeBatch:
             raise RuntimeError("block status unavailable (download first)")
         return st[:k]
 
+    def file_blocks(self, i: int):
+        """(end_frame, status) per block of file i (wvg_batch_file_blocks)."""
+        n = self.num_blocks + 1
+        ends = np.zeros(n, dtype=np.int64)
+        st = np.zeros(n, dtype=np.uint32)
+        k = self._L.wvg_batch_file_blocks(self._b, int(i), ends.ctypes.data, st.ctypes.data, n)
+        if k < 0:
+            raise RuntimeError("file blocks unavailable (download first)")
+        return ends[:k], st[:k]
+
     def format(self, dsd: bool = False, stream=None):
         """WavpackFormatSamples (WavPackUtils.cs:288-341) over the decoded batch, on the device."""
         self._check(self._L.wvg_batch_format(self._b, int(bool(dsd)), stream))
@@ -149,6 +169,8 @@ class DecodeBatch:
         return r
 
     def _check(self, rc: int):
+        if rc == _L.WVG_ERR_TIMEOUT:
+            raise DecoderTimeout(self._L.wvg_last_error(_context()).decode())
         if rc != 0:
             raise RuntimeError(f"libwvgpu error {rc}: {self._L.wvg_last_error(_context()).decode()}")
 
@@ -173,25 +195,48 @@ class WavpackContext:
         self._info = _L.WvgFileInfo()
         self._decoded = None
         self._result = None
-        self._pos = 0  # frames already handed out
+        self._pos = 0            # frames handed out since the decode's start
+        self._limit = 0          # frames the calls return before the end (or before the throwing call)
+        self._throws = False     # the call starting at _limit raises
+        self._block_end = None   # per block: frames handed out when its last frame is unpacked
+        self._block_err = None   # per block: check_crc_error verdict
+        self._errors_before = 0  # crc_errors of calls made before a SetSample
+        self._index0 = 0         # stream.sample_index when the decode's first call starts
         self._chunk = None
         self._seek = None  # SetSample target, applied when the file is decoded
+        self.schedule_changed = False
         self.error_message = None
 
     def _decode(self, chunk: int):
         b = DecodeBatch(chunk)
-        idx = b.add_file(self._data, self._flags, self._seek)
-        if idx < 0:
-            raise RuntimeError("file cannot be opened: " + self._info.error.decode())
-        b.decode()
-        out = b.download()
-        self._result = b.result(idx)
-        b.close()
-        if self._result.exception:
-            raise WavpackException("the reference decoder raises an exception on this file")
-        nch = max(self._info.reduced_channels, 1)
-        self._decoded = out.reshape(-1, nch) if out.size else np.zeros((0, nch), np.int32)
+        try:
+            idx = b.add_file(self._data, self._flags, self._seek)
+            if idx < 0:
+                raise RuntimeError("file cannot be opened: " + self._info.error.decode())
+            b.decode()
+            out = b.download()
+            res = b.result(idx)
+            info = b.infos[idx]
+            ends, sts = b.file_blocks(idx)
+        finally:
+            b.close()
+        nch = max(int(info.reduced_channels), 1)
+        self._result = res
+        self._throws = bool(res.exception)
+        self._limit = int(res.exception_frame) if res.exception else int(info.out_frames)
+        lo = int(info.out_offset)
+        self._decoded = out[lo: lo + self._limit * nch].reshape(-1, nch)
+        self._block_end = ends
+        self._block_err = (sts & _L.WVG_ST_CRC_ERROR) != 0
+        self._index0 = int(info.sample_index0)
         self._chunk = chunk
+        self._pos = 0
+
+    def _crc_errors(self) -> int:
+        if self._block_end is None:
+            return self._errors_before
+        done = self._block_end <= self._pos
+        return self._errors_before + int(np.count_nonzero(self._block_err & done))
 
 
 def WavpackOpenFileInput(reader, flags: int = 0) -> WavpackContext:
@@ -210,9 +255,15 @@ def WavpackUnpackSamples(wpc: WavpackContext, buffer: np.ndarray, samples: int) 
     """WavPackUtils.cs:200-282: fill `buffer` (int32, >= samples * reduced channels)."""
     if wpc.error_message:
         return 0
-    if wpc._decoded is None:
-        wpc._decode(int(samples))
-    n = min(int(samples), wpc._decoded.shape[0] - wpc._pos)
+    if wpc._decoded is None or (int(samples) != wpc._chunk and wpc._pos == 0):
+        wpc._decode(int(samples))  # (re)decode scheduled at this request size: nothing handed out yet
+    elif int(samples) != wpc._chunk:
+        wpc.schedule_changed = True
+    if wpc._pos >= wpc._limit:
+        if wpc._throws:
+            raise WavpackException("the reference decoder raises an exception in this call")
+        return 0
+    n = min(int(samples), wpc._limit - wpc._pos)
     if n <= 0:
         return 0
     nch = wpc._decoded.shape[1]
@@ -241,10 +292,16 @@ def SetSample(wpc: WavpackContext, sample: int) -> bool:
     if info.seek_result < 0:
         raise WavpackException("the reference's SetSample raises an exception on this file")
     if info.seek_result == 1:
+        wpc._errors_before = wpc._crc_errors()
         wpc._seek = int(sample)
         wpc._decoded = None
+        wpc._block_end = wpc._block_err = None
         wpc._pos = 0
+        wpc._limit = 0
+        wpc._index0 = int(sample)
         wpc._result = None
+        # decode now: the discard calls' block ends count towards GetNumErrors at once
+        wpc._decode(wpc._chunk or SAMPLE_BUFFER_SIZE)
     return info.seek_result == 1
 
 
@@ -258,8 +315,10 @@ def WavpackFormatSamples(src: np.ndarray, samcnt: int, bps: int, pcm_buffer: byt
     """WavPackUtils.cs:288-341 (host C implementation in libwvgpu)."""
     L = _L.lib()
     s = np.ascontiguousarray(src, dtype=np.int32)
-    if pcm_buffer is None:
+    if pcm_buffer is None or len(pcm_buffer) < int(samcnt) * int(bps) + int(offset):
         return False
+    if int(bps) in (1, 2, 3, 4) and int(samcnt) > s.size:  # src[counter2++] past the array
+        raise WavpackException("IndexOutOfRangeException in WavpackFormatSamples")
     view = (ctypes.c_uint8 * len(pcm_buffer)).from_buffer(pcm_buffer)
     return bool(L.wvg_format_samples(s.ctypes.data, int(samcnt), int(bps), ctypes.addressof(view), len(pcm_buffer),
                                      int(offset), int(bool(dsd))))
@@ -289,11 +348,16 @@ def WavpackGetNumSamples(wpc, native: bool = False) -> int:
 
 
 def WavpackGetSampleIndex(wpc) -> int:
-    return wpc._pos
+    """stream.sample_index (WavPackUtils.cs:355-358): where the next call starts."""
+    if wpc._decoded is None and wpc._seek is None:
+        return int(wpc._info.sample_index0)
+    return wpc._index0 + wpc._pos
 
 
 def WavpackGetNumErrors(wpc) -> int:
-    return int(wpc._result.crc_errors) if wpc._result is not None else 0
+    """crc_errors: blocks whose last frame a call has unpacked and whose check failed
+    (WavPackUtils.cs:273-275), SetSample's discard calls included."""
+    return wpc._crc_errors()
 
 
 def WavpackLossy(wpc) -> bool:

@@ -14,8 +14,8 @@
 
 namespace wvg {
 hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint32_t n_pcm, const uint32_t *dsd_list,
-                         uint32_t n_dsd, const uint8_t *blob, const uint8_t *tables, int32_t *ptables, int32_t *out,
-                         uint32_t *status, uint32_t *aux, hipStream_t s_pcm, hipStream_t s_dsd);
+                         uint32_t n_dsd, const uint8_t *blob, const uint8_t *tables, int32_t *out, uint32_t *status,
+                         uint32_t *aux, hipStream_t s_pcm, hipStream_t s_dsd);
 int term_set_of(const BlockDesc &d);
 hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, uint32_t n, const uint8_t *blob,
                         int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s);
@@ -28,7 +28,7 @@ constexpr uint32_t kFormatSeg = 65536;  // values per format work item
 
 using namespace wvg;
 
-// The kernels of one decode (a two-wave launch per term set, the PCM lane
+// The kernels of one decode (a two-wave launch per term set, the generic PCM
 // kernel, the DSD kernels) are independent: they fork from the caller's stream
 // onto side streams and join back, so small groups run concurrently.
 constexpr int kSide = kMaxTermSets + 2;
@@ -49,10 +49,10 @@ struct wvg_batch {
     std::vector<FileInfo> finfo;
     std::vector<wvg_file_info> infos;
     int64_t out_ints = 0;
-    std::vector<uint32_t> pcm_list, dsd_list;           // lane kernels (generic PCM, DSD)
+    std::vector<uint32_t> pcm_list, dsd_list;           // wave-per-block kernels (generic PCM, DSD)
     std::vector<uint32_t> ts_list[kMaxTermSets];        // two-wave kernels per term set
     uint32_t *d_ts[kMaxTermSets] = {nullptr};
-    int force_lane = 0;                                 // WVG_FORCE_LANE=1: everything on the lane kernel
+    int force_lane = 0;                                 // WVG_FORCE_LANE=1: every PCM block on the generic kernel
     std::vector<uint32_t> h_status, h_aux;
     int64_t bytes_in = 0, frames = 0;
     // format epilogue: per-file byte image of WavpackFormatSamples
@@ -65,7 +65,7 @@ struct wvg_batch {
     MetaItem *d_items = nullptr;  // deferred metadata values (wv_meta.h), applied once per upload
     MetaJob *d_jobs = nullptr;
     FormatSeg *d_segs = nullptr;
-    int32_t *d_out = nullptr, *d_ptables = nullptr;
+    int32_t *d_out = nullptr;
     uint32_t *d_status = nullptr, *d_mute = nullptr, *d_pcml = nullptr, *d_dsd = nullptr;
     bool uploaded = false, downloaded = false, formatted = false;
 };
@@ -143,7 +143,6 @@ static void free_dev(wvg_batch *b) {
     hipFree(b->d_jobs);
     hipFree(b->d_segs);
     hipFree(b->d_out);
-    hipFree(b->d_ptables);
     hipFree(b->d_status);
     hipFree(b->d_mute);
     hipFree(b->d_pcml);
@@ -157,7 +156,7 @@ static void free_dev(wvg_batch *b) {
     b->d_items = nullptr;
     b->d_jobs = nullptr;
     b->d_segs = nullptr;
-    b->d_out = b->d_ptables = nullptr;
+    b->d_out = nullptr;
     b->d_status = b->d_mute = b->d_pcml = b->d_dsd = nullptr;
     b->uploaded = b->formatted = false;
 }
@@ -190,6 +189,7 @@ static void fill_info(const FileInfo &fi, wvg_file_info &wi) {
     wi.out_frames = fi.out_frames;
     wi.out_offset = 0;
     wi.seek_result = fi.seek_result;
+    wi.sample_index0 = fi.sample_index0;
 }
 
 int wvg_probe_file(const uint8_t *file, size_t len, uint32_t open_flags, int chunk_frames, wvg_file_info *info) {
@@ -296,9 +296,8 @@ int wvg_batch_upload(wvg_batch *b) {
     for (size_t k = 0; k < nd; k++) st[k] = b->fo.descs[k].fstatus;
     HIPCHK(c, hipMemcpyAsync(b->d_status, st.data(), sizeof(uint32_t) * st.size(), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemsetAsync(b->d_mute, 0, sizeof(uint32_t) * (nd ? nd : 1), c->stream));
-    // lane kernels run 64 blocks per wave in lock-step: group blocks of one DSD
-    // mode and of similar length into the same waves (order is free: every
-    // block writes its own output range; DSD fills follow on the same stream)
+    // longest blocks first within a kind, so the long tail starts early (order is
+    // free: every block writes its own output range; DSD fills follow on the same stream)
     auto by_kind_len = [&](uint32_t x, uint32_t y) {
         const BlockDesc &p = b->fo.descs[x], &q = b->fo.descs[y];
         return p.kind != q.kind ? p.kind < q.kind : (p.nframes != q.nframes ? p.nframes > q.nframes : x < y);
@@ -310,7 +309,6 @@ int wvg_batch_upload(wvg_batch *b) {
     HIPCHK(c, hipMalloc(&b->d_dsd, sizeof(uint32_t) * (ns ? ns : 1)));
     if (np) HIPCHK(c, hipMemcpyAsync(b->d_pcml, b->pcm_list.data(), sizeof(uint32_t) * np, hipMemcpyHostToDevice, c->stream));
     if (ns) HIPCHK(c, hipMemcpyAsync(b->d_dsd, b->dsd_list.data(), sizeof(uint32_t) * ns, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMalloc(&b->d_ptables, sizeof(int32_t) * 256 * (ns ? ns : 1)));
     for (int t = 0; t < kMaxTermSets; t++) {
         size_t nl = b->ts_list[t].size();
         if (!nl) continue;
@@ -327,7 +325,7 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
     if (!b || !b->uploaded) return WVG_ERR_ARG;
     wvg_ctx *c = b->ctx;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    // one stream slot per non-empty launch group: term sets 0..7, PCM lane, DSD
+    // one stream slot per non-empty launch group: term sets 0..7, generic PCM, DSD
     int used[kSide], n = 0;
     for (int t = 0; t < kMaxTermSets; t++)
         if (!b->ts_list[t].empty()) used[n++] = t;
@@ -343,8 +341,8 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
             HIPCHK(c, launch_2wave(t, b->d_descs, b->d_ts[t], (uint32_t)b->ts_list[t].size(), b->d_blob, b->d_out,
                                    b->d_status, b->d_mute, slot(t)));
     HIPCHK(c, launch_decode(b->d_descs, b->d_pcml, (uint32_t)b->pcm_list.size(), b->d_dsd, (uint32_t)b->dsd_list.size(),
-                            b->d_blob, b->d_tables, b->d_ptables, b->d_out, b->d_status, b->d_mute,
-                            slot(kMaxTermSets), slot(kMaxTermSets + 1)));
+                            b->d_blob, b->d_tables, b->d_out, b->d_status, b->d_mute, slot(kMaxTermSets),
+                            slot(kMaxTermSets + 1)));
     if (n > 1) {
         for (int i = 0; i < n; i++) {
             HIPCHK(c, hipEventRecord(c->join[used[i]], c->side[used[i]]));
@@ -409,29 +407,75 @@ static int64_t first_exception_block(const wvg_batch *b, const FileInfo &fi) {
     return -1;
 }
 
+// frames the file's calls return before the call that throws: the call holding the
+// device-reported frame of the first block that raised (-1: no device exception)
+static int64_t exception_call_frame(const wvg_batch *b, const FileInfo &fi, const wvg_file_info &wi) {
+    const int64_t kx = first_exception_block(b, fi);
+    if (kx < 0) return -1;
+    const int nch = wi.reduced_channels ? wi.reduced_channels : 1;
+    const BlockDesc &d = b->fo.descs[(size_t)kx];
+    const int64_t start = ((int64_t)d.out_off - wi.out_offset) / nch;  // block's first output frame
+    const int64_t t = b->h_aux[(size_t)kx];
+    if (t < (int64_t)d.first_chunk) return start - (int64_t)d.first_bsp / nch;
+    return start + d.first_chunk + (t - d.first_chunk) / d.chunk * d.chunk;
+}
+
+// the status word a block contributes to the file result
+static uint32_t block_verdict(const wvg_batch *b, int64_t k) {
+    const BlockDesc &d = b->fo.descs[(size_t)k];
+    uint32_t st = b->h_status[(size_t)k];
+    // a block decoded from state the device cannot see (only in malformed
+    // files): the reference decodes garbage and its CRC check fails
+    if ((st & ST_UNSUPPORTED) && d.nframes == d.block_samples) st |= ST_CRC_CHECKED | ST_CRC_ERROR;
+    return st;
+}
+
 int wvg_batch_file_result(wvg_batch *b, int file, wvg_file_result *res) {
     if (!b || !b->downloaded || file < 0 || file >= (int)b->finfo.size() || !res) return WVG_ERR_ARG;
     const FileInfo &fi = b->finfo[(size_t)file];
     memset(res, 0, sizeof(*res));
     res->frames = fi.out_frames;
     res->exception = fi.exception;
+    res->exception_frame = -1;
     res->num_blocks = (int32_t)fi.num_desc;
     res->lossy = fi.lossy_blocks || (fi.config_flags & 8) != 0;
+    bool timeout = false;
     for (int64_t k = fi.first_desc; k < fi.first_desc + fi.num_desc; k++) {
-        const BlockDesc &d = b->fo.descs[(size_t)k];
-        uint32_t st = b->h_status[(size_t)k];
-        // a block decoded from state the device cannot see (only in malformed
-        // files): the reference decodes garbage and its CRC check fails
-        if ((st & ST_UNSUPPORTED) && d.nframes == d.block_samples) st |= ST_CRC_CHECKED | ST_CRC_ERROR;
+        const uint32_t st = block_verdict(b, k);
         res->status_or |= st;
+        if (st & ST_TIMEOUT) timeout = true;
         if (st & ST_CRC_ERROR) res->crc_errors++;
         if (st & ST_EXCEPTION) {
             res->exception = 1;
             break;
         }
     }
-    if (res->exception) res->frames = -1;
+    if (res->exception) {
+        res->exception_frame = exception_call_frame(b, fi, b->infos[(size_t)file]);
+        if (res->exception_frame < 0 || res->exception_frame > fi.out_frames) res->exception_frame = fi.out_frames;
+        res->frames = -1;
+    }
+    if (timeout) {
+        b->ctx->err = "a decode kernel's bounded wait ran out (ST_TIMEOUT): output of this file is invalid";
+        return WVG_ERR_TIMEOUT;
+    }
     return WVG_OK;
+}
+
+int wvg_batch_file_blocks(wvg_batch *b, int file, int64_t *end_frame, uint32_t *status, int64_t cap) {
+    if (!b || !b->downloaded || file < 0 || file >= (int)b->finfo.size()) return WVG_ERR_ARG;
+    const FileInfo &fi = b->finfo[(size_t)file];
+    const wvg_file_info &wi = b->infos[(size_t)file];
+    if (cap < fi.num_desc) return WVG_ERR_SPACE;
+    const int nch = wi.reduced_channels ? wi.reduced_channels : 1;
+    for (int64_t k = 0; k < fi.num_desc; k++) {
+        const BlockDesc &d = b->fo.descs[(size_t)(fi.first_desc + k)];
+        // out_off is the block's first output frame (a seek's dropped frames lie before the file's output)
+        const int64_t start = ((int64_t)d.out_off - wi.out_offset) / nch;
+        if (end_frame) end_frame[k] = start + (int64_t)d.nframes;
+        if (status) status[k] = block_verdict(b, fi.first_desc + k);
+    }
+    return (int)fi.num_desc;
 }
 
 int wvg_batch_time(wvg_batch *b, int iters, float *ms) {
@@ -577,7 +621,7 @@ int wvg_batch_wav(wvg_batch *b, int file, uint8_t *out, int64_t cap, int64_t *wa
         if (rc) return rc;
     }
     wvg_file_result r;
-    wvg_batch_file_result(b, file, &r);
+    if (wvg_batch_file_result(b, file, &r) == WVG_ERR_TIMEOUT) return WVG_ERR_TIMEOUT;
     const int nch = wi.reduced_channels, bps = wi.bytes_per_sample;
     const int64_t block_align = (int64_t)bps * nch;
     const int64_t total_native = fi.total_samples * (wi.dsd_multiplier > 0 ? 8 : 1);  // WavpackGetNumSamples(wpc, true)
@@ -585,14 +629,8 @@ int wvg_batch_wav(wvg_batch *b, int file, uint8_t *out, int64_t cap, int64_t *wa
     // frames written: whole calls before the one that threw (WvDemo.cs:144 catch)
     int64_t limit = fi.out_frames;
     bool exc = fi.exception != 0;
-    const int64_t kx = first_exception_block(b, fi);
-    if (kx >= 0) {
-        const BlockDesc &d = b->fo.descs[(size_t)kx];
-        const int64_t start = ((int64_t)d.out_off - wi.out_offset) / (nch ? nch : 1);  // block's first output frame
-        const int64_t t = b->h_aux[(size_t)kx];
-        int64_t call;
-        if (t < (int64_t)d.first_chunk) call = start - (int64_t)d.first_bsp / (nch ? nch : 1);
-        else call = start + d.first_chunk + (t - d.first_chunk) / d.chunk * d.chunk;
+    const int64_t call = exception_call_frame(b, fi, wi);
+    if (call >= 0) {
         limit = call < limit ? call : limit;
         exc = true;
     }

@@ -10,8 +10,6 @@
 //                         fixup -> int32 store) fused, sample-major.
 //   wv_decode_dsd_wave  : one wave-uniform decode per DSD block (DsdUtils modes
 //                         0/1/3, each a scalar specialisation).
-//   wv_decode_*_lane    : the same decodes one lane per block (A/B runs only,
-//                         WVG_LANE_KERNELS=1).
 //   wv_dsd_fill         : post-pass writing the 0x55 mute fills of DSD blocks in
 //                         call-buffer coordinates (DsdUtils.cs:104-117, quirk B-9).
 //   wv_meta_parse       : one lane per block finishing its descriptor with the
@@ -34,57 +32,11 @@
 
 namespace wvg {
 
-// output of one block: value i (frame * ints per frame + channel) at out[i];
-// the first `skip` values belong to a seek's discard calls and are dropped
-struct DevStore {
-    int32_t *out;
-    uint64_t skip;
-    __device__ __forceinline__ void put(uint64_t i, int32_t v) {
-        if (i >= skip) out[i] = v;
-    }
-};
-
-extern "C" __global__ void __launch_bounds__(64) wv_decode_pcm_lane(const BlockDesc *__restrict__ descs,
-                                                                    const uint32_t *__restrict__ list, uint32_t n,
-                                                                    const uint8_t *__restrict__ blob,
-                                                                    int32_t *__restrict__ out,
-                                                                    uint32_t *__restrict__ status,
-                                                                    uint32_t *__restrict__ aux) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    uint32_t bi = list[i];
-    const BlockDesc &d = descs[bi];
-    DevStore st{out + d.out_off, (uint64_t)d.pre_end * d.out_nch};
-    status[bi] = d.fstatus | decode_pcm_block(d, blob, st, &aux[bi]);
-}
-
-extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_lane(const BlockDesc *__restrict__ descs,
-                                                                    const uint32_t *__restrict__ list, uint32_t n,
-                                                                    const uint8_t *__restrict__ blob,
-                                                                    const uint8_t *__restrict__ tables,
-                                                                    int32_t *__restrict__ ptables,
-                                                                    int32_t *__restrict__ out,
-                                                                    uint32_t *__restrict__ status,
-                                                                    uint32_t *__restrict__ mute_chunk) {
-    // mode 3's adaptive ptable (DsdUtils.cs:409-421) is read and written once per
-    // decoded bit on the serial path: keep it in LDS (1 KiB per lane), not in HBM
-    __shared__ int32_t pt_lds[64 * 256];
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    (void)ptables;
-    uint32_t bi = list[i];
-    const BlockDesc &d = descs[bi];
-    DevStore st{out + d.out_off, (uint64_t)d.pre_end * d.out_nch};
-    DsdResult r = decode_dsd_block(d, blob, tables, pt_lds + threadIdx.x * 256, st);
-    status[bi] = d.fstatus | r.status;
-    mute_chunk[bi] = r.mute_chunk;
-}
-
-// The same two decoders with one 64-lane wave per block instead of one lane:
-// every value derives from blockIdx.x, so the compiler keeps the decode
-// wave-uniform (SGPRs, scalar branches, no divergence between blocks sharing a
-// wave) and lane 0 alone stores.  Blocks spread over the SIMDs instead of 64 of
-// them sharing one wave's lock-step issue.
+// One 64-lane wave per block: every value derives from blockIdx.x, so the
+// compiler keeps the decode wave-uniform (SGPRs, scalar branches, no
+// divergence) and lane 0 alone stores.  Output value i of a block (frame * ints
+// per frame + channel) goes to out[i]; the first `skip` values belong to a
+// seek's discard calls and are dropped.
 struct DevStoreWave {
     int32_t *out;
     uint64_t skip;
@@ -489,6 +441,7 @@ __global__ void __launch_bounds__(128) wv_pcm_2wave(const BlockDesc *__restrict_
 #define WVG_TS_HIGH 2, 18, -1, 8, 6, 3, 5, 7, 4, 2, 18, -2, 3, 2, 18, 18
 #define WVG_TS_MHIGH 1, 17, 2, 18, 8, 6, 3, 5, 7, 4, 2, 18, 3, 2, 18, 18
 #define WVG_TS_M5 18, 3, 2, 18, 18
+#define WVG_TS_HIGH10 4, 17, -1, 5, 3, 2, -2, 18, 18, 18
 
 static const int8_t kTermSets[][17] = {
     // {count, terms...}
@@ -497,10 +450,11 @@ static const int8_t kTermSets[][17] = {
     {16, WVG_TS_HIGH},
     {16, WVG_TS_MHIGH},
     {5, WVG_TS_M5},
+    {10, WVG_TS_HIGH10},
 };
-constexpr int kNumTermSets = 5;
+constexpr int kNumTermSets = 6;
 
-// which specialised kernel decodes this block (-1: the generic lane kernel)
+// which specialised kernel decodes this block (-1: the generic wave kernel)
 int term_set_of(const BlockDesc &d) {
     using namespace wvf;
     if (d.kind != KIND_PCM) return -1;
@@ -529,6 +483,7 @@ hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, ui
     case 2: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_HIGH>), g, b, 0, s, descs, list, blob, out, status, aux); break;
     case 3: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_MHIGH>), g, b, 0, s, descs, list, blob, out, status, aux); break;
     case 4: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_M5>), g, b, 0, s, descs, list, blob, out, status, aux); break;
+    case 5: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_HIGH10>), g, b, 0, s, descs, list, blob, out, status, aux); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -541,31 +496,16 @@ hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, ui
 // ---------------------------------------------------------------------------
 namespace wvg {
 
-// generic PCM blocks (lane kernel) on s_pcm; DSD blocks (decode, then the mute
-// fills that depend on it) on s_dsd
+// PCM blocks without a two-wave instantiation (generic wave kernel) on s_pcm;
+// DSD blocks (decode, then the mute fills that depend on it) on s_dsd
 hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint32_t n_pcm, const uint32_t *dsd_list,
-                         uint32_t n_dsd, const uint8_t *blob, const uint8_t *tables, int32_t *ptables, int32_t *out,
-                         uint32_t *status, uint32_t *aux, hipStream_t s_pcm, hipStream_t s_dsd) {
-    // WVG_LANE_KERNELS=1: the lane-per-block kernels (A/B comparisons)
-    static const bool lanes = [] {
-        const char *e = getenv("WVG_LANE_KERNELS");
-        return e && e[0] == '1';
-    }();
-    if (n_pcm) {
-        if (lanes)
-            hipLaunchKernelGGL(wv_decode_pcm_lane, dim3((n_pcm + 63) / 64), dim3(64), 0, s_pcm, descs, pcm_list,
-                               n_pcm, blob, out, status, aux);
-        else
-            hipLaunchKernelGGL(wv_decode_pcm_wave, dim3(n_pcm), dim3(64), 0, s_pcm, descs, pcm_list, blob, out, status,
-                               aux);
-    }
+                         uint32_t n_dsd, const uint8_t *blob, const uint8_t *tables, int32_t *out, uint32_t *status,
+                         uint32_t *aux, hipStream_t s_pcm, hipStream_t s_dsd) {
+    if (n_pcm)
+        hipLaunchKernelGGL(wv_decode_pcm_wave, dim3(n_pcm), dim3(64), 0, s_pcm, descs, pcm_list, blob, out, status, aux);
     if (n_dsd) {
-        if (lanes)
-            hipLaunchKernelGGL(wv_decode_dsd_lane, dim3((n_dsd + 63) / 64), dim3(64), 0, s_dsd, descs, dsd_list, n_dsd,
-                               blob, tables, ptables, out, status, aux);
-        else
-            hipLaunchKernelGGL(wv_decode_dsd_wave, dim3(n_dsd), dim3(64), 0, s_dsd, descs, dsd_list, blob, tables, out,
-                               status, aux);
+        hipLaunchKernelGGL(wv_decode_dsd_wave, dim3(n_dsd), dim3(64), 0, s_dsd, descs, dsd_list, blob, tables, out,
+                           status, aux);
         hipLaunchKernelGGL(wv_dsd_fill, dim3((n_dsd + 63) / 64), dim3(64), 0, s_dsd, descs, dsd_list, n_dsd, status,
                            aux, out);
     }

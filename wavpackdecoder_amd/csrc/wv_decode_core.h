@@ -58,7 +58,7 @@ WVF_HD int tab_log2(int i) {
 #endif
 }
 
-enum { DEC_OK = 0, DEC_BITS_ERROR = 1, DEC_EXCEPTION = 2 };
+enum { DEC_OK = 0, DEC_BITS_ERROR = 1, DEC_EXCEPTION = 2, DEC_TIMEOUT = 3 };
 
 // exp2s (WordsUtils.cs:633-646); int.MinValue recurses forever in C# -> exception
 WVF_HD int32_t dev_exp2s(int32_t log, int &exc) {
@@ -94,17 +94,19 @@ WVF_HD int dev_mylog2(int64_t avalue, int &exc) {
 // ---------------------------------------------------------------------------
 struct BitReader {
     const uint8_t *base;
-    uint64_t pos, end;
+    uint64_t pos, end, start;
     uint64_t win;
     int nb;
 
     WVF_HD void init(const uint8_t *blob, uint64_t off, uint64_t len) {
         base = blob;
-        pos = off;
+        pos = start = off;
         end = off + len;
         win = 0;
         nb = 0;
     }
+    // bits consumed since the (byte-aligned) start
+    WVF_HD uint64_t consumed() const { return (pos - start) * 8 - (uint64_t)nb; }
     // keep at least 33 valid bits in the window
     WVF_HD void refill() {
         while (nb <= 56) {
@@ -132,6 +134,18 @@ struct BitReader {
         if (n <= 0) return 0;
         need(n);
         uint32_t v = (uint32_t)(win & ((n == 64) ? ~0ull : ((1ull << n) - 1)));
+        skip(n);
+        return v;
+    }
+    // BitsUtils.getbits (:37-68) as its callers see it: the returned value is
+    // the unmasked shift register, i.e. every bit up to the byte boundary the
+    // read stops at (at most 32), not just the n bits consumed.  n <= 32.
+    WVF_HD uint32_t getbits_reg(int n) {
+        const uint64_t p = consumed();
+        int bc = n + (int)((8u - ((uint32_t)(p + (uint64_t)n) & 7u)) & 7u);
+        if (bc > 32) bc = 32;
+        need(bc);
+        uint32_t v = (uint32_t)(win & ((1ull << bc) - 1));
         skip(n);
         return v;
     }
@@ -558,23 +572,27 @@ WVF_HD int32_t fixup_tail(const Fixup &f, int32_t x) {
     return f.shift ? shl32(x, f.shift) : x;
 }
 
-// int32 + wvx (UnpackUtils.cs:1271-1314): reads the extra stream, updates crc_x
-WVF_HD int32_t fixup_wvx(const Fixup &f, BitReader &xb, int32_t x, int32_t &crc_x) {
+// int32 + wvx (UnpackUtils.cs:1271-1314): reads the extra stream, updates
+// crc_x.  The wvx reader has no 0xFF fill: bs_open_read starts it 4 bytes into
+// the sub-block while `end` stays at its length (UnpackUtils.cs:130), so a read
+// past the payload indexes past the array first -> C# exception (B-10), raised
+// through `exc`.  `xlen` = payload bytes after the 4 crc bytes.
+WVF_HD int32_t fixup_wvx(const Fixup &f, BitReader &xb, uint32_t xlen, int32_t x, int32_t &crc_x, int &exc) {
     using namespace wvf;
     if (f.sent_bits > 0) {
+        int bits_to_read = f.sent_bits;
+        bool read = true;
         if (f.max_width > 0) {
             int32_t pvalue = x < 0 ? ~x : x;
             int width = (pvalue ? 32 - __builtin_clz((uint32_t)pvalue) : 0) + f.sent_bits;
-            int bits_to_read = f.sent_bits;
-            if (width <= f.max_width || (bits_to_read -= width - f.max_width) > 0) {
-                uint32_t data = xb.getbits(bits_to_read) & f.mask;
-                x = shl32((int32_t)((uint32_t)shl32(x, bits_to_read) | data), f.sent_bits - bits_to_read);
-            } else
-                x = shl32(x, f.sent_bits);
-        } else {
-            uint32_t data = xb.getbits(f.sent_bits) & f.mask;
-            x = (int32_t)((uint32_t)shl32(x, f.sent_bits) | data);
+            read = width <= f.max_width || (bits_to_read -= width - f.max_width) > 0;
         }
+        if (read) {
+            if (xb.consumed() + (uint64_t)bits_to_read > 8ull * xlen) exc = 1;
+            const uint32_t data = xb.getbits_reg(bits_to_read) & f.mask;
+            x = shl32((int32_t)((uint32_t)shl32(x, bits_to_read) | data), f.sent_bits - bits_to_read);
+        } else
+            x = shl32(x, f.sent_bits);
     }
     x = zod(f, x);
     crc_x = add32(add32(mul32(crc_x, 9), mul32(x & 0xffff, 3)), (x >> 16) & 0xffff);
@@ -712,8 +730,13 @@ WVF_HD uint32_t decode_pcm_block(const BlockDesc &d, const uint8_t *blob, Store 
             // fixup + store
             int32_t oL, oR;
             if (fx.mode == 2) {
-                oL = fixup_wvx(fx, xb, L, crc_x);
-                oR = mono ? 0 : fixup_wvx(fx, xb, R, crc_x);
+                int xexc = 0;
+                oL = fixup_wvx(fx, xb, d.wvx_len, L, crc_x, xexc);
+                oR = mono ? 0 : fixup_wvx(fx, xb, d.wvx_len, R, crc_x, xexc);
+                if (xexc) {  // fixup_samples of this call threw (the call's frame)
+                    if (exc_frame) *exc_frame = t;
+                    return status | ST_EXCEPTION;
+                }
             } else {
                 oL = fixup_tail(fx, L);
                 oR = mono ? 0 : fixup_tail(fx, R);
@@ -739,8 +762,13 @@ WVF_HD uint32_t decode_pcm_block(const BlockDesc &d, const uint8_t *blob, Store 
             for (uint32_t j = 0; j < n; j++) {
                 int32_t z0, z1 = 0;
                 if (fx.mode == 2) {
-                    z0 = fixup_wvx(fx, xb, 0, crc_x);
-                    if (!mono) z1 = fixup_wvx(fx, xb, 0, crc_x);
+                    int xexc = 0;
+                    z0 = fixup_wvx(fx, xb, d.wvx_len, 0, crc_x, xexc);
+                    if (!mono) z1 = fixup_wvx(fx, xb, d.wvx_len, 0, crc_x, xexc);
+                    if (xexc) {
+                        if (exc_frame) *exc_frame = f + j;
+                        return status | ST_EXCEPTION;
+                    }
                 } else {
                     z0 = fixup_tail(fx, 0);
                     z1 = mono ? 0 : fixup_tail(fx, 0);

@@ -29,6 +29,7 @@ enum StatusBits : uint32_t {
     ST_UNSUPPORTED = 1u << 5,  // state depends on data the device cannot see (sticky decode state)
     ST_DSD_MUTE = 1u << 6,     // DSD chunk(s) muted with 0x55 (post-pass fill, DsdUtils.cs:104-117)
     ST_NONDET = 1u << 7,       // reference output depends on stale caller-buffer contents
+    ST_TIMEOUT = 1u << 8,      // a kernel's bounded LDS wait ran out (decoder fault, not a reference outcome)
 };
 
 constexpr int MAXP = 16;  // MAX_NTERMS

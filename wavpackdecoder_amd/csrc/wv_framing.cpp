@@ -1075,9 +1075,11 @@ void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t ou
         return;
     }
     // ---- the caller's loop (WvDemo.cs:117-135) over WavpackUnpackSamples (WavPackUtils.cs:200-282)
+    info.sample_index0 = F.sample_index;
     try {
         for (;;) {
             const bool disc_call = discard > 0;
+            if (!disc_call && info.first_call_frames < 0) info.sample_index0 = F.sample_index;
             int64_t samples = disc_call ? (discard < dchunk ? discard : dchunk) : chunk, unpacked = 0;
             int64_t buf_idx = 0;
             while (samples > 0) {

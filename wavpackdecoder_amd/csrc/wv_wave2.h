@@ -4,10 +4,9 @@
 //
 //   wave 0  PARSER   get_words (WordsUtils.cs:272-511) as wave-uniform scalar
 //                    code (SALU + scalar branches).  The compressed payload is
-//                    staged HBM -> LDS 1 KiB at a time with coalesced dwordx4
-//                    loads two slots ahead of the read pointer; residuals are
-//                    packed 64 per VGPR with v_writelane and handed over through
-//                    an LDS ring.
+//                    read through the scalar cache (s_load, a dword or two
+//                    ahead of a 64-bit bit window); residuals are packed 64 per
+//                    VGPR with v_writelane and handed over through an LDS ring.
 //   wave 1  RECON    decorr passes (UnpackUtils.cs:688-1240) + joint stereo +
 //                    mute test + CRC (:549-664) + fixup (:1251-1404) per frame,
 //                    pass state in registers (term set fixed at compile time,
@@ -29,41 +28,18 @@ namespace wvg {
 namespace w2 {
 
 constexpr int RES_RING = 4096;  // residual words in flight (16 KiB)
-constexpr int SLOT_DW = 256;    // one staging slot = 1 KiB
-constexpr int NSLOT = 4;
 constexpr uint32_t SPIN_LIMIT = 1u << 26;  // bounded waits: a bug ends the kernel, never hangs the GPU
 
-// Performance experiments (never in the shipped build): 1 = reconstruction
-// wave only drains the ring, 2 = parser wave publishes zeros without parsing.
-// 3 = as 1, plus parser counters written over the block's first output ints;
-// 4 = full decode, parser counters in ints 0-7 and recon cycles in ints 8-11.
-#ifndef WV2_EXP
-#define WV2_EXP 0
-#endif
-#ifndef WV2_NARROW
-#define WV2_NARROW 1  // 0: lossless_run only (experiment builds)
-#endif
 // The reconstruction wave keeps the parser's payload ahead of it in the CU's
-// scalar cache: a scalar load per 64-byte line up to WV2_PF_AHEAD bytes past
-// the position the parser last published (0: off, experiment builds).
-#ifndef WV2_PF
-#define WV2_PF 1
-#endif
-#ifndef WV2_PF_AHEAD
-#define WV2_PF_AHEAD 1024u
-#endif
-#if WV2_EXP == 3 || WV2_EXP == 4
-#define WV2_PROF(x) x
-#else
-#define WV2_PROF(x)
-#endif
+// scalar cache: a scalar load per 64-byte line up to PF_AHEAD bytes past the
+// position the parser last published.
+constexpr uint32_t PF_AHEAD = 1024u;
 
 struct Shared {
-    uint32_t stream[NSLOT * SLOT_DW];
     int32_t res[RES_RING];
     uint32_t produced;  // words available in res (parser -> recon)
     uint32_t consumed;  // words released (recon -> parser)
-    uint32_t err;       // parser outcome: 0 running/ok, DEC_BITS_ERROR, DEC_EXCEPTION, 3 timeout
+    uint32_t err;       // parser outcome: 0 running/ok, DEC_BITS_ERROR, DEC_EXCEPTION, DEC_TIMEOUT
     uint32_t stop;      // recon asks the parser to stop (block muted)
     uint32_t pos;       // parser's read position (dword index), a prefetch hint
 };
@@ -90,124 +66,6 @@ __device__ __forceinline__ int32_t writelane(int32_t val, int lane_sel, int32_t 
 }
 
 // ---------------------------------------------------------------------------
-// LDS-staged, wave-uniform bit reader with the BitReader interface used by
-// get_word (64-bit window, past-the-end bytes read as 0xFF).
-// ---------------------------------------------------------------------------
-struct LdsReader {
-    const uint8_t *blob;
-    uint64_t A;  // 16-byte aligned start of the staged byte range
-    uint64_t E;  // end of the real bytes
-    uint32_t *ring;
-    uint64_t win;
-    int nb;
-    uint32_t rd;      // next dword index (relative to A) to enter the window
-    uint32_t nextv;   // dword rd as loaded from LDS (VGPR; read lane 0 only when it is needed)
-    uint4 stage;      // chunk in flight (per lane 16 B)
-    int lane;
-    WV2_PROF(uint32_t n_fast = 0; uint32_t n_zr = 0; uint32_t n_slow = 0; uint32_t n_refill = 0; uint64_t t_wait = 0;)
-
-    // Branch-free on purpose: a divergent branch anywhere in the parser makes
-    // the compiler move the (uniform) bit window into VGPRs.
-    __device__ __forceinline__ uint4 load_chunk(uint32_t c) const {
-        uint64_t a = A + (uint64_t)c * (SLOT_DW * 4) + (uint64_t)lane * 16;
-        const bool in = a < E;
-        const uint4 v = *(const uint4 *)(blob + (in ? a : A));  // A is always a valid address
-        const int64_t keep = in ? (int64_t)(E - a) : 0;          // real bytes in this 16 B
-        uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            int64_t kb = keep - 4 * k;
-            uint32_t sh8 = (uint32_t)(kb < 0 ? 0 : (kb > 4 ? 4 : kb)) * 8;
-            uint32_t m = sh8 >= 32 ? 0u : (0xFFFFFFFFu << sh8);  // bytes past the end read 0xFF
-            w[k] |= m;
-        }
-        return make_uint4(w[0], w[1], w[2], w[3]);
-    }
-    __device__ __forceinline__ void put_chunk(uint32_t c, uint4 v) {
-        *(uint4 *)&ring[(c & (NSLOT - 1)) * SLOT_DW + lane * 4] = v;
-    }
-    __device__ __forceinline__ uint32_t lds_dw(uint32_t i) const { return uni(ring[i & (NSLOT * SLOT_DW - 1)]); }
-
-    __device__ __forceinline__ void init(const uint8_t *b, uint64_t off, uint64_t len, uint32_t *r, int ln) {
-        blob = b;
-        A = off & ~(uint64_t)15;
-        E = off + len;
-        ring = r;
-        lane = ln;
-        put_chunk(0, load_chunk(0));
-        put_chunk(1, load_chunk(1));
-        stage = load_chunk(2);
-        int skip = (int)(off - A) * 8;  // 0..120 bits
-        win = (uint64_t)lds_dw(0) | ((uint64_t)lds_dw(1) << 32);
-        nb = 64;
-        rd = 2;
-        nextv = ring[2];
-        while (skip >= 32) {
-            win >>= 32;
-            nb -= 32;
-            skip -= 32;
-            refill32();
-        }
-        if (skip) {
-            win >>= skip;
-            nb -= skip;
-        }
-    }
-    __device__ __forceinline__ void refill32() {
-        win |= (uint64_t)uni(nextv) << nb;
-        nb += 32;
-        rd++;
-        if ((rd & (SLOT_DW - 1)) == 0) {  // entering chunk c = rd / 256
-            uint32_t c = rd / SLOT_DW;
-            put_chunk(c + 1, stage);
-            stage = load_chunk(c + 2);
-        }
-        nextv = ring[rd & (NSLOT * SLOT_DW - 1)];  // waited for at the next refill, not here
-    }
-    // 32-bit refills keep the window invariant: bits at and above nb are 0,
-    // so a refill is only legal while nb <= 32; every caller needs <= 32 bits.
-    __device__ __forceinline__ void need(int n) {
-        if (nb < n) refill32();
-    }
-    __device__ __forceinline__ void skip(int n) {
-        win >>= n;
-        nb -= n;
-    }
-    __device__ __forceinline__ int getbit() {
-        need(1);
-        int b = (int)(win & 1);
-        skip(1);
-        return b;
-    }
-    __device__ __forceinline__ uint32_t getbits(int n) {
-        if (n <= 0) return 0;
-        need(n);
-        uint32_t v = (uint32_t)(win & ((1ull << n) - 1));
-        skip(n);
-        return v;
-    }
-    __device__ __forceinline__ int consume_ones(int cap) {
-        int total = 0;
-        for (;;) {
-            if (nb <= 32) refill32();  // nb in [33, 64]
-            uint64_t inv = ~win;       // ones above nb stop the count at nb
-            int r = inv ? __builtin_ctzll(inv) : 64;
-            if (total + r >= cap) {
-                skip(cap - total);
-                return cap;
-            }
-            if (r < nb) {
-                skip(r + 1);
-                return total + r;
-            }
-            total += nb;  // the whole window was ones
-            win = 0;
-            nb = 0;
-        }
-    }
-};
-
-// ---------------------------------------------------------------------------
 // Scalar-memory bit reader with the BitReader interface used by get_word:
 // the payload is read dword by dword with s_load (constant address space, so
 // the loads are scalar and go through the scalar cache), two dwords ahead of
@@ -223,7 +81,6 @@ struct SmemReader {
     int nb;
     uint32_t rd;    // index of the next dword to enter the window (== n0)
     uint32_t n0, n1;
-    WV2_PROF(uint32_t n_fast = 0; uint32_t n_zr = 0; uint32_t n_slow = 0; uint32_t n_refill = 0; uint64_t t_wait = 0;)
 
     __device__ __forceinline__ uint32_t ld(uint32_t i) const {
         const uint32_t b = 4u * i;
@@ -294,18 +151,7 @@ struct SmemReader {
     }
 };
 
-#ifndef WV2_READER
-#define WV2_READER SmemReader
-#endif
-typedef WV2_READER Reader;
-
-__device__ __forceinline__ void init_reader(SmemReader &rd, const uint8_t *blob, const BlockDesc &d, Shared &, int) {
-    rd.init(blob, d.bits_off, d.bits_len);
-}
-__device__ __forceinline__ void init_reader(LdsReader &rd, const uint8_t *blob, const BlockDesc &d, Shared &sh,
-                                            int lane) {
-    rd.init(blob, d.bits_off, d.bits_len, sh.stream, lane);
-}
+typedef SmemReader Reader;
 
 // ---------------------------------------------------------------------------
 // parser wave.  Everything here must stay wave-uniform (SGPRs, scalar
@@ -1022,17 +868,14 @@ __device__ __forceinline__ int parse_word(Entropy &w, Reader &rd, uint32_t flags
         if (__builtin_expect(!zr, 1)) {
             if (__builtin_expect(rd.nb < 32, 0)) rd.refill32();
             if (__builtin_expect(fast_word<C>(w, rd, v), 1)) {
-                WV2_PROF(rd.n_fast++;)
                 return DEC_OK;
             }
         } else if (w.zeros_acc > 1) {  // inside a zero run (WordsUtils.cs:306-311; slow_level is dead here)
             w.zeros_acc--;
             v = 0;
-            WV2_PROF(rd.n_zr++;)
             return DEC_OK;
         }
     }
-    WV2_PROF(rd.n_slow++;)
     return get_word(w, rd, flags, C, C == 0, v);
 }
 
@@ -1050,18 +893,17 @@ __device__ __forceinline__ void parse_loop(const BlockDesc &d, Reader &rd, Entro
             // inside a zero run (WordsUtils.cs:304-317): the next zeros_acc - 1
             // words are 0 and change nothing but zeros_acc (slow_level is dead
             // in lossless blocks) -> a whole stretch of the batch at once
-            if (LOSSLESS && WV2_EXP != 2 && __builtin_expect(w.zeros_acc > 1, 0) &&
+            if (LOSSLESS && __builtin_expect(w.zeros_acc > 1, 0) &&
                 (uint32_t)(w.med[0][0] | w.med[1][0]) <= 1u && (w.h0 | w.h1) == 0) {
                 const uint32_t n = (uint32_t)min((int64_t)(kend - k), w.zeros_acc - 1);
                 const uint32_t lo = k & 63u;
                 resv = ((uint32_t)lane - lo < n) ? 0 : resv;
                 w.zeros_acc -= n;
                 k += n;
-                WV2_PROF(rd.n_zr += n;)
                 continue;
             }
-            if (LOSSLESS && WV2_EXP != 2 && (MONO || (k & 1) == 0)) {
-                if (WV2_NARROW && narrow_ok<MONO>(w, rd)) {
+            if (LOSSLESS && (MONO || (k & 1) == 0)) {
+                if (narrow_ok<MONO>(w, rd)) {
                     if (lossless_run_narrow<MONO>(w, rd, k, kend, resv)) break;
                 } else if (lossless_run<MONO>(w, rd, k, kend, resv)) {
                     break;
@@ -1071,9 +913,9 @@ __device__ __forceinline__ void parse_loop(const BlockDesc &d, Reader &rd, Entro
             int32_t v = 0;
             int rc = DEC_OK;
             if (MONO || (k & 1) == 0) {
-                rc = WV2_EXP == 2 ? DEC_OK : parse_word<0, LOSSLESS>(w, rd, flags, v);
+                rc = parse_word<0, LOSSLESS>(w, rd, flags, v);
             } else {
-                rc = WV2_EXP == 2 ? DEC_OK : parse_word<1, LOSSLESS>(w, rd, flags, v);
+                rc = parse_word<1, LOSSLESS>(w, rd, flags, v);
             }
             if (__builtin_expect(rc != DEC_OK, 0)) {
                 err = (uint32_t)rc;
@@ -1087,20 +929,18 @@ __device__ __forceinline__ void parse_loop(const BlockDesc &d, Reader &rd, Entro
             // wait for ring space, publish the batch
             uint32_t base = (k - 1) & ~63u;
             uint32_t spins = 0;
-            WV2_PROF(uint64_t tw0 = clock64();)
             while (base + 64 - consumed > (uint32_t)RES_RING) {
                 __builtin_amdgcn_s_sleep(2);
                 consumed = uni(lds_load_acq(&sh.consumed));
                 if (uni(lds_load_acq(&sh.stop))) return;  // the block was muted
                 if (++spins > SPIN_LIMIT) {
-                    err = 3;
+                    err = DEC_TIMEOUT;
                     break;
                 }
             }
-            WV2_PROF(rd.t_wait += clock64() - tw0;)
             if (err) break;
             sh.res[(base % RES_RING) + lane] = resv;
-            if (WV2_PF) __hip_atomic_store(&sh.pos, rd.rd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(&sh.pos, rd.rd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             lds_publish(&sh.produced, k);
             if (uni(lds_load_acq(&sh.stop))) return;
         }
@@ -1108,7 +948,7 @@ __device__ __forceinline__ void parse_loop(const BlockDesc &d, Reader &rd, Entro
     if (err) {
         // publish the complete words before the error, then the outcome
         uint32_t base = k & ~63u;
-        if ((k & 63) && err != 3) {
+        if ((k & 63) && err != DEC_TIMEOUT) {
             uint32_t spins = 0;
             while (base + 64 - consumed > (uint32_t)RES_RING && ++spins < SPIN_LIMIT) {
                 __builtin_amdgcn_s_sleep(2);
@@ -1122,10 +962,9 @@ __device__ __forceinline__ void parse_loop(const BlockDesc &d, Reader &rd, Entro
     }
 }
 
-__device__ __forceinline__ void parser(const BlockDesc &d, const uint8_t *blob, Shared &sh, int lane, int32_t *dbg) {
-    WV2_PROF(const uint64_t t_start = clock64();)
+__device__ __forceinline__ void parser(const BlockDesc &d, const uint8_t *blob, Shared &sh, int lane) {
     Reader rd;
-    init_reader(rd, blob, d, sh, lane);
+    rd.init(blob, d.bits_off, d.bits_len);
     Entropy w;
 #pragma unroll
     for (int c = 0; c < 2; c++) {
@@ -1146,19 +985,6 @@ __device__ __forceinline__ void parser(const BlockDesc &d, const uint8_t *blob, 
         if (lossless) parse_loop<false, true>(d, rd, w, sh, lane);
         else parse_loop<false, false>(d, rd, w, sh, lane);
     }
-#if WV2_EXP == 3 || WV2_EXP == 4
-    const uint64_t t_total = clock64() - t_start;
-    uint32_t vals[8] = {rd.n_fast, rd.n_zr, rd.n_slow, rd.n_refill, (uint32_t)t_total, (uint32_t)(t_total >> 32),
-                        (uint32_t)rd.t_wait, (uint32_t)(rd.t_wait >> 32)};
-    if (lane < 8) {
-        uint32_t x = vals[0];
-#pragma unroll
-        for (int i = 1; i < 8; i++) x = lane == i ? vals[i] : x;
-        dbg[lane] = (int32_t)x;
-    }
-#else
-    (void)dbg;
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1449,13 +1275,13 @@ __device__ __forceinline__ void recon_batch(CH &ch, const Fixup &fx, const int32
 }
 
 // Reconstruction-wave side of the payload prefetch: touch every 64-byte line
-// from pf up to WV2_PF_AHEAD bytes past the parser's published position
+// from pf up to PF_AHEAD bytes past the parser's published position
 // (at most 4 lines per call), so the parser's s_loads hit the CU's scalar
 // cache.  Byte offsets are relative to the dword-aligned payload base and
 // stay <= pf_end (the last whole dword of the payload).
 __device__ __forceinline__ void scalar_prefetch(uint32_t &pf, cdw_ptr base, uint32_t pf_end, Shared &sh) {
     const uint32_t pos = uni(__hip_atomic_load(&sh.pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) * 4u;
-    uint32_t tgt = pos + WV2_PF_AHEAD;
+    uint32_t tgt = pos + PF_AHEAD;
     if (tgt > pf_end) tgt = pf_end;
     if (pf > tgt) return;
     const uint32_t o0 = pf, o1 = min(pf + 64u, tgt), o2 = min(pf + 128u, tgt), o3 = min(pf + 192u, tgt);
@@ -1511,14 +1337,12 @@ __device__ __forceinline__ void recon_impl(const BlockDesc &d, const uint8_t *bl
     const cdw_ptr pf_base = (cdw_ptr)(blob + (d.bits_off & ~(uint64_t)3));
     const uint32_t pf_end = d.bits_len + (uint32_t)(d.bits_off & 3) >= 4u ? d.bits_len + (uint32_t)(d.bits_off & 3) - 4u : 0u;
     uint32_t pf = 0;
-    WV2_PROF(const uint64_t r_start = clock64(); uint64_t r_wait = 0;)
 
     for (uint32_t t0 = 0; t0 < nfr; t0 += BF) {
         uint32_t tend = t0 + BF < nfr ? t0 + BF : nfr;
         uint32_t need = tend * WPF;
         uint32_t spins = 0;
         uint32_t perr = 0;
-        WV2_PROF(const uint64_t rw0 = clock64();)
         while (produced < need) {
             produced = uni(lds_load_acq(&sh.produced));
             if (produced >= need) break;
@@ -1529,15 +1353,19 @@ __device__ __forceinline__ void recon_impl(const BlockDesc &d, const uint8_t *bl
             }
             __builtin_amdgcn_s_sleep(2);
             if (++spins > SPIN_LIMIT) {
-                perr = 3;
+                perr = DEC_TIMEOUT;
                 break;
             }
         }
-        WV2_PROF(r_wait += clock64() - rw0;)
-        if (WV2_PF) scalar_prefetch(pf, pf_base, pf_end, sh);
-        if (perr == DEC_EXCEPTION || perr == 3) {
+        scalar_prefetch(pf, pf_base, pf_end, sh);
+        if (perr == DEC_EXCEPTION) {
             status |= ST_EXCEPTION;
             if (lane == 0) *exc_out = produced / WPF;  // block frame of the word that threw
+            lds_store_rel(&sh.stop, 1);
+            break;
+        }
+        if (perr == DEC_TIMEOUT) {  // a handshake bug, never a property of the stream
+            status |= ST_TIMEOUT;
             lds_store_rel(&sh.stop, 1);
             break;
         }
@@ -1551,8 +1379,7 @@ __device__ __forceinline__ void recon_impl(const BlockDesc &d, const uint8_t *bl
                              (sm.chunk_end - 1 >= t0 && sm.chunk_end - 1 <= tlast);
         const bool quirk_in =
             MONO && (sm.crc_stop || (sm.bsp > 0 && sm.chunk_end - sm.bsp >= t0 && sm.chunk_end - sm.bsp <= tlast));
-        if (WV2_EXP == 1 || WV2_EXP == 3) {
-        } else if (tvalid == t0 + BF && !seam_in && !quirk_in) {
+        if (tvalid == t0 + BF && !seam_in && !quirk_in) {
             if (joint) {
                 if (ident) recon_batch<LAYOUT, true, true, true>(ch, fx, sh.res, rbase, o0, o1, crc, ml, t0, tvalid, sm, mute_at, lane);
                 else recon_batch<LAYOUT, true, true, false>(ch, fx, sh.res, rbase, o0, o1, crc, ml, t0, tvalid, sm, mute_at, lane);
@@ -1569,7 +1396,7 @@ __device__ __forceinline__ void recon_impl(const BlockDesc &d, const uint8_t *bl
         // store the batch: 64 ints per instruction, one per lane
         const uint32_t nv = (mute_at >= 0 ? (uint32_t)mute_at : tvalid) - t0;
         const uint64_t base = (uint64_t)t0 * OCH;
-        if (WV2_EXP != 3 && (uint32_t)lane < nv * OCH && base + lane >= skip) out[base + lane] = o0;
+        if ((uint32_t)lane < nv * OCH && base + lane >= skip) out[base + lane] = o0;
         if (LAYOUT == 2 && (uint32_t)lane + 64 < nv * OCH && base + 64 + lane >= skip) out[base + 64 + lane] = o1;
         const bool bits_err = tvalid < tend;
         if (mute_at >= 0 || bits_err) {
@@ -1585,20 +1412,11 @@ __device__ __forceinline__ void recon_impl(const BlockDesc &d, const uint8_t *bl
             break;
         }
     }
-    if (!(status & ST_EXCEPTION) && nfr == d.block_samples) {
+    if (!(status & (ST_EXCEPTION | ST_TIMEOUT)) && nfr == d.block_samples) {
         status |= ST_CRC_CHECKED;
         if (crc_garbage || (int32_t)uni((uint32_t)crc) != d.crc) status |= ST_CRC_ERROR;
     }
     if (lane == 0) *status_out = d.fstatus | status;
-#if WV2_EXP == 4
-    const uint64_t r_total = clock64() - r_start;
-    if (lane == 0) {
-        out[8] = (int32_t)(uint32_t)r_total;
-        out[9] = (int32_t)(uint32_t)(r_total >> 32);
-        out[10] = (int32_t)(uint32_t)r_wait;
-        out[11] = (int32_t)(uint32_t)(r_wait >> 32);
-    }
-#endif
 }
 
 template <int... Ts>
@@ -1628,28 +1446,10 @@ __device__ __forceinline__ void block_2wave(const BlockDesc *descs, const uint32
         sh.pos = 0;
     }
     __syncthreads();
-#if WV2_EXP == 5
-    uint32_t hw, xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    const uint64_t t_beg = __builtin_amdgcn_s_memrealtime();
-#endif
     if (wave == 0)
-        parser(d, blob, sh, lane, out + d.out_off);
+        parser(d, blob, sh, lane);
     else
         recon<Ts...>(d, blob, sh, out, &status[bi], &aux[bi], lane);
-#if WV2_EXP == 5
-    // placement + timeline probe: ints 12-15 (parser) / 16-19 (recon) of the block's output
-    const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
-    __syncthreads();
-    if (lane == 0) {
-        int32_t *o = out + d.out_off + 12 + wave * 4;
-        o[0] = (int32_t)hw;
-        o[1] = (int32_t)xcc;
-        o[2] = (int32_t)(uint32_t)t_beg;
-        o[3] = (int32_t)(uint32_t)t_end;
-    }
-#endif
 }
 
 }  // namespace w2
