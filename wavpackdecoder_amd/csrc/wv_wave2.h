@@ -1358,14 +1358,12 @@ __device__ __forceinline__ void recon_impl(const BlockDesc &d, const uint8_t *bl
             }
         }
         scalar_prefetch(pf, pf_base, pf_end, sh);
-        if (perr == DEC_EXCEPTION) {
-            status |= ST_EXCEPTION;
+        // one exit for both (a second branch here costs the 16-term kernels ~110 VGPRs
+        // of structurised control flow); a timeout is a handshake bug, never a
+        // property of the stream, and gets its own status bit
+        if (perr == DEC_EXCEPTION || perr == DEC_TIMEOUT) {
+            status |= perr == DEC_EXCEPTION ? ST_EXCEPTION : ST_TIMEOUT;
             if (lane == 0) *exc_out = produced / WPF;  // block frame of the word that threw
-            lds_store_rel(&sh.stop, 1);
-            break;
-        }
-        if (perr == DEC_TIMEOUT) {  // a handshake bug, never a property of the stream
-            status |= ST_TIMEOUT;
             lds_store_rel(&sh.stop, 1);
             break;
         }
