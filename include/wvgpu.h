@@ -117,13 +117,21 @@ int wvg_batch_add_file(wvg_batch *b, const uint8_t *file, size_t len, uint32_t o
 int wvg_batch_add_file_at(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open_flags, int64_t start_sample,
                           wvg_file_info *info);
 
-/* Copy blob + descriptors to the device and zero the output. */
+/* Copy blob + descriptors to the device and zero the output (device buffers are
+ * kept across uploads of a refilled batch and only grown). */
 int wvg_batch_upload(wvg_batch *b);
 
-/* Enqueue the decode kernels on `stream` (hipStream_t, NULL = the context's
- * stream).  Input and output stay in HBM. */
+/* Enqueue the decode kernels on `stream` (hipStream_t, NULL = the batch's own
+ * stream).  Input and output stay in HBM.  Every batch owns its streams, so
+ * batches decode concurrently; nothing synchronises the whole device. */
 int wvg_batch_decode(wvg_batch *b, void *stream);
+/* Wait for the batch's last decode / format (an event on the stream it ran on). */
 int wvg_batch_sync(wvg_batch *b);
+void *wvg_batch_stream(wvg_batch *b);  /* the batch's own hipStream_t */
+/* Device timing of every following decode (an event pair around each launch, on its
+ * stream); wvg_batch_timed waits for them and returns the mean and the count. */
+int wvg_batch_set_timing(wvg_batch *b, int on);
+int wvg_batch_timed(wvg_batch *b, float *avg_ms, int *count);
 
 int64_t wvg_batch_out_ints(const wvg_batch *b);
 int32_t *wvg_batch_device_out(wvg_batch *b);      /* device pointer to the int32 output */

@@ -12,17 +12,26 @@ from wavpackdecoder_amd._lib import WVG_ST_TIMEOUT
 pytestmark = pytest.mark.gpu
 
 
+# kernel routes: "2wave" (the product routing: compile-time shallow term lists,
+# the pipelined kernel for every other list, the generic kernel for int32+wvx),
+# "generic" (the wave-per-block kernel for every PCM block), "pipe" (the
+# pipelined kernel for every PCM block without wvx)
+ROUTES = {"2wave": ("0", "0"), "generic": ("1", "0"), "pipe": ("0", "2"), False: ("0", "0"), True: ("1", "0")}
+
+
 def _gpu_decode(files, chunk, batch_cls, force_lane=False):
     import os
-    old = os.environ.get("WVG_FORCE_LANE")
-    os.environ["WVG_FORCE_LANE"] = "1" if force_lane else "0"
+    env = dict(zip(("WVG_FORCE_LANE", "WVG_PIPE"), ROUTES[force_lane]))
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         b = batch_cls(chunk)
     finally:
-        if old is None:
-            os.environ.pop("WVG_FORCE_LANE", None)
-        else:
-            os.environ["WVG_FORCE_LANE"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     idx = [b.add_file(d) for d in files]
     b.decode()
     out = b.download()
@@ -52,7 +61,7 @@ def _check_one(data, chunk, batch_cls, name, force_lane=False):
     np.testing.assert_array_equal(got, ref.samples, err_msg=name)
 
 
-@pytest.mark.parametrize("lane", [False, True], ids=["2wave", "generic"])
+@pytest.mark.parametrize("lane", ["2wave", "generic", "pipe"])
 @pytest.mark.parametrize("case", V.pcm_cases(), ids=lambda c: c[0])
 def test_pcm_modes(case, lane, gpu_batch_cls):
     name, data, chunk = case
@@ -72,7 +81,7 @@ def test_corrupted_streams(gpu_batch_cls):
     base = S.encode_pcm(x, S.EncParams(terms=S.TERMS_DEFAULT, block_samples=4000))
     basem = S.encode_pcm(m, S.EncParams(nch=1, terms=S.TERMS_MONO_HIGH, block_samples=3001))
     basex = V.int32_file(x, sent_bits=6, ones=2, wvx=2, max_width=21)
-    for lane in (False, True):
+    for lane in ("2wave", "generic", "pipe"):
         for k in range(10):
             _check_one(V.corrupt(base, k), 4096, gpu_batch_cls, f"stereo#{k}", lane)
             _check_one(V.corrupt(basem, 100 + k), 1000, gpu_batch_cls, f"mono#{k}", lane)
@@ -113,9 +122,10 @@ def test_c3_full_block_high24(gpu_batch_cls):
     from synth import wvsynth as S
     x = S.audio_like(2 * 44100 + 777, 2, 24, seed=0xC3)
     data = S.encode_pcm(x, S.EncParams(terms=S.TERMS_HIGH, bytes_per_sample=3, block_samples=44100))
-    _check_one(data, 4096, gpu_batch_cls, "c3_full_block")
-    out, res, infos = _gpu_decode([data], 4096, gpu_batch_cls)
-    np.testing.assert_array_equal(out[: x.size], x.reshape(-1))
+    for route in ("2wave", "pipe"):
+        _check_one(data, 4096, gpu_batch_cls, "c3_full_block", route)
+        out, res, infos = _gpu_decode([data], 4096, gpu_batch_cls, route)
+        np.testing.assert_array_equal(out[: x.size], x.reshape(-1))
 
 
 def test_golden_fixtures(gpu_batch_cls):

@@ -80,6 +80,9 @@ def lib():
         "wvg_batch_upload": (i32, [vp]),
         "wvg_batch_decode": (i32, [vp, vp]),
         "wvg_batch_sync": (i32, [vp]),
+        "wvg_batch_stream": (vp, [vp]),
+        "wvg_batch_set_timing": (i32, [vp, i32]),
+        "wvg_batch_timed": (i32, [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]),
         "wvg_batch_out_ints": (i64, [vp]),
         "wvg_batch_device_out": (vp, [vp]),
         "wvg_batch_num_blocks": (i64, [vp]),
@@ -111,7 +114,8 @@ def lib():
 
 EXPORTED = ("wvg_open", "wvg_close", "wvg_last_error", "wvg_batch_new", "wvg_batch_free", "wvg_batch_add_file",
             "wvg_batch_add_file_at",
-            "wvg_batch_upload", "wvg_batch_decode", "wvg_batch_sync", "wvg_batch_out_ints", "wvg_batch_device_out",
+            "wvg_batch_upload", "wvg_batch_decode", "wvg_batch_sync", "wvg_batch_stream", "wvg_batch_set_timing",
+            "wvg_batch_timed", "wvg_batch_out_ints", "wvg_batch_device_out",
             "wvg_batch_num_blocks", "wvg_batch_bytes_in", "wvg_batch_frames", "wvg_batch_download",
             "wvg_batch_file_result", "wvg_batch_block_status", "wvg_batch_file_blocks", "wvg_batch_time", "wvg_decode_file",
             "wvg_probe_file", "wvg_format_samples", "wvg_batch_format", "wvg_batch_pcm_bytes", "wvg_batch_pcm_offset",

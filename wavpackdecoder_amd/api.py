@@ -95,6 +95,16 @@ class DecodeBatch:
     def sync(self):
         self._check(self._L.wvg_batch_sync(self._b))
 
+    def set_timing(self, on: bool = True):
+        """Record a device event pair around every following decode (wvg_batch_set_timing)."""
+        self._check(self._L.wvg_batch_set_timing(self._b, int(bool(on))))
+
+    def timed(self):
+        """(mean ms, count) of the decodes recorded since set_timing(True)."""
+        ms, n = ctypes.c_float(), ctypes.c_int()
+        self._check(self._L.wvg_batch_timed(self._b, ctypes.byref(ms), ctypes.byref(n)))
+        return float(ms.value), int(n.value)
+
     def time(self, iters: int) -> float:
         ms = ctypes.c_float()
         self._check(self._L.wvg_batch_time(self._b, int(iters), ctypes.byref(ms)))

@@ -16,7 +16,7 @@ namespace wvg {
 hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint32_t n_pcm, const uint32_t *dsd_list,
                          uint32_t n_dsd, const uint8_t *blob, const uint8_t *tables, int32_t *out, uint32_t *status,
                          uint32_t *aux, hipStream_t s_pcm, hipStream_t s_dsd);
-int term_set_of(const BlockDesc &d);
+int term_set_of(const BlockDesc &d, int prefer_pipe);
 hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, uint32_t n, const uint8_t *blob,
                         int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s);
 hipError_t launch_format(const FormatSeg *segs, uint32_t nseg, const int32_t *in, uint8_t *out, int dsd, hipStream_t s);
@@ -29,21 +29,30 @@ constexpr uint32_t kFormatSeg = 65536;  // values per format work item
 using namespace wvg;
 
 // The kernels of one decode (a two-wave launch per term set, the generic PCM
-// kernel, the DSD kernels) are independent: they fork from the caller's stream
-// onto side streams and join back, so small groups run concurrently.
+// kernel, the DSD kernels) are independent: they fork from the batch's stream
+// onto the batch's side streams and join back, so small groups run concurrently.
+// Every batch owns its streams, so batches of one context (or of several host
+// threads) run concurrently on the device; nothing synchronises the whole device.
 constexpr int kSide = kMaxTermSets + 2;
 
 struct wvg_ctx {
     int device = 0;
-    hipStream_t stream = nullptr;
-    hipStream_t side[kSide] = {nullptr};
-    hipEvent_t fork = nullptr, join[kSide] = {nullptr};
     std::string err;
 };
 
 struct wvg_batch {
     wvg_ctx *ctx = nullptr;
     int chunk = 4096;
+    hipStream_t stream = nullptr;          // the batch's own stream (default for decode/format/download)
+    hipStream_t side[kSide] = {nullptr};
+    hipEvent_t fork = nullptr, join[kSide] = {nullptr};
+    hipEvent_t done = nullptr;             // end of the last decode/format, on whatever stream it ran
+    bool timing = false;                   // wvg_batch_set_timing: an event pair around every decode
+    std::vector<hipEvent_t> tev;
+    // device buffers are kept across uploads and only grown (capacities in bytes)
+    size_t cap_blob = 0, cap_descs = 0, cap_items = 0, cap_jobs = 0, cap_tables = 0, cap_out = 0, cap_st = 0,
+           cap_pcml = 0, cap_dsd = 0, cap_pcm = 0, cap_segs = 0, cap_ts[kMaxTermSets] = {0};
+    bool segs_uploaded = false;
     std::vector<uint8_t> blob;
     FramingOutput fo;
     std::vector<FileInfo> finfo;
@@ -53,6 +62,7 @@ struct wvg_batch {
     std::vector<uint32_t> ts_list[kMaxTermSets];        // two-wave kernels per term set
     uint32_t *d_ts[kMaxTermSets] = {nullptr};
     int force_lane = 0;                                 // WVG_FORCE_LANE=1: every PCM block on the generic kernel
+    int prefer_pipe = 0;                                // WVG_PIPE=2: every PCM list on the pipelined kernel (A/B)
     std::vector<uint32_t> h_status, h_aux;
     int64_t bytes_in = 0, frames = 0;
     // format epilogue: per-file byte image of WavpackFormatSamples
@@ -80,53 +90,67 @@ static int hip_fail(wvg_ctx *c, hipError_t e, const char *what) {
         if (_e != hipSuccess) return hip_fail((c), _e, #x); \
     } while (0)
 
+// grow-only device allocation: a batch that is refilled and re-uploaded keeps its buffers
+template <class T>
+static hipError_t ensure(T *&p, size_t &cap, size_t bytes) {
+    if (bytes <= cap && p) return hipSuccess;
+    hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e == hipSuccess) cap = bytes;
+    return e;
+}
+
 extern "C" {
 
 wvg_ctx *wvg_open(int device) {
-    wvg_ctx *c = new wvg_ctx();
     int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
-        delete c;
-        return nullptr;
-    }
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return nullptr;
     if (device < 0) hipGetDevice(&device);
-    if (hipSetDevice(device) != hipSuccess) {
-        delete c;
-        return nullptr;
-    }
+    if (device >= n || hipSetDevice(device) != hipSuccess) return nullptr;
+    wvg_ctx *c = new wvg_ctx();
     c->device = device;
-    bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
-              hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess;
-    for (int i = 0; ok && i < kSide; i++)
-        ok = hipStreamCreateWithFlags(&c->side[i], hipStreamNonBlocking) == hipSuccess &&
-             hipEventCreateWithFlags(&c->join[i], hipEventDisableTiming) == hipSuccess;
-    if (!ok) {
-        wvg_close(c);
-        return nullptr;
-    }
     return c;
 }
 
-void wvg_close(wvg_ctx *c) {
-    if (!c) return;
-    for (int i = 0; i < kSide; i++) {
-        if (c->side[i]) hipStreamDestroy(c->side[i]);
-        if (c->join[i]) hipEventDestroy(c->join[i]);
-    }
-    if (c->fork) hipEventDestroy(c->fork);
-    if (c->stream) hipStreamDestroy(c->stream);
-    delete c;
-}
+void wvg_close(wvg_ctx *c) { delete c; }
 
 const char *wvg_last_error(wvg_ctx *c) { return c ? c->err.c_str() : "no context"; }
 
+static void free_streams(wvg_batch *b) {
+    for (int i = 0; i < kSide; i++) {
+        if (b->side[i]) hipStreamDestroy(b->side[i]);
+        if (b->join[i]) hipEventDestroy(b->join[i]);
+    }
+    if (b->fork) hipEventDestroy(b->fork);
+    if (b->done) hipEventDestroy(b->done);
+    if (b->stream) hipStreamDestroy(b->stream);
+    for (auto &e : b->tev) hipEventDestroy(e);
+    b->tev.clear();
+}
+
 wvg_batch *wvg_batch_new(wvg_ctx *c, int chunk_frames) {
     if (!c || chunk_frames <= 0) return nullptr;
+    if (hipSetDevice(c->device) != hipSuccess) return nullptr;
     wvg_batch *b = new wvg_batch();
     b->ctx = c;
     b->chunk = chunk_frames;
+    // side streams are created on first use (a batch with one launch group needs
+    // none): every stream takes one of the process's few hardware queues
+    // (GPU_MAX_HW_QUEUES), and batches in flight should each get their own
+    bool ok = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) == hipSuccess &&
+              hipEventCreateWithFlags(&b->fork, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&b->done, hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        free_streams(b);
+        delete b;
+        return nullptr;
+    }
     const char *fl = getenv("WVG_FORCE_LANE");
     b->force_lane = fl && fl[0] == '1';
+    const char *pp = getenv("WVG_PIPE");
+    b->prefer_pipe = pp ? atoi(pp) : 0;
     // the decorr/entropy values of each block are parsed on the device (wv_meta_parse);
     // WVG_HOST_META=1 keeps them on the host framing (A/B comparisons)
     const char *hm = getenv("WVG_HOST_META");
@@ -150,6 +174,7 @@ static void free_dev(wvg_batch *b) {
     for (int t = 0; t < kMaxTermSets; t++) {
         hipFree(b->d_ts[t]);
         b->d_ts[t] = nullptr;
+        b->cap_ts[t] = 0;
     }
     b->d_blob = b->d_tables = b->d_pcm = nullptr;
     b->d_descs = nullptr;
@@ -158,13 +183,17 @@ static void free_dev(wvg_batch *b) {
     b->d_segs = nullptr;
     b->d_out = nullptr;
     b->d_status = b->d_mute = b->d_pcml = b->d_dsd = nullptr;
-    b->uploaded = b->formatted = false;
+    b->cap_blob = b->cap_descs = b->cap_items = b->cap_jobs = b->cap_tables = b->cap_out = b->cap_st = 0;
+    b->cap_pcml = b->cap_dsd = b->cap_pcm = b->cap_segs = 0;
+    b->uploaded = b->formatted = b->segs_uploaded = false;
 }
 
 void wvg_batch_free(wvg_batch *b) {
     if (!b) return;
     hipSetDevice(b->ctx->device);
+    if (b->stream) hipStreamSynchronize(b->stream);
     free_dev(b);
+    free_streams(b);
     delete b;
 }
 
@@ -204,7 +233,7 @@ int wvg_probe_file(const uint8_t *file, size_t len, uint32_t open_flags, int chu
 static int add_file(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open_flags, int64_t seek_to,
                     wvg_file_info *info) {
     if (!b || (!file && len)) return WVG_ERR_ARG;
-    if (b->uploaded) free_dev(b);
+    b->uploaded = b->formatted = false;
     size_t base = (b->blob.size() + 15) & ~(size_t)15;
     b->blob.resize(base + len);
     if (len) memcpy(b->blob.data() + base, file, len);
@@ -242,7 +271,7 @@ static int add_file(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open
     b->out_ints += extent;
     for (int64_t k = fi.first_desc; k < fi.first_desc + fi.num_desc; k++) {
         const BlockDesc &d = b->fo.descs[(size_t)k];
-        int ts = (d.kind == KIND_PCM && !b->force_lane) ? term_set_of(d) : -1;
+        int ts = (d.kind == KIND_PCM && !b->force_lane) ? term_set_of(d, b->prefer_pipe) : -1;
         if (ts >= 0) b->ts_list[ts].push_back((uint32_t)k);
         else if (d.kind == KIND_PCM) b->pcm_list.push_back((uint32_t)k);
         else if (d.kind != KIND_SKIP) b->dsd_list.push_back((uint32_t)k);
@@ -266,36 +295,39 @@ int wvg_batch_add_file_at(wvg_batch *b, const uint8_t *file, size_t len, uint32_
 int wvg_batch_upload(wvg_batch *b) {
     if (!b) return WVG_ERR_ARG;
     wvg_ctx *c = b->ctx;
+    hipStream_t s = b->stream;
     HIPCHK(c, hipSetDevice(c->device));
-    free_dev(b);
-    size_t blob_n = b->blob.size() + 64;
-    HIPCHK(c, hipMalloc(&b->d_blob, blob_n));
-    HIPCHK(c, hipMemsetAsync(b->d_blob, 0xFF, blob_n, c->stream));
-    if (!b->blob.empty()) HIPCHK(c, hipMemcpyAsync(b->d_blob, b->blob.data(), b->blob.size(), hipMemcpyHostToDevice, c->stream));
-    size_t nd = b->fo.descs.size();
-    HIPCHK(c, hipMalloc(&b->d_descs, sizeof(BlockDesc) * (nd ? nd : 1)));
-    if (nd) HIPCHK(c, hipMemcpyAsync(b->d_descs, b->fo.descs.data(), sizeof(BlockDesc) * nd, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(s));  // earlier work on these buffers
+    b->formatted = false;
+    // the blob is followed by 64 B of 0xFF (the reader's past-end fill)
+    const size_t blob_n = b->blob.size() + 64;
+    HIPCHK(c, ensure(b->d_blob, b->cap_blob, blob_n));
+    HIPCHK(c, hipMemsetAsync(b->d_blob + b->blob.size(), 0xFF, 64, s));
+    if (!b->blob.empty()) HIPCHK(c, hipMemcpyAsync(b->d_blob, b->blob.data(), b->blob.size(), hipMemcpyHostToDevice, s));
+    const size_t nd = b->fo.descs.size();
+    HIPCHK(c, ensure(b->d_descs, b->cap_descs, sizeof(BlockDesc) * (nd ? nd : 1)));
+    if (nd) HIPCHK(c, hipMemcpyAsync(b->d_descs, b->fo.descs.data(), sizeof(BlockDesc) * nd, hipMemcpyHostToDevice, s));
     if (!b->fo.jobs.empty()) {  // device-side metadata parse: finishes the descriptors in place
         const size_t ni = b->fo.items.size(), nj = b->fo.jobs.size();
-        HIPCHK(c, hipMalloc(&b->d_items, sizeof(MetaItem) * ni));
-        HIPCHK(c, hipMalloc(&b->d_jobs, sizeof(MetaJob) * nj));
-        HIPCHK(c, hipMemcpyAsync(b->d_items, b->fo.items.data(), sizeof(MetaItem) * ni, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(c, hipMemcpyAsync(b->d_jobs, b->fo.jobs.data(), sizeof(MetaJob) * nj, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(c, launch_meta(b->d_descs, b->d_jobs, (uint32_t)nj, b->d_items, b->d_blob, c->stream));
+        HIPCHK(c, ensure(b->d_items, b->cap_items, sizeof(MetaItem) * ni));
+        HIPCHK(c, ensure(b->d_jobs, b->cap_jobs, sizeof(MetaJob) * nj));
+        HIPCHK(c, hipMemcpyAsync(b->d_items, b->fo.items.data(), sizeof(MetaItem) * ni, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(b->d_jobs, b->fo.jobs.data(), sizeof(MetaJob) * nj, hipMemcpyHostToDevice, s));
+        HIPCHK(c, launch_meta(b->d_descs, b->d_jobs, (uint32_t)nj, b->d_items, b->d_blob, s));
     }
-    size_t nt = b->fo.tables.size() + 16;
-    HIPCHK(c, hipMalloc(&b->d_tables, nt));
+    HIPCHK(c, ensure(b->d_tables, b->cap_tables, b->fo.tables.size() + 16));
     if (!b->fo.tables.empty())
-        HIPCHK(c, hipMemcpyAsync(b->d_tables, b->fo.tables.data(), b->fo.tables.size(), hipMemcpyHostToDevice, c->stream));
-    size_t no = (size_t)(b->out_ints ? b->out_ints : 1);
-    HIPCHK(c, hipMalloc(&b->d_out, sizeof(int32_t) * no));
-    HIPCHK(c, hipMemsetAsync(b->d_out, 0, sizeof(int32_t) * no, c->stream));
-    HIPCHK(c, hipMalloc(&b->d_status, sizeof(uint32_t) * (nd ? nd : 1)));
-    HIPCHK(c, hipMalloc(&b->d_mute, sizeof(uint32_t) * (nd ? nd : 1)));
-    std::vector<uint32_t> st(nd ? nd : 1);
-    for (size_t k = 0; k < nd; k++) st[k] = b->fo.descs[k].fstatus;
-    HIPCHK(c, hipMemcpyAsync(b->d_status, st.data(), sizeof(uint32_t) * st.size(), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemsetAsync(b->d_mute, 0, sizeof(uint32_t) * (nd ? nd : 1), c->stream));
+        HIPCHK(c, hipMemcpyAsync(b->d_tables, b->fo.tables.data(), b->fo.tables.size(), hipMemcpyHostToDevice, s));
+    const size_t no = (size_t)(b->out_ints ? b->out_ints : 1);
+    HIPCHK(c, ensure(b->d_out, b->cap_out, sizeof(int32_t) * no));
+    HIPCHK(c, hipMemsetAsync(b->d_out, 0, sizeof(int32_t) * no, s));
+    size_t cst = b->cap_st;
+    HIPCHK(c, ensure(b->d_status, cst, sizeof(uint32_t) * (nd ? nd : 1)));
+    HIPCHK(c, ensure(b->d_mute, b->cap_st, sizeof(uint32_t) * (nd ? nd : 1)));
+    b->h_status.assign(nd ? nd : 1, 0);
+    for (size_t k = 0; k < nd; k++) b->h_status[k] = b->fo.descs[k].fstatus;
+    HIPCHK(c, hipMemcpyAsync(b->d_status, b->h_status.data(), sizeof(uint32_t) * b->h_status.size(), hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemsetAsync(b->d_mute, 0, sizeof(uint32_t) * (nd ? nd : 1), s));
     // longest blocks first within a kind, so the long tail starts early (order is
     // free: every block writes its own output range; DSD fills follow on the same stream)
     auto by_kind_len = [&](uint32_t x, uint32_t y) {
@@ -304,37 +336,54 @@ int wvg_batch_upload(wvg_batch *b) {
     };
     std::sort(b->pcm_list.begin(), b->pcm_list.end(), by_kind_len);
     std::sort(b->dsd_list.begin(), b->dsd_list.end(), by_kind_len);
-    size_t np = b->pcm_list.size(), ns = b->dsd_list.size();
-    HIPCHK(c, hipMalloc(&b->d_pcml, sizeof(uint32_t) * (np ? np : 1)));
-    HIPCHK(c, hipMalloc(&b->d_dsd, sizeof(uint32_t) * (ns ? ns : 1)));
-    if (np) HIPCHK(c, hipMemcpyAsync(b->d_pcml, b->pcm_list.data(), sizeof(uint32_t) * np, hipMemcpyHostToDevice, c->stream));
-    if (ns) HIPCHK(c, hipMemcpyAsync(b->d_dsd, b->dsd_list.data(), sizeof(uint32_t) * ns, hipMemcpyHostToDevice, c->stream));
+    const size_t np = b->pcm_list.size(), ns = b->dsd_list.size();
+    HIPCHK(c, ensure(b->d_pcml, b->cap_pcml, sizeof(uint32_t) * (np ? np : 1)));
+    HIPCHK(c, ensure(b->d_dsd, b->cap_dsd, sizeof(uint32_t) * (ns ? ns : 1)));
+    if (np) HIPCHK(c, hipMemcpyAsync(b->d_pcml, b->pcm_list.data(), sizeof(uint32_t) * np, hipMemcpyHostToDevice, s));
+    if (ns) HIPCHK(c, hipMemcpyAsync(b->d_dsd, b->dsd_list.data(), sizeof(uint32_t) * ns, hipMemcpyHostToDevice, s));
     for (int t = 0; t < kMaxTermSets; t++) {
-        size_t nl = b->ts_list[t].size();
-        if (!nl) continue;
-        HIPCHK(c, hipMalloc(&b->d_ts[t], sizeof(uint32_t) * nl));
-        HIPCHK(c, hipMemcpyAsync(b->d_ts[t], b->ts_list[t].data(), sizeof(uint32_t) * nl, hipMemcpyHostToDevice, c->stream));
+        std::vector<uint32_t> &L = b->ts_list[t];
+        if (L.empty()) continue;
+        std::sort(L.begin(), L.end(), by_kind_len);
+        HIPCHK(c, ensure(b->d_ts[t], b->cap_ts[t], sizeof(uint32_t) * L.size()));
+        HIPCHK(c, hipMemcpyAsync(b->d_ts[t], L.data(), sizeof(uint32_t) * L.size(), hipMemcpyHostToDevice, s));
     }
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipStreamSynchronize(s));  // the host vectors may change after this call
     b->uploaded = true;
     b->downloaded = false;
+    b->segs_uploaded = false;
     return WVG_OK;
 }
 
 int wvg_batch_decode(wvg_batch *b, void *stream) {
     if (!b || !b->uploaded) return WVG_ERR_ARG;
     wvg_ctx *c = b->ctx;
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t s = stream ? (hipStream_t)stream : b->stream;
+    if (b->timing) {
+        hipEvent_t e0, e1;
+        HIPCHK(c, hipEventCreate(&e0));
+        HIPCHK(c, hipEventCreate(&e1));
+        b->tev.push_back(e0);
+        b->tev.push_back(e1);
+        HIPCHK(c, hipEventRecord(e0, s));
+    }
     // one stream slot per non-empty launch group: term sets 0..7, generic PCM, DSD
     int used[kSide], n = 0;
     for (int t = 0; t < kMaxTermSets; t++)
         if (!b->ts_list[t].empty()) used[n++] = t;
     if (!b->pcm_list.empty()) used[n++] = kMaxTermSets;
     if (!b->dsd_list.empty()) used[n++] = kMaxTermSets + 1;
-    auto slot = [&](int g) -> hipStream_t { return n > 1 ? c->side[g] : s; };
+    auto slot = [&](int g) -> hipStream_t { return n > 1 ? b->side[g] : s; };
+    for (int i = 0; n > 1 && i < n; i++) {
+        const int g = used[i];
+        if (!b->side[g]) {
+            HIPCHK(c, hipStreamCreateWithFlags(&b->side[g], hipStreamNonBlocking));
+            HIPCHK(c, hipEventCreateWithFlags(&b->join[g], hipEventDisableTiming));
+        }
+    }
     if (n > 1) {
-        HIPCHK(c, hipEventRecord(c->fork, s));
-        for (int i = 0; i < n; i++) HIPCHK(c, hipStreamWaitEvent(c->side[used[i]], c->fork, 0));
+        HIPCHK(c, hipEventRecord(b->fork, s));
+        for (int i = 0; i < n; i++) HIPCHK(c, hipStreamWaitEvent(b->side[used[i]], b->fork, 0));
     }
     for (int t = 0; t < kMaxTermSets; t++)
         if (!b->ts_list[t].empty())
@@ -345,10 +394,12 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
                             slot(kMaxTermSets + 1)));
     if (n > 1) {
         for (int i = 0; i < n; i++) {
-            HIPCHK(c, hipEventRecord(c->join[used[i]], c->side[used[i]]));
-            HIPCHK(c, hipStreamWaitEvent(s, c->join[used[i]], 0));
+            HIPCHK(c, hipEventRecord(b->join[used[i]], b->side[used[i]]));
+            HIPCHK(c, hipStreamWaitEvent(s, b->join[used[i]], 0));
         }
     }
+    if (b->timing) HIPCHK(c, hipEventRecord(b->tev.back(), s));
+    HIPCHK(c, hipEventRecord(b->done, s));
     b->downloaded = false;
     b->formatted = false;
     return WVG_OK;
@@ -356,8 +407,33 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
 
 int wvg_batch_sync(wvg_batch *b) {
     if (!b) return WVG_ERR_ARG;
-    HIPCHK(b->ctx, hipStreamSynchronize(b->ctx->stream));
-    HIPCHK(b->ctx, hipDeviceSynchronize());
+    HIPCHK(b->ctx, hipEventSynchronize(b->done));
+    HIPCHK(b->ctx, hipStreamSynchronize(b->stream));
+    return WVG_OK;
+}
+
+void *wvg_batch_stream(wvg_batch *b) { return b ? (void *)b->stream : nullptr; }
+
+int wvg_batch_set_timing(wvg_batch *b, int on) {
+    if (!b) return WVG_ERR_ARG;
+    for (auto &e : b->tev) hipEventDestroy(e);
+    b->tev.clear();
+    b->timing = on != 0;
+    return WVG_OK;
+}
+
+int wvg_batch_timed(wvg_batch *b, float *avg_ms, int *count) {
+    if (!b || !avg_ms || !count) return WVG_ERR_ARG;
+    const int n = (int)(b->tev.size() / 2);
+    double tot = 0;
+    for (int i = 0; i < n; i++) {
+        float t = 0;
+        HIPCHK(b->ctx, hipEventSynchronize(b->tev[2 * i + 1]));
+        HIPCHK(b->ctx, hipEventElapsedTime(&t, b->tev[2 * i], b->tev[2 * i + 1]));
+        tot += t;
+    }
+    *avg_ms = n ? (float)(tot / n) : 0.f;
+    *count = n;
     return WVG_OK;
 }
 
@@ -373,8 +449,10 @@ static int download_status(wvg_batch *b) {
     b->h_status.assign(nd, 0);
     b->h_aux.assign(nd, 0);
     if (nd) {
-        HIPCHK(c, hipMemcpy(b->h_status.data(), b->d_status, sizeof(uint32_t) * nd, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(b->h_aux.data(), b->d_mute, sizeof(uint32_t) * nd, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipStreamWaitEvent(b->stream, b->done, 0));
+        HIPCHK(c, hipMemcpyAsync(b->h_status.data(), b->d_status, sizeof(uint32_t) * nd, hipMemcpyDeviceToHost, b->stream));
+        HIPCHK(c, hipMemcpyAsync(b->h_aux.data(), b->d_mute, sizeof(uint32_t) * nd, hipMemcpyDeviceToHost, b->stream));
+        HIPCHK(c, hipStreamSynchronize(b->stream));
     }
     b->downloaded = true;
     return WVG_OK;
@@ -383,11 +461,13 @@ static int download_status(wvg_batch *b) {
 int wvg_batch_download(wvg_batch *b, int32_t *host_out, int64_t cap_ints) {
     if (!b || !b->uploaded) return WVG_ERR_ARG;
     wvg_ctx *c = b->ctx;
-    HIPCHK(c, hipDeviceSynchronize());
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamWaitEvent(b->stream, b->done, 0));  // the decode, on whatever stream it ran
     if (host_out) {
         if (cap_ints < b->out_ints) return WVG_ERR_SPACE;
         if (b->out_ints)
-            HIPCHK(c, hipMemcpy(host_out, b->d_out, sizeof(int32_t) * (size_t)b->out_ints, hipMemcpyDeviceToHost));
+            HIPCHK(c, hipMemcpyAsync(host_out, b->d_out, sizeof(int32_t) * (size_t)b->out_ints, hipMemcpyDeviceToHost,
+                                     b->stream));
     }
     return download_status(b);
 }
@@ -486,10 +566,10 @@ int wvg_batch_time(wvg_batch *b, int iters, float *ms) {
     std::vector<hipEvent_t> ev((size_t)iters * 2);
     for (auto &e : ev) HIPCHK(c, hipEventCreate(&e));
     for (int i = 0; i < iters; i++) {
-        HIPCHK(c, hipEventRecord(ev[2 * i], c->stream));
+        HIPCHK(c, hipEventRecord(ev[2 * i], b->stream));
         int rc = wvg_batch_decode(b, nullptr);
         if (rc) return rc;
-        HIPCHK(c, hipEventRecord(ev[2 * i + 1], c->stream));
+        HIPCHK(c, hipEventRecord(ev[2 * i + 1], b->stream));
     }
     HIPCHK(c, hipEventSynchronize(ev.back()));
     double tot = 0;
@@ -565,16 +645,21 @@ int wvg_format_samples(const int32_t *src, int64_t samcnt, int bps, uint8_t *pcm
 int wvg_batch_format(wvg_batch *b, int dsd, void *stream) {
     if (!b || !b->uploaded) return WVG_ERR_ARG;
     wvg_ctx *c = b->ctx;
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    if (!b->d_pcm) {
-        HIPCHK(c, hipMalloc(&b->d_pcm, (size_t)(b->pcm_bytes ? b->pcm_bytes : 1)));
-        HIPCHK(c, hipMemsetAsync(b->d_pcm, 0, (size_t)(b->pcm_bytes ? b->pcm_bytes : 1), s));
-        HIPCHK(c, hipMalloc(&b->d_segs, sizeof(FormatSeg) * (b->segs.empty() ? 1 : b->segs.size())));
+    hipStream_t s = stream ? (hipStream_t)stream : b->stream;
+    HIPCHK(c, hipStreamWaitEvent(s, b->done, 0));
+    if (!b->segs_uploaded) {  // once per upload (the file set may have changed)
+        const size_t pb = (size_t)(b->pcm_bytes ? b->pcm_bytes : 1);
+        HIPCHK(c, ensure(b->d_pcm, b->cap_pcm, pb));
+        HIPCHK(c, hipMemsetAsync(b->d_pcm, 0, pb, s));
+        HIPCHK(c, ensure(b->d_segs, b->cap_segs, sizeof(FormatSeg) * (b->segs.empty() ? 1 : b->segs.size())));
         if (!b->segs.empty())
             HIPCHK(c, hipMemcpyAsync(b->d_segs, b->segs.data(), sizeof(FormatSeg) * b->segs.size(),
                                      hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipStreamSynchronize(s));  // b->segs may change after this call
+        b->segs_uploaded = true;
     }
     HIPCHK(c, launch_format(b->d_segs, (uint32_t)b->segs.size(), b->d_out, b->d_pcm, dsd ? 1 : 0, s));
+    HIPCHK(c, hipEventRecord(b->done, s));
     b->formatted = true;
     return WVG_OK;
 }
@@ -592,8 +677,10 @@ int wvg_batch_download_pcm(wvg_batch *b, uint8_t *host, int64_t cap) {
     if (!b || !b->formatted || (!host && b->pcm_bytes)) return WVG_ERR_ARG;
     if (cap < b->pcm_bytes) return WVG_ERR_SPACE;
     wvg_ctx *c = b->ctx;
-    HIPCHK(c, hipDeviceSynchronize());
-    if (b->pcm_bytes) HIPCHK(c, hipMemcpy(host, b->d_pcm, (size_t)b->pcm_bytes, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipStreamWaitEvent(b->stream, b->done, 0));
+    if (b->pcm_bytes)
+        HIPCHK(c, hipMemcpyAsync(host, b->d_pcm, (size_t)b->pcm_bytes, hipMemcpyDeviceToHost, b->stream));
+    HIPCHK(c, hipStreamSynchronize(b->stream));
     return WVG_OK;
 }
 
@@ -615,7 +702,7 @@ int wvg_batch_wav(wvg_batch *b, int file, uint8_t *out, int64_t cap, int64_t *wa
     *wav_len = 0;
     *exit_code = 1;
     if (!fi.open_ok) return WVG_OK;  // WvDemo.cs:41-46: error message, no .wav
-    HIPCHK(c, hipDeviceSynchronize());
+    HIPCHK(c, hipEventSynchronize(b->done));
     if (!b->downloaded) {
         int rc = download_status(b);
         if (rc) return rc;
@@ -686,7 +773,11 @@ int wvg_batch_wav(wvg_batch *b, int file, uint8_t *out, int64_t cap, int64_t *wa
     if (!out) return WVG_OK;  // size query
     if (cap < total) return WVG_ERR_SPACE;
     memcpy(out, hdr, (size_t)hlen);
-    if (pcm) HIPCHK(c, hipMemcpy(out + hlen, b->d_pcm + b->pcm_off[(size_t)file], (size_t)pcm, hipMemcpyDeviceToHost));
+    if (pcm) {
+        HIPCHK(c, hipMemcpyAsync(out + hlen, b->d_pcm + b->pcm_off[(size_t)file], (size_t)pcm, hipMemcpyDeviceToHost,
+                                 b->stream));
+        HIPCHK(c, hipStreamSynchronize(b->stream));
+    }
     if (tlen) memcpy(out + hlen + pcm, b->blob.data() + (size_t)fi.trailer_off, (size_t)tlen);
     return WVG_OK;
 }

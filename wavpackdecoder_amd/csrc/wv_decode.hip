@@ -2,10 +2,15 @@
 //
 // Kernel map:
 //   wv_pcm_2wave<terms> : one workgroup (parser wave + reconstruction wave) per
-//                         PCM block whose decorrelation term list has a
-//                         specialised instantiation (wv_wave2.h).
-//   wv_decode_pcm_wave  : one wave-uniform decode per PCM block without a
-//                         specialised term set; runs decode_pcm_block
+//                         PCM block whose decorrelation term list is one of the
+//                         shallow compile-time lists (fast, default, mono-5;
+//                         wv_wave2.h).
+//   wv_pcm_pipe<neg12>  : the same parser wave with the pipelined
+//                         reconstruction wave (one pass per lane pair,
+//                         wv_pipe.h) for every other term list (high, very
+//                         high, 'extra', any list up to 16 terms).
+//   wv_decode_pcm_wave  : one wave-uniform decode per PCM block whose fixup
+//                         reads the int32 wvx stream; runs decode_pcm_block
 //                         (get_words -> decorr passes -> joint/CRC/mute ->
 //                         fixup -> int32 store) fused, sample-major.
 //   wv_decode_dsd_wave  : one wave-uniform decode per DSD block (DsdUtils modes
@@ -29,6 +34,7 @@
 #include "wv_decode_core.h"
 #include "wv_meta.h"
 #include "wv_wave2.h"
+#include "wv_pipe.h"
 
 namespace wvg {
 
@@ -436,30 +442,48 @@ __global__ void __launch_bounds__(128) wv_pcm_2wave(const BlockDesc *__restrict_
     w2::block_2wave<Ts...>(descs, list, blob, out, status, aux);
 }
 
+// pipelined reconstruction (wv_pipe.h): any term list, one kernel per "has -1/-2"
+template <bool NEG12>
+__global__ void __launch_bounds__(128) wv_pcm_pipe(const BlockDesc *__restrict__ descs,
+                                                   const uint32_t *__restrict__ list,
+                                                   const uint8_t *__restrict__ blob, int32_t *__restrict__ out,
+                                                   uint32_t *__restrict__ status, uint32_t *__restrict__ aux) {
+    w2::block_pipe<NEG12>(descs, list, blob, out, status, aux);
+}
+
+// the shallow lists WavPack writes most (decoder order, the reverse of the
+// encoder's): each is a compile-time VALU chain (wv_wave2.h); deeper or other
+// lists run the pipelined kernel
 #define WVG_TS_FAST 17, 17
 #define WVG_TS_DEFAULT -2, 3, 2, 18, 18
-#define WVG_TS_HIGH 2, 18, -1, 8, 6, 3, 5, 7, 4, 2, 18, -2, 3, 2, 18, 18
-#define WVG_TS_MHIGH 1, 17, 2, 18, 8, 6, 3, 5, 7, 4, 2, 18, 3, 2, 18, 18
 #define WVG_TS_M5 18, 3, 2, 18, 18
-#define WVG_TS_HIGH10 4, 17, -1, 5, 3, 2, -2, 18, 18, 18
 
 static const int8_t kTermSets[][17] = {
     // {count, terms...}
     {2, WVG_TS_FAST},
     {5, WVG_TS_DEFAULT},
-    {16, WVG_TS_HIGH},
-    {16, WVG_TS_MHIGH},
     {5, WVG_TS_M5},
-    {10, WVG_TS_HIGH10},
 };
-constexpr int kNumTermSets = 6;
+constexpr int kNumTermSets = 3;
 
-// which specialised kernel decodes this block (-1: the generic wave kernel)
-int term_set_of(const BlockDesc &d) {
+// launch groups 0..kNumTermSets-1: the two-wave kernels with a compile-time term
+// list; kPipe / kPipe + 1: the pipelined kernel without / with stereo -1/-2 terms
+constexpr int kPipe = 3;
+static_assert(kNumTermSets <= kPipe, "term-set slots");
+
+// which two-wave kernel decodes this block (-1: the generic wave kernel, for
+// int32 + wvx blocks).  prefer_pipe 2: every list goes to the pipelined kernel
+// (A/B tests)
+int term_set_of(const BlockDesc &d, int prefer_pipe) {
     using namespace wvf;
     if (d.kind != KIND_PCM) return -1;
     if (d.wvx_state & 0x100) return -1;  // int32 + wvx fixup reads a second stream
     const bool mono = (d.flags & MONO_DATA) != 0;
+    if (d.num_terms < 0 || d.num_terms > MAXP) return -1;
+    bool neg12 = false;
+    for (int i = 0; i < d.num_terms; i++) neg12 |= !mono && (d.term[i] == -1 || d.term[i] == -2);
+    const int pipe = kPipe + (neg12 ? 1 : 0);
+    if (prefer_pipe >= 2) return pipe;
     for (int s = 0; s < kNumTermSets; s++) {
         if (kTermSets[s][0] != d.num_terms) continue;
         bool ok = true;
@@ -470,7 +494,7 @@ int term_set_of(const BlockDesc &d) {
         }
         if (ok) return s;
     }
-    return -1;
+    return pipe;
 }
 
 hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, uint32_t n, const uint8_t *blob,
@@ -480,10 +504,9 @@ hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, ui
     switch (ts) {
     case 0: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_FAST>), g, b, 0, s, descs, list, blob, out, status, aux); break;
     case 1: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_DEFAULT>), g, b, 0, s, descs, list, blob, out, status, aux); break;
-    case 2: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_HIGH>), g, b, 0, s, descs, list, blob, out, status, aux); break;
-    case 3: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_MHIGH>), g, b, 0, s, descs, list, blob, out, status, aux); break;
-    case 4: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_M5>), g, b, 0, s, descs, list, blob, out, status, aux); break;
-    case 5: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_HIGH10>), g, b, 0, s, descs, list, blob, out, status, aux); break;
+    case 2: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_M5>), g, b, 0, s, descs, list, blob, out, status, aux); break;
+    case kPipe: hipLaunchKernelGGL((wv_pcm_pipe<false>), g, b, 0, s, descs, list, blob, out, status, aux); break;
+    case kPipe + 1: hipLaunchKernelGGL((wv_pcm_pipe<true>), g, b, 0, s, descs, list, blob, out, status, aux); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

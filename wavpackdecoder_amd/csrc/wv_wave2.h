@@ -27,7 +27,7 @@
 namespace wvg {
 namespace w2 {
 
-constexpr int RES_RING = 4096;  // residual words in flight (16 KiB)
+constexpr int RES_RING = 2048;  // residual words in flight (8 KiB: 2 waves x 8 KiB lets 16 blocks share a CU)
 constexpr uint32_t SPIN_LIMIT = 1u << 26;  // bounded waits: a bug ends the kernel, never hangs the GPU
 
 // The reconstruction wave keeps the parser's payload ahead of it in the CU's
