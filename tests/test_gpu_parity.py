@@ -87,6 +87,17 @@ def test_corrupted_streams(gpu_batch_cls):
             _check_one(V.corrupt(basem, 100 + k), 1000, gpu_batch_cls, f"mono#{k}", lane)
     for k in range(10):
         _check_one(V.corrupt(basex, 200 + k), 4096, gpu_batch_cls, f"int32_wvx#{k}")
+    # hybrid streams (the parser's hybrid fast path and its bails to get_word)
+    h = S.encode_pcm(x, S.EncParams(terms=S.TERMS_DEFAULT, hybrid=True, hybrid_bitrate=True, bitrate_x256=768,
+                                    block_samples=5000))
+    hb = S.encode_pcm(x, S.EncParams(terms=S.TERMS_HIGH, hybrid=True, hybrid_bitrate=True, hybrid_balance=True,
+                                     bitrate_x256=1024, block_samples=5000))
+    hm = S.encode_pcm(m, S.EncParams(nch=1, terms=S.TERMS_MONO_HIGH, hybrid=True, hybrid_bitrate=True,
+                                     bitrate_x256=640, block_samples=3001))
+    for k in range(8):
+        _check_one(V.corrupt(h, 300 + k, start=150), 4096, gpu_batch_cls, f"hybrid#{k}")
+        _check_one(V.corrupt(hb, 400 + k, start=150), 4096, gpu_batch_cls, f"hybrid_balance#{k}")
+        _check_one(V.corrupt(hm, 500 + k, start=150), 1000, gpu_batch_cls, f"hybrid_mono#{k}")
 
 
 def test_batch_of_many_files_matches_per_file(gpu_batch_cls):

@@ -60,22 +60,30 @@ WVF_HD int tab_log2(int i) {
 
 enum { DEC_OK = 0, DEC_BITS_ERROR = 1, DEC_EXCEPTION = 2, DEC_TIMEOUT = 3 };
 
+// the exp2 / log2 byte tables through memory (scalar cache on the device)
+struct MemTabs {
+    WVF_HD int exp2(int i) const { return tab_exp2(i); }
+    WVF_HD int log2(int i) const { return tab_log2(i); }
+};
+
 // exp2s (WordsUtils.cs:633-646); int.MinValue recurses forever in C# -> exception
-WVF_HD int32_t dev_exp2s(int32_t log, int &exc) {
+template <class TB = MemTabs>
+WVF_HD int32_t dev_exp2s(int32_t log, int &exc, const TB &tb = TB()) {
     bool neg = log < 0;
     if (log == INT32_MIN) {
         exc = 1;
         return 0;
     }
     if (neg) log = -log;
-    int64_t value = tab_exp2(log & 0xff) | 0x100;
+    int64_t value = tb.exp2(log & 0xff) | 0x100;
     int e = log >> 8;
     int32_t r = (e <= 9) ? (int32_t)wvf::sar64(value, 9 - e) : (int32_t)wvf::shl64(value, e - 9);
     return neg ? (int32_t)(0u - (uint32_t)r) : r;
 }
 
 // mylog2 (WordsUtils.cs:588-608); out-of-table indices are C# exceptions
-WVF_HD int dev_mylog2(int64_t avalue, int &exc) {
+template <class TB = MemTabs>
+WVF_HD int dev_mylog2(int64_t avalue, int &exc, const TB &tb = TB()) {
     avalue += avalue >> 9;
     if (avalue < 0 || avalue >= (1LL << 32)) {
         exc = 1;
@@ -83,8 +91,8 @@ WVF_HD int dev_mylog2(int64_t avalue, int &exc) {
     }
     uint32_t a = (uint32_t)avalue;
     int dbits = a ? 32 - __builtin_clz(a) : 0;
-    if (a < 256) return (dbits << 8) + tab_log2((int)(((uint64_t)a << (9 - dbits)) & 0xff));
-    return (dbits << 8) + tab_log2((int)((a >> (dbits - 9)) & 0xff));
+    if (a < 256) return (dbits << 8) + tb.log2((int)(((uint64_t)a << (9 - dbits)) & 0xff));
+    return (dbits << 8) + tb.log2((int)((a >> (dbits - 9)) & 0xff));
 }
 
 // ---------------------------------------------------------------------------
@@ -178,15 +186,16 @@ struct Entropy {
 };
 
 // update_error_limit (WordsUtils.cs:195-261)
-WVF_HD void update_error_limit(Entropy &w, uint32_t flags, int &exc) {
+template <class TB = MemTabs>
+WVF_HD void update_error_limit(Entropy &w, uint32_t flags, int &exc, const TB &tb = TB()) {
     using namespace wvf;
     int32_t bitrate_0 = (int32_t)((w.acc[0] += w.dlt[0]) >> 16);
     if (flags & MONO_DATA) {
         if (flags & HYBRID_BITRATE) {
             int32_t slow_log_0 = add32(w.slow[0], SLO) >> SLS;
-            w.errlim[0] = (sub32(slow_log_0, bitrate_0) > -0x100) ? dev_exp2s(add32(sub32(slow_log_0, bitrate_0), 0x100), exc) : 0;
+            w.errlim[0] = (sub32(slow_log_0, bitrate_0) > -0x100) ? dev_exp2s(add32(sub32(slow_log_0, bitrate_0), 0x100), exc, tb) : 0;
         } else
-            w.errlim[0] = dev_exp2s(bitrate_0, exc);
+            w.errlim[0] = dev_exp2s(bitrate_0, exc, tb);
     } else {
         int32_t bitrate_1 = (int32_t)((w.acc[1] += w.dlt[1]) >> 16);
         if (flags & HYBRID_BITRATE) {
@@ -205,19 +214,19 @@ WVF_HD void update_error_limit(Entropy &w, uint32_t flags, int &exc) {
                     bitrate_0 = sub32(bitrate_0, balance);
                 }
             }
-            w.errlim[0] = (sub32(slow_log_0, bitrate_0) > -0x100) ? dev_exp2s(add32(sub32(slow_log_0, bitrate_0), 0x100), exc) : 0;
-            w.errlim[1] = (sub32(slow_log_1, bitrate_1) > -0x100) ? dev_exp2s(add32(sub32(slow_log_1, bitrate_1), 0x100), exc) : 0;
+            w.errlim[0] = (sub32(slow_log_0, bitrate_0) > -0x100) ? dev_exp2s(add32(sub32(slow_log_0, bitrate_0), 0x100), exc, tb) : 0;
+            w.errlim[1] = (sub32(slow_log_1, bitrate_1) > -0x100) ? dev_exp2s(add32(sub32(slow_log_1, bitrate_1), 0x100), exc, tb) : 0;
         } else {
-            w.errlim[0] = dev_exp2s(bitrate_0, exc);
-            w.errlim[1] = dev_exp2s(bitrate_1, exc);
+            w.errlim[0] = dev_exp2s(bitrate_0, exc, tb);
+            w.errlim[1] = dev_exp2s(bitrate_1, exc, tb);
         }
     }
 }
 
 // One residual of get_words (WordsUtils.cs:290-503).  `c` is entidx, `even`
 // is ((csamples & 1) == 0).  Returns DEC_* and the value in `out`.
-template <class BR>
-WVF_HD int get_word(Entropy &w, BR &bs, uint32_t flags, int c, bool even, int32_t &out) {
+template <class BR, class TB = MemTabs>
+WVF_HD int get_word(Entropy &w, BR &bs, uint32_t flags, int c, bool even, int32_t &out, const TB &tb = TB()) {
     using namespace wvf;
     int exc = 0;
     const bool mono = (flags & MONO_DATA) != 0;
@@ -273,7 +282,7 @@ WVF_HD int get_word(Entropy &w, BR &bs, uint32_t flags, int c, bool even, int32_
         w.h0 = !w.h1;
     }
 
-    if ((flags & HYBRID_FLAG) && (mono || even)) update_error_limit(w, flags, exc);
+    if ((flags & HYBRID_FLAG) && (mono || even)) update_error_limit(w, flags, exc, tb);
 
     int32_t *m = w.med[c];
     int64_t low, high;
@@ -360,7 +369,7 @@ WVF_HD int get_word(Entropy &w, BR &bs, uint32_t flags, int c, bool even, int32_
     }
     out = bs.getbit() ? (int32_t)~(uint32_t)(uint64_t)mid : (int32_t)(uint32_t)(uint64_t)mid;
     if (flags & HYBRID_BITRATE) {
-        int lg = dev_mylog2(mid, exc);
+        int lg = dev_mylog2(mid, exc, tb);
         w.slow[c] = add32(sub32(w.slow[c], add32(w.slow[c], SLO) >> SLS), lg);
     }
     return exc ? DEC_EXCEPTION : DEC_OK;

@@ -858,10 +858,27 @@ __device__ __forceinline__ bool lossless_run_narrow(Entropy &w, SmemReader &rd, 
 #undef NW_COLD
 #undef NW_CHECK
 
+// The exp2 / log2 byte tables of the hybrid words (update_error_limit's exp2s,
+// the slow-level mylog2: WordsUtils.cs:195-261, 588-646) as one VGPR each,
+// dword i in lane i, read with v_readlane: the general get_word otherwise
+// loads them through scalar memory on the serial chain.
+struct VTab {
+    int32_t v;
+    __device__ __forceinline__ uint32_t byte(uint32_t i) const {
+        const uint32_t dw = (uint32_t)__builtin_amdgcn_readlane(v, (int)(i >> 2));
+        return (dw >> ((i & 3u) * 8u)) & 0xFFu;
+    }
+};
+struct VTabs {
+    VTab e, l;
+    __device__ __forceinline__ int exp2(int i) const { return (int)e.byte((uint32_t)i); }
+    __device__ __forceinline__ int log2(int i) const { return (int)l.byte((uint32_t)i); }
+};
+
 // one residual: the fast path for lossless blocks, the zero-run countdown,
 // else the general get_word (wv_decode_core.h)
 template <int C, bool LOSSLESS>
-__device__ __forceinline__ int parse_word(Entropy &w, Reader &rd, uint32_t flags, int32_t &v) {
+__device__ __forceinline__ int parse_word(Entropy &w, Reader &rd, uint32_t flags, int32_t &v, const VTabs &tb) {
     if (LOSSLESS) {
         const uint32_t m00 = (uint32_t)(w.med[0][0] | w.med[1][0]);
         const bool zr = __builtin_expect(m00 <= 1u, 0) && (w.h0 | w.h1) == 0;
@@ -876,12 +893,15 @@ __device__ __forceinline__ int parse_word(Entropy &w, Reader &rd, uint32_t flags
             return DEC_OK;
         }
     }
-    return get_word(w, rd, flags, C, C == 0, v);
+    return get_word(w, rd, flags, C, C == 0, v, tb);
 }
 
 template <bool MONO, bool LOSSLESS>
 __device__ __forceinline__ void parse_loop(const BlockDesc &d, Reader &rd, Entropy &w, Shared &sh, int lane) {
     const uint32_t flags = d.flags;
+    VTabs tb;  // exp2 / log2 tables, dword `lane` in each lane (hybrid words)
+    tb.e.v = LOSSLESS ? 0 : (int32_t)((const __attribute__((address_space(4))) uint32_t *)c_exp2_table)[lane];
+    tb.l.v = LOSSLESS ? 0 : (int32_t)((const __attribute__((address_space(4))) uint32_t *)c_log2_table)[lane];
     const uint32_t total = MONO ? d.nframes : 2u * d.nframes;
     int32_t resv = 0;
     uint32_t k = 0;
@@ -909,13 +929,14 @@ __device__ __forceinline__ void parse_loop(const BlockDesc &d, Reader &rd, Entro
                     break;
                 }
             }
+
             // the word at k (and, in stereo, its pair) through the general path
             int32_t v = 0;
             int rc = DEC_OK;
             if (MONO || (k & 1) == 0) {
-                rc = parse_word<0, LOSSLESS>(w, rd, flags, v);
+                rc = parse_word<0, LOSSLESS>(w, rd, flags, v, tb);
             } else {
-                rc = parse_word<1, LOSSLESS>(w, rd, flags, v);
+                rc = parse_word<1, LOSSLESS>(w, rd, flags, v, tb);
             }
             if (__builtin_expect(rc != DEC_OK, 0)) {
                 err = (uint32_t)rc;
