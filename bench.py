@@ -296,8 +296,7 @@ def run_rank(args) -> None:
     batches = []
     for _ in range(max(1, args.inflight)):
         bb = DecodeBatch(4096)
-        for f in files:
-            bb.add_file(f)
+        bb.add_files(files)  # host framing on worker threads
         bb.upload()
         batches.append(bb)
     b = batches[0]
@@ -364,16 +363,19 @@ def run_rank(args) -> None:
         if pg is not None:
             pg.destroy_process_group()
         return
-    t_e2e = time.perf_counter()
-    be = DecodeBatch(4096)
-    for f in files:
-        be.add_file(f)
-    be.upload()
-    be.decode()
-    host_out = np.empty(max(be.out_ints, 1), dtype=np.int32)
-    be._check(be._L.wvg_batch_download(be._b, host_out.ctypes.data, host_out.size))
-    t_e2e = time.perf_counter() - t_e2e
-    be.close()
+    # a decode server's request on a warm batch: reset, frame the files on the host,
+    # upload (page-locked), decode, download into page-locked memory; median of 3
+    be = batches[-1]
+    t_runs = []
+    for _ in range(3):
+        t_e2e = time.perf_counter()
+        be.reset()
+        be.add_files(files)
+        be.upload()
+        be.decode()
+        be.download(pinned=True)
+        t_runs.append(time.perf_counter() - t_e2e)
+    t_e2e = float(np.median(t_runs))
     e2e = frames_rank / t_e2e / 1e6
 
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
@@ -419,8 +421,8 @@ def run_rank(args) -> None:
                           "what": "device time of one decode launch (hipEvents on its stream): mean over the timed "
                                   "region's launches, and with no other batch in flight"},
             "pcie_inclusive": {"value": round(e2e, 2), "unit": "Msamples/s", "ms": round(t_e2e * 1e3, 3),
-                               "what": "host framing + upload of the compressed batch + decode + download of "
-                                       "int32 PCM, rank 0"},
+                               "what": "warm batch: host framing + upload of the compressed batch (page-locked) + "
+                                       "decode + download of int32 PCM into page-locked memory, rank 0, median of 3"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": None if traffic is None else int(traffic),

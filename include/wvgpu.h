@@ -108,6 +108,12 @@ void wvg_batch_free(wvg_batch *b);
  * WVG_ERR_OPEN (info->error set; the file contributes no output). */
 int wvg_batch_add_file(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open_flags, wvg_file_info *info);
 
+/* n files at once, framed on `threads` host threads (<= 0: WVG_FRAME_THREADS or
+ * the hardware concurrency, at most 16); the same result as n wvg_batch_add_file
+ * calls in order.  indices[i] receives file i's index or WVG_ERR_OPEN; returns n. */
+int wvg_batch_add_files(wvg_batch *b, int n, const uint8_t *const *files, const size_t *lens, uint32_t open_flags,
+                        int threads, wvg_file_info *infos, int32_t *indices);
+
 /* The same, for a caller that calls WavPackUtils.SetSample(wpc, start_sample)
  * (WavPackUtils.cs:509-594: the block search, then decode-and-discard up to the
  * sample in calls of 4096 / reduced-channels frames) right after opening: the
@@ -116,6 +122,10 @@ int wvg_batch_add_file(wvg_batch *b, const uint8_t *file, size_t len, uint32_t o
  * at the beginning, as the reference's context does. */
 int wvg_batch_add_file_at(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open_flags, int64_t start_sample,
                           wvg_file_info *info);
+
+/* Drop every file of the batch but keep its device and page-locked host
+ * buffers (a decode server refills one batch per request). */
+int wvg_batch_reset(wvg_batch *b);
 
 /* Copy blob + descriptors to the device and zero the output (device buffers are
  * kept across uploads of a refilled batch and only grown). */
@@ -139,8 +149,12 @@ int64_t wvg_batch_num_blocks(const wvg_batch *b);
 int64_t wvg_batch_bytes_in(const wvg_batch *b);   /* compressed bytes of all decoded blocks */
 int64_t wvg_batch_frames(const wvg_batch *b);     /* frames of all decoded blocks */
 
-/* Download output (and per-block statuses) and fill per-file results. */
+/* Download output (and per-block statuses) and fill per-file results.
+ * host_out == NULL with cap_ints == -1: into the batch's own page-locked
+ * buffer (full PCIe rate), read through wvg_batch_host_out until the next
+ * download or wvg_batch_free; host_out == NULL otherwise: statuses only. */
 int wvg_batch_download(wvg_batch *b, int32_t *host_out, int64_t cap_ints);
+int32_t *wvg_batch_host_out(wvg_batch *b);
 int wvg_batch_file_result(wvg_batch *b, int file, wvg_file_result *res);
 /* per-block status words (after download), one per decoded block in file order */
 int wvg_batch_block_status(wvg_batch *b, uint32_t *out, int64_t cap);

@@ -32,8 +32,7 @@ from wavpackdecoder_amd.api import DecodeBatch  # noqa: E402
 def run(name, files, pcm=None, iters=5, fmt=False):
     t0 = time.perf_counter()
     b = DecodeBatch(4096)
-    for f in files:
-        b.add_file(f)
+    b.add_files(files)  # host framing on worker threads
     t_frame = time.perf_counter() - t0
     b.upload()
     b.decode()

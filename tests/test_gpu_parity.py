@@ -115,6 +115,36 @@ def test_batch_of_many_files_matches_per_file(gpu_batch_cls):
         np.testing.assert_array_equal(got, ref.samples, err_msg=name)
 
 
+def test_parallel_framing_matches_sequential(gpu_batch_cls):
+    """wvg_batch_add_files (host threads, merged offsets) decodes exactly like the
+    same files added one by one: C5-style mixed files, DSD, seeks' neighbours,
+    exceptions, unopenable inputs, and the .wav images of a formatted batch."""
+    from synth import corpora
+    files = [c[1] for c in V.pcm_cases() + V.dsd_cases()] + corpora.c5(40) + [b"", b"RIFF" + b"\0" * 60]
+    a = gpu_batch_cls(4096)
+    ia = [a.add_file(f) for f in files]
+    a.decode()
+    a.format()
+    oa = a.download()
+    b = gpu_batch_cls(4096)
+    ib = b.add_files(files, threads=8)
+    b.decode()
+    b.format()
+    ob = b.download()
+    assert ia == ib
+    np.testing.assert_array_equal(oa, ob)
+    for k, i in enumerate(ia):
+        if i < 0:
+            continue
+        ra, rb = a.result(i), b.result(i)
+        assert (ra.frames, ra.crc_errors, ra.exception, ra.status_or) == (rb.frames, rb.crc_errors, rb.exception,
+                                                                          rb.status_or), k
+        assert a.wav(i) == b.wav(i), k
+    np.testing.assert_array_equal(a.download_pcm(), b.download_pcm())
+    a.close()
+    b.close()
+
+
 def test_c2_full_size_roundtrip(gpu_batch_cls):
     """BASELINE config 2 at full size (1,024 blocks x 22,050 frames): lossless
     round trip to the generator's PCM, zero CRC errors (size-independent

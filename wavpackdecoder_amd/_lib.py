@@ -77,7 +77,9 @@ def lib():
         "wvg_batch_free": (None, [vp]),
         "wvg_batch_add_file": (i32, [vp, ctypes.c_char_p, ctypes.c_size_t, u32, ctypes.POINTER(WvgFileInfo)]),
         "wvg_batch_add_file_at": (i32, [vp, ctypes.c_char_p, ctypes.c_size_t, u32, i64, ctypes.POINTER(WvgFileInfo)]),
+        "wvg_batch_add_files": (i32, [vp, i32, vp, vp, u32, i32, vp, vp]),
         "wvg_batch_upload": (i32, [vp]),
+        "wvg_batch_reset": (i32, [vp]),
         "wvg_batch_decode": (i32, [vp, vp]),
         "wvg_batch_sync": (i32, [vp]),
         "wvg_batch_stream": (vp, [vp]),
@@ -89,6 +91,7 @@ def lib():
         "wvg_batch_bytes_in": (i64, [vp]),
         "wvg_batch_frames": (i64, [vp]),
         "wvg_batch_download": (i32, [vp, vp, i64]),
+        "wvg_batch_host_out": (vp, [vp]),
         "wvg_batch_file_result": (i32, [vp, i32, ctypes.POINTER(WvgFileResult)]),
         "wvg_batch_block_status": (i32, [vp, vp, i64]),
         "wvg_batch_file_blocks": (i32, [vp, i32, vp, vp, i64]),
@@ -113,10 +116,10 @@ def lib():
 
 
 EXPORTED = ("wvg_open", "wvg_close", "wvg_last_error", "wvg_batch_new", "wvg_batch_free", "wvg_batch_add_file",
-            "wvg_batch_add_file_at",
-            "wvg_batch_upload", "wvg_batch_decode", "wvg_batch_sync", "wvg_batch_stream", "wvg_batch_set_timing",
+            "wvg_batch_add_file_at", "wvg_batch_add_files",
+            "wvg_batch_upload", "wvg_batch_reset", "wvg_batch_decode", "wvg_batch_sync", "wvg_batch_stream", "wvg_batch_set_timing",
             "wvg_batch_timed", "wvg_batch_out_ints", "wvg_batch_device_out",
-            "wvg_batch_num_blocks", "wvg_batch_bytes_in", "wvg_batch_frames", "wvg_batch_download",
+            "wvg_batch_num_blocks", "wvg_batch_bytes_in", "wvg_batch_frames", "wvg_batch_download", "wvg_batch_host_out",
             "wvg_batch_file_result", "wvg_batch_block_status", "wvg_batch_file_blocks", "wvg_batch_time", "wvg_decode_file",
             "wvg_probe_file", "wvg_format_samples", "wvg_batch_format", "wvg_batch_pcm_bytes", "wvg_batch_pcm_offset",
             "wvg_batch_device_pcm", "wvg_batch_download_pcm", "wvg_batch_wav")

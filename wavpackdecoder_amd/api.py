@@ -83,6 +83,31 @@ class DecodeBatch:
         self._uploaded = False
         return idx
 
+    def reset(self):
+        """Drop every file, keep the device and page-locked buffers (wvg_batch_reset)."""
+        self._check(self._L.wvg_batch_reset(self._b))
+        self.infos = []
+        self._uploaded = False
+
+    def add_files(self, files, open_flags: int = 0, threads: int = 0):
+        """Frame many files on host threads (wvg_batch_add_files); returns their indices."""
+        n = len(files)
+        if n == 0:
+            return []
+        bufs = [bytes(f) for f in files]
+        ptrs = (ctypes.c_char_p * n)(*bufs)
+        lens = (ctypes.c_size_t * n)(*[len(f) for f in bufs])
+        infos = (_L.WvgFileInfo * n)()
+        idx = (ctypes.c_int32 * n)()
+        rc = self._L.wvg_batch_add_files(self._b, n, ctypes.cast(ptrs, ctypes.c_void_p),
+                                         ctypes.cast(lens, ctypes.c_void_p), int(open_flags), int(threads),
+                                         ctypes.cast(infos, ctypes.c_void_p), ctypes.cast(idx, ctypes.c_void_p))
+        if rc < 0:
+            self._check(rc)
+        self.infos.extend(infos[i] for i in range(n))
+        self._uploaded = False
+        return [int(idx[i]) for i in range(n)]
+
     def upload(self):
         self._check(self._L.wvg_batch_upload(self._b))
         self._uploaded = True
@@ -129,7 +154,16 @@ class DecodeBatch:
     def device_out_ptr(self) -> int:
         return int(self._L.wvg_batch_device_out(self._b) or 0)
 
-    def download(self) -> np.ndarray:
+    def download(self, pinned: bool = False) -> np.ndarray:
+        """The int32 output.  pinned=True: DMA into the batch's page-locked buffer and
+        return a view of it (valid until the next download or close)."""
+        if pinned:
+            self._check(self._L.wvg_batch_download(self._b, None, -1))
+            p = self._L.wvg_batch_host_out(self._b)
+            n = self.out_ints
+            if not p or n == 0:
+                return np.zeros(0, dtype=np.int32)
+            return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_int32)), shape=(n,))
         out = np.empty(max(self.out_ints, 1), dtype=np.int32)
         self._check(self._L.wvg_batch_download(self._b, out.ctypes.data, out.size))
         return out[: self.out_ints]

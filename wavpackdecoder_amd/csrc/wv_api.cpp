@@ -4,7 +4,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/wvgpu.h"
@@ -40,6 +42,53 @@ struct wvg_ctx {
     std::string err;
 };
 
+// Page-locked, grow-only host buffer: the batch's file bytes live here from
+// add_file on, so the upload is one DMA at PCIe rate (no pageable staging), and
+// the decoded output can be downloaded into one (wvg_batch_host_out).
+struct PinnedBuf {
+    uint8_t *p = nullptr;
+    size_t n = 0, cap = 0;
+    bool pinned = false;
+    PinnedBuf() = default;
+    PinnedBuf(const PinnedBuf &) = delete;
+    PinnedBuf &operator=(const PinnedBuf &) = delete;
+    ~PinnedBuf() { release(); }
+    void release() {
+        if (p) {
+            if (pinned) hipHostFree(p);
+            else free(p);
+        }
+        p = nullptr;
+        n = cap = 0;
+    }
+    bool reserve(size_t m) {
+        if (m <= cap) return true;
+        size_t nc = cap ? cap : (size_t)1 << 20;
+        while (nc < m) nc *= 2;
+        uint8_t *q = nullptr;
+        bool pin = hipHostMalloc((void **)&q, nc, hipHostMallocDefault) == hipSuccess;
+        if (!pin) q = (uint8_t *)malloc(nc);  // no device memory for page-locking: plain pages
+        if (!q) return false;
+        if (n) memcpy(q, p, n);
+        const size_t keep = n;
+        release();
+        p = q;
+        cap = nc;
+        n = keep;
+        pinned = pin;
+        return true;
+    }
+    bool resize(size_t m) {
+        if (!reserve(m)) return false;
+        n = m;
+        return true;
+    }
+    uint8_t *data() { return p; }
+    const uint8_t *data() const { return p; }
+    size_t size() const { return n; }
+    bool empty() const { return n == 0; }
+};
+
 struct wvg_batch {
     wvg_ctx *ctx = nullptr;
     int chunk = 4096;
@@ -53,7 +102,8 @@ struct wvg_batch {
     size_t cap_blob = 0, cap_descs = 0, cap_items = 0, cap_jobs = 0, cap_tables = 0, cap_out = 0, cap_st = 0,
            cap_pcml = 0, cap_dsd = 0, cap_pcm = 0, cap_segs = 0, cap_ts[kMaxTermSets] = {0};
     bool segs_uploaded = false;
-    std::vector<uint8_t> blob;
+    PinnedBuf blob;                                     // every file's bytes, 16-B aligned
+    PinnedBuf hout;                                     // wvg_batch_host_out: the output, downloaded
     FramingOutput fo;
     std::vector<FileInfo> finfo;
     std::vector<wvg_file_info> infos;
@@ -230,15 +280,10 @@ int wvg_probe_file(const uint8_t *file, size_t len, uint32_t open_flags, int chu
     return fi.open_ok ? WVG_OK : WVG_ERR_OPEN;
 }
 
-static int add_file(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open_flags, int64_t seek_to,
-                    wvg_file_info *info) {
-    if (!b || (!file && len)) return WVG_ERR_ARG;
-    b->uploaded = b->formatted = false;
-    size_t base = (b->blob.size() + 15) & ~(size_t)15;
-    b->blob.resize(base + len);
-    if (len) memcpy(b->blob.data() + base, file, len);
-    FileInfo fi;
-    frame_file(b->blob.data() + base, len, base, (uint64_t)b->out_ints, open_flags, b->chunk, b->fo, fi, seek_to);
+// Record a framed file in the batch: the getters' view, its output range, its
+// WavpackFormatSamples segments and its blocks' launch groups.  `fi` refers to
+// descriptors already in b->fo.
+static int commit_file(wvg_batch *b, const FileInfo &fi, size_t len, wvg_file_info *info) {
     wvg_file_info wi;
     fill_info(fi, wi);
     wi.out_offset = b->out_ints;
@@ -282,8 +327,114 @@ static int add_file(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open
     return (int)b->infos.size() - 1;
 }
 
+static int add_file(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open_flags, int64_t seek_to,
+                    wvg_file_info *info) {
+    if (!b || (!file && len)) return WVG_ERR_ARG;
+    b->uploaded = b->formatted = false;
+    size_t base = (b->blob.size() + 15) & ~(size_t)15;
+    if (!b->blob.resize(base + len)) {
+        b->ctx->err = "out of host memory";
+        return WVG_ERR_ARG;
+    }
+    if (len) memcpy(b->blob.data() + base, file, len);
+    FileInfo fi;
+    frame_file(b->blob.data() + base, len, base, (uint64_t)b->out_ints, open_flags, b->chunk, b->fo, fi, seek_to);
+    return commit_file(b, fi, len, info);
+}
+
+int wvg_batch_reset(wvg_batch *b) {
+    if (!b) return WVG_ERR_ARG;
+    if (b->stream) hipStreamSynchronize(b->stream);  // nothing in flight reads the old contents
+    b->blob.resize(0);
+    const bool defer = b->fo.defer_values;
+    b->fo = FramingOutput();
+    b->fo.defer_values = defer;
+    b->finfo.clear();
+    b->infos.clear();
+    b->out_ints = 0;
+    b->pcm_list.clear();
+    b->dsd_list.clear();
+    for (auto &l : b->ts_list) l.clear();
+    b->h_status.clear();
+    b->h_aux.clear();
+    b->bytes_in = b->frames = 0;
+    b->pcm_off.clear();
+    b->pcm_bytes = 0;
+    b->segs.clear();
+    b->uploaded = b->downloaded = b->formatted = b->segs_uploaded = false;
+    return WVG_OK;
+}
+
 int wvg_batch_add_file(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open_flags, wvg_file_info *info) {
     return add_file(b, file, len, open_flags, -1, info);
+}
+
+// Many files at once: the bytes are copied into the blob, the files are framed
+// on host threads (each into its own FramingOutput, out offsets relative to 0),
+// then merged in file order with their offsets moved to the batch's.
+int wvg_batch_add_files(wvg_batch *b, int n, const uint8_t *const *files, const size_t *lens, uint32_t open_flags,
+                        int threads, wvg_file_info *infos, int32_t *indices) {
+    if (!b || n < 0 || (n && (!files || !lens))) return WVG_ERR_ARG;
+    b->uploaded = b->formatted = false;
+    std::vector<size_t> base((size_t)n);
+    size_t end = b->blob.size();
+    for (int i = 0; i < n; i++) {
+        if (!files[i] && lens[i]) return WVG_ERR_ARG;
+        base[(size_t)i] = (end + 15) & ~(size_t)15;
+        end = base[(size_t)i] + lens[i];
+    }
+    if (!b->blob.resize(end)) {
+        b->ctx->err = "out of host memory";
+        return WVG_ERR_ARG;
+    }
+    for (int i = 0; i < n; i++)
+        if (lens[i]) memcpy(b->blob.data() + base[(size_t)i], files[i], lens[i]);
+    if (threads <= 0) {
+        const char *e = getenv("WVG_FRAME_THREADS");
+        threads = e ? atoi(e) : (int)std::thread::hardware_concurrency();
+        if (threads > 16) threads = 16;  // the lease's CPU share on the GPU boxes
+    }
+    if (threads < 1) threads = 1;
+    if (threads > n) threads = n > 0 ? n : 1;
+    std::vector<FramingOutput> fos((size_t)n);
+    std::vector<FileInfo> fis((size_t)n);
+    for (auto &f : fos) f.defer_values = b->fo.defer_values;
+    std::atomic<int> next(0);
+    auto work = [&]() {
+        for (int i; (i = next.fetch_add(1)) < n;)
+            frame_file(b->blob.data() + base[(size_t)i], lens[i], base[(size_t)i], 0, open_flags, b->chunk,
+                       fos[(size_t)i], fis[(size_t)i], -1);
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < threads; t++) pool.emplace_back(work);
+    work();
+    for (auto &t : pool) t.join();
+    for (int i = 0; i < n; i++) {
+        FramingOutput &f = fos[(size_t)i];
+        FileInfo &fi = fis[(size_t)i];
+        const uint64_t ob = (uint64_t)b->out_ints;
+        const uint32_t d0 = (uint32_t)b->fo.descs.size(), i0 = (uint32_t)b->fo.items.size();
+        const size_t t0 = (b->fo.tables.size() + 15) & ~(size_t)15;
+        for (BlockDesc &d : f.descs) {
+            d.out_off += ob;  // wrapping add: a seek's offsets may lie before the file's output
+            d.dsd_table_off += t0;
+        }
+        for (MetaJob &j : f.jobs) {
+            j.desc += d0;
+            j.first += i0;
+        }
+        b->fo.descs.insert(b->fo.descs.end(), f.descs.begin(), f.descs.end());
+        b->fo.items.insert(b->fo.items.end(), f.items.begin(), f.items.end());
+        b->fo.jobs.insert(b->fo.jobs.end(), f.jobs.begin(), f.jobs.end());
+        if (!f.tables.empty()) {
+            b->fo.tables.resize(t0);
+            b->fo.tables.insert(b->fo.tables.end(), f.tables.begin(), f.tables.end());
+        }
+        fi.first_desc += d0;
+        const int idx = commit_file(b, fi, lens[i], infos ? &infos[i] : nullptr);
+        if (indices) indices[i] = idx;
+    }
+    return n;
 }
 
 int wvg_batch_add_file_at(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open_flags, int64_t start_sample,
@@ -463,6 +614,11 @@ int wvg_batch_download(wvg_batch *b, int32_t *host_out, int64_t cap_ints) {
     wvg_ctx *c = b->ctx;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamWaitEvent(b->stream, b->done, 0));  // the decode, on whatever stream it ran
+    if (!host_out && cap_ints == -1) {  // into the batch's page-locked buffer (wvg_batch_host_out)
+        if (!b->hout.resize(sizeof(int32_t) * (size_t)(b->out_ints ? b->out_ints : 1))) return WVG_ERR_SPACE;
+        host_out = (int32_t *)b->hout.data();
+        cap_ints = b->out_ints;
+    }
     if (host_out) {
         if (cap_ints < b->out_ints) return WVG_ERR_SPACE;
         if (b->out_ints)
@@ -471,6 +627,8 @@ int wvg_batch_download(wvg_batch *b, int32_t *host_out, int64_t cap_ints) {
     }
     return download_status(b);
 }
+
+int32_t *wvg_batch_host_out(wvg_batch *b) { return b && !b->hout.empty() ? (int32_t *)b->hout.data() : nullptr; }
 
 int wvg_batch_block_status(wvg_batch *b, uint32_t *out, int64_t cap) {
     if (!b || !b->downloaded) return WVG_ERR_ARG;
@@ -742,7 +900,7 @@ int wvg_batch_wav(wvg_batch *b, int file, uint8_t *out, int64_t cap, int64_t *wa
     const uint8_t *hdr = nullptr;
     int64_t hlen = 0;
     if (fi.header_off >= 0 && !wi.is_float) {
-        hdr = b->blob.data() + (size_t)fi.header_off;
+        hdr = b->blob.data() + (size_t)(fi.blob_base + fi.header_off);
         hlen = fi.header_len;
     } else {
         memcpy(synth, "RIFF", 4);
@@ -778,7 +936,7 @@ int wvg_batch_wav(wvg_batch *b, int file, uint8_t *out, int64_t cap, int64_t *wa
                                  b->stream));
         HIPCHK(c, hipStreamSynchronize(b->stream));
     }
-    if (tlen) memcpy(out + hlen + pcm, b->blob.data() + (size_t)fi.trailer_off, (size_t)tlen);
+    if (tlen) memcpy(out + hlen + pcm, b->blob.data() + (size_t)(fi.blob_base + fi.trailer_off), (size_t)tlen);
     return WVG_OK;
 }
 

@@ -1014,6 +1014,7 @@ void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t ou
     F.in.len = (int64_t)len;
     info = FileInfo();
     info.first_desc = (int64_t)out.descs.size();
+    info.blob_base = blob_base;
     try {
         std::string err;
         if (!open_input(F, open_flags, err)) {

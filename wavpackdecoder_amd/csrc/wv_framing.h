@@ -37,6 +37,7 @@ struct FileInfo {
     int64_t first_call_frames = -1;  // frames the first call returns (-1: it threw)
     int32_t seek_result = 0;    // SetSample: 1 positioned, 0 false, -1 exception (0 when no seek was asked)
     int64_t sample_index0 = 0;  // stream.sample_index when the caller's first (non-discard) call starts
+    uint64_t blob_base = 0;     // the file's first byte inside the batch blob (header/trailer offsets are file-relative)
     int64_t header_off = -1, header_len = 0, trailer_off = -1, trailer_len = 0;  // RIFF/ALT header+trailer
     // blocks of this file inside the batch descriptor array
     int64_t first_desc = 0, num_desc = 0;
