@@ -67,6 +67,8 @@ struct wvenc_params {
     int32_t wvx_max_width;     // NEW variant: the 5-bit int32_max_width field (0 = none)
     int32_t wvx_short;         // drop this many bytes from the end of every wvx payload (over-read tests)
     int64_t total_override;    // > 0: header total_samples (a file encoded in parallel parts, then concatenated)
+    int32_t sticky_passes;     // blocks after the first omit DECORR_TERMS/WEIGHTS/SAMPLES: the decoder
+                               // continues the passes of the block before (sticky state, B-8)
 };
 
 struct wvenc_dsd_params {
@@ -770,12 +772,13 @@ struct PcmEncoder {
                                            (uint8_t)(P.sample_rate >> 16)};
                 put_subblock(md, ID_SAMPLE_RATE, sr);
             }
-            {  // terms (encoder order)
+            const bool pass_meta = !(P.sticky_passes && bi > 0);
+            if (pass_meta) {  // terms (encoder order)
                 std::vector<uint8_t> t;
                 for (int e = 0; e < n; e++) t.push_back((uint8_t)(((P.terms[e] + 5) & 0x1f) | ((P.deltas[e] & 7) << 5)));
                 put_subblock(md, ID_DECORR_TERMS, t);
             }
-            if (n) {  // weights, encoder order; the decoder fills from its last pass
+            if (n && pass_meta) {  // weights, encoder order; the decoder fills from its last pass
                 std::vector<uint8_t> wt;
                 for (int e = 0; e < n; e++) {
                     Pass &p = passes[n - 1 - e];
@@ -791,7 +794,11 @@ struct PcmEncoder {
                 }
                 put_subblock(md, ID_DECORR_WEIGHTS, wt);
             }
-            if (n && P.write_history) {
+            if (!pass_meta) {
+                // the decoder's passes continue as the previous block left them:
+                // weights stored back as (short) (in range, checked below) and the
+                // rings in the layout every pass call ends with
+            } else if (n && P.write_history) {
                 // Entries for every pass, decoder index n-1 down to 0, all in the
                 // layout of the decoder's LAST pass term (quirk B-7); then the
                 // start state is whatever read_decorr_samples rebuilds.

@@ -39,7 +39,7 @@ class _Params(ctypes.Structure):
             "bitrate_x256", "float_data", "float_flags", "float_shift", "float_max_exp", "float_norm_exp",
             "int32_zeros", "write_riff", "config_flags", "write_history", "reset_state", "block_index_start",
             "total_unknown", "extras", "mag_override", "int32_sent_bits", "int32_ones", "int32_dups", "wvx",
-            "wvx_max_width", "wvx_short")] + [("total_override", ctypes.c_int64)]
+            "wvx_max_width", "wvx_short")] + [("total_override", ctypes.c_int64), ("sticky_passes", ctypes.c_int32)]
 
 
 class _DsdParams(ctypes.Structure):
@@ -85,6 +85,7 @@ class EncParams:
     wvx_max_width: int = 0  # NEW variant's int32_max_width
     wvx_short: int = 0      # bytes dropped from every wvx payload (the reference then over-reads and throws)
     total_override: int = 0  # > 0: header total_samples (parts encoded in parallel, then concatenated)
+    sticky_passes: bool = False  # blocks after the first continue the decoder's passes (no pass metadata)
 
     def to_c(self) -> _Params:
         p = _Params()
@@ -101,7 +102,7 @@ class EncParams:
                   "wvx_short", "total_override"):
             setattr(p, n, int(getattr(self, n)))
         for n in ("hybrid", "hybrid_bitrate", "hybrid_balance", "float_data", "write_riff", "write_history",
-                  "reset_state", "total_unknown"):
+                  "reset_state", "total_unknown", "sticky_passes"):
             setattr(p, n, int(bool(getattr(self, n))))
         return p
 

@@ -71,10 +71,14 @@ int64_t emu_decode_from(const uint8_t *file, size_t len, int64_t seek_to, int ch
     std::vector<int32_t> ptable(256);
     bool exception = info.exception != 0;
     std::vector<std::pair<int64_t, int64_t>> fills;
+    PcmState chain;  // the state a chain carries from block to block (wv_decode_chain)
     for (auto &d : fo.descs) {
         uint32_t st = d.fstatus;
         HostStore hs{out, d.out_off, (uint64_t)d.pre_end * d.out_nch};
-        if (d.kind == KIND_PCM) {
+        if (d.kind == KIND_PCM && (d.chain_len || (d.inherit & INH_MEMBER))) {
+            st |= pcm_state_load(chain, d, file);
+            st |= decode_pcm_run<HostStore, true>(chain, d, hs, nullptr);
+        } else if (d.kind == KIND_PCM) {
             st |= decode_pcm_block(d, file, hs);
         } else if (d.kind != KIND_SKIP) {
             DsdResult r = decode_dsd_block(d, file, fo.tables.data(), ptable.data(), hs);

@@ -74,6 +74,24 @@ def test_dsd_modes(case, gpu_batch_cls):
     _check_one(data, chunk, gpu_batch_cls, name)
 
 
+@pytest.mark.parametrize("case", V.sticky_cases(), ids=lambda c: c[0])
+def test_sticky_state_chains(case, gpu_batch_cls):
+    """Blocks continuing the previous decode's state (B-8): one chain per file run
+    in order by wv_decode_pcm_wave, bit-exact with the oracle (tests/test_sticky.py)."""
+    name, data, chunk = case
+    _check_one(data, chunk, gpu_batch_cls, name)
+
+
+def test_sticky_passes_lossless(gpu_batch_cls):
+    """Files that decode correctly only by continuing the passes: back to the input PCM."""
+    cases = V.sticky_clean_cases()
+    for name, data, chunk, pcm in cases:
+        out, res, infos = _gpu_decode([data], chunk, gpu_batch_cls)
+        r, info = res[0], infos[0]
+        assert r.exception == 0 and r.crc_errors == 0 and r.frames == pcm.shape[0], name
+        np.testing.assert_array_equal(out[info.out_offset: info.out_offset + pcm.size], pcm.reshape(-1), err_msg=name)
+
+
 def test_corrupted_streams(gpu_batch_cls):
     from synth import wvsynth as S
     x = S.audio_like(20000, 2, 16, seed=11)

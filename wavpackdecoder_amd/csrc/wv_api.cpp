@@ -316,11 +316,12 @@ static int commit_file(wvg_batch *b, const FileInfo &fi, size_t len, wvg_file_in
     b->out_ints += extent;
     for (int64_t k = fi.first_desc; k < fi.first_desc + fi.num_desc; k++) {
         const BlockDesc &d = b->fo.descs[(size_t)k];
+        b->frames += d.nframes;
+        if (d.inherit & INH_MEMBER) continue;  // decoded by its chain's first block (wv_decode_pcm_wave)
         int ts = (d.kind == KIND_PCM && !b->force_lane) ? term_set_of(d, b->prefer_pipe) : -1;
         if (ts >= 0) b->ts_list[ts].push_back((uint32_t)k);
         else if (d.kind == KIND_PCM) b->pcm_list.push_back((uint32_t)k);
         else if (d.kind != KIND_SKIP) b->dsd_list.push_back((uint32_t)k);
-        b->frames += d.nframes;
     }
     // compressed bytes of the file's decoded blocks (whole file is a fine proxy)
     b->bytes_in += (int64_t)len;

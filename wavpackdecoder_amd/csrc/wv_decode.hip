@@ -12,7 +12,8 @@
 //   wv_decode_pcm_wave  : one wave-uniform decode per PCM block whose fixup
 //                         reads the int32 wvx stream; runs decode_pcm_block
 //                         (get_words -> decorr passes -> joint/CRC/mute ->
-//                         fixup -> int32 store) fused, sample-major.
+//                         fixup -> int32 store) fused, sample-major.  Also one
+//                         wave per chain of blocks that inherit decode state.
 //   wv_decode_dsd_wave  : one wave-uniform decode per DSD block (DsdUtils modes
 //                         0/1/3, each a scalar specialisation).
 //   wv_dsd_fill         : post-pass writing the 0x55 mute fills of DSD blocks in
@@ -52,6 +53,29 @@ struct DevStoreWave {
     }
 };
 
+// A chain of blocks that inherit decode state (BlockDesc::inherit, B-8): the
+// blocks in order, the PcmState of one handed to the next; a block that raises
+// the reference's exception ends the chain (the reference stops there).
+__device__ __noinline__ void decode_chain(const BlockDesc *__restrict__ descs, uint32_t head, const uint8_t *blob,
+                                          int32_t *out, uint32_t *status, uint32_t *aux) {
+    const bool lead = threadIdx.x == 0;
+    PcmState s;
+    const uint32_t n = descs[head].chain_len;
+    for (uint32_t k = 0; k < n; k++) {
+        const uint32_t bi = head + k;
+        const BlockDesc &d = descs[bi];
+        DevStoreWave st{out + d.out_off, (uint64_t)d.pre_end * d.out_nch, lead};
+        uint32_t exc = aux[bi];
+        uint32_t r = d.fstatus | pcm_state_load(s, d, blob);
+        r |= decode_pcm_run<DevStoreWave, true>(s, d, st, &exc);
+        if (lead) {
+            status[bi] = r;
+            aux[bi] = exc;
+        }
+        if (r & ST_EXCEPTION) break;
+    }
+}
+
 extern "C" __global__ void __launch_bounds__(64) wv_decode_pcm_wave(const BlockDesc *__restrict__ descs,
                                                                     const uint32_t *__restrict__ list,
                                                                     const uint8_t *__restrict__ blob,
@@ -60,6 +84,10 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_pcm_wave(const BlockD
                                                                     uint32_t *__restrict__ aux) {
     const uint32_t bi = list[blockIdx.x];
     const BlockDesc &d = descs[bi];
+    if (d.chain_len >= 2) {
+        decode_chain(descs, bi, blob, out, status, aux);
+        return;
+    }
     const bool lead = threadIdx.x == 0;
     DevStoreWave st{out + d.out_off, (uint64_t)d.pre_end * d.out_nch, lead};
     uint32_t exc = aux[bi];
@@ -477,6 +505,7 @@ static_assert(kNumTermSets <= kPipe, "term-set slots");
 int term_set_of(const BlockDesc &d, int prefer_pipe) {
     using namespace wvf;
     if (d.kind != KIND_PCM) return -1;
+    if (d.chain_len >= 2 || (d.inherit & INH_MEMBER)) return -1;  // sticky-state chain (wv_decode_pcm_wave)
     if (d.wvx_state & 0x100) return -1;  // int32 + wvx fixup reads a second stream
     const bool mono = (d.flags & MONO_DATA) != 0;
     if (d.num_terms < 0 || d.num_terms > MAXP) return -1;

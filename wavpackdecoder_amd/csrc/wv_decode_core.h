@@ -609,10 +609,113 @@ WVF_HD int32_t fixup_wvx(const Fixup &f, BitReader &xb, uint32_t xlen, int32_t x
 }
 
 // ---------------------------------------------------------------------------
-// one PCM block
+// one PCM block.  PcmState is the part of the WavpackStream a decode adapts:
+// pcm_state_load fills it from the descriptor and, inside a chain, keeps what
+// the block did not re-send from the decode before it (Appendix B-8).
 // ---------------------------------------------------------------------------
-template <class Store>
-WVF_HD uint32_t decode_pcm_block(const BlockDesc &d, const uint8_t *blob, Store &out, uint32_t *exc_frame = nullptr) {
+struct PcmState {
+    BitReader bs, xb;
+    Entropy w;
+    PassState ps[MAXP];
+    int32_t crc, crc_x;   // wps.crc / wps.crc_x
+    bool muted;           // wps.mute_error
+    bool crc_garbage;     // the running crc went over stale buffer contents
+    bool pass_garbage;    // a pass ran over stale residuals (get_words stopped short)
+};
+
+// Every reference pass call leaves its ring rotated so that slot 0 is the
+// oldest value (UnpackUtils.cs:920-936, 1139-1146, 1225-1233); sample-major
+// decoding keeps value t in slot t & 7 instead, t counting the frames the
+// passes ran over in the block.  Rotating by t gives the reference's layout.
+WVF_HD bool ring_term(int term, bool mono) { return mono ? (term != 17 && term != 18) : (term >= 0 && term <= 8); }
+WVF_HD void ring_normalize(PassState &p, uint32_t t, bool mono) {
+    const int r = (int)(t & 7u);
+    if (!r) return;
+    int32_t a[8], b[8];
+    for (int k = 0; k < 8; k++) {
+        a[k] = p.rA[(r + k) & 7];
+        b[k] = p.rB[(r + k) & 7];
+    }
+    for (int k = 0; k < 8; k++) {
+        p.rA[k] = a[k];
+        if (!mono) p.rB[k] = b[k];  // decorr_mono_pass rotates samples_A only
+    }
+}
+
+// the block's starting state: the descriptor's values, except what d.inherit /
+// d.inherit_passes take from `s` as the previous decode left it.  Returns the
+// status bits that follow from the carried state (ST_NONDET).
+WVF_HD uint32_t pcm_state_load(PcmState &s, const BlockDesc &d, const uint8_t *blob) {
+    const uint32_t inh = d.inherit;
+    uint32_t status = 0;
+    if (!(inh & INH_BITS)) {
+        s.bs.init(blob, d.bits_off, d.bits_len);
+    } else if (!(inh & INH_NOINIT)) {
+        // unpack_init clears the register but not its bit count (UnpackUtils.cs:34):
+        // the rest of the current byte reads as zeros
+        s.bs.win &= ~((1ull << (s.bs.nb & 7)) - 1ull);
+    }
+    if (!(inh & INH_WVX)) {
+        s.xb.init(blob, d.wvx_off, d.wvx_len);
+        if (d.wvx_state & 0x100) {
+            int skip = (d.wvx_state >> 1) & 0x7f;
+            if (skip) s.xb.getbits(skip);
+        }
+    }
+    Entropy &w = s.w;
+    if (!(inh & INH_ENTROPY)) {
+        for (int c = 0; c < 2; c++) {
+            for (int k = 0; k < 3; k++) w.med[c][k] = d.median[c][k];
+            w.slow[c] = d.slow_level[c];
+            w.errlim[c] = 0;
+            w.acc[c] = d.bitrate_acc[c];
+            w.dlt[c] = d.bitrate_delta[c];
+        }
+        w.zeros_acc = 0;
+        w.h0 = w.h1 = 0;
+    } else {  // read_hybrid_profile without read_entropy_vars: those fields only
+        for (int c = 0; c < 2; c++) {
+            if (!(inh & (INH_SLOW0 << c))) w.slow[c] = d.slow_level[c];
+            if (!(inh & (INH_ACC0 << c))) w.acc[c] = d.bitrate_acc[c];
+            if (!(inh & (INH_DLT0 << c))) w.dlt[c] = d.bitrate_delta[c];
+        }
+    }
+    bool fresh_passes = true;
+    for (int i = 0; i < d.num_terms && i < MAXP; i++) {
+        PassState &p = s.ps[i];
+        p.term = d.term[i];
+        p.delta = d.delta[i];
+        if ((d.inherit_passes >> i) & 1u) {
+            fresh_passes = false;
+        } else {
+            p.wA = d.weight_A[i];
+            p.wB = d.weight_B[i];
+        }
+        if ((d.inherit_passes >> (16 + i)) & 1u) {
+            fresh_passes = false;
+        } else {
+            for (int k = 0; k < 8; k++) {
+                p.rA[k] = d.samples_A[i][k];
+                p.rB[k] = d.samples_B[i][k];
+            }
+        }
+    }
+    if (fresh_passes) s.pass_garbage = false;
+    else if (s.pass_garbage) status |= ST_NONDET;  // carried from passes over stale residuals
+    if (!(inh & INH_NOINIT)) {  // unpack_init (UnpackUtils.cs:32-33)
+        s.crc = s.crc_x = -1;
+        s.muted = false;
+        s.crc_garbage = false;
+    }
+    return status;
+}
+
+// The block's frames from state `s`.  CHAIN: leave `s` as the reference's
+// stream is left for the next block -- the muting chunk's remaining words and
+// passes still run (UnpackUtils.cs:556-607 precede the mute test), and the
+// rings end in the reference's layout.
+template <class Store, bool CHAIN>
+WVF_HD uint32_t decode_pcm_run(PcmState &s, const BlockDesc &d, Store &out, uint32_t *exc_frame) {
     using namespace wvf;
     const uint32_t flags = d.flags;
     const bool mono = (flags & MONO_DATA) != 0;       // decode path (UnpackUtils.cs:549)
@@ -623,55 +726,25 @@ WVF_HD uint32_t decode_pcm_block(const BlockDesc &d, const uint8_t *blob, Store 
     const int nt = d.num_terms;
     const uint32_t nfr = d.nframes;
     const int och = mono_out ? 1 : 2;
-
-    BitReader bs;
-    bs.init(blob, d.bits_off, d.bits_len);
-    BitReader xb;
-    xb.init(blob, d.wvx_off, d.wvx_len);
-    if (d.wvx_state & 0x100) {
-        int skip = (d.wvx_state >> 1) & 0x7f;
-        if (skip) xb.getbits(skip);
-    }
-
-    Entropy w;
-    for (int c = 0; c < 2; c++) {
-        for (int k = 0; k < 3; k++) w.med[c][k] = d.median[c][k];
-        w.slow[c] = d.slow_level[c];
-        w.errlim[c] = 0;
-        w.acc[c] = d.bitrate_acc[c];
-        w.dlt[c] = d.bitrate_delta[c];
-    }
-    w.zeros_acc = 0;
-    w.h0 = w.h1 = 0;
-
-    PassState ps[MAXP];
-    for (int i = 0; i < nt; i++) {
-        ps[i].term = d.term[i];
-        ps[i].delta = d.delta[i];
-        ps[i].wA = d.weight_A[i];
-        ps[i].wB = d.weight_B[i];
-        for (int k = 0; k < 8; k++) {
-            ps[i].rA[k] = d.samples_A[i][k];
-            ps[i].rB[k] = d.samples_B[i][k];
-        }
-    }
+    BitReader &bs = s.bs;
+    BitReader &xb = s.xb;
+    Entropy &w = s.w;
+    PassState *ps = s.ps;
 
     Fixup fx;
     fixup_init(fx, d);
 
     uint32_t status = 0;
     if (fstereo && fx.mode == 2) status |= ST_NONDET;  // fixup reads wvx bits for 2n values (n stale)
-    bool crc_garbage = false;
-    int32_t crc = -1, crc_x = -1;
-    bool muted = false;
-    uint32_t f = 0;  // block frame index (also the ring clock)
+    uint32_t f = 0;   // block frame index (also the ring clock)
+    uint32_t tp = 0;  // frames the passes ran over (CHAIN)
     uint32_t chunk_len = d.first_chunk;
     uint32_t bsp = d.first_bsp;
     bool first = true;
     while (f < nfr) {
         uint32_t n = chunk_len;
         if (n > nfr - f) n = nfr - f;
-        if (muted) {  // mute_error set: unpack_samples zero-fills (UnpackUtils.cs:527-543)
+        if (s.muted) {  // mute_error set: unpack_samples zero-fills (UnpackUtils.cs:527-543)
             for (uint32_t j = 0; j < n; j++)
                 for (int c = 0; c < och; c++) out.put((uint64_t)(f + j) * och + c, 0);
             f += n;
@@ -682,9 +755,10 @@ WVF_HD uint32_t decode_pcm_block(const BlockDesc &d, const uint8_t *blob, Store 
         }
         // state at the chunk start, for the wvx rewind on muting
         BitReader xb0 = xb;
-        int32_t crcx0 = crc_x;
+        int32_t crcx0 = s.crc_x;
         bool crc_stop = false;
         int mute_at = -1;  // chunk-relative frame that mutes the chunk
+        bool words_short = false;
         for (uint32_t j = 0; j < n; j++) {
             uint32_t t = f + j;
             int32_t L, R = 0;
@@ -700,7 +774,8 @@ WVF_HD uint32_t decode_pcm_block(const BlockDesc &d, const uint8_t *blob, Store 
                 status |= ST_BITS_ERROR;
                 if (mono && first && bsp > 0) status |= ST_NONDET;
                 mute_at = (int)j;
-                crc_garbage = true;  // the verdict at block end is "error" (w.p. 1 - 2^-32)
+                s.crc_garbage = true;  // the verdict at block end is "error" (w.p. 1 - 2^-32)
+                words_short = true;
                 break;
             }
             if (mono) {
@@ -714,7 +789,7 @@ WVF_HD uint32_t decode_pcm_block(const BlockDesc &d, const uint8_t *blob, Store 
                     }
                     crc_stop = true;
                 }
-                if (!crc_stop) crc = add32(mul32(crc, 3), L);
+                if (!crc_stop) s.crc = add32(mul32(s.crc, 3), L);
             } else {
                 for (int i = 0; i < nt; i++) pass_stereo(ps[i], t, L, R);
                 if (joint) {
@@ -727,7 +802,7 @@ WVF_HD uint32_t decode_pcm_block(const BlockDesc &d, const uint8_t *blob, Store 
                     mute_at = (int)j;
                     break;
                 }
-                crc = add32(mul32(add32(mul32(crc, 3), L), 3), R);
+                s.crc = add32(mul32(add32(mul32(s.crc, 3), L), 3), R);
             }
             // (short) weight stores at the pass-call seams (B-4)
             if ((!mono && n >= 16 && j == 7) || j == n - 1) {
@@ -740,8 +815,8 @@ WVF_HD uint32_t decode_pcm_block(const BlockDesc &d, const uint8_t *blob, Store 
             int32_t oL, oR;
             if (fx.mode == 2) {
                 int xexc = 0;
-                oL = fixup_wvx(fx, xb, d.wvx_len, L, crc_x, xexc);
-                oR = mono ? 0 : fixup_wvx(fx, xb, d.wvx_len, R, crc_x, xexc);
+                oL = fixup_wvx(fx, xb, d.wvx_len, L, s.crc_x, xexc);
+                oR = mono ? 0 : fixup_wvx(fx, xb, d.wvx_len, R, s.crc_x, xexc);
                 if (xexc) {  // fixup_samples of this call threw (the call's frame)
                     if (exc_frame) *exc_frame = t;
                     return status | ST_EXCEPTION;
@@ -761,19 +836,55 @@ WVF_HD uint32_t decode_pcm_block(const BlockDesc &d, const uint8_t *blob, Store 
                 out.put(o + 1, oR);
             }
         }
+        if (CHAIN && mute_at >= 0) {
+            if (words_short) {
+                s.pass_garbage = nt > 0;  // the passes ran over the chunk's stale residuals
+            } else {
+                // the rest of the chunk's words and passes (their values are discarded)
+                for (uint32_t j = (uint32_t)mute_at; j < n; j++) {
+                    const uint32_t t = f + j;
+                    if (j > (uint32_t)mute_at) {
+                        int32_t L, R = 0;
+                        int rc = get_word(w, bs, flags, 0, true, L);
+                        if (rc == DEC_OK && !mono) rc = get_word(w, bs, flags, 1, false, R);
+                        if (rc == DEC_EXCEPTION) {
+                            if (exc_frame) *exc_frame = t;
+                            return status | ST_EXCEPTION;
+                        }
+                        if (rc != DEC_OK) {
+                            status |= ST_BITS_ERROR;
+                            s.pass_garbage = nt > 0;
+                            break;
+                        }
+                        if (mono) {
+                            for (int i = 0; i < nt; i++) pass_mono(ps[i], t, L);
+                        } else {
+                            for (int i = 0; i < nt; i++) pass_stereo(ps[i], t, L, R);
+                        }
+                    }
+                    if ((!mono && n >= 16 && j == 7) || j == n - 1) {
+                        for (int i = 0; i < nt; i++) {
+                            ps[i].wA = (int16_t)ps[i].wA;
+                            ps[i].wB = (int16_t)ps[i].wB;
+                        }
+                    }
+                }
+            }
+        }
+        tp = f + n;
         if (mute_at >= 0) {
             // UnpackUtils.cs:649-664: zero the whole chunk, then fixup_samples runs on
             // the zeros (which is not always 0: int32 'ones', wvx reads)
             status |= ST_MUTED;
-            muted = true;
+            s.muted = true;
             xb = xb0;
-            crc_x = crcx0;
+            s.crc_x = crcx0;
             for (uint32_t j = 0; j < n; j++) {
                 int32_t z0, z1 = 0;
                 if (fx.mode == 2) {
                     int xexc = 0;
-                    z0 = fixup_wvx(fx, xb, d.wvx_len, 0, crc_x, xexc);
-                    if (!mono) z1 = fixup_wvx(fx, xb, d.wvx_len, 0, crc_x, xexc);
+                    z0 = fixup_wvx(fx, xb, d.wvx_len, 0, s.crc_x, xexc);
+                    if (!mono) z1 = fixup_wvx(fx, xb, d.wvx_len, 0, s.crc_x, xexc);
                     if (xexc) {
                         if (exc_frame) *exc_frame = f + j;
                         return status | ST_EXCEPTION;
@@ -799,13 +910,24 @@ WVF_HD uint32_t decode_pcm_block(const BlockDesc &d, const uint8_t *blob, Store 
         bsp = 0;
         first = false;
     }
+    if (CHAIN)
+        for (int i = 0; i < nt; i++)
+            if (ring_term(ps[i].term, mono)) ring_normalize(ps[i], tp, mono);
     if (nfr == d.block_samples) {  // check_crc_error at block end (WavPackUtils.cs:273-275)
         status |= ST_CRC_CHECKED;
-        bool err = crc_garbage || crc != d.crc;
-        if (!(flags & FLOAT_DATA) && (d.wvx_state & 1) && crc_x != d.crc_mvx) err = true;
+        bool err = s.crc_garbage || s.crc != d.crc;
+        if (!(flags & FLOAT_DATA) && (d.wvx_state & 1) && s.crc_x != d.crc_mvx) err = true;
         if (err) status |= ST_CRC_ERROR;
     }
     return status;
+}
+
+// one block from its descriptor alone
+template <class Store>
+WVF_HD uint32_t decode_pcm_block(const BlockDesc &d, const uint8_t *blob, Store &out, uint32_t *exc_frame = nullptr) {
+    PcmState s;
+    pcm_state_load(s, d, blob);
+    return decode_pcm_run<Store, false>(s, d, out, exc_frame);
 }
 
 // ---------------------------------------------------------------------------

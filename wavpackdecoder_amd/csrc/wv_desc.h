@@ -26,7 +26,7 @@ enum StatusBits : uint32_t {
     ST_MUTED = 1u << 2,        // mute_error was raised in some chunk
     ST_BITS_ERROR = 1u << 3,   // get_words hit the 33-ones / 17-ones break
     ST_EXCEPTION = 1u << 4,    // the reference would raise a C# exception here
-    ST_UNSUPPORTED = 1u << 5,  // state depends on data the device cannot see (sticky decode state)
+    ST_UNSUPPORTED = 1u << 5,  // a layout the device does not decode (stereo term 0, ...; malformed files only)
     ST_DSD_MUTE = 1u << 6,     // DSD chunk(s) muted with 0x55 (post-pass fill, DsdUtils.cs:104-117)
     ST_NONDET = 1u << 7,       // reference output depends on stale caller-buffer contents
     ST_TIMEOUT = 1u << 8,      // a kernel's bounded LDS wait ran out (decoder fault, not a reference outcome)
@@ -84,7 +84,30 @@ struct alignas(16) BlockDesc {
     // pre_end * out_nch ints before the file's output, as a wrapped offset)
     uint32_t pre_end;       // 0: no discard phase
     uint32_t pre_chunk;     // SAMPLE_BUFFER_SIZE / reduced channels (WavPackUtils.cs:576)
-    int32_t pad_[3];
+    // --- sticky state (UnpackUtils.cs:24-68, Appendix B-8): what this block takes
+    // from the decode of the block before it instead of from its own metadata
+    uint32_t inherit;         // InheritBits (0: everything comes from the descriptor)
+    uint32_t inherit_passes;  // bit i: pass i's weights, bit 16 + i: its samples continue
+    uint32_t chain_len;       // first block of a chain: blocks decoded in sequence from it (>= 2)
+};
+
+// A block that starts from state an earlier decode left behind: a block without
+// one of the metadata sub-blocks that reset it, or one read without unpack_init
+// (a header whose block_index is ahead of the stream: WavPackUtils.cs:219-251).
+// The framing groups it with the blocks before it, back to one whose state is
+// all known, into a chain that one wave decodes in order (wv_decode_chain).
+enum InheritBits : uint32_t {
+    INH_BITS = 1u << 0,     // main bitstream: no ID_WV_BITSTREAM since the last decode
+    INH_WVX = 1u << 1,      // wvx bitstream continues
+    INH_ENTROPY = 1u << 2,  // words_data continues (no ID_ENTROPY_VARS), except the fields below left clear
+    INH_SLOW0 = 1u << 3,    // ... slow_level / bitrate_acc / bitrate_delta per channel: continues
+    INH_SLOW1 = 1u << 4,    //     (clear: a hybrid profile re-sent it; the descriptor holds it)
+    INH_ACC0 = 1u << 5,
+    INH_ACC1 = 1u << 6,
+    INH_DLT0 = 1u << 7,
+    INH_DLT1 = 1u << 8,
+    INH_NOINIT = 1u << 9,   // no unpack_init since the last decode: crc, crc_x, mute_error, bit register continue
+    INH_MEMBER = 1u << 31,  // decoded by the chain kernel after its predecessor
 };
 static_assert(sizeof(BlockDesc) % 16 == 0, "BlockDesc is loaded with 16-B alignment");
 

@@ -38,6 +38,8 @@ struct Words {  // words_data.cs
     int32_t slow[2] = {0, 0};
     int64_t acc[2] = {0, 0}, dlt[2] = {0, 0};
     bool known = true;
+    // with !known: the fields a later read_hybrid_profile re-sent
+    bool known_slow[2] = {true, true}, known_acc[2] = {true, true}, known_dlt[2] = {true, true};
 };
 
 struct BitsRef {  // a Bitstream reference: where its bytes are and whether it is untouched
@@ -128,6 +130,7 @@ class Framer {
     int64_t sample_index = 0;
     DsdState dsd;
     bool inited_this_block = false;  // unpack_init ran for the current header
+    bool decoded_since_init = false; // a block was decoded after the last unpack_init
     // deferred metadata values (wv_meta.h): reads whose values the device
     // computes; until materialize() the host copies of those values are stale
     bool defer = false;
@@ -434,8 +437,27 @@ class Framer {
         w = nw;
         return true;
     }
+    // the fields read_hybrid_profile writes (WordsUtils.cs:132-181)
+    void hybrid_known(int byte_length) {
+        const bool mono = (wphdr.flags & MONO_DATA) != 0;
+        const int w2 = mono ? 2 : 4;
+        int bc = w2;
+        if (wphdr.flags & HYBRID_BITRATE) {
+            w.known_slow[0] = true;
+            if (!mono) w.known_slow[1] = true;
+            bc += w2;
+        }
+        w.known_acc[0] = true;
+        if (!mono) w.known_acc[1] = true;
+        if (bc < byte_length) {
+            w.known_dlt[0] = true;
+            if (!mono) w.known_dlt[1] = true;
+        } else
+            w.known_dlt[0] = w.known_dlt[1] = true;
+    }
     bool read_hybrid_profile(Md &m) {  // WordsUtils.cs:124-187
         bool mono = (wphdr.flags & MONO_DATA) != 0;
+        hybrid_known(m.byte_length);
         if (defer) {  // deferred when it reads exactly the sub-block (no stale bytes, no failure)
             const int w2 = mono ? 2 : 4;
             int need = ((wphdr.flags & HYBRID_BITRATE) ? w2 : 0) + w2;
@@ -710,6 +732,7 @@ class Framer {
         Md m;
         if (wphdr.block_samples > 0 && wphdr.block_index != 0xFFFFFFFFLL) sample_index = wphdr.block_index;
         inited_this_block = true;
+        decoded_since_init = false;
         // anything the previous decode adapted is now unknown unless re-sent
         wvbits.fresh = false;
         wvxbits.fresh = false;
@@ -760,9 +783,11 @@ class Framer {
         d.int32_dups = int32_dups;
         d.int32_max_width = int32_max_width;
         // a header whose block was not unpack_init'ed decodes with the stream state
-        // left from earlier metadata (sticky state, B-8): fine while that state is
-        // unconsumed (the fresh/known flags below), unsupported once consumed
-        (void)inited_this_block;
+        // left from earlier metadata (sticky state, B-8): known while that state is
+        // unconsumed (the fresh/known flags below); once a decode consumed it, the
+        // block inherits it from that decode (d.inherit, chained in frame_file)
+        uint32_t inh = 0, inhp = 0;
+        if (!inited_this_block && decoded_since_init) inh |= INH_NOINIT;
         if (flags & DSD_FLAG) {
             if (!dsd.fresh) status |= ST_UNSUPPORTED;
             d.kind = dsd.mode == 0 ? KIND_DSD_RAW : dsd.mode == 1 ? KIND_DSD_FAST : KIND_DSD_HIGH;
@@ -790,21 +815,28 @@ class Framer {
             }
         } else {
             d.kind = KIND_PCM;
-            if (!wvbits.fresh) status |= ST_UNSUPPORTED;  // would continue a consumed bitstream
+            if (!wvbits.fresh) inh |= INH_BITS;  // continues a consumed bitstream
             d.bits_off = blob_base + (uint64_t)wvbits.file_off;
             d.bits_len = (uint32_t)wvbits.byte_length;
             if (wvxbits.valid) {
                 d.wvx_state = 1 | (wvx_skip_bits << 1);
                 d.crc_mvx = crc_mvx;
+                d.wvx_off = blob_base + (uint64_t)wvxbits.file_off;
+                d.wvx_len = (uint32_t)(wvxbits.data_len - 4);
                 if ((flags & INT32_DATA) && !(flags & FLOAT_DATA)) {
                     // fixup_samples reads it (UnpackUtils.cs:1271-1314)
-                    if (!wvxbits.fresh) status |= ST_UNSUPPORTED;
+                    if (!wvxbits.fresh) inh |= INH_WVX;
                     d.wvx_state |= 0x100;
-                    d.wvx_off = blob_base + (uint64_t)wvxbits.file_off;
-                    d.wvx_len = (uint32_t)(wvxbits.data_len - 4);
                 }
             }
-            if (!w.known) status |= ST_UNSUPPORTED;
+            if (!w.known) {
+                inh |= INH_ENTROPY;
+                for (int c = 0; c < 2; c++) {
+                    if (!w.known_slow[c]) inh |= INH_SLOW0 << c;
+                    if (!w.known_acc[c]) inh |= INH_ACC0 << c;
+                    if (!w.known_dlt[c]) inh |= INH_DLT0 << c;
+                }
+            }
             memcpy(d.median, w.med, sizeof(d.median));
             memcpy(d.slow_level, w.slow, sizeof(d.slow_level));
             memcpy(d.bitrate_acc, w.acc, sizeof(d.bitrate_acc));
@@ -812,7 +844,8 @@ class Framer {
             d.num_terms = num_terms;
             for (int i = 0; i < num_terms && i < 16; i++) {
                 const Pass &p = passes[i];
-                if (!p.known_w || !p.known_s) status |= ST_UNSUPPORTED;
+                if (!p.known_w) inhp |= 1u << i;
+                if (!p.known_s) inhp |= 1u << (16 + i);
                 d.term[i] = (int8_t)p.term;
                 d.delta[i] = (int8_t)p.delta;
                 d.weight_A[i] = p.wA;
@@ -841,7 +874,16 @@ class Framer {
             if ((flags & FALSE_STEREO) && (flags & MONO_FLAG)) status |= ST_UNSUPPORTED;
             if (int32_sent_bits > 32 || int32_sent_bits < 0) status |= ST_UNSUPPORTED;
         }
-        if (status & ST_UNSUPPORTED) d.kind = KIND_SKIP;
+        if (d.kind == KIND_PCM) {
+            d.inherit = inh;
+            d.inherit_passes = inhp;
+        } else if (inh & INH_NOINIT) {
+            status |= ST_UNSUPPORTED;  // a DSD block continuing the crc / mute state
+        }
+        if (status & ST_UNSUPPORTED) {
+            d.kind = KIND_SKIP;
+            d.inherit = d.inherit_passes = 0;
+        }
         // the framing reports its verdicts through the same status word
         d.fstatus = status;
         return d;
@@ -851,6 +893,8 @@ class Framer {
     void mark_adapted() {
         for (auto &p : passes) p.known_w = p.known_s = false;
         w.known = false;
+        for (int c = 0; c < 2; c++) w.known_slow[c] = w.known_acc[c] = w.known_dlt[c] = false;
+        decoded_since_init = true;
         wvbits.fresh = false;
         wvxbits.fresh = false;
         dsd.fresh = false;
@@ -930,6 +974,7 @@ void take_stream(Framer &F, const Framer &c) {
     F.sample_index = c.sample_index;
     F.dsd = c.dsd;
     F.inited_this_block = c.inited_this_block;
+    F.decoded_since_init = c.decoded_since_init;
     F.pending = c.pending;
 }
 
@@ -1003,6 +1048,31 @@ int64_t file_out_extent(const FramingOutput &out, const FileInfo &info, uint64_t
 
 int compute_mode(const FileInfo &info) {  // WavPackUtils.cs:133-167 (fields captured at open)
     return info.mode;
+}
+
+// Blocks that inherit decode state (d.inherit) join the block decoded before
+// them into a chain, back to a block whose state is all in its descriptor; the
+// chain's first descriptor records the chain length.  A block whose
+// predecessor cannot be decoded on the device (a DSD or skipped block) stays
+// unsupported.
+static void chain_blocks(FramingOutput &out, int64_t first, int64_t count) {
+    int64_t head = -1;
+    for (int64_t k = first; k < first + count; k++) {
+        BlockDesc &d = out.descs[(size_t)k];
+        if (d.kind != KIND_PCM || (d.inherit == 0 && d.inherit_passes == 0)) {
+            head = d.kind == KIND_PCM ? k : -1;
+            continue;
+        }
+        if (head < 0) {
+            d.kind = KIND_SKIP;
+            d.fstatus |= ST_UNSUPPORTED;
+            d.inherit = d.inherit_passes = 0;
+            continue;
+        }
+        BlockDesc &h = out.descs[(size_t)head];
+        h.chain_len = h.chain_len ? h.chain_len + 1 : 2;
+        d.inherit |= INH_MEMBER;
+    }
 }
 
 void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t out_base_ints, uint32_t open_flags,
@@ -1134,6 +1204,7 @@ void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t ou
                     if (bch != nch) {
                         d.kind = KIND_SKIP;
                         d.fstatus |= ST_UNSUPPORTED;
+                        d.inherit = d.inherit_passes = 0;
                     }
                     if ((hh.flags & DSD_FLAG) && F.dsd.mode == 0 && (hh.flags & FALSE_STEREO)) {
                         // DsdUtils.cs:81 advances bufferStartPos, then :119-131 duplicates
@@ -1184,6 +1255,7 @@ void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t ou
     info.trailer_len = F.trailer_len;
     info.num_desc = (int64_t)out.descs.size() - info.first_desc;
     (void)cur;
+    chain_blocks(out, info.first_desc, info.num_desc);
 }
 
 }  // namespace wvg
