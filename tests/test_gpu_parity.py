@@ -74,10 +74,11 @@ def test_dsd_modes(case, gpu_batch_cls):
     _check_one(data, chunk, gpu_batch_cls, name)
 
 
-@pytest.mark.parametrize("case", V.sticky_cases(), ids=lambda c: c[0])
+@pytest.mark.parametrize("case", V.sticky_cases() + V.term0_cases(), ids=lambda c: c[0])
 def test_sticky_state_chains(case, gpu_batch_cls):
     """Blocks continuing the previous decode's state (B-8): one chain per file run
-    in order by wv_decode_pcm_wave, bit-exact with the oracle (tests/test_sticky.py)."""
+    in order by wv_decode_pcm_wave, bit-exact with the oracle (tests/test_sticky.py);
+    and stereo term 0, whose decode depends on the call seams (generic kernel)."""
     name, data, chunk = case
     _check_one(data, chunk, gpu_batch_cls, name)
 

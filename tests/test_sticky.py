@@ -60,3 +60,17 @@ def test_chain_layout():
     # a well-formed file has no chains
     plain = V.pcm_cases()[0][1]
     assert all(t[0] == 0 and t[1] == 0 and t[2] == 0 for t in _descs(plain))
+
+
+@pytest.mark.parametrize("case", V.term0_cases(), ids=lambda c: c[0])
+def test_stereo_term0_matches_oracle(case):
+    name, data, chunk = case
+    r = O.decode_file(data, chunk=chunk)
+    n, out, crc, st = E.decode(data, chunk)
+    assert not (st & ST_UNSUPPORTED), name
+    if r.status != 0:
+        assert n == r.status, name
+        return
+    assert n == r.frames and crc == r.crc_errors, name
+    if not (st & ST_NONDET):
+        np.testing.assert_array_equal(out, r.samples, err_msg=name)

@@ -510,7 +510,10 @@ int term_set_of(const BlockDesc &d, int prefer_pipe) {
     const bool mono = (d.flags & MONO_DATA) != 0;
     if (d.num_terms < 0 || d.num_terms > MAXP) return -1;
     bool neg12 = false;
-    for (int i = 0; i < d.num_terms; i++) neg12 |= !mono && (d.term[i] == -1 || d.term[i] == -2);
+    for (int i = 0; i < d.num_terms; i++) {
+        neg12 |= !mono && (d.term[i] == -1 || d.term[i] == -2);
+        if (!mono && d.term[i] == 0) return -1;  // term 0's call-position rule: pass_stereo's `cont`
+    }
     const int pipe = kPipe + (neg12 ? 1 : 0);
     if (prefer_pipe >= 2) return pipe;
     for (int s = 0; s < kNumTermSets; s++) {

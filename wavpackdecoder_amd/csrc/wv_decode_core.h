@@ -397,8 +397,10 @@ WVF_HD void upd_wc(int32_t &w, int32_t s, int32_t b, int32_t delta) {  // negati
     }
 }
 
-// one stereo frame through one pass (UnpackUtils.cs:688-944 / 946-1154)
-WVF_HD void pass_stereo(PassState &p, uint32_t t, int32_t &L, int32_t &R) {
+// one stereo frame through one pass (UnpackUtils.cs:688-944 / 946-1154).
+// `cont`: the frame is past the first 8 of a call of >= 16 frames, i.e. in
+// decorr_stereo_pass_cont -- which only term 0 (a malformed list) notices.
+WVF_HD void pass_stereo(PassState &p, uint32_t t, int32_t &L, int32_t &R, bool cont = false) {
     using namespace wvf;
     const int32_t d = p.delta;
     switch (p.term) {
@@ -461,6 +463,17 @@ WVF_HD void pass_stereo(PassState &p, uint32_t t, int32_t &L, int32_t &R) {
     }
     default: {
         int m = t & 7, k = (t + (p.term & 7)) & 7;
+        if (p.term == 0 && cont) {
+            // decorr_stereo_pass_cont with term 0 (UnpackUtils.cs:1119-1146): the
+            // source is the sample itself; the last 8 outputs become the ring
+            int32_t oa = add32(apply_weight(p.wA, L), L);
+            upd_w(p.wA, L, L, d);
+            int32_t ob = add32(apply_weight(p.wB, R), R);
+            upd_w(p.wB, R, R, d);
+            p.rA[m] = L = oa;
+            p.rB[m] = R = ob;
+            break;
+        }
         int32_t sa = p.rA[m];
         int32_t oa = add32(apply_weight(p.wA, sa), L);
         upd_w(p.wA, sa, L, d);
@@ -791,7 +804,7 @@ WVF_HD uint32_t decode_pcm_run(PcmState &s, const BlockDesc &d, Store &out, uint
                 }
                 if (!crc_stop) s.crc = add32(mul32(s.crc, 3), L);
             } else {
-                for (int i = 0; i < nt; i++) pass_stereo(ps[i], t, L, R);
+                for (int i = 0; i < nt; i++) pass_stereo(ps[i], t, L, R, n >= 16 && j >= 8);
                 if (joint) {
                     R = sub32(R, L >> 1);
                     L = add32(L, R);
@@ -859,7 +872,7 @@ WVF_HD uint32_t decode_pcm_run(PcmState &s, const BlockDesc &d, Store &out, uint
                         if (mono) {
                             for (int i = 0; i < nt; i++) pass_mono(ps[i], t, L);
                         } else {
-                            for (int i = 0; i < nt; i++) pass_stereo(ps[i], t, L, R);
+                            for (int i = 0; i < nt; i++) pass_stereo(ps[i], t, L, R, n >= 16 && j >= 8);
                         }
                     }
                     if ((!mono && n >= 16 && j == 7) || j == n - 1) {

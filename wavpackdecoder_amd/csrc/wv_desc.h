@@ -26,7 +26,7 @@ enum StatusBits : uint32_t {
     ST_MUTED = 1u << 2,        // mute_error was raised in some chunk
     ST_BITS_ERROR = 1u << 3,   // get_words hit the 33-ones / 17-ones break
     ST_EXCEPTION = 1u << 4,    // the reference would raise a C# exception here
-    ST_UNSUPPORTED = 1u << 5,  // a layout the device does not decode (stereo term 0, ...; malformed files only)
+    ST_UNSUPPORTED = 1u << 5,  // a layout the device does not decode (malformed files only; wv_framing.cpp)
     ST_DSD_MUTE = 1u << 6,     // DSD chunk(s) muted with 0x55 (post-pass fill, DsdUtils.cs:104-117)
     ST_NONDET = 1u << 7,       // reference output depends on stale caller-buffer contents
     ST_TIMEOUT = 1u << 8,      // a kernel's bounded LDS wait ran out (decoder fault, not a reference outcome)
@@ -95,7 +95,8 @@ struct alignas(16) BlockDesc {
 // one of the metadata sub-blocks that reset it, or one read without unpack_init
 // (a header whose block_index is ahead of the stream: WavPackUtils.cs:219-251).
 // The framing groups it with the blocks before it, back to one whose state is
-// all known, into a chain that one wave decodes in order (wv_decode_chain).
+// all known, into a chain that one wave decodes in order (decode_chain,
+// wv_decode.hip).
 enum InheritBits : uint32_t {
     INH_BITS = 1u << 0,     // main bitstream: no ID_WV_BITSTREAM since the last decode
     INH_WVX = 1u << 1,      // wvx bitstream continues

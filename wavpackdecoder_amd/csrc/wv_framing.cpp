@@ -866,10 +866,6 @@ class Framer {
                 out.jobs.push_back(j);
             }
             if (num_terms < 0 || num_terms > 16) status |= ST_UNSUPPORTED;
-            // term 0 in a stereo block behaves differently in the first 8 frames
-            // and in decorr_stereo_pass_cont (UnpackUtils.cs:1118-1121)
-            for (int i = 0; i < num_terms && i < 16; i++)
-                if (passes[i].term == 0 && !(flags & MONO_DATA)) status |= ST_UNSUPPORTED;
             // FALSE_STEREO together with MONO_FLAG writes 2 ints/frame at a 1-int stride
             if ((flags & FALSE_STEREO) && (flags & MONO_FLAG)) status |= ST_UNSUPPORTED;
             if (int32_sent_bits > 32 || int32_sent_bits < 0) status |= ST_UNSUPPORTED;
