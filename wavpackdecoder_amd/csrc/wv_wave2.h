@@ -620,15 +620,19 @@ __device__ __forceinline__ bool lossless_run(Entropy &w, SmemReader &rd, uint32_
 // read_code(maxcode = mc) + sign + window advance + residual into lane M0
 // (WordsUtils.cs:477-503, 546-570).  z = clz(mc|1), n1 = 31 - z = bitcount-1
 // (mc|1 makes maxcode 0 read no code bits), extras = 2^(n1+1) - 1 - mc.
+// The scalar issue port bounds the in-flight bench, so the word
+// is written for instruction count: n1 carries 0x10000 (bit offset n1, width
+// 1 for s_bfe_i32: the sign as 0 / -1 in one instruction) and c1 carries
+// -0x10000 (shift counts read only the low bits), so n1 + c1 is unbiased.
 #define NW_TAIL(I, S, LOWOP)                                        \
     "s_or_b32 %[t0], %[mc], 1\n"                                    \
     "s_flbit_i32_b32 %[z], %[t0]\n"                                 \
     "s_lshr_b32 %[t], vcc_lo, %[c1]\n"                              \
     "s_lshr_b32 %[ex], -1, %[z]\n"                                  \
     "s_sub_u32 %[ex], %[ex], %[mc]\n"                               \
-    "s_lshr_b32 %[t0], 0x7fffffff, %[z]\n"                          \
+    "s_lshr_b32 %[t0], %[k7f], %[z]\n"                              \
     "s_and_b32 %[v], %[t], %[t0]\n"                                 \
-    "s_sub_u32 %[n1], 31, %[z]\n"                                   \
+    "s_sub_u32 %[n1], %[kn], %[z]\n"                                \
     "s_cmp_lt_u32 %[v], %[ex]\n"                                    \
     "s_cbranch_scc1 NS" I S "_%=\n"                                 \
     "s_lshl_b32 %[v], %[v], 1\n"                                    \
@@ -638,8 +642,7 @@ __device__ __forceinline__ bool lossless_run(Entropy &w, SmemReader &rd, uint32_
     "s_add_u32 %[n1], %[n1], 1\n"                                   \
     "NS" I S "_%=:\n"                                               \
     LOWOP                                                           \
-    "s_bitcmp1_b32 %[t], %[n1]\n"                                   \
-    "s_cselect_b32 %[t0], -1, 0\n"                                  \
+    "s_bfe_i32 %[t0], %[t], %[n1]\n"                                \
     "s_xor_b32 %[v], %[v], %[t0]\n"                                 \
     "s_add_u32 %[n1], %[n1], %[c1]\n"                               \
     "s_add_u32 %[n1], %[n1], 1\n"                                   \
@@ -648,24 +651,28 @@ __device__ __forceinline__ bool lossless_run(Entropy &w, SmemReader &rd, uint32_
     "v_writelane_b32 %[resv], %[v], m0\n"                           \
     "s_add_u32 m0, m0, 1\n"
 // hot part of word I (channel medians MA): refill test, unary + holding
-// flags, ones == 0 inline; falls through to the next word
+// flags, ones == 0 inline; falls through to the next word.  holding_zero
+// (:354-356: the word reads no unary bits, ones 0) is a virtual 0 bit shifted
+// in front of the window: the unary count then finds 0 ones and c1 = u + 1
+// consumes the virtual bit (nb counts it too), with no select on h0.  The
+// window's uncounted bits above nb move up one and lose bit 63; they return to
+// their places when the word's shift consumes the virtual bit, and the lost bit
+// is re-ORed by the next refill (nb <= 63 keeps it uncounted).
 #define NW_WORD(I, MA)                                              \
     "NW" I "_%=:\n"                                                 \
     "s_cmp_lt_u32 %[nb], 32\n"                                      \
     "s_cbranch_scc1 NR" I "_%=\n"                                   \
     "NA" I "_%=:\n"                                                 \
-    "s_orn2_b32 %[t0], 0x10000, vcc_lo\n"                           \
+    "s_lshl_b64 vcc, vcc, %[h0]\n"                                  \
+    "s_add_u32 %[nb], %[nb], %[h0]\n"                               \
+    "s_orn2_b32 %[t0], %[k16], vcc_lo\n"                            \
     "s_ff1_i32_b32 %[u], %[t0]\n"                                   \
-    "s_cmp_lg_u32 %[h0], 0\n"                                       \
-    "s_cselect_b32 %[u], 0, %[u]\n"                                 \
-    "s_lshr_b32 %[ones], %[u], 1\n"                                 \
-    "s_add_u32 %[ones], %[ones], %[h1]\n"                           \
+    "s_lshl1_add_u32 %[t0], %[h1], %[u]\n"                          \
     "s_and_b32 %[h1], %[u], 1\n"                                    \
-    "s_add_u32 %[c1], %[u], 1\n"                                    \
-    "s_sub_u32 %[c1], %[c1], %[h0]\n"                               \
-    "s_xor_b32 %[t0], %[h1], 1\n"                                   \
-    "s_sub_u32 %[h0], %[t0], %[h0]\n"                               \
-    "s_cmp_lg_u32 %[ones], 0\n"                                     \
+    "s_add_u32 %[c1], %[u], %[kc1]\n"                               \
+    "s_xor_b32 %[ex], %[h1], 1\n"                                   \
+    "s_sub_u32 %[h0], %[ex], %[h0]\n"                               \
+    "s_lshr_b32 %[ones], %[t0], 1\n" /* SCC = ones != 0 */          \
     "s_cbranch_scc1 NG" I "_%=\n"                                   \
     "s_lshr_b32 %[mc], " MA ", 4\n"                                 \
     NW_DEC(MA, "126", "6")                                          \
@@ -721,7 +728,8 @@ __device__ __forceinline__ bool lossless_run(Entropy &w, SmemReader &rd, uint32_
     "s_cbranch_scc1 NB" I "_%=\n"                                   \
     "s_or_b32 %[t0], %[mc], 1\n"                                    \
     "s_flbit_i32_b32 %[t0], %[t0]\n"                                \
-    "s_cmp_lt_u32 %[c1], %[t0]\n" /* c1 + n1 + 2 <= 32 */           \
+    "s_add_u32 %[t], %[u], 1\n" /* c1 (no holding_zero here) */     \
+    "s_cmp_lt_u32 %[t], %[t0]\n" /* c1 + n1 + 2 <= 32 */            \
     "s_cbranch_scc1 NJ" I "_%=\n"                                   \
     "NB" I "_%=:\n" /* leave before the word commits: restore h0/h1 */ \
     "s_lshr_b32 %[t0], %[u], 1\n"                                   \
@@ -788,7 +796,8 @@ __device__ __forceinline__ bool lossless_run_narrow(Entropy &w, SmemReader &rd, 
               [z] "=&s"(z), [n1] "=&s"(n1), [low] "=&s"(low), [ex] "=&s"(ex), [v] "=&s"(v), [keep] "=&s"(keep),
               [tq] "=&s"(tq), [win] "+s"(win), [nb] "+s"(nb), [off] "+s"(off), [q] "+s"(q), [m00] "+s"(m00),
               [m01] "+s"(m01), [m02] "+s"(m02), [h0] "+s"(h0), [h1] "+s"(h1), [lane] "+s"(lane), [resv] "+v"(resv)
-            : [lend] "s"(lend), [elim] "s"(elim), [base] "s"(rd.base)
+            : [lend] "s"(lend), [elim] "s"(elim), [base] "s"(rd.base), [k16] "s"(0x10000u), [k7f] "s"(0x7fffffffu),
+              [kc1] "s"(1u - 0x10000u), [kn] "s"(0x10000u + 31u)
             : "vcc", "scc");
     } else {
         asm volatile(
@@ -832,7 +841,8 @@ __device__ __forceinline__ bool lossless_run_narrow(Entropy &w, SmemReader &rd, 
               [tq] "=&s"(tq), [win] "+s"(win), [nb] "+s"(nb), [off] "+s"(off), [q] "+s"(q), [m00] "+s"(m00),
               [m01] "+s"(m01), [m02] "+s"(m02), [m10] "+s"(m10), [m11] "+s"(m11), [m12] "+s"(m12), [h0] "+s"(h0),
               [h1] "+s"(h1), [lane] "+s"(lane), [resv] "+v"(resv)
-            : [lend] "s"(lend), [elim] "s"(elim), [base] "s"(rd.base)
+            : [lend] "s"(lend), [elim] "s"(elim), [base] "s"(rd.base), [k16] "s"(0x10000u), [k7f] "s"(0x7fffffffu),
+              [kc1] "s"(1u - 0x10000u), [kn] "s"(0x10000u + 31u)
             : "vcc", "scc");
     }
     rd.win = win;
