@@ -330,7 +330,7 @@ __device__ __forceinline__ void recon_pipe(const BlockDesc &d, PipeShared &ps, i
                 produced = uni(lds_load_acq(&sh.produced));
                 break;
             }
-            __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_s_sleep(WV2_RECON_SLEEP);
             if (++spins > SPIN_LIMIT) {
                 perr = DEC_TIMEOUT;
                 break;

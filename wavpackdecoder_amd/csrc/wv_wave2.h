@@ -29,6 +29,11 @@ namespace w2 {
 
 constexpr int RES_RING = 2048;  // residual words in flight (8 KiB: 2 waves x 8 KiB lets 16 blocks share a CU)
 constexpr uint32_t SPIN_LIMIT = 1u << 26;  // bounded waits: a bug ends the kernel, never hangs the GPU
+// the reconstruction wave's poll interval (s_sleep units of 64 cycles): its
+// polls issue scalar instructions on the SIMD the parser waves are bound on
+#ifndef WV2_RECON_SLEEP
+#define WV2_RECON_SLEEP 16
+#endif
 
 // The reconstruction wave keeps the parser's payload ahead of it in the CU's
 // scalar cache: a scalar load per 64-byte line up to PF_AHEAD bytes past the
@@ -615,7 +620,7 @@ __device__ __forceinline__ bool lossless_run(Entropy &w, SmemReader &rd, uint32_
 #define NW_INC(M, ADD, SH) /* m += ((m + ADD) >> SH) * 5 */         \
     "s_add_i32 %[t0], " M ", " ADD "\n"                             \
     "s_ashr_i32 %[t0], %[t0], " SH "\n"                             \
-    "s_mul_i32 %[t0], %[t0], 5\n"                                   \
+    "s_lshl2_add_u32 %[t0], %[t0], %[t0]\n"                         \
     "s_add_i32 " M ", " M ", %[t0]\n"
 // read_code(maxcode = mc) + sign + window advance + residual into lane M0
 // (WordsUtils.cs:477-503, 546-570).  z = clz(mc|1), n1 = 31 - z = bitcount-1
@@ -624,7 +629,9 @@ __device__ __forceinline__ bool lossless_run(Entropy &w, SmemReader &rd, uint32_
 // is written for instruction count: n1 carries 0x10000 (bit offset n1, width
 // 1 for s_bfe_i32: the sign as 0 / -1 in one instruction) and c1 carries
 // -0x10000 (shift counts read only the low bits), so n1 + c1 is unbiased.
-#define NW_TAIL(I, S, LOWOP)                                        \
+// nb holds (bits in the window - 32): the window advance's borrow is the next
+// word's refill test (branch to NR<J>, J the next word), with no compare.
+#define NW_TAIL(I, S, LOWOP, J)                                     \
     "s_or_b32 %[t0], %[mc], 1\n"                                    \
     "s_flbit_i32_b32 %[z], %[t0]\n"                                 \
     "s_lshr_b32 %[t], vcc_lo, %[c1]\n"                              \
@@ -646,22 +653,20 @@ __device__ __forceinline__ bool lossless_run(Entropy &w, SmemReader &rd, uint32_
     "s_xor_b32 %[v], %[v], %[t0]\n"                                 \
     "s_add_u32 %[n1], %[n1], %[c1]\n"                               \
     "s_add_u32 %[n1], %[n1], 1\n"                                   \
-    "s_lshr_b64 vcc, vcc, %[n1]\n"                                  \
-    "s_sub_u32 %[nb], %[nb], %[n1]\n"                               \
     "v_writelane_b32 %[resv], %[v], m0\n"                           \
-    "s_add_u32 m0, m0, 1\n"
-// hot part of word I (channel medians MA): refill test, unary + holding
-// flags, ones == 0 inline; falls through to the next word.  holding_zero
-// (:354-356: the word reads no unary bits, ones 0) is a virtual 0 bit shifted
-// in front of the window: the unary count then finds 0 ones and c1 = u + 1
-// consumes the virtual bit (nb counts it too), with no select on h0.  The
-// window's uncounted bits above nb move up one and lose bit 63; they return to
-// their places when the word's shift consumes the virtual bit, and the lost bit
-// is re-ORed by the next refill (nb <= 63 keeps it uncounted).
-#define NW_WORD(I, MA)                                              \
-    "NW" I "_%=:\n"                                                 \
-    "s_cmp_lt_u32 %[nb], 32\n"                                      \
-    "s_cbranch_scc1 NR" I "_%=\n"                                   \
+    "s_add_u32 m0, m0, 1\n"                                         \
+    "s_lshr_b64 vcc, vcc, %[n1]\n"                                  \
+    "s_sub_u32 %[nb], %[nb], %[n1]\n" /* SCC: fewer than 32 left */ \
+    "s_cbranch_scc1 NR" J "_%=\n"
+// hot part of word I (channel medians MA): unary + holding flags, ones == 0
+// inline; falls through to the next word.  holding_zero (:354-356: the word
+// reads no unary bits, ones 0) is a virtual 0 bit shifted in front of the
+// window: the unary count then finds 0 ones and c1 = u + 1 consumes the
+// virtual bit (nb counts it too), with no select on h0.  The window's uncounted
+// bits above nb move up one and lose bit 63; they return to their places when
+// the word's shift consumes the virtual bit, and the lost bit is re-ORed by the
+// next refill (at most 63 bits are counted, so bit 63 is never one of them).
+#define NW_WORD(I, MA, J)                                           \
     "NA" I "_%=:\n"                                                 \
     "s_lshl_b64 vcc, vcc, %[h0]\n"                                  \
     "s_add_u32 %[nb], %[nb], %[h0]\n"                               \
@@ -676,19 +681,23 @@ __device__ __forceinline__ bool lossless_run(Entropy &w, SmemReader &rd, uint32_
     "s_cbranch_scc1 NG" I "_%=\n"                                   \
     "s_lshr_b32 %[mc], " MA ", 4\n"                                 \
     NW_DEC(MA, "126", "6")                                          \
-    NW_TAIL(I, "a", "")
-// cold parts of word I, placed after the loop; NEXT = label of the next word
-#define NW_COLD(I, NEXT, MA, MB, MC)                                \
-    "NR" I "_%=:\n" /* refill 32 bits, prefetch the next dword */   \
+    NW_TAIL(I, "a", "", J)
+// refill 32 bits from the prefetched dwords before word J, prefetch the next
+// dword (or leave near the payload end), continue at DEST (the batch-end test
+// in front of word J, or word J itself)
+#define NW_REFILL(J, DEST)                                          \
+    "NR" J "_%=:\n"                                                 \
     "s_cmp_gt_u32 %[off], %[elim]\n"                                \
     "s_cbranch_scc1 NX_%=\n"                                        \
     "s_waitcnt lgkmcnt(0)\n"                                        \
+    "s_add_u32 %[nb], %[nb], 32\n" /* = bits in the window */       \
     "s_lshl_b64 %[tq], %[q], %[nb]\n"                               \
     "s_or_b64 vcc, vcc, %[tq]\n"                                    \
-    "s_add_u32 %[nb], %[nb], 32\n"                                  \
     "s_load_dwordx2 %[q], %[base], %[off]\n"                        \
     "s_add_u32 %[off], %[off], 4\n"                                 \
-    "s_branch NA" I "_%=\n"                                         \
+    "s_branch " DEST "_%=\n"
+// cold parts of word I, placed after the loop; NEXT = label of the next word
+#define NW_COLD(I, NEXT, MA, MB, MC, J)                             \
     "NG" I "_%=:\n" /* ones == 1 */                                 \
     "s_cmp_eq_u32 %[ones], 1\n"                                     \
     "s_cbranch_scc0 NH" I "_%=\n"                                   \
@@ -697,7 +706,7 @@ __device__ __forceinline__ bool lossless_run(Entropy &w, SmemReader &rd, uint32_
     "s_lshr_b32 %[mc], " MB ", 4\n"                                 \
     NW_INC(MA, "128", "7")                                          \
     NW_DEC(MB, "62", "5")                                           \
-    NW_TAIL(I, "b", "s_add_u32 %[v], %[v], %[low]\n")               \
+    NW_TAIL(I, "b", "s_add_u32 %[v], %[v], %[low]\n", J)            \
     "s_branch " NEXT "_%=\n"                                        \
     "NH" I "_%=:\n" /* ones >= 2 */                                 \
     "s_lshr_b32 %[mc], " MC ", 4\n"                                 \
@@ -713,7 +722,7 @@ __device__ __forceinline__ bool lossless_run(Entropy &w, SmemReader &rd, uint32_
     "s_cmp_eq_u32 %[ones], 2\n"                                     \
     "s_cbranch_scc0 NM" I "_%=\n"                                   \
     NW_DEC(MC, "30", "4")                                           \
-    NW_TAIL(I, "c", "s_add_u32 %[v], %[v], %[low]\n")               \
+    NW_TAIL(I, "c", "s_add_u32 %[v], %[v], %[low]\n", J)            \
     "s_branch " NEXT "_%=\n"                                        \
     "NM" I "_%=:\n" /* ones >= 3 */                                 \
     "s_add_u32 %[t0], %[mc], 1\n"                                   \
@@ -721,7 +730,7 @@ __device__ __forceinline__ bool lossless_run(Entropy &w, SmemReader &rd, uint32_
     "s_mul_i32 %[t0], %[t0], %[v]\n"                                \
     "s_add_u32 %[low], %[low], %[t0]\n"                             \
     NW_INC(MC, "32", "5")                                           \
-    NW_TAIL(I, "d", "s_add_u32 %[v], %[v], %[low]\n")               \
+    NW_TAIL(I, "d", "s_add_u32 %[v], %[v], %[low]\n", J)            \
     "s_branch " NEXT "_%=\n"                                        \
     "NK" I "_%=:\n" /* 8..16 unary ones: escape, or test the bound */ \
     "s_cmp_gt_u32 %[u], 15\n"                                       \
@@ -772,22 +781,29 @@ __device__ __forceinline__ bool lossless_run_narrow(Entropy &w, SmemReader &rd, 
             "s_mov_b32 %[keep], m0\n"
             "s_mov_b32 m0, %[lane]\n"
             "s_mov_b64 vcc, %[win]\n"
+            "s_sub_u32 %[nb], %[nb], 32\n"
+            "s_cbranch_scc1 NR0_%=\n"
             NW_CHECK("NL")
-            NW_WORD("0", "%[m00]")
+            NW_WORD("0", "%[m00]", "1")
             NW_CHECK("NC0")
-            NW_WORD("1", "%[m00]")
+            NW_WORD("1", "%[m00]", "2")
             NW_CHECK("NC1")
-            NW_WORD("2", "%[m00]")
+            NW_WORD("2", "%[m00]", "3")
             NW_CHECK("NC2")
-            NW_WORD("3", "%[m00]")
+            NW_WORD("3", "%[m00]", "0")
             "NC3_%=:\n"
             "s_branch NL_%=\n"
-            NW_COLD("0", "NC0", "%[m00]", "%[m01]", "%[m02]")
-            NW_COLD("1", "NC1", "%[m00]", "%[m01]", "%[m02]")
-            NW_COLD("2", "NC2", "%[m00]", "%[m01]", "%[m02]")
-            NW_COLD("3", "NC3", "%[m00]", "%[m01]", "%[m02]")
+            NW_REFILL("0", "NL")
+            NW_REFILL("1", "NC0")
+            NW_REFILL("2", "NC1")
+            NW_REFILL("3", "NC2")
+            NW_COLD("0", "NC0", "%[m00]", "%[m01]", "%[m02]", "1")
+            NW_COLD("1", "NC1", "%[m00]", "%[m01]", "%[m02]", "2")
+            NW_COLD("2", "NC2", "%[m00]", "%[m01]", "%[m02]", "3")
+            NW_COLD("3", "NC3", "%[m00]", "%[m01]", "%[m02]", "0")
             "NX_%=:\n"
             "NE_%=:\n"
+            "s_add_u32 %[nb], %[nb], 32\n"
             "s_waitcnt lgkmcnt(0)\n"
             "s_mov_b64 %[win], vcc\n"
             "s_mov_b32 %[lane], m0\n"
@@ -804,34 +820,44 @@ __device__ __forceinline__ bool lossless_run_narrow(Entropy &w, SmemReader &rd, 
             "s_mov_b32 %[keep], m0\n"
             "s_mov_b32 m0, %[lane]\n"
             "s_mov_b64 vcc, %[win]\n"
-            "s_cmp_ge_u32 m0, %[lend]\n"
-            "s_cbranch_scc1 NE_%=\n"
+            "s_sub_u32 %[nb], %[nb], 32\n"
+            "s_cbranch_scc1 NR0_%=\n"
+            "s_branch NC7_%=\n"
             "NL_%=:\n"
-            NW_WORD("0", "%[m00]")
-            NW_WORD("1", "%[m10]")
+            NW_WORD("0", "%[m00]", "1")
+            NW_WORD("1", "%[m10]", "2")
             NW_CHECK("NC1")
-            NW_WORD("2", "%[m00]")
-            NW_WORD("3", "%[m10]")
+            NW_WORD("2", "%[m00]", "3")
+            NW_WORD("3", "%[m10]", "4")
             NW_CHECK("NC3")
-            NW_WORD("4", "%[m00]")
-            NW_WORD("5", "%[m10]")
+            NW_WORD("4", "%[m00]", "5")
+            NW_WORD("5", "%[m10]", "6")
             NW_CHECK("NC5")
-            NW_WORD("6", "%[m00]")
-            NW_WORD("7", "%[m10]")
+            NW_WORD("6", "%[m00]", "7")
+            NW_WORD("7", "%[m10]", "0")
             "NC7_%=:\n"
             "s_cmp_lt_u32 m0, %[lend]\n"
             "s_cbranch_scc1 NL_%=\n"
             "s_branch NE_%=\n"
-            NW_COLD("0", "NW1", "%[m00]", "%[m01]", "%[m02]")
-            NW_COLD("1", "NC1", "%[m10]", "%[m11]", "%[m12]")
-            NW_COLD("2", "NW3", "%[m00]", "%[m01]", "%[m02]")
-            NW_COLD("3", "NC3", "%[m10]", "%[m11]", "%[m12]")
-            NW_COLD("4", "NW5", "%[m00]", "%[m01]", "%[m02]")
-            NW_COLD("5", "NC5", "%[m10]", "%[m11]", "%[m12]")
-            NW_COLD("6", "NW7", "%[m00]", "%[m01]", "%[m02]")
-            NW_COLD("7", "NC7", "%[m10]", "%[m11]", "%[m12]")
+            NW_REFILL("0", "NC7")
+            NW_REFILL("1", "NA1")
+            NW_REFILL("2", "NC1")
+            NW_REFILL("3", "NA3")
+            NW_REFILL("4", "NC3")
+            NW_REFILL("5", "NA5")
+            NW_REFILL("6", "NC5")
+            NW_REFILL("7", "NA7")
+            NW_COLD("0", "NA1", "%[m00]", "%[m01]", "%[m02]", "1")
+            NW_COLD("1", "NC1", "%[m10]", "%[m11]", "%[m12]", "2")
+            NW_COLD("2", "NA3", "%[m00]", "%[m01]", "%[m02]", "3")
+            NW_COLD("3", "NC3", "%[m10]", "%[m11]", "%[m12]", "4")
+            NW_COLD("4", "NA5", "%[m00]", "%[m01]", "%[m02]", "5")
+            NW_COLD("5", "NC5", "%[m10]", "%[m11]", "%[m12]", "6")
+            NW_COLD("6", "NA7", "%[m00]", "%[m01]", "%[m02]", "7")
+            NW_COLD("7", "NC7", "%[m10]", "%[m11]", "%[m12]", "0")
             "NX_%=:\n"
             "NE_%=:\n"
+            "s_add_u32 %[nb], %[nb], 32\n"
             "s_waitcnt lgkmcnt(0)\n"
             "s_mov_b64 %[win], vcc\n"
             "s_mov_b32 %[lane], m0\n"
@@ -866,6 +892,7 @@ __device__ __forceinline__ bool lossless_run_narrow(Entropy &w, SmemReader &rd, 
 #undef NW_TAIL
 #undef NW_WORD
 #undef NW_COLD
+#undef NW_REFILL
 #undef NW_CHECK
 
 // The exp2 / log2 byte tables of the hybrid words (update_error_limit's exp2s,
@@ -1382,7 +1409,7 @@ __device__ __forceinline__ void recon_impl(const BlockDesc &d, const uint8_t *bl
                 produced = uni(lds_load_acq(&sh.produced));
                 break;
             }
-            __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_s_sleep(WV2_RECON_SLEEP);
             if (++spins > SPIN_LIMIT) {
                 perr = DEC_TIMEOUT;
                 break;
