@@ -32,7 +32,7 @@ constexpr uint32_t SPIN_LIMIT = 1u << 26;  // bounded waits: a bug ends the kern
 // the reconstruction wave's poll interval (s_sleep units of 64 cycles): its
 // polls issue scalar instructions on the SIMD the parser waves are bound on
 #ifndef WV2_RECON_SLEEP
-#define WV2_RECON_SLEEP 16
+#define WV2_RECON_SLEEP 64
 #endif
 
 // The reconstruction wave keeps the parser's payload ahead of it in the CU's
