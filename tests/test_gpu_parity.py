@@ -188,6 +188,14 @@ def test_c3_full_block_high24(gpu_batch_cls):
         np.testing.assert_array_equal(out[: x.size], x.reshape(-1))
 
 
+def test_c4_blocks_match_oracle(gpu_batch_cls):
+    """C4-shaped blocks (float32, hybrid + bitrate, default terms, 22,050 frames):
+    the parser's hybrid narrow run against the oracle."""
+    from synth import corpora
+    data = corpora.c4(nblocks=24)
+    _check_one(data, 4096, gpu_batch_cls, "c4x24")
+
+
 def test_golden_fixtures(gpu_batch_cls):
     """The committed fixtures (tests/golden) decode to the manifest's SHA-256, all in one batch."""
     import hashlib

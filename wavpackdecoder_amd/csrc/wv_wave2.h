@@ -595,13 +595,14 @@ __device__ __forceinline__ bool lossless_run(Entropy &w, SmemReader &rd, uint32_
 //     m -= 2*((m+126)>>7) >= m - (m+126)/64 per word, so after <= 64 words
 //     m + 126 >= (63/64)^64 * 382 > 139: neither zero-run test (:304) can
 //     become true inside the batch -> no zero-run check per word;
-//   * every median < 2^21 (stereo: <= 32 updates per channel) or < 2^19
+//   * every median < 2^24 (stereo: <= 32 updates per channel) or < 2^22
 //     (mono: <= 64) at batch start.  m += 5*((m+128)>>7) gives
-//     m + 128 <= (133/128)^n (m0 + 128): every median stays in [0, 2^23)
-//     (decrements never cross 0), so maxcode = m >> 4 < 2^19, n1 <= 18, and a
-//     word with <= 7 unary ones (c1 <= 8 bits) needs c1 + n1 + 2 <= 28 bits:
-//     it fits the >= 32 bits the window holds at word start, all in its low
-//     dword -> no negative-median test, no window bound test.  Words with
+//     m + 128 <= (133/128)^n (m0 + 128) (x3.4 for 32 updates, x11.7 for 64):
+//     every median stays in [0, 2^25.8) (decrements never cross 0), so
+//     maxcode = m >> 4 < 2^21.8, bitcount <= 22, n1 <= 21, and a word with
+//     <= 7 unary ones (c1 <= 8 bits) needs c1 + n1 + 2 <= 31 bits: it fits
+//     the >= 32 bits the window holds at word start, all in its low dword ->
+//     no negative-median test, no window bound test.  Words with
 //     8..15 unary ones (ones_count >= 4, out of line) test the bound; 16
 //     (the escape, :386) leaves the run.
 // The unary count and the holding_one/holding_zero pairing (:354-428) are
@@ -756,7 +757,7 @@ template <bool MONO>
 __device__ __forceinline__ bool narrow_ok(const Entropy &w, const SmemReader &rd) {
     const int32_t mx = max(w.med[0][0], w.med[1][0]);
     const uint32_t all = (uint32_t)(w.med[0][0] | w.med[0][1] | w.med[0][2] | w.med[1][0] | w.med[1][1] | w.med[1][2]);
-    return mx >= 256 && all < (MONO ? (1u << 19) : (1u << 21)) && rd.E >= 16u;
+    return mx >= 256 && all < (MONO ? (1u << 22) : (1u << 24)) && rd.E >= 16u;
 }
 
 // returns true when k reached kend, false when the word at k needs get_word
@@ -887,13 +888,6 @@ __device__ __forceinline__ bool lossless_run_narrow(Entropy &w, SmemReader &rd, 
     k = kbase + lane;
     return k >= kend;
 }
-#undef NW_DEC
-#undef NW_INC
-#undef NW_TAIL
-#undef NW_WORD
-#undef NW_COLD
-#undef NW_REFILL
-#undef NW_CHECK
 
 // The exp2 / log2 byte tables of the hybrid words (update_error_limit's exp2s,
 // the slow-level mylog2: WordsUtils.cs:195-261, 588-646) as one VGPR each,
@@ -911,6 +905,314 @@ struct VTabs {
     __device__ __forceinline__ int exp2(int i) const { return (int)e.byte((uint32_t)i); }
     __device__ __forceinline__ int log2(int i) const { return (int)l.byte((uint32_t)i); }
 };
+
+// ---------------------------------------------------------------------------
+// Narrow hybrid run (HYBRID_FLAG + HYBRID_BITRATE, no HYBRID_BALANCE, zero
+// bitrate deltas): the words of get_word for a batch whose entropy state
+// bounds every word, as lossless_run_narrow does for lossless blocks
+// (WordsUtils.cs:195-261 update_error_limit, :354-503 the word, :588-608
+// mylog2).  With bitrate_delta == 0 the bitrate accumulators never move, so
+// update_error_limit is a pure function of slow_level: errlim =
+// exp2s(((slow + 128) >> 8) - bitrate + 0x100), 0 when that is <= 0.  It runs
+// once per frame (the channel-0 word, or every mono word) before the word
+// touches any state, so a word whose errlim is 0 (read_code instead of the
+// bisection) can leave to get_word, which recomputes the same errlim.
+// Batch bounds (hybrid_ok): the lossless narrow bounds on the medians (no
+// zero-run, high - low <= maxcode < 2^21.8 for the whole batch, so the
+// bisection -- which at least halves high - low per bit -- takes <= 22 bits and
+// the word <= 8 + 22 + 1 bits of the window's low dword), slow_level < 0x1C0000
+// and bitrate in [-0x100, 0x1000] (exp2s's exponent <= 29: its shifts stay
+// inside 32 bits; slow_level cannot grow past that bound in 64 words since
+// mylog2 of a mid < 2^26 is < 0x1B00).
+// The exp2 / log2 byte tables come from VGPRs (v_readlane, VTabs).
+// ---------------------------------------------------------------------------
+// errlim of one channel: EL = x > 0 ? exp2s(x) : 0, x = slow_log - BR + 0x100
+#define HW_EL(SLOW, BR, EL)                                         \
+    "s_add_u32 %[x], " SLOW ", 128\n"                               \
+    "s_ashr_i32 %[x], %[x], 8\n"                                    \
+    "s_sub_i32 %[x], %[x], " BR "\n"                                \
+    "s_add_i32 %[x], %[x], 0x100\n"                                 \
+    "s_bfe_u32 %[b], %[x], 0x60002\n" /* dword (x & 0xff) >> 2 */   \
+    "v_readlane_b32 %[t0], %[etab], %[b]\n"                         \
+    "s_lshl_b32 %[b], %[x], 3\n" /* (x & 3) * 8 as a shift count */ \
+    "s_lshr_b32 %[t0], %[t0], %[b]\n"                               \
+    "s_and_b32 %[t0], %[t0], 0xff\n"                                \
+    "s_or_b32 %[t0], %[t0], 0x100\n"                                \
+    "s_lshr_b32 %[b], %[x], 8\n" /* exponent */                     \
+    "s_sub_u32 %[lo], 9, %[b]\n"                                    \
+    "s_lshr_b32 %[lo], %[t0], %[lo]\n"                              \
+    "s_sub_u32 %[hi], %[b], 9\n"                                    \
+    "s_lshl_b32 %[hi], %[t0], %[hi]\n"                              \
+    "s_cmp_le_u32 %[b], 9\n"                                        \
+    "s_cselect_b32 " EL ", %[lo], %[hi]\n"                          \
+    "s_cmp_gt_i32 %[x], 0\n"                                        \
+    "s_cselect_b32 " EL ", " EL ", 0\n"
+// bisection (:477-492, high - low > errlim), sign (:494-497), residual into
+// lane M0, slow_level += mylog2(mid) - ((slow + 128) >> 8) (:501-502), window
+// advance; the borrow of the advance is the next word's refill test
+#define HW_TAIL(I, S, SLOW, EL, J)                                  \
+    "s_lshr_b32 %[t], vcc_lo, %[c1]\n"                              \
+    "s_mov_b32 %[kb], %[k16]\n" /* bit index, s_bfe width 1 */      \
+    "s_add_u32 %[md], %[hi], %[lo]\n"                               \
+    "s_add_u32 %[md], %[md], 1\n"                                   \
+    "s_lshr_b32 %[md], %[md], 1\n"                                  \
+    "HB" I S "_%=:\n"                                               \
+    "s_sub_u32 %[x], %[hi], %[lo]\n"                                \
+    "s_cmp_le_i32 %[x], " EL "\n"                                   \
+    "s_cbranch_scc1 HD" I S "_%=\n"                                 \
+    "s_add_u32 %[x], %[md], -1\n"                                   \
+    "s_bitcmp1_b32 %[t], %[kb]\n"                                   \
+    "s_cselect_b32 %[lo], %[md], %[lo]\n"                           \
+    "s_cselect_b32 %[hi], %[hi], %[x]\n"                            \
+    "s_add_u32 %[kb], %[kb], 1\n"                                   \
+    "s_add_u32 %[md], %[hi], %[lo]\n"                               \
+    "s_add_u32 %[md], %[md], 1\n"                                   \
+    "s_lshr_b32 %[md], %[md], 1\n"                                  \
+    "s_branch HB" I S "_%=\n"                                       \
+    "HD" I S "_%=:\n"                                               \
+    "s_bfe_i32 %[x], %[t], %[kb]\n"                                 \
+    "s_xor_b32 %[b], %[md], %[x]\n"                                 \
+    "v_writelane_b32 %[resv], %[b], m0\n"                           \
+    "s_add_u32 m0, m0, 1\n"                                         \
+    "s_lshr_b32 %[x], %[md], 9\n"                                   \
+    "s_add_u32 %[x], %[md], %[x]\n" /* avalue */                    \
+    "s_flbit_i32_b32 %[lo], %[x]\n"                                 \
+    "s_min_u32 %[lo], %[lo], 32\n"                                  \
+    "s_lshl_b32 %[x], %[x], %[lo]\n" /* leading one at bit 31 */    \
+    "s_bfe_u32 %[hi], %[x], 0x60019\n" /* log2 index >> 2 */        \
+    "v_readlane_b32 %[b], %[ltab], %[hi]\n"                         \
+    "s_bfe_u32 %[hi], %[x], 0x20017\n"                              \
+    "s_lshl_b32 %[hi], %[hi], 3\n"                                  \
+    "s_lshr_b32 %[b], %[b], %[hi]\n"                                \
+    "s_and_b32 %[b], %[b], 0xff\n"                                  \
+    "s_sub_u32 %[lo], 32, %[lo]\n" /* dbits */                      \
+    "s_lshl_b32 %[lo], %[lo], 8\n"                                  \
+    "s_add_u32 %[b], %[b], %[lo]\n" /* mylog2(mid) */               \
+    "s_add_u32 %[x], " SLOW ", 128\n"                               \
+    "s_ashr_i32 %[x], %[x], 8\n"                                    \
+    "s_sub_u32 " SLOW ", " SLOW ", %[x]\n"                          \
+    "s_add_u32 " SLOW ", " SLOW ", %[b]\n"                          \
+    "s_add_u32 %[c1], %[c1], %[kb]\n" /* biases cancel */           \
+    "s_add_u32 %[c1], %[c1], 1\n"                                   \
+    "s_lshr_b64 vcc, vcc, %[c1]\n"                                  \
+    "s_sub_u32 %[nb], %[nb], %[c1]\n"                               \
+    "s_cbranch_scc1 HR" J "_%=\n"
+// hot part of hybrid word I: errlim update (UPD), errlim == 0 -> leave,
+// unary + holding flags (as NW_WORD), ones == 0 inline
+#define HW_WORD(I, MA, SLOW, EL, J, UPD)                            \
+    "HA" I "_%=:\n"                                                 \
+    UPD                                                             \
+    "s_cmp_eq_u32 " EL ", 0\n"                                      \
+    "s_cbranch_scc1 HX_%=\n"                                        \
+    "s_lshl_b64 vcc, vcc, %[h0]\n"                                  \
+    "s_add_u32 %[nb], %[nb], %[h0]\n"                               \
+    "s_orn2_b32 %[t0], %[k16], vcc_lo\n"                            \
+    "s_ff1_i32_b32 %[u], %[t0]\n"                                   \
+    "s_lshl1_add_u32 %[t0], %[h1], %[u]\n"                          \
+    "s_and_b32 %[h1], %[u], 1\n"                                    \
+    "s_add_u32 %[c1], %[u], %[kc1]\n"                               \
+    "s_xor_b32 %[b], %[h1], 1\n"                                    \
+    "s_sub_u32 %[h0], %[b], %[h0]\n"                                \
+    "s_lshr_b32 %[ones], %[t0], 1\n" /* SCC = ones != 0 */          \
+    "s_cbranch_scc1 HG" I "_%=\n"                                   \
+    "s_mov_b32 %[lo], 0\n"                                          \
+    "s_lshr_b32 %[hi], " MA ", 4\n"                                 \
+    NW_DEC(MA, "126", "6")                                          \
+    HW_TAIL(I, "a", SLOW, EL, J)
+#define HW_REFILL(J, DEST)                                          \
+    "HR" J "_%=:\n"                                                 \
+    "s_cmp_gt_u32 %[off], %[elim]\n"                                \
+    "s_cbranch_scc1 HX_%=\n"                                        \
+    "s_waitcnt lgkmcnt(0)\n"                                        \
+    "s_add_u32 %[nb], %[nb], 32\n"                                  \
+    "s_lshl_b64 %[tq], %[q], %[nb]\n"                               \
+    "s_or_b64 vcc, vcc, %[tq]\n"                                    \
+    "s_load_dwordx2 %[q], %[base], %[off]\n"                        \
+    "s_add_u32 %[off], %[off], 4\n"                                 \
+    "s_branch " DEST "_%=\n"
+// cold parts of hybrid word I (ones >= 1; >= 8 unary bits leave)
+#define HW_COLD(I, NEXT, MA, MB, MC, SLOW, EL, J)                   \
+    "HG" I "_%=:\n"                                                 \
+    "s_cmp_gt_u32 %[u], 7\n"                                        \
+    "s_cbranch_scc1 HK" I "_%=\n"                                   \
+    "s_lshr_b32 %[lo], " MA ", 4\n"                                 \
+    "s_add_u32 %[lo], %[lo], 1\n"                                   \
+    NW_INC(MA, "128", "7")                                          \
+    "s_cmp_eq_u32 %[ones], 1\n"                                     \
+    "s_cbranch_scc0 HH" I "_%=\n"                                   \
+    "s_lshr_b32 %[hi], " MB ", 4\n"                                 \
+    "s_add_u32 %[hi], %[hi], %[lo]\n"                               \
+    NW_DEC(MB, "62", "5")                                           \
+    HW_TAIL(I, "b", SLOW, EL, J)                                    \
+    "s_branch " NEXT "_%=\n"                                        \
+    "HH" I "_%=:\n" /* ones >= 2 */                                 \
+    "s_lshr_b32 %[t0], " MB ", 4\n"                                 \
+    "s_add_u32 %[lo], %[lo], %[t0]\n"                               \
+    "s_add_u32 %[lo], %[lo], 1\n"                                   \
+    NW_INC(MB, "64", "6")                                           \
+    "s_lshr_b32 %[hi], " MC ", 4\n"                                 \
+    "s_cmp_eq_u32 %[ones], 2\n"                                     \
+    "s_cbranch_scc0 HM" I "_%=\n"                                   \
+    "s_add_u32 %[hi], %[hi], %[lo]\n"                               \
+    NW_DEC(MC, "30", "4")                                           \
+    HW_TAIL(I, "c", SLOW, EL, J)                                    \
+    "s_branch " NEXT "_%=\n"                                        \
+    "HM" I "_%=:\n" /* ones >= 3: low += (ones-2) * A2 */           \
+    "s_add_u32 %[t0], %[hi], 1\n"                                   \
+    "s_sub_u32 %[b], %[ones], 2\n"                                  \
+    "s_mul_i32 %[t0], %[t0], %[b]\n"                                \
+    "s_add_u32 %[lo], %[lo], %[t0]\n"                               \
+    "s_add_u32 %[hi], %[hi], %[lo]\n"                               \
+    NW_INC(MC, "32", "5")                                           \
+    HW_TAIL(I, "d", SLOW, EL, J)                                    \
+    "s_branch " NEXT "_%=\n"                                        \
+    "HK" I "_%=:\n" /* leave before the word commits: restore h0/h1 */ \
+    "s_lshr_b32 %[t0], %[u], 1\n"                                   \
+    "s_sub_u32 %[h1], %[ones], %[t0]\n"                             \
+    "s_mov_b32 %[h0], 0\n"                                          \
+    "s_branch HX_%=\n"
+#define HW_CHECK(L)                                                 \
+    L "_%=:\n"                                                      \
+    "s_cmp_ge_u32 m0, %[lend]\n"                                    \
+    "s_cbranch_scc1 HE_%=\n"
+
+template <bool MONO>
+__device__ __forceinline__ bool hybrid_ok(const Entropy &w, const SmemReader &rd, uint32_t flags) {
+    using namespace wvf;
+    if ((flags & (HYBRID_FLAG | HYBRID_BITRATE)) != (HYBRID_FLAG | HYBRID_BITRATE)) return false;
+    if (!MONO && (flags & HYBRID_BALANCE)) return false;
+    if ((w.dlt[0] | w.dlt[1]) != 0) return false;
+    const int32_t mx = MONO ? w.med[0][0] : max(w.med[0][0], w.med[1][0]);
+    const uint32_t all = (uint32_t)(w.med[0][0] | w.med[0][1] | w.med[0][2] |
+                                    (MONO ? 0 : (w.med[1][0] | w.med[1][1] | w.med[1][2])));
+    const uint32_t sl = (uint32_t)(w.slow[0] | (MONO ? 0 : w.slow[1]));
+    const int32_t b0 = (int32_t)(w.acc[0] >> 16), b1 = MONO ? 0 : (int32_t)(w.acc[1] >> 16);
+    return mx >= 256 && all < (MONO ? (1u << 22) : (1u << 24)) && sl < 0x1C0000u && b0 >= -0x100 && b0 <= 0x1000 &&
+           b1 >= -0x100 && b1 <= 0x1000 && rd.E >= 16u;
+}
+
+// returns true when k reached kend, false when the word at k needs get_word
+template <bool MONO>
+__device__ __forceinline__ bool hybrid_run_narrow(Entropy &w, SmemReader &rd, uint32_t &k, uint32_t kend,
+                                                  int32_t &resv, const VTabs &tb) {
+    uint32_t t0, t, u, ones, c1, lo, hi, md, kb, x, b, keep;
+    uint64_t tq;
+    uint32_t nb = (uint32_t)rd.nb;
+    uint32_t off = 4u * (rd.rd + 1u);
+    uint64_t q = (uint64_t)rd.n0 | ((uint64_t)rd.n1 << 32);
+    const uint32_t elim = rd.E - 8u;
+    int32_t m00 = w.med[0][0], m01 = w.med[0][1], m02 = w.med[0][2];
+    int32_t m10 = w.med[1][0], m11 = w.med[1][1], m12 = w.med[1][2];
+    int32_t h0 = w.h0, h1 = w.h1;
+    int32_t s0 = w.slow[0], s1 = w.slow[1];
+    int32_t e0 = w.errlim[0], e1 = w.errlim[1];
+    const int32_t b0 = (int32_t)(w.acc[0] >> 16), b1 = (int32_t)(w.acc[1] >> 16);
+    const uint32_t kbase = k & ~63u;
+    uint32_t lane = k - kbase;
+    const uint32_t lend = kend - kbase;
+    uint64_t win = rd.win;
+    if (MONO) {
+        asm volatile(
+            "s_mov_b32 %[keep], m0\n"
+            "s_mov_b32 m0, %[lane]\n"
+            "s_mov_b64 vcc, %[win]\n"
+            "s_sub_u32 %[nb], %[nb], 32\n"
+            "s_cbranch_scc1 HR0_%=\n"
+            HW_CHECK("HL")
+            HW_WORD("0", "%[m00]", "%[s0]", "%[e0]", "1", HW_EL("%[s0]", "%[b0]", "%[e0]"))
+            HW_CHECK("HC0")
+            HW_WORD("1", "%[m00]", "%[s0]", "%[e0]", "0", HW_EL("%[s0]", "%[b0]", "%[e0]"))
+            "HC1_%=:\n"
+            "s_branch HL_%=\n"
+            HW_REFILL("0", "HL")
+            HW_REFILL("1", "HC0")
+            HW_COLD("0", "HC0", "%[m00]", "%[m01]", "%[m02]", "%[s0]", "%[e0]", "1")
+            HW_COLD("1", "HC1", "%[m00]", "%[m01]", "%[m02]", "%[s0]", "%[e0]", "0")
+            "HX_%=:\n"
+            "HE_%=:\n"
+            "s_add_u32 %[nb], %[nb], 32\n"
+            "s_waitcnt lgkmcnt(0)\n"
+            "s_mov_b64 %[win], vcc\n"
+            "s_mov_b32 %[lane], m0\n"
+            "s_mov_b32 m0, %[keep]\n"
+            : [t0] "=&s"(t0), [t] "=&s"(t), [u] "=&s"(u), [ones] "=&s"(ones), [c1] "=&s"(c1), [lo] "=&s"(lo),
+              [hi] "=&s"(hi), [md] "=&s"(md), [kb] "=&s"(kb), [x] "=&s"(x), [b] "=&s"(b), [keep] "=&s"(keep),
+              [tq] "=&s"(tq), [win] "+s"(win), [nb] "+s"(nb), [off] "+s"(off), [q] "+s"(q), [m00] "+s"(m00),
+              [m01] "+s"(m01), [m02] "+s"(m02), [h0] "+s"(h0), [h1] "+s"(h1), [s0] "+s"(s0), [e0] "+s"(e0),
+              [lane] "+s"(lane), [resv] "+v"(resv)
+            : [lend] "s"(lend), [elim] "s"(elim), [base] "s"(rd.base), [k16] "s"(0x10000u), [kc1] "s"(1u - 0x10000u),
+              [b0] "s"(b0), [etab] "v"(tb.e.v), [ltab] "v"(tb.l.v)
+            : "vcc", "scc");
+    } else {
+        asm volatile(
+            "s_mov_b32 %[keep], m0\n"
+            "s_mov_b32 m0, %[lane]\n"
+            "s_mov_b64 vcc, %[win]\n"
+            "s_sub_u32 %[nb], %[nb], 32\n"
+            "s_cbranch_scc1 HR0_%=\n"
+            "s_branch HC1_%=\n"
+            "HL_%=:\n"
+            HW_WORD("0", "%[m00]", "%[s0]", "%[e0]", "1",
+                    HW_EL("%[s0]", "%[b0]", "%[e0]") HW_EL("%[s1]", "%[b1]", "%[e1]"))
+            HW_WORD("1", "%[m10]", "%[s1]", "%[e1]", "0", "")
+            "HC1_%=:\n"
+            "s_cmp_lt_u32 m0, %[lend]\n"
+            "s_cbranch_scc1 HL_%=\n"
+            "s_branch HE_%=\n"
+            HW_REFILL("0", "HC1")
+            HW_REFILL("1", "HA1")
+            HW_COLD("0", "HA1", "%[m00]", "%[m01]", "%[m02]", "%[s0]", "%[e0]", "1")
+            HW_COLD("1", "HC1", "%[m10]", "%[m11]", "%[m12]", "%[s1]", "%[e1]", "0")
+            "HX_%=:\n"
+            "HE_%=:\n"
+            "s_add_u32 %[nb], %[nb], 32\n"
+            "s_waitcnt lgkmcnt(0)\n"
+            "s_mov_b64 %[win], vcc\n"
+            "s_mov_b32 %[lane], m0\n"
+            "s_mov_b32 m0, %[keep]\n"
+            : [t0] "=&s"(t0), [t] "=&s"(t), [u] "=&s"(u), [ones] "=&s"(ones), [c1] "=&s"(c1), [lo] "=&s"(lo),
+              [hi] "=&s"(hi), [md] "=&s"(md), [kb] "=&s"(kb), [x] "=&s"(x), [b] "=&s"(b), [keep] "=&s"(keep),
+              [tq] "=&s"(tq), [win] "+s"(win), [nb] "+s"(nb), [off] "+s"(off), [q] "+s"(q), [m00] "+s"(m00),
+              [m01] "+s"(m01), [m02] "+s"(m02), [m10] "+s"(m10), [m11] "+s"(m11), [m12] "+s"(m12), [h0] "+s"(h0),
+              [h1] "+s"(h1), [s0] "+s"(s0), [s1] "+s"(s1), [e0] "+s"(e0), [e1] "+s"(e1), [lane] "+s"(lane),
+              [resv] "+v"(resv)
+            : [lend] "s"(lend), [elim] "s"(elim), [base] "s"(rd.base), [k16] "s"(0x10000u), [kc1] "s"(1u - 0x10000u),
+              [b0] "s"(b0), [b1] "s"(b1), [etab] "v"(tb.e.v), [ltab] "v"(tb.l.v)
+            : "vcc", "scc");
+    }
+    rd.win = win;
+    rd.nb = (int)nb;
+    rd.rd = off / 4u - 1u;
+    rd.n0 = (uint32_t)q;
+    rd.n1 = (uint32_t)(q >> 32);
+    w.med[0][0] = m00;
+    w.med[0][1] = m01;
+    w.med[0][2] = m02;
+    w.med[1][0] = m10;
+    w.med[1][1] = m11;
+    w.med[1][2] = m12;
+    w.h0 = h0;
+    w.h1 = h1;
+    w.slow[0] = s0;
+    w.slow[1] = s1;
+    w.errlim[0] = e0;
+    w.errlim[1] = e1;
+    k = kbase + lane;
+    return k >= kend;
+}
+#undef HW_EL
+#undef HW_TAIL
+#undef HW_WORD
+#undef HW_REFILL
+#undef HW_COLD
+#undef HW_CHECK
+#undef NW_DEC
+#undef NW_INC
+#undef NW_TAIL
+#undef NW_WORD
+#undef NW_COLD
+#undef NW_REFILL
+#undef NW_CHECK
 
 // one residual: the fast path for lossless blocks, the zero-run countdown,
 // else the general get_word (wv_decode_core.h)
@@ -966,6 +1268,11 @@ __device__ __forceinline__ void parse_loop(const BlockDesc &d, Reader &rd, Entro
                     break;
                 }
             }
+#ifndef WV2_NO_HYBRID_NARROW
+            if (!LOSSLESS && (MONO || (k & 1) == 0) && hybrid_ok<MONO>(w, rd, flags)) {
+                if (hybrid_run_narrow<MONO>(w, rd, k, kend, resv, tb)) break;
+            }
+#endif
 
             // the word at k (and, in stereo, its pair) through the general path
             int32_t v = 0;
