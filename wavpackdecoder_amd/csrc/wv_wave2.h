@@ -917,13 +917,17 @@ struct VTabs {
 // once per frame (the channel-0 word, or every mono word) before the word
 // touches any state, so a word whose errlim is 0 (read_code instead of the
 // bisection) can leave to get_word, which recomputes the same errlim.
-// Batch bounds (hybrid_ok): the lossless narrow bounds on the medians (no
-// zero-run, high - low <= maxcode < 2^21.8 for the whole batch, so the
-// bisection -- which at least halves high - low per bit -- takes <= 22 bits and
-// the word <= 8 + 22 + 1 bits of the window's low dword), slow_level < 0x1C0000
-// and bitrate in [-0x100, 0x1000] (exp2s's exponent <= 29: its shifts stay
-// inside 32 bits; slow_level cannot grow past that bound in 64 words since
-// mylog2 of a mid < 2^26 is < 0x1B00).
+// The unary part is shifted out of the window first, and the window is
+// refilled right there when fewer than 32 bits remain, so the bisection and
+// the sign always read from a full low dword.
+// Batch bounds (hybrid_ok): no zero-run can start (a median[0] >= 256); every
+// median < 2^28 (mono 2^26), so for the whole batch high - low < 2^25.8 (the
+// bisection at least halves it per bit: <= 26 bits + sign <= 32) and mid <
+// 2^28.1; slow_level < 0x1E0000 and bitrate in [0, 0x1000]: mylog2 of such a
+// mid is < 0x1E00, so slow_level's log stays <= 0x1E00 and exp2s's argument
+// < 0x2000 (exponent <= 31: its shift stays inside 32 bits, errlim >= 0);
+// >= 320 payload bytes left (64 words of <= 36 bits), so no refill of the
+// batch reads past the payload.
 // The exp2 / log2 byte tables come from VGPRs (v_readlane, VTabs).
 // ---------------------------------------------------------------------------
 // errlim of one channel: EL = x > 0 ? exp2s(x) : 0, x = slow_log - BR + 0x100
@@ -947,11 +951,11 @@ struct VTabs {
     "s_cselect_b32 " EL ", %[lo], %[hi]\n"                          \
     "s_cmp_gt_i32 %[x], 0\n"                                        \
     "s_cselect_b32 " EL ", " EL ", 0\n"
-// bisection (:477-492, high - low > errlim), sign (:494-497), residual into
-// lane M0, slow_level += mylog2(mid) - ((slow + 128) >> 8) (:501-502), window
-// advance; the borrow of the advance is the next word's refill test
+// bisection (:477-492, high - low > errlim) on the window's low dword, sign
+// (:494-497), residual into lane M0, slow_level += mylog2(mid) - ((slow +
+// 128) >> 8) (:501-502), window advance; the advance's borrow is the next
+// word's refill test
 #define HW_TAIL(I, S, SLOW, EL, J)                                  \
-    "s_lshr_b32 %[t], vcc_lo, %[c1]\n"                              \
     "s_mov_b32 %[kb], %[k16]\n" /* bit index, s_bfe width 1 */      \
     "s_add_u32 %[md], %[hi], %[lo]\n"                               \
     "s_add_u32 %[md], %[md], 1\n"                                   \
@@ -961,7 +965,7 @@ struct VTabs {
     "s_cmp_le_i32 %[x], " EL "\n"                                   \
     "s_cbranch_scc1 HD" I S "_%=\n"                                 \
     "s_add_u32 %[x], %[md], -1\n"                                   \
-    "s_bitcmp1_b32 %[t], %[kb]\n"                                   \
+    "s_bitcmp1_b32 vcc_lo, %[kb]\n"                                 \
     "s_cselect_b32 %[lo], %[md], %[lo]\n"                           \
     "s_cselect_b32 %[hi], %[hi], %[x]\n"                            \
     "s_add_u32 %[kb], %[kb], 1\n"                                   \
@@ -970,7 +974,7 @@ struct VTabs {
     "s_lshr_b32 %[md], %[md], 1\n"                                  \
     "s_branch HB" I S "_%=\n"                                       \
     "HD" I S "_%=:\n"                                               \
-    "s_bfe_i32 %[x], %[t], %[kb]\n"                                 \
+    "s_bfe_i32 %[x], vcc_lo, %[kb]\n"                               \
     "s_xor_b32 %[b], %[md], %[x]\n"                                 \
     "v_writelane_b32 %[resv], %[b], m0\n"                           \
     "s_add_u32 m0, m0, 1\n"                                         \
@@ -992,37 +996,43 @@ struct VTabs {
     "s_ashr_i32 %[x], %[x], 8\n"                                    \
     "s_sub_u32 " SLOW ", " SLOW ", %[x]\n"                          \
     "s_add_u32 " SLOW ", " SLOW ", %[b]\n"                          \
-    "s_add_u32 %[c1], %[c1], %[kb]\n" /* biases cancel */           \
-    "s_add_u32 %[c1], %[c1], 1\n"                                   \
+    "s_add_u32 %[c1], %[kb], %[kc1]\n" /* bisection bits + sign */  \
     "s_lshr_b64 vcc, vcc, %[c1]\n"                                  \
     "s_sub_u32 %[nb], %[nb], %[c1]\n"                               \
     "s_cbranch_scc1 HR" J "_%=\n"
-// hot part of hybrid word I: errlim update (UPD), errlim == 0 -> leave,
-// unary + holding flags (as NW_WORD), ones == 0 inline
+// hot part of hybrid word I: errlim update (UPD), errlim == 0 or >= 8 unary
+// bits -> leave, unary + holding flags (as NW_WORD), the unary bits out of the
+// window (HQ: refill below 32), ones == 0 inline
 #define HW_WORD(I, MA, SLOW, EL, J, UPD)                            \
     "HA" I "_%=:\n"                                                 \
     UPD                                                             \
     "s_cmp_eq_u32 " EL ", 0\n"                                      \
     "s_cbranch_scc1 HX_%=\n"                                        \
+    "s_lshl_b32 %[t0], vcc_lo, %[h0]\n"                             \
+    "s_orn2_b32 %[t0], %[k16], %[t0]\n"                             \
+    "s_ff1_i32_b32 %[u], %[t0]\n"                                   \
+    "s_cmp_gt_u32 %[u], 7\n"                                        \
+    "s_cbranch_scc1 HX_%=\n"                                        \
     "s_lshl_b64 vcc, vcc, %[h0]\n"                                  \
     "s_add_u32 %[nb], %[nb], %[h0]\n"                               \
-    "s_orn2_b32 %[t0], %[k16], vcc_lo\n"                            \
-    "s_ff1_i32_b32 %[u], %[t0]\n"                                   \
     "s_lshl1_add_u32 %[t0], %[h1], %[u]\n"                          \
     "s_and_b32 %[h1], %[u], 1\n"                                    \
-    "s_add_u32 %[c1], %[u], %[kc1]\n"                               \
     "s_xor_b32 %[b], %[h1], 1\n"                                    \
     "s_sub_u32 %[h0], %[b], %[h0]\n"                                \
+    "s_add_u32 %[c1], %[u], 1\n"                                    \
+    "s_lshr_b64 vcc, vcc, %[c1]\n"                                  \
+    "s_sub_u32 %[nb], %[nb], %[c1]\n"                               \
+    "s_cbranch_scc1 HQ" I "_%=\n"                                   \
+    "HU" I "_%=:\n"                                                 \
     "s_lshr_b32 %[ones], %[t0], 1\n" /* SCC = ones != 0 */          \
     "s_cbranch_scc1 HG" I "_%=\n"                                   \
     "s_mov_b32 %[lo], 0\n"                                          \
     "s_lshr_b32 %[hi], " MA ", 4\n"                                 \
     NW_DEC(MA, "126", "6")                                          \
     HW_TAIL(I, "a", SLOW, EL, J)
-#define HW_REFILL(J, DEST)                                          \
-    "HR" J "_%=:\n"                                                 \
-    "s_cmp_gt_u32 %[off], %[elim]\n"                                \
-    "s_cbranch_scc1 HX_%=\n"                                        \
+// refill 32 bits (no payload-end test: hybrid_ok keeps the batch clear of it)
+#define HW_REFILL(L, DEST)                                          \
+    L "_%=:\n"                                                      \
     "s_waitcnt lgkmcnt(0)\n"                                        \
     "s_add_u32 %[nb], %[nb], 32\n"                                  \
     "s_lshl_b64 %[tq], %[q], %[nb]\n"                               \
@@ -1030,11 +1040,10 @@ struct VTabs {
     "s_load_dwordx2 %[q], %[base], %[off]\n"                        \
     "s_add_u32 %[off], %[off], 4\n"                                 \
     "s_branch " DEST "_%=\n"
-// cold parts of hybrid word I (ones >= 1; >= 8 unary bits leave)
+// cold parts of hybrid word I (ones >= 1)
 #define HW_COLD(I, NEXT, MA, MB, MC, SLOW, EL, J)                   \
+    HW_REFILL("HQ" I, "HU" I)                                       \
     "HG" I "_%=:\n"                                                 \
-    "s_cmp_gt_u32 %[u], 7\n"                                        \
-    "s_cbranch_scc1 HK" I "_%=\n"                                   \
     "s_lshr_b32 %[lo], " MA ", 4\n"                                 \
     "s_add_u32 %[lo], %[lo], 1\n"                                   \
     NW_INC(MA, "128", "7")                                          \
@@ -1065,12 +1074,7 @@ struct VTabs {
     "s_add_u32 %[hi], %[hi], %[lo]\n"                               \
     NW_INC(MC, "32", "5")                                           \
     HW_TAIL(I, "d", SLOW, EL, J)                                    \
-    "s_branch " NEXT "_%=\n"                                        \
-    "HK" I "_%=:\n" /* leave before the word commits: restore h0/h1 */ \
-    "s_lshr_b32 %[t0], %[u], 1\n"                                   \
-    "s_sub_u32 %[h1], %[ones], %[t0]\n"                             \
-    "s_mov_b32 %[h0], 0\n"                                          \
-    "s_branch HX_%=\n"
+    "s_branch " NEXT "_%=\n"
 #define HW_CHECK(L)                                                 \
     L "_%=:\n"                                                      \
     "s_cmp_ge_u32 m0, %[lend]\n"                                    \
@@ -1085,22 +1089,21 @@ __device__ __forceinline__ bool hybrid_ok(const Entropy &w, const SmemReader &rd
     const int32_t mx = MONO ? w.med[0][0] : max(w.med[0][0], w.med[1][0]);
     const uint32_t all = (uint32_t)(w.med[0][0] | w.med[0][1] | w.med[0][2] |
                                     (MONO ? 0 : (w.med[1][0] | w.med[1][1] | w.med[1][2])));
-    const uint32_t sl = (uint32_t)(w.slow[0] | (MONO ? 0 : w.slow[1]));
-    const int32_t b0 = (int32_t)(w.acc[0] >> 16), b1 = MONO ? 0 : (int32_t)(w.acc[1] >> 16);
-    return mx >= 256 && all < (MONO ? (1u << 22) : (1u << 24)) && sl < 0x1C0000u && b0 >= -0x100 && b0 <= 0x1000 &&
-           b1 >= -0x100 && b1 <= 0x1000 && rd.E >= 16u;
+    const uint32_t sl = MONO ? (uint32_t)w.slow[0] : max((uint32_t)w.slow[0], (uint32_t)w.slow[1]);
+    const uint32_t b0 = (uint32_t)(int32_t)(w.acc[0] >> 16), b1 = MONO ? 0u : (uint32_t)(int32_t)(w.acc[1] >> 16);
+    return mx >= 256 && all < (MONO ? (1u << 26) : (1u << 28)) && sl < 0x1E0000u && b0 <= 0x1000u &&
+           b1 <= 0x1000u && rd.E >= 4u * rd.rd + 320u;
 }
 
 // returns true when k reached kend, false when the word at k needs get_word
 template <bool MONO>
 __device__ __forceinline__ bool hybrid_run_narrow(Entropy &w, SmemReader &rd, uint32_t &k, uint32_t kend,
                                                   int32_t &resv, const VTabs &tb) {
-    uint32_t t0, t, u, ones, c1, lo, hi, md, kb, x, b, keep;
+    uint32_t t0, u, ones, c1, lo, hi, md, kb, x, b, keep;
     uint64_t tq;
     uint32_t nb = (uint32_t)rd.nb;
     uint32_t off = 4u * (rd.rd + 1u);
     uint64_t q = (uint64_t)rd.n0 | ((uint64_t)rd.n1 << 32);
-    const uint32_t elim = rd.E - 8u;
     int32_t m00 = w.med[0][0], m01 = w.med[0][1], m02 = w.med[0][2];
     int32_t m10 = w.med[1][0], m11 = w.med[1][1], m12 = w.med[1][2];
     int32_t h0 = w.h0, h1 = w.h1;
@@ -1124,8 +1127,8 @@ __device__ __forceinline__ bool hybrid_run_narrow(Entropy &w, SmemReader &rd, ui
             HW_WORD("1", "%[m00]", "%[s0]", "%[e0]", "0", HW_EL("%[s0]", "%[b0]", "%[e0]"))
             "HC1_%=:\n"
             "s_branch HL_%=\n"
-            HW_REFILL("0", "HL")
-            HW_REFILL("1", "HC0")
+            HW_REFILL("HR0", "HL")
+            HW_REFILL("HR1", "HC0")
             HW_COLD("0", "HC0", "%[m00]", "%[m01]", "%[m02]", "%[s0]", "%[e0]", "1")
             HW_COLD("1", "HC1", "%[m00]", "%[m01]", "%[m02]", "%[s0]", "%[e0]", "0")
             "HX_%=:\n"
@@ -1135,13 +1138,13 @@ __device__ __forceinline__ bool hybrid_run_narrow(Entropy &w, SmemReader &rd, ui
             "s_mov_b64 %[win], vcc\n"
             "s_mov_b32 %[lane], m0\n"
             "s_mov_b32 m0, %[keep]\n"
-            : [t0] "=&s"(t0), [t] "=&s"(t), [u] "=&s"(u), [ones] "=&s"(ones), [c1] "=&s"(c1), [lo] "=&s"(lo),
-              [hi] "=&s"(hi), [md] "=&s"(md), [kb] "=&s"(kb), [x] "=&s"(x), [b] "=&s"(b), [keep] "=&s"(keep),
-              [tq] "=&s"(tq), [win] "+s"(win), [nb] "+s"(nb), [off] "+s"(off), [q] "+s"(q), [m00] "+s"(m00),
-              [m01] "+s"(m01), [m02] "+s"(m02), [h0] "+s"(h0), [h1] "+s"(h1), [s0] "+s"(s0), [e0] "+s"(e0),
-              [lane] "+s"(lane), [resv] "+v"(resv)
-            : [lend] "s"(lend), [elim] "s"(elim), [base] "s"(rd.base), [k16] "s"(0x10000u), [kc1] "s"(1u - 0x10000u),
-              [b0] "s"(b0), [etab] "v"(tb.e.v), [ltab] "v"(tb.l.v)
+            : [t0] "=&s"(t0), [u] "=&s"(u), [ones] "=&s"(ones), [c1] "=&s"(c1), [lo] "=&s"(lo), [hi] "=&s"(hi),
+              [md] "=&s"(md), [kb] "=&s"(kb), [x] "=&s"(x), [b] "=&s"(b), [keep] "=&s"(keep), [tq] "=&s"(tq),
+              [win] "+s"(win), [nb] "+s"(nb), [off] "+s"(off), [q] "+s"(q), [m00] "+s"(m00), [m01] "+s"(m01),
+              [m02] "+s"(m02), [h0] "+s"(h0), [h1] "+s"(h1), [s0] "+s"(s0), [e0] "+s"(e0), [lane] "+s"(lane),
+              [resv] "+v"(resv)
+            : [lend] "s"(lend), [base] "s"(rd.base), [k16] "s"(0x10000u), [kc1] "s"(1u - 0x10000u), [b0] "s"(b0),
+              [etab] "v"(tb.e.v), [ltab] "v"(tb.l.v)
             : "vcc", "scc");
     } else {
         asm volatile(
@@ -1159,8 +1162,8 @@ __device__ __forceinline__ bool hybrid_run_narrow(Entropy &w, SmemReader &rd, ui
             "s_cmp_lt_u32 m0, %[lend]\n"
             "s_cbranch_scc1 HL_%=\n"
             "s_branch HE_%=\n"
-            HW_REFILL("0", "HC1")
-            HW_REFILL("1", "HA1")
+            HW_REFILL("HR0", "HC1")
+            HW_REFILL("HR1", "HA1")
             HW_COLD("0", "HA1", "%[m00]", "%[m01]", "%[m02]", "%[s0]", "%[e0]", "1")
             HW_COLD("1", "HC1", "%[m10]", "%[m11]", "%[m12]", "%[s1]", "%[e1]", "0")
             "HX_%=:\n"
@@ -1170,14 +1173,13 @@ __device__ __forceinline__ bool hybrid_run_narrow(Entropy &w, SmemReader &rd, ui
             "s_mov_b64 %[win], vcc\n"
             "s_mov_b32 %[lane], m0\n"
             "s_mov_b32 m0, %[keep]\n"
-            : [t0] "=&s"(t0), [t] "=&s"(t), [u] "=&s"(u), [ones] "=&s"(ones), [c1] "=&s"(c1), [lo] "=&s"(lo),
-              [hi] "=&s"(hi), [md] "=&s"(md), [kb] "=&s"(kb), [x] "=&s"(x), [b] "=&s"(b), [keep] "=&s"(keep),
-              [tq] "=&s"(tq), [win] "+s"(win), [nb] "+s"(nb), [off] "+s"(off), [q] "+s"(q), [m00] "+s"(m00),
-              [m01] "+s"(m01), [m02] "+s"(m02), [m10] "+s"(m10), [m11] "+s"(m11), [m12] "+s"(m12), [h0] "+s"(h0),
-              [h1] "+s"(h1), [s0] "+s"(s0), [s1] "+s"(s1), [e0] "+s"(e0), [e1] "+s"(e1), [lane] "+s"(lane),
-              [resv] "+v"(resv)
-            : [lend] "s"(lend), [elim] "s"(elim), [base] "s"(rd.base), [k16] "s"(0x10000u), [kc1] "s"(1u - 0x10000u),
-              [b0] "s"(b0), [b1] "s"(b1), [etab] "v"(tb.e.v), [ltab] "v"(tb.l.v)
+            : [t0] "=&s"(t0), [u] "=&s"(u), [ones] "=&s"(ones), [c1] "=&s"(c1), [lo] "=&s"(lo), [hi] "=&s"(hi),
+              [md] "=&s"(md), [kb] "=&s"(kb), [x] "=&s"(x), [b] "=&s"(b), [keep] "=&s"(keep), [tq] "=&s"(tq),
+              [win] "+s"(win), [nb] "+s"(nb), [off] "+s"(off), [q] "+s"(q), [m00] "+s"(m00), [m01] "+s"(m01),
+              [m02] "+s"(m02), [m10] "+s"(m10), [m11] "+s"(m11), [m12] "+s"(m12), [h0] "+s"(h0), [h1] "+s"(h1),
+              [s0] "+s"(s0), [s1] "+s"(s1), [e0] "+s"(e0), [e1] "+s"(e1), [lane] "+s"(lane), [resv] "+v"(resv)
+            : [lend] "s"(lend), [base] "s"(rd.base), [k16] "s"(0x10000u), [kc1] "s"(1u - 0x10000u), [b0] "s"(b0),
+              [b1] "s"(b1), [etab] "v"(tb.e.v), [ltab] "v"(tb.l.v)
             : "vcc", "scc");
     }
     rd.win = win;
