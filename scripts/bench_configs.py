@@ -54,6 +54,30 @@ def run(name, files, pcm=None, iters=5, fmt=False):
             "compressed_bytes": b.bytes_in, "kernel_ms": round(ms, 3),
             "Mframes_per_s": round(b.frames / ms / 1e3, 1), "crc_errors": int(crc),
             "lossless_roundtrip": ok, "host_framing_s": round(t_frame, 3)}
+    if INFLIGHT > 1:
+        # the same batch as INFLIGHT copies on their own streams, decodes issued
+        # round-robin (bench.py's --inflight): throughput with launches overlapping
+        copies = [b]
+        for _ in range(INFLIGHT - 1):
+            c = DecodeBatch(4096)
+            c.add_files(files)
+            c.upload()
+            copies.append(c)
+        steps = 4 * INFLIGHT
+        for c in copies:
+            c.decode()
+        for c in copies:
+            c.sync()
+        t = time.perf_counter()
+        for k in range(steps):
+            copies[k % INFLIGHT].decode()
+        for c in copies:
+            c.sync()
+        dt = time.perf_counter() - t
+        line["inflight"] = INFLIGHT
+        line["Mframes_per_s_inflight"] = round(b.frames * steps / dt / 1e6, 1)
+        for c in copies[1:]:
+            c.close()
     if fmt_ms is not None:
         line["format_epilogue_ms_wall"] = round(fmt_ms, 3)
     if CPU_THREADS:
@@ -64,6 +88,7 @@ def run(name, files, pcm=None, iters=5, fmt=False):
 
 
 CPU_THREADS = 0
+INFLIGHT = 1
 
 
 def cpu_rate(files):
@@ -92,9 +117,11 @@ def main():
     ap.add_argument("--c3-copies", type=int, default=4)
     ap.add_argument("--c5-files", type=int, default=4000)
     ap.add_argument("--cpu-threads", type=int, default=0, help="also time the oracle on this many host threads")
+    ap.add_argument("--inflight", type=int, default=1, help="also time this many copies of each batch in flight")
     a = ap.parse_args()
-    global CPU_THREADS
+    global CPU_THREADS, INFLIGHT
     CPU_THREADS = a.cpu_threads
+    INFLIGHT = a.inflight
     from wavpackdecoder_amd import _lib
     import wavpackdecoder_amd.api as api
     api._ctx = _lib.lib().wvg_open(0)

@@ -591,10 +591,12 @@ __device__ __forceinline__ bool lossless_run(Entropy &w, SmemReader &rd, uint32_
 // Narrow lossless run: the words of lossless_run for a batch whose entropy
 // state bounds every word, so that the per-word tests of lossless_run leave
 // the hot path (WordsUtils.cs:304-503 otherwise unchanged):
-//   * max(med[0][0], med[1][0]) >= 256 at batch start.  median[0] falls by
-//     m -= 2*((m+126)>>7) >= m - (m+126)/64 per word, so after <= 64 words
-//     m + 126 >= (63/64)^64 * 382 > 139: neither zero-run test (:304) can
-//     become true inside the batch -> no zero-run check per word;
+//   * max(med[0][0], med[1][0]) >= 66 (stereo: <= 32 updates of each
+//     channel's median) or med[0][0] >= 132 (mono: <= 64) at batch start.
+//     median[0] falls by m -= 2*((m+126)>>7) per update (2 while m < 130), and
+//     from those starts it is still >= 2 after the batch's updates (checked
+//     exhaustively): the zero-run test (:304) cannot become true inside the
+//     batch -> no zero-run check per word;
 //   * every median < 2^24 (stereo: <= 32 updates per channel) or < 2^22
 //     (mono: <= 64) at batch start.  m += 5*((m+128)>>7) gives
 //     m + 128 <= (133/128)^n (m0 + 128) (x3.4 for 32 updates, x11.7 for 64):
@@ -757,7 +759,7 @@ template <bool MONO>
 __device__ __forceinline__ bool narrow_ok(const Entropy &w, const SmemReader &rd) {
     const int32_t mx = max(w.med[0][0], w.med[1][0]);
     const uint32_t all = (uint32_t)(w.med[0][0] | w.med[0][1] | w.med[0][2] | w.med[1][0] | w.med[1][1] | w.med[1][2]);
-    return mx >= 256 && all < (MONO ? (1u << 22) : (1u << 24)) && rd.E >= 16u;
+    return mx >= (MONO ? 132 : 66) && all < (MONO ? (1u << 22) : (1u << 24)) && rd.E >= 16u;
 }
 
 // returns true when k reached kend, false when the word at k needs get_word
@@ -920,7 +922,7 @@ struct VTabs {
 // The unary part is shifted out of the window first, and the window is
 // refilled right there when fewer than 32 bits remain, so the bisection and
 // the sign always read from a full low dword.
-// Batch bounds (hybrid_ok): no zero-run can start (a median[0] >= 256); every
+// Batch bounds (hybrid_ok): no zero-run can start (median[0] as in narrow_ok); every
 // median < 2^28 (mono 2^26), so for the whole batch high - low < 2^25.8 (the
 // bisection at least halves it per bit: <= 26 bits + sign <= 32) and mid <
 // 2^28.1; slow_level < 0x1E0000 and bitrate in [0, 0x1000]: mylog2 of such a
@@ -941,14 +943,11 @@ struct VTabs {
     "s_lshl_b32 %[b], %[x], 3\n" /* (x & 3) * 8 as a shift count */ \
     "s_lshr_b32 %[t0], %[t0], %[b]\n"                               \
     "s_and_b32 %[t0], %[t0], 0xff\n"                                \
-    "s_or_b32 %[t0], %[t0], 0x100\n"                                \
-    "s_lshr_b32 %[b], %[x], 8\n" /* exponent */                     \
-    "s_sub_u32 %[lo], 9, %[b]\n"                                    \
-    "s_lshr_b32 %[lo], %[t0], %[lo]\n"                              \
-    "s_sub_u32 %[hi], %[b], 9\n"                                    \
-    "s_lshl_b32 %[hi], %[t0], %[hi]\n"                              \
-    "s_cmp_le_u32 %[b], 9\n"                                        \
-    "s_cselect_b32 " EL ", %[lo], %[hi]\n"                          \
+    "s_lshl_b32 %[t0], %[t0], 22\n"                                 \
+    "s_or_b32 %[t0], %[t0], %[k30]\n" /* (table | 0x100) << 22 */   \
+    "s_lshr_b32 %[b], %[x], 8\n" /* exponent e <= 31 */             \
+    "s_sub_u32 %[b], 31, %[b]\n"                                    \
+    "s_lshr_b32 " EL ", %[t0], %[b]\n" /* e<=9: >> (9-e), else << (e-9) */ \
     "s_cmp_gt_i32 %[x], 0\n"                                        \
     "s_cselect_b32 " EL ", " EL ", 0\n"
 // bisection (:477-492, high - low > errlim) on the window's low dword, sign
@@ -1091,7 +1090,7 @@ __device__ __forceinline__ bool hybrid_ok(const Entropy &w, const SmemReader &rd
                                     (MONO ? 0 : (w.med[1][0] | w.med[1][1] | w.med[1][2])));
     const uint32_t sl = MONO ? (uint32_t)w.slow[0] : max((uint32_t)w.slow[0], (uint32_t)w.slow[1]);
     const uint32_t b0 = (uint32_t)(int32_t)(w.acc[0] >> 16), b1 = MONO ? 0u : (uint32_t)(int32_t)(w.acc[1] >> 16);
-    return mx >= 256 && all < (MONO ? (1u << 26) : (1u << 28)) && sl < 0x1E0000u && b0 <= 0x1000u &&
+    return mx >= (MONO ? 132 : 66) && all < (MONO ? (1u << 26) : (1u << 28)) && sl < 0x1E0000u && b0 <= 0x1000u &&
            b1 <= 0x1000u && rd.E >= 4u * rd.rd + 320u;
 }
 
@@ -1144,7 +1143,7 @@ __device__ __forceinline__ bool hybrid_run_narrow(Entropy &w, SmemReader &rd, ui
               [m02] "+s"(m02), [h0] "+s"(h0), [h1] "+s"(h1), [s0] "+s"(s0), [e0] "+s"(e0), [lane] "+s"(lane),
               [resv] "+v"(resv)
             : [lend] "s"(lend), [base] "s"(rd.base), [k16] "s"(0x10000u), [kc1] "s"(1u - 0x10000u), [b0] "s"(b0),
-              [etab] "v"(tb.e.v), [ltab] "v"(tb.l.v)
+              [k30] "s"(1u << 30), [etab] "v"(tb.e.v), [ltab] "v"(tb.l.v)
             : "vcc", "scc");
     } else {
         asm volatile(
@@ -1179,7 +1178,7 @@ __device__ __forceinline__ bool hybrid_run_narrow(Entropy &w, SmemReader &rd, ui
               [m02] "+s"(m02), [m10] "+s"(m10), [m11] "+s"(m11), [m12] "+s"(m12), [h0] "+s"(h0), [h1] "+s"(h1),
               [s0] "+s"(s0), [s1] "+s"(s1), [e0] "+s"(e0), [e1] "+s"(e1), [lane] "+s"(lane), [resv] "+v"(resv)
             : [lend] "s"(lend), [base] "s"(rd.base), [k16] "s"(0x10000u), [kc1] "s"(1u - 0x10000u), [b0] "s"(b0),
-              [b1] "s"(b1), [etab] "v"(tb.e.v), [ltab] "v"(tb.l.v)
+              [b1] "s"(b1), [k30] "s"(1u << 30), [etab] "v"(tb.e.v), [ltab] "v"(tb.l.v)
             : "vcc", "scc");
     }
     rd.win = win;
@@ -1259,6 +1258,24 @@ __device__ __forceinline__ void parse_loop(const BlockDesc &d, Reader &rd, Entro
                 const uint32_t n = (uint32_t)min((int64_t)(kend - k), w.zeros_acc - 1);
                 const uint32_t lo = k & 63u;
                 resv = ((uint32_t)lane - lo < n) ? 0 : resv;
+                w.zeros_acc -= n;
+                k += n;
+                continue;
+            }
+            // the same stretch in a hybrid block: each zero word also decays its
+            // channel's slow_level (WordsUtils.cs:309-313; no update_error_limit)
+            if (!LOSSLESS && __builtin_expect(w.zeros_acc > 1, 0) &&
+                (uint32_t)(w.med[0][0] | w.med[1][0]) <= 1u && (w.h0 | w.h1) == 0 && (w.slow[0] | w.slow[1]) >= 0) {
+                const uint32_t n = (uint32_t)min((int64_t)(kend - k), w.zeros_acc - 1);
+                const uint32_t lo = k & 63u;
+                resv = ((uint32_t)lane - lo < n) ? 0 : resv;
+                // words of channel 0 among k .. k+n-1 (stereo alternates, k even = channel 0)
+                uint32_t n0 = MONO ? n : (n + 1u - (k & 1u)) / 2u, n1 = MONO ? 0u : n - n0;
+                int32_t s0 = w.slow[0], s1 = w.slow[1];
+                for (; n0 && s0 >= 128; n0--) s0 -= (s0 + 128) >> 8;  // below 128 it is a fixed point
+                for (; n1 && s1 >= 128; n1--) s1 -= (s1 + 128) >> 8;
+                w.slow[0] = s0;
+                w.slow[1] = s1;
                 w.zeros_acc -= n;
                 k += n;
                 continue;
