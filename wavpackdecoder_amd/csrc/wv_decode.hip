@@ -237,6 +237,117 @@ __device__ __forceinline__ DsdResult dsd_high_wave(const BlockDesc &d, const uin
     return res;
 }
 
+// Stereo mode 3 with the two channels' filter chains on the VALU: lane 0
+// holds channel 0's filter state (filter1..6, factor, value, the output byte)
+// and lane 1 channel 1's, so one instruction updates both channels (the chains
+// are independent; only the range coder is shared).  The range coder and the
+// adaptive ptable stay scalar.  Per bit: both channels' ptable entries are
+// read from LDS at once (channel 1's is forwarded from channel 0's update when
+// they share an entry), the two binary decisions run back to back on the
+// scalar unit, then one VALU pass updates both filters (DsdUtils.cs:401-489).
+// Same results and status bits as dsd_high_wave<2>.
+__device__ __forceinline__ DsdResult dsd_high_vwave(const BlockDesc &d, const uint8_t *blob, const uint8_t *tables,
+                                                    int32_t *ptable, DevStoreWave &out) {
+    using namespace wvf;
+    const uint32_t dlen = d.dsd_data_len;
+    const int ch = threadIdx.x & 1;
+    ByteSrcWave src;
+    src.init(blob + d.bits_off);
+    uint32_t bp = 0;
+    int32_t crc = -1;
+    DsdResult res = {0, 0};
+    bool mute = false;
+    uint32_t low = 0, high = 0xFFFFFFFFu, value = 0;
+    for (int i = 0; i < 4; i++) value = (value << 8) | src.byte(bp++);
+    {
+        const int32_t *pt0 = (const int32_t *)(tables + d.dsd_table_off);
+        for (uint32_t i = threadIdx.x; i < 256; i += 64) ptable[i] = pt0[i];
+        __syncthreads();
+    }
+    // per-lane (VGPR) filter state: lane & 1 = channel
+    int32_t q2 = d.dsd_filters[ch][0], q3 = d.dsd_filters[ch][1], q4 = d.dsd_filters[ch][2];
+    int32_t q5 = d.dsd_filters[ch][3], q6 = d.dsd_filters[ch][4], q8 = d.dsd_filters[ch][5];
+    int32_t q7 = 0, bytei = 0, q0;
+    uint32_t f = 0, chunk_len = d.first_chunk, ci = 0;
+    while (f < d.nframes) {
+        uint32_t n = chunk_len;
+        if (n > d.nframes - f) n = d.nframes - f;
+        if (!mute) {
+            for (uint32_t j = 0; j < n; j++) {
+                q0 = add32(sub32(q2, q6), mul32(q7, q8) >> 2);
+                for (int bit = 0; bit < 8; bit++) {
+                    const uint32_t pp0 = ((uint32_t)__builtin_amdgcn_readlane(q0, 0) >> 8) & 255u;
+                    const uint32_t pp1 = ((uint32_t)__builtin_amdgcn_readlane(q0, 1) >> 8) & 255u;
+                    const int32_t p0 = __builtin_amdgcn_readfirstlane(ptable[pp0]);
+                    int32_t pv1 = __builtin_amdgcn_readfirstlane(ptable[pp1]);
+                    // channel 0's decision
+                    uint32_t split = low + ((high - low) >> 8) * ((uint32_t)p0 >> 16);
+                    const bool z0 = value <= split;
+                    high = z0 ? split : high;
+                    low = z0 ? low : split + 1;
+                    const int32_t np0 = p0 + (((z0 ? 0x010000FE : 0x00010000) - p0) >> 8);
+                    ptable[pp0] = np0;
+                    pv1 = pp1 == pp0 ? np0 : pv1;
+                    if (__builtin_expect((high ^ low) < 0x1000000u, 0)) {  // renormalise (rare)
+                        while ((high ^ low) < 0x1000000u && bp < dlen) {
+                            value = (value << 8) | src.byte(bp++);
+                            high = (high << 8) | 0xFF;
+                            low <<= 8;
+                        }
+                    }
+                    // channel 1's decision
+                    split = low + ((high - low) >> 8) * ((uint32_t)pv1 >> 16);
+                    const bool z1 = value <= split;
+                    high = z1 ? split : high;
+                    low = z1 ? low : split + 1;
+                    ptable[pp1] = pv1 + (((z1 ? 0x010000FE : 0x00010000) - pv1) >> 8);
+                    if (__builtin_expect((high ^ low) < 0x1000000u, 0)) {  // renormalise (rare)
+                        while ((high ^ low) < 0x1000000u && bp < dlen) {
+                            value = (value << 8) | src.byte(bp++);
+                            high = (high << 8) | 0xFF;
+                            low <<= 8;
+                        }
+                    }
+                    // both channels' filters, one lane each
+                    const int32_t q1 = (ch ? z1 : z0) ? -1 : 0;
+                    q0 = add32(q0, mul32(q7, 8));
+                    bytei = shl32(bytei, 1) | (q1 & 1);
+                    q8 = add32(q8, (((q0 ^ q1) >> 31) | 1) & ((q0 ^ sub32(q0, mul32(q7, 16))) >> 31));
+                    q2 = add32(q2, sub32(q1 & (1 << 20), q2) >> 6);
+                    q3 = add32(q3, sub32(q1 & (1 << 20), q3) >> 4);
+                    q4 = add32(q4, sub32(q3, q4) >> 4);
+                    q5 = add32(q5, sub32(q4, q5) >> 4);
+                    q0 = sub32(q5, q6) >> 4;
+                    q6 = add32(q6, q0);
+                    q7 = add32(q7, sub32(q0, q7) >> 3);
+                    q0 = add32(sub32(q2, q6), mul32(q7, q8) >> 2);
+                }
+                const int32_t v0 = __builtin_amdgcn_readlane(bytei, 0) & 0xFF;
+                const int32_t v1 = __builtin_amdgcn_readlane(bytei, 1) & 0xFF;
+                q8 = sub32(q8, add32(q8, 512) >> 10);
+                crc = add32(crc, add32(shl32(crc, 1), v0));
+                crc = add32(crc, add32(shl32(crc, 1), v1));
+                const uint64_t o = (uint64_t)(f + j) * 2u;
+                out.put(o, v0);
+                out.put(o + 1, v1);
+            }
+            if (f + n == d.block_samples && crc != d.crc) mute = true;
+        }
+        if (mute && !(res.status & ST_DSD_MUTE)) {
+            res.status |= ST_DSD_MUTE;
+            res.mute_chunk = ci;
+        }
+        f += n;
+        chunk_len = next_call_len(d, f);
+        ci++;
+    }
+    if (d.nframes == d.block_samples) {
+        res.status |= ST_CRC_CHECKED;
+        if (crc != d.crc) res.status |= ST_CRC_ERROR;
+    }
+    return res;
+}
+
 // DsdUtils mode 1's tables (prob u8, summed u16, lookup u8, value_lookup i32;
 // 16-B aligned by the framing) read through the scalar cache: a data-dependent
 // table read costs a scalar-cache hit, not a vector load's memory latency
@@ -374,7 +485,11 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_wave(const BlockD
     DsdResult r;
     if (d.kind == KIND_DSD_HIGH)
         r = (d.flags & wvf::MONO_DATA) ? dsd_high_wave<1>(d, blob, tables, pt_lds, st)
+#ifdef WV_DSD_HIGH_SCALAR
                                        : dsd_high_wave<2>(d, blob, tables, pt_lds, st);
+#else
+                                       : dsd_high_vwave(d, blob, tables, pt_lds, st);
+#endif
     else if (d.kind == KIND_DSD_FAST)
         r = (d.flags & wvf::MONO_DATA) ? dsd_simple_wave<1, true>(d, blob, tables, st)
                                        : dsd_simple_wave<2, true>(d, blob, tables, st);
