@@ -245,6 +245,7 @@ __device__ __forceinline__ DsdResult dsd_high_wave(const BlockDesc &d, const uin
 // read from LDS at once (channel 1's is forwarded from channel 0's update when
 // they share an entry), the two binary decisions run back to back on the
 // scalar unit, then one VALU pass updates both filters (DsdUtils.cs:401-489).
+// Both entries come from one per-lane LDS read addressed by the filter lanes.
 // Same results and status bits as dsd_high_wave<2>.
 __device__ __forceinline__ DsdResult dsd_high_vwave(const BlockDesc &d, const uint8_t *blob, const uint8_t *tables,
                                                     int32_t *ptable, DevStoreWave &out) {
@@ -276,10 +277,13 @@ __device__ __forceinline__ DsdResult dsd_high_vwave(const BlockDesc &d, const ui
             for (uint32_t j = 0; j < n; j++) {
                 q0 = add32(sub32(q2, q6), mul32(q7, q8) >> 2);
                 for (int bit = 0; bit < 8; bit++) {
-                    const uint32_t pp0 = ((uint32_t)__builtin_amdgcn_readlane(q0, 0) >> 8) & 255u;
-                    const uint32_t pp1 = ((uint32_t)__builtin_amdgcn_readlane(q0, 1) >> 8) & 255u;
-                    const int32_t p0 = __builtin_amdgcn_readfirstlane(ptable[pp0]);
-                    int32_t pv1 = __builtin_amdgcn_readfirstlane(ptable[pp1]);
+                    // each lane reads its channel's ptable entry (one LDS read for both)
+                    const uint32_t ppv = ((uint32_t)q0 >> 8) & 255u;
+                    const int32_t pvv = ptable[ppv];
+                    const uint32_t pp0 = (uint32_t)__builtin_amdgcn_readlane((int32_t)ppv, 0);
+                    const uint32_t pp1 = (uint32_t)__builtin_amdgcn_readlane((int32_t)ppv, 1);
+                    const int32_t p0 = __builtin_amdgcn_readlane(pvv, 0);
+                    int32_t pv1 = __builtin_amdgcn_readlane(pvv, 1);
                     // channel 0's decision
                     uint32_t split = low + ((high - low) >> 8) * ((uint32_t)p0 >> 16);
                     const bool z0 = value <= split;
