@@ -16,8 +16,9 @@
 
 namespace wvg {
 hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint32_t n_pcm, const uint32_t *dsd_list,
-                         uint32_t n_dsd, const uint8_t *blob, const uint8_t *tables, int32_t *out, uint32_t *status,
-                         uint32_t *aux, hipStream_t s_pcm, hipStream_t s_dsd);
+                         uint32_t n_dsd, uint32_t fast_lo, uint32_t n_fast, const uint8_t *blob, const uint8_t *tables,
+                         int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s_pcm, hipStream_t s_dsd,
+                         hipStream_t s_fast);
 int term_set_of(const BlockDesc &d, int prefer_pipe);
 hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, uint32_t n, const uint8_t *blob,
                         int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s);
@@ -35,7 +36,7 @@ using namespace wvg;
 // onto the batch's side streams and join back, so small groups run concurrently.
 // Every batch owns its streams, so batches of one context (or of several host
 // threads) run concurrently on the device; nothing synchronises the whole device.
-constexpr int kSide = kMaxTermSets + 2;
+constexpr int kSide = kMaxTermSets + 3;  // term sets, generic PCM, DSD, DSD mode 1
 
 struct wvg_ctx {
     int device = 0;
@@ -109,6 +110,7 @@ struct wvg_batch {
     std::vector<wvg_file_info> infos;
     int64_t out_ints = 0;
     std::vector<uint32_t> pcm_list, dsd_list;           // wave-per-block kernels (generic PCM, DSD)
+    uint32_t dsd_fast_lo = 0, dsd_fast_n = 0;          // the mode-1 range of dsd_list (sorted by kind)
     std::vector<uint32_t> ts_list[kMaxTermSets];        // two-wave kernels per term set
     uint32_t *d_ts[kMaxTermSets] = {nullptr};
     int force_lane = 0;                                 // WVG_FORCE_LANE=1: every PCM block on the generic kernel
@@ -488,6 +490,13 @@ int wvg_batch_upload(wvg_batch *b) {
     };
     std::sort(b->pcm_list.begin(), b->pcm_list.end(), by_kind_len);
     std::sort(b->dsd_list.begin(), b->dsd_list.end(), by_kind_len);
+    // the mode-1 blocks are one range of the kind-sorted list (their own kernel)
+    b->dsd_fast_lo = b->dsd_fast_n = 0;
+    for (size_t k = 0; k < b->dsd_list.size(); k++) {
+        if (b->fo.descs[b->dsd_list[k]].kind != KIND_DSD_FAST) continue;
+        if (!b->dsd_fast_n) b->dsd_fast_lo = (uint32_t)k;
+        b->dsd_fast_n++;
+    }
     const size_t np = b->pcm_list.size(), ns = b->dsd_list.size();
     HIPCHK(c, ensure(b->d_pcml, b->cap_pcml, sizeof(uint32_t) * (np ? np : 1)));
     HIPCHK(c, ensure(b->d_dsd, b->cap_dsd, sizeof(uint32_t) * (ns ? ns : 1)));
@@ -525,6 +534,7 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
         if (!b->ts_list[t].empty()) used[n++] = t;
     if (!b->pcm_list.empty()) used[n++] = kMaxTermSets;
     if (!b->dsd_list.empty()) used[n++] = kMaxTermSets + 1;
+    if (b->dsd_fast_n) used[n++] = kMaxTermSets + 2;
     auto slot = [&](int g) -> hipStream_t { return n > 1 ? b->side[g] : s; };
     for (int i = 0; n > 1 && i < n; i++) {
         const int g = used[i];
@@ -542,8 +552,8 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
             HIPCHK(c, launch_2wave(t, b->d_descs, b->d_ts[t], (uint32_t)b->ts_list[t].size(), b->d_blob, b->d_out,
                                    b->d_status, b->d_mute, slot(t)));
     HIPCHK(c, launch_decode(b->d_descs, b->d_pcml, (uint32_t)b->pcm_list.size(), b->d_dsd, (uint32_t)b->dsd_list.size(),
-                            b->d_blob, b->d_tables, b->d_out, b->d_status, b->d_mute, slot(kMaxTermSets),
-                            slot(kMaxTermSets + 1)));
+                            b->dsd_fast_lo, b->dsd_fast_n, b->d_blob, b->d_tables, b->d_out, b->d_status, b->d_mute,
+                            slot(kMaxTermSets), slot(kMaxTermSets + 1), slot(kMaxTermSets + 2)));
     if (n > 1) {
         for (int i = 0; i < n; i++) {
             HIPCHK(c, hipEventRecord(b->join[used[i]], b->side[used[i]]));

@@ -15,7 +15,9 @@
 //                         fixup -> int32 store) fused, sample-major.  Also one
 //                         wave per chain of blocks that inherit decode state.
 //   wv_decode_dsd_wave  : one wave-uniform decode per DSD block (DsdUtils modes
-//                         0/1/3, each a scalar specialisation).
+//                         0 and 3; stereo mode 3 with both channels' filters on
+//                         the VALU).
+//   wv_decode_dsd_fast  : mode 1, one wave per block with its tables in LDS.
 //   wv_dsd_fill         : post-pass writing the 0x55 mute fills of DSD blocks in
 //                         call-buffer coordinates (DsdUtils.cs:104-117, quirk B-9).
 //   wv_meta_parse       : one lane per block finishing its descriptor with the
@@ -371,17 +373,39 @@ struct DsdTablesWave {
 // DsdUtils modes 0 (raw bytes) and 1 (init_dsd_block_fast + decode_fast,
 // DsdUtils.cs:149-304), wave-uniform, channel count a template parameter.
 // Same results and status bits as decode_dsd_block (wv_decode_core.h).
-template <int WCH, bool FAST>
+// the same tables staged in LDS by the mode-1 kernel (wv_decode_dsd_fast):
+// a data-dependent read then costs an LDS round trip instead of a scalar-cache
+// miss (up to 32 bins x 2,052 B exceed the scalar cache)
+struct DsdTablesLds {
+    const uint8_t *t;  // LDS
+    int bins;
+    __device__ __forceinline__ uint32_t prob(uint32_t i) const { return __builtin_amdgcn_readfirstlane(t[i]); }
+    __device__ __forceinline__ uint32_t summed(uint32_t i) const {
+        return __builtin_amdgcn_readfirstlane(((const uint16_t *)(t + (uint32_t)bins * 256u))[i]);
+    }
+    __device__ __forceinline__ uint32_t lookup(uint32_t i) const {
+        return __builtin_amdgcn_readfirstlane(t[(uint32_t)bins * 768u + i]);
+    }
+    __device__ __forceinline__ int32_t vlook(uint32_t i) const {
+        return __builtin_amdgcn_readfirstlane(((const int32_t *)(t + (uint32_t)bins * 2048u))[i]);
+    }
+};
+
+template <int WCH, bool FAST, class TT = DsdTablesWave>
 __device__ __forceinline__ DsdResult dsd_simple_wave(const BlockDesc &d, const uint8_t *blob, const uint8_t *tables,
-                                                     DevStoreWave &out) {
+                                                     DevStoreWave &out, const uint8_t *lds_tables = nullptr) {
     using namespace wvf;
     const bool fstereo = (d.flags & FALSE_STEREO) != 0;
     const uint32_t och = (d.flags & MONO_FLAG) ? 1u : 2u;
     const uint32_t dlen = d.dsd_data_len;
     ByteSrcWave src;
     src.init(blob + d.bits_off);
-    DsdTablesWave tb;
-    tb.t = (w2::cdw_ptr)(tables + d.dsd_table_off);
+    TT tb;
+    if constexpr (__is_same(TT, DsdTablesLds)) {
+        tb.t = lds_tables;
+    } else {
+        tb.t = (w2::cdw_ptr)(tables + d.dsd_table_off);
+    }
     tb.bins = d.dsd_history_bins;
     const uint32_t bmask = (uint32_t)d.dsd_history_bins - 1u;
     uint32_t bp = 0;
@@ -480,10 +504,12 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_wave(const BlockD
                                                                     const uint8_t *__restrict__ tables,
                                                                     int32_t *__restrict__ out,
                                                                     uint32_t *__restrict__ status,
-                                                                    uint32_t *__restrict__ mute_chunk) {
+                                                                    uint32_t *__restrict__ mute_chunk,
+                                                                    uint32_t skip_fast) {
     __shared__ int32_t pt_lds[256];  // mode 3's adaptive ptable, one per block
     const uint32_t bi = list[blockIdx.x];
     const BlockDesc &d = descs[bi];
+    if (skip_fast && d.kind == KIND_DSD_FAST) return;  // wv_decode_dsd_fast's
     const bool lead = threadIdx.x == 0;
     DevStoreWave st{out + d.out_off, (uint64_t)d.pre_end * d.out_nch, lead};
     DsdResult r;
@@ -508,17 +534,53 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_wave(const BlockD
     }
 }
 
+// DsdUtils mode 1 (decode_fast, DsdUtils.cs:149-304), one wave per block with
+// the block's prob / summed / lookup / value_lookup tables copied to LDS first
+// (at most 32 history bins: 65,664 B).  Launched over the mode-1 part of the
+// DSD list (the list is sorted by kind); wv_decode_dsd_wave skips those blocks.
+constexpr uint32_t kDsdFastLds = 32u * 2052u;
+extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_fast(const BlockDesc *__restrict__ descs,
+                                                                    const uint32_t *__restrict__ list,
+                                                                    const uint8_t *__restrict__ blob,
+                                                                    const uint8_t *__restrict__ tables,
+                                                                    int32_t *__restrict__ out,
+                                                                    uint32_t *__restrict__ status,
+                                                                    uint32_t *__restrict__ mute_chunk) {
+    __shared__ uint32_t tab[kDsdFastLds / 4];
+    const uint32_t bi = list[blockIdx.x];
+    const BlockDesc &d = descs[bi];
+    const bool lead = threadIdx.x == 0;
+    const uint32_t bins = (uint32_t)d.dsd_history_bins;
+    const uint32_t nw = bins <= 32u ? (bins * 2052u + 3u) / 4u : 0u;
+    const uint32_t *src = (const uint32_t *)(tables + d.dsd_table_off);  // 16-B aligned by the framing
+    for (uint32_t i = threadIdx.x; i < nw; i += 64) tab[i] = src[i];
+    __syncthreads();
+    DevStoreWave st{out + d.out_off, (uint64_t)d.pre_end * d.out_nch, lead};
+    DsdResult r;
+    if (bins > 32u)  // not produced by the framing (init_dsd_block_fast rejects > 5 history bits)
+        r = decode_dsd_block(d, blob, tables, nullptr, st);
+    else
+        r = (d.flags & wvf::MONO_DATA)
+                ? dsd_simple_wave<1, true, DsdTablesLds>(d, blob, tables, st, (const uint8_t *)tab)
+                : dsd_simple_wave<2, true, DsdTablesLds>(d, blob, tables, st, (const uint8_t *)tab);
+    if (lead) {
+        status[bi] = d.fstatus | r.status;
+        mute_chunk[bi] = r.mute_chunk;
+    }
+}
+
 // one thread per DSD block; fills only for blocks that muted
 extern "C" __global__ void __launch_bounds__(64) wv_dsd_fill(const BlockDesc *__restrict__ descs,
                                                              const uint32_t *__restrict__ list, uint32_t n,
                                                              const uint32_t *__restrict__ status,
                                                              const uint32_t *__restrict__ mute_chunk,
-                                                             int32_t *__restrict__ out) {
+                                                             int32_t *__restrict__ out, uint32_t skip_fast) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint32_t bi = list[i];
-    if (!(status[bi] & ST_DSD_MUTE)) return;
     const BlockDesc &d = descs[bi];
+    if (skip_fast && d.kind == KIND_DSD_FAST) return;  // filled on the mode-1 stream
+    if (!(status[bi] & ST_DSD_MUTE)) return;
     uint32_t f = 0, cl = d.first_chunk, mc = mute_chunk[bi];
     for (uint32_t ci = 0; f < d.nframes; ci++) {
         uint32_t len = cl < d.nframes - f ? cl : d.nframes - f;
@@ -672,16 +734,28 @@ namespace wvg {
 
 // PCM blocks without a two-wave instantiation (generic wave kernel) on s_pcm;
 // DSD blocks (decode, then the mute fills that depend on it) on s_dsd
+// DSD blocks: the mode-1 range [fast_lo, fast_lo + n_fast) of the kind-sorted
+// list by wv_decode_dsd_fast on its own stream (then its mute fills), every
+// other DSD block by one wv_decode_dsd_wave launch (then their fills)
 hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint32_t n_pcm, const uint32_t *dsd_list,
-                         uint32_t n_dsd, const uint8_t *blob, const uint8_t *tables, int32_t *out, uint32_t *status,
-                         uint32_t *aux, hipStream_t s_pcm, hipStream_t s_dsd) {
+                         uint32_t n_dsd, uint32_t fast_lo, uint32_t n_fast, const uint8_t *blob, const uint8_t *tables,
+                         int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s_pcm, hipStream_t s_dsd,
+                         hipStream_t s_fast) {
     if (n_pcm)
         hipLaunchKernelGGL(wv_decode_pcm_wave, dim3(n_pcm), dim3(64), 0, s_pcm, descs, pcm_list, blob, out, status, aux);
-    if (n_dsd) {
+    const uint32_t skip = n_fast ? 1u : 0u;
+    if (n_dsd > n_fast) {
         hipLaunchKernelGGL(wv_decode_dsd_wave, dim3(n_dsd), dim3(64), 0, s_dsd, descs, dsd_list, blob, tables, out,
-                           status, aux);
+                           status, aux, skip);
         hipLaunchKernelGGL(wv_dsd_fill, dim3((n_dsd + 63) / 64), dim3(64), 0, s_dsd, descs, dsd_list, n_dsd, status,
-                           aux, out);
+                           aux, out, skip);
+    }
+    if (n_fast) {
+        const uint32_t *fl = dsd_list + fast_lo;
+        hipLaunchKernelGGL(wv_decode_dsd_fast, dim3(n_fast), dim3(64), 0, s_fast, descs, fl, blob, tables, out, status,
+                           aux);
+        hipLaunchKernelGGL(wv_dsd_fill, dim3((n_fast + 63) / 64), dim3(64), 0, s_fast, descs, fl, n_fast, status, aux,
+                           out, 0u);
     }
     return hipGetLastError();
 }
