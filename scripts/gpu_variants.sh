@@ -4,7 +4,7 @@
 cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && mkdir -p gpurun_out/var
 LIBS=${LIBS:-"build/libwvgpu.so"}
 if [ -z "$NO_TESTS" ]; then
-  timeout -k 10 600 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/var/pytest.log 2>&1; rc=$?
+  timeout -k 10 600 python -u -m pytest tests/ -m gpu -x -q --timeout 100 --timeout-method thread > gpurun_out/var/pytest.log 2>&1; rc=$?
   echo "pytest rc=$rc"; tail -2 gpurun_out/var/pytest.log
   [ $rc -ne 0 ] && exit $rc
 fi

@@ -331,7 +331,7 @@ __device__ __forceinline__ void recon_pipe(const BlockDesc &d, PipeShared &ps, i
                 break;
             }
             __builtin_amdgcn_s_sleep(WV2_RECON_SLEEP);
-            if (++spins > SPIN_LIMIT) {
+            if (++spins > RECON_SPIN_LIMIT) {
                 perr = DEC_TIMEOUT;
                 break;
             }

@@ -34,6 +34,9 @@ constexpr uint32_t SPIN_LIMIT = 1u << 26;  // bounded waits: a bug ends the kern
 #ifndef WV2_RECON_SLEEP
 #define WV2_RECON_SLEEP 64
 #endif
+// the reconstruction wave's wait bound in polls: about the same wall time
+// (~4 s) as SPIN_LIMIT polls of s_sleep 2
+constexpr uint32_t RECON_SPIN_LIMIT = SPIN_LIMIT / (WV2_RECON_SLEEP > 2 ? WV2_RECON_SLEEP / 2 : 1);
 
 // The reconstruction wave keeps the parser's payload ahead of it in the CU's
 // scalar cache: a scalar load per 64-byte line up to PF_AHEAD bytes past the
@@ -1207,6 +1210,246 @@ __device__ __forceinline__ bool hybrid_run_narrow(Entropy &w, SmemReader &rd, ui
 #undef HW_REFILL
 #undef HW_COLD
 #undef HW_CHECK
+
+// ---------------------------------------------------------------------------
+// Full narrow batch (a whole 64-word batch from lane 0, narrow_ok): the
+// narrow loop with the residual's value finished on the VALU.  The in-flight
+// bench is bound by the SIMD's scalar issue while its VALU issue
+// is half idle, and a word's sign, extra-bit value and `low` are off the serial
+// chain (only the consumed bit count and the medians feed the next word): the
+// scalar side keeps the extra-bit decision, the VALU builds
+// ((v or 2v - ex + bit) + low) ^ sign and merges it into the residual VGPR
+// with a lane mask (v_cndmask) that moves one lane per word.  With the batch
+// starting at lane 0 and 64 words long, the unrolled loop's end test is the
+// lane mask running out (once per 8 stereo / 4 mono words), so no M0 counter.
+// Each VALU instruction reads at most one SGPR (gfx9 constant bus).
+// ---------------------------------------------------------------------------
+#define FW_TAIL(I, S, LOWOP, J)                                     \
+    "s_or_b32 %[t0], %[mc], 1\n"                                    \
+    "s_flbit_i32_b32 %[z], %[t0]\n"                                 \
+    "s_lshr_b32 %[t], vcc_lo, %[c1]\n"                              \
+    "s_lshr_b32 %[ex], -1, %[z]\n"                                  \
+    "s_sub_u32 %[ex], %[ex], %[mc]\n"                               \
+    "s_lshr_b32 %[t0], %[k7f], %[z]\n"                              \
+    "s_and_b32 %[v], %[t], %[t0]\n"                                 \
+    "s_sub_u32 %[n1], %[kn], %[z]\n"                                \
+    "v_mov_b32 %[vt], %[t]\n"                                       \
+    "s_cmp_lt_u32 %[v], %[ex]\n"                                    \
+    "s_cbranch_scc1 FS" I S "_%=\n"                                 \
+    "v_lshlrev_b32_e64 %[r], 1, %[v]\n"                             \
+    "v_subrev_u32 %[r], %[ex], %[r]\n"                              \
+    "v_bfe_u32 %[rb], %[vt], %[n1], 1\n"                            \
+    "v_add_u32 %[r], %[r], %[rb]\n"                                 \
+    "s_add_u32 %[n1], %[n1], 1\n"                                   \
+    "s_branch FT" I S "_%=\n"                                       \
+    "FS" I S "_%=:\n"                                               \
+    "v_mov_b32 %[r], %[v]\n"                                        \
+    "FT" I S "_%=:\n"                                               \
+    LOWOP                                                           \
+    "v_bfe_i32 %[rb], %[vt], %[n1], 1\n"                            \
+    "v_xor_b32 %[r], %[r], %[rb]\n"                                 \
+    "v_cndmask_b32_e64 %[resv], %[resv], %[r], %[lm]\n"             \
+    "s_lshl_b64 %[lm], %[lm], 1\n"                                  \
+    "s_add_u32 %[n1], %[n1], %[c1]\n"                               \
+    "s_add_u32 %[n1], %[n1], 1\n"                                   \
+    "s_lshr_b64 vcc, vcc, %[n1]\n"                                  \
+    "s_sub_u32 %[nb], %[nb], %[n1]\n" /* SCC: fewer than 32 left */ \
+    "s_cbranch_scc1 FR" J "_%=\n"
+#define FW_WORD(I, MA, J)                                           \
+    "FA" I "_%=:\n"                                                 \
+    "s_lshl_b64 vcc, vcc, %[h0]\n"                                  \
+    "s_add_u32 %[nb], %[nb], %[h0]\n"                               \
+    "s_orn2_b32 %[t0], %[k16], vcc_lo\n"                            \
+    "s_ff1_i32_b32 %[u], %[t0]\n"                                   \
+    "s_lshl1_add_u32 %[t0], %[h1], %[u]\n"                          \
+    "s_and_b32 %[h1], %[u], 1\n"                                    \
+    "s_add_u32 %[c1], %[u], %[kc1]\n"                               \
+    "s_xor_b32 %[ex], %[h1], 1\n"                                   \
+    "s_sub_u32 %[h0], %[ex], %[h0]\n"                               \
+    "s_lshr_b32 %[ones], %[t0], 1\n" /* SCC = ones != 0 */          \
+    "s_cbranch_scc1 FG" I "_%=\n"                                   \
+    "s_lshr_b32 %[mc], " MA ", 4\n"                                 \
+    NW_DEC(MA, "126", "6")                                          \
+    FW_TAIL(I, "a", "", J)
+#define FW_REFILL(J, DEST)                                          \
+    "FR" J "_%=:\n"                                                 \
+    "s_cmp_gt_u32 %[off], %[elim]\n"                                \
+    "s_cbranch_scc1 FX_%=\n"                                        \
+    "s_waitcnt lgkmcnt(0)\n"                                        \
+    "s_add_u32 %[nb], %[nb], 32\n"                                  \
+    "s_lshl_b64 %[tq], %[q], %[nb]\n"                               \
+    "s_or_b64 vcc, vcc, %[tq]\n"                                    \
+    "s_load_dwordx2 %[q], %[base], %[off]\n"                        \
+    "s_add_u32 %[off], %[off], 4\n"                                 \
+    "s_branch " DEST "_%=\n"
+#define FW_COLD(I, NEXT, MA, MB, MC, J)                             \
+    "FG" I "_%=:\n" /* ones == 1 */                                 \
+    "s_cmp_eq_u32 %[ones], 1\n"                                     \
+    "s_cbranch_scc0 FH" I "_%=\n"                                   \
+    "s_lshr_b32 %[low], " MA ", 4\n"                                \
+    "s_add_u32 %[low], %[low], 1\n"                                 \
+    "s_lshr_b32 %[mc], " MB ", 4\n"                                 \
+    NW_INC(MA, "128", "7")                                          \
+    NW_DEC(MB, "62", "5")                                           \
+    FW_TAIL(I, "b", "v_add_u32 %[r], %[low], %[r]\n", J)            \
+    "s_branch " NEXT "_%=\n"                                        \
+    "FH" I "_%=:\n" /* ones >= 2 */                                 \
+    "s_lshr_b32 %[mc], " MC ", 4\n"                                 \
+    "s_cmp_gt_u32 %[u], 7\n"                                        \
+    "s_cbranch_scc1 FK" I "_%=\n"                                   \
+    "FJ" I "_%=:\n"                                                 \
+    "s_lshr_b32 %[low], " MA ", 4\n"                                \
+    "s_lshr_b32 %[t0], " MB ", 4\n"                                 \
+    "s_add_u32 %[low], %[low], %[t0]\n"                             \
+    "s_add_u32 %[low], %[low], 2\n"                                 \
+    NW_INC(MA, "128", "7")                                          \
+    NW_INC(MB, "64", "6")                                           \
+    "s_cmp_eq_u32 %[ones], 2\n"                                     \
+    "s_cbranch_scc0 FM" I "_%=\n"                                   \
+    NW_DEC(MC, "30", "4")                                           \
+    FW_TAIL(I, "c", "v_add_u32 %[r], %[low], %[r]\n", J)            \
+    "s_branch " NEXT "_%=\n"                                        \
+    "FM" I "_%=:\n" /* ones >= 3 */                                 \
+    "s_add_u32 %[t0], %[mc], 1\n"                                   \
+    "s_sub_u32 %[v], %[ones], 2\n"                                  \
+    "s_mul_i32 %[t0], %[t0], %[v]\n"                                \
+    "s_add_u32 %[low], %[low], %[t0]\n"                             \
+    NW_INC(MC, "32", "5")                                           \
+    FW_TAIL(I, "d", "v_add_u32 %[r], %[low], %[r]\n", J)            \
+    "s_branch " NEXT "_%=\n"                                        \
+    "FK" I "_%=:\n" /* 8..16 unary ones: escape, or test the bound */ \
+    "s_cmp_gt_u32 %[u], 15\n"                                       \
+    "s_cbranch_scc1 FB" I "_%=\n"                                   \
+    "s_or_b32 %[t0], %[mc], 1\n"                                    \
+    "s_flbit_i32_b32 %[t0], %[t0]\n"                                \
+    "s_add_u32 %[t], %[u], 1\n" /* c1 (no holding_zero here) */     \
+    "s_cmp_lt_u32 %[t], %[t0]\n" /* c1 + n1 + 2 <= 32 */            \
+    "s_cbranch_scc1 FJ" I "_%=\n"                                   \
+    "FB" I "_%=:\n" /* leave before the word commits: restore h0/h1 */ \
+    "s_lshr_b32 %[t0], %[u], 1\n"                                   \
+    "s_sub_u32 %[h1], %[ones], %[t0]\n"                             \
+    "s_mov_b32 %[h0], 0\n"                                          \
+    "s_branch FX_%=\n"
+
+// a whole batch (k at a batch start, 64 words to go); returns true when the
+// batch is done, false when the word at k needs get_word
+template <bool MONO>
+__device__ __forceinline__ bool lossless_run_full(Entropy &w, SmemReader &rd, uint32_t &k, int32_t &resv) {
+    uint32_t t0, t, u, ones, c1, mc, z, n1, low, ex, v;
+    int32_t r, rb, vt;
+    uint64_t tq, lm = 1;
+    uint32_t nb = (uint32_t)rd.nb;
+    uint32_t off = 4u * (rd.rd + 1u);
+    uint64_t q = (uint64_t)rd.n0 | ((uint64_t)rd.n1 << 32);
+    const uint32_t elim = rd.E - 8u;
+    int32_t m00 = w.med[0][0], m01 = w.med[0][1], m02 = w.med[0][2];
+    int32_t m10 = w.med[1][0], m11 = w.med[1][1], m12 = w.med[1][2];
+    int32_t h0 = w.h0, h1 = w.h1;
+    uint64_t win = rd.win;
+    if (MONO) {
+        asm volatile(
+            "s_mov_b64 vcc, %[win]\n"
+            "s_sub_u32 %[nb], %[nb], 32\n"
+            "s_cbranch_scc1 FR0_%=\n"
+            "FL_%=:\n"
+            FW_WORD("0", "%[m00]", "1")
+            FW_WORD("1", "%[m00]", "2")
+            FW_WORD("2", "%[m00]", "3")
+            FW_WORD("3", "%[m00]", "0")
+            "FC3_%=:\n"
+            "s_cmp_lg_u64 %[lm], 0\n"
+            "s_cbranch_scc1 FL_%=\n"
+            "s_branch FE_%=\n"
+            FW_REFILL("0", "FC3")
+            FW_REFILL("1", "FA1")
+            FW_REFILL("2", "FA2")
+            FW_REFILL("3", "FA3")
+            FW_COLD("0", "FA1", "%[m00]", "%[m01]", "%[m02]", "1")
+            FW_COLD("1", "FA2", "%[m00]", "%[m01]", "%[m02]", "2")
+            FW_COLD("2", "FA3", "%[m00]", "%[m01]", "%[m02]", "3")
+            FW_COLD("3", "FC3", "%[m00]", "%[m01]", "%[m02]", "0")
+            "FX_%=:\n"
+            "FE_%=:\n"
+            "s_add_u32 %[nb], %[nb], 32\n"
+            "s_waitcnt lgkmcnt(0)\n"
+            "s_mov_b64 %[win], vcc\n"
+            : [t0] "=&s"(t0), [t] "=&s"(t), [u] "=&s"(u), [ones] "=&s"(ones), [c1] "=&s"(c1), [mc] "=&s"(mc),
+              [z] "=&s"(z), [n1] "=&s"(n1), [low] "=&s"(low), [ex] "=&s"(ex), [v] "=&s"(v), [tq] "=&s"(tq),
+              [r] "=&v"(r), [rb] "=&v"(rb), [vt] "=&v"(vt), [win] "+s"(win), [nb] "+s"(nb), [off] "+s"(off),
+              [q] "+s"(q), [m00] "+s"(m00), [m01] "+s"(m01), [m02] "+s"(m02), [h0] "+s"(h0), [h1] "+s"(h1),
+              [lm] "+s"(lm), [resv] "+v"(resv)
+            : [elim] "s"(elim), [base] "s"(rd.base), [k16] "s"(0x10000u), [k7f] "s"(0x7fffffffu),
+              [kc1] "s"(1u - 0x10000u), [kn] "s"(0x10000u + 31u)
+            : "vcc", "scc");
+    } else {
+        asm volatile(
+            "s_mov_b64 vcc, %[win]\n"
+            "s_sub_u32 %[nb], %[nb], 32\n"
+            "s_cbranch_scc1 FR0_%=\n"
+            "FL_%=:\n"
+            FW_WORD("0", "%[m00]", "1")
+            FW_WORD("1", "%[m10]", "2")
+            FW_WORD("2", "%[m00]", "3")
+            FW_WORD("3", "%[m10]", "4")
+            FW_WORD("4", "%[m00]", "5")
+            FW_WORD("5", "%[m10]", "6")
+            FW_WORD("6", "%[m00]", "7")
+            FW_WORD("7", "%[m10]", "0")
+            "FC7_%=:\n"
+            "s_cmp_lg_u64 %[lm], 0\n"
+            "s_cbranch_scc1 FL_%=\n"
+            "s_branch FE_%=\n"
+            FW_REFILL("0", "FC7")
+            FW_REFILL("1", "FA1")
+            FW_REFILL("2", "FA2")
+            FW_REFILL("3", "FA3")
+            FW_REFILL("4", "FA4")
+            FW_REFILL("5", "FA5")
+            FW_REFILL("6", "FA6")
+            FW_REFILL("7", "FA7")
+            FW_COLD("0", "FA1", "%[m00]", "%[m01]", "%[m02]", "1")
+            FW_COLD("1", "FA2", "%[m10]", "%[m11]", "%[m12]", "2")
+            FW_COLD("2", "FA3", "%[m00]", "%[m01]", "%[m02]", "3")
+            FW_COLD("3", "FA4", "%[m10]", "%[m11]", "%[m12]", "4")
+            FW_COLD("4", "FA5", "%[m00]", "%[m01]", "%[m02]", "5")
+            FW_COLD("5", "FA6", "%[m10]", "%[m11]", "%[m12]", "6")
+            FW_COLD("6", "FA7", "%[m00]", "%[m01]", "%[m02]", "7")
+            FW_COLD("7", "FC7", "%[m10]", "%[m11]", "%[m12]", "0")
+            "FX_%=:\n"
+            "FE_%=:\n"
+            "s_add_u32 %[nb], %[nb], 32\n"
+            "s_waitcnt lgkmcnt(0)\n"
+            "s_mov_b64 %[win], vcc\n"
+            : [t0] "=&s"(t0), [t] "=&s"(t), [u] "=&s"(u), [ones] "=&s"(ones), [c1] "=&s"(c1), [mc] "=&s"(mc),
+              [z] "=&s"(z), [n1] "=&s"(n1), [low] "=&s"(low), [ex] "=&s"(ex), [v] "=&s"(v), [tq] "=&s"(tq),
+              [r] "=&v"(r), [rb] "=&v"(rb), [vt] "=&v"(vt), [win] "+s"(win), [nb] "+s"(nb), [off] "+s"(off),
+              [q] "+s"(q), [m00] "+s"(m00), [m01] "+s"(m01), [m02] "+s"(m02), [m10] "+s"(m10), [m11] "+s"(m11),
+              [m12] "+s"(m12), [h0] "+s"(h0), [h1] "+s"(h1), [lm] "+s"(lm), [resv] "+v"(resv)
+            : [elim] "s"(elim), [base] "s"(rd.base), [k16] "s"(0x10000u), [k7f] "s"(0x7fffffffu),
+              [kc1] "s"(1u - 0x10000u), [kn] "s"(0x10000u + 31u)
+            : "vcc", "scc");
+    }
+    rd.win = win;
+    rd.nb = (int)nb;
+    rd.rd = off / 4u - 1u;
+    rd.n0 = (uint32_t)q;
+    rd.n1 = (uint32_t)(q >> 32);
+    w.med[0][0] = m00;
+    w.med[0][1] = m01;
+    w.med[0][2] = m02;
+    w.med[1][0] = m10;
+    w.med[1][1] = m11;
+    w.med[1][2] = m12;
+    w.h0 = h0;
+    w.h1 = h1;
+    const uint32_t done = lm ? (uint32_t)__builtin_ctzll(lm) : 64u;  // words written (lane of the next)
+    k += done;
+    return done == 64u;
+}
+#undef FW_TAIL
+#undef FW_WORD
+#undef FW_REFILL
+#undef FW_COLD
 #undef NW_DEC
 #undef NW_INC
 #undef NW_TAIL
@@ -1282,6 +1525,12 @@ __device__ __forceinline__ void parse_loop(const BlockDesc &d, Reader &rd, Entro
             }
             if (LOSSLESS && (MONO || (k & 1) == 0)) {
                 if (narrow_ok<MONO>(w, rd)) {
+#ifndef WV2_NO_FULL_BATCH
+                    if ((k & 63u) == 0 && kend - k == 64u) {
+                        // false: the word at k (the run stopped there) takes the general path
+                        if (lossless_run_full<MONO>(w, rd, k, resv)) break;
+                    } else
+#endif
                     if (lossless_run_narrow<MONO>(w, rd, k, kend, resv)) break;
                 } else if (lossless_run<MONO>(w, rd, k, kend, resv)) {
                     break;
@@ -1736,7 +1985,7 @@ __device__ __forceinline__ void recon_impl(const BlockDesc &d, const uint8_t *bl
                 break;
             }
             __builtin_amdgcn_s_sleep(WV2_RECON_SLEEP);
-            if (++spins > SPIN_LIMIT) {
+            if (++spins > RECON_SPIN_LIMIT) {
                 perr = DEC_TIMEOUT;
                 break;
             }
