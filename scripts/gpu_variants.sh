@@ -13,6 +13,6 @@ for rep in 1 2; do
   for L in $LIBS; do
     i=$((i+1))
     WVG_LIB=$GRAFT_REPO_ROOT/wavpackdecoder_amd/$L timeout -k 10 300 python bench.py --steps 30 --warmup 4 --no-cpu ${BENCH_ARGS} > gpurun_out/var/b$i.log 2>&1 || { tail -3 gpurun_out/var/b$i.log; exit 1; }
-    python -c "import json; d=json.loads(open('gpurun_out/var/b$i.log').read().strip().splitlines()[-1]); print('$L', d['value'], d.get('value_one_batch_at_a_time'), d.get('launch_ms',{}).get('in_flight_mean'), d.get('launch_ms',{}).get('alone'))"
+    python -c "import json; d=json.loads(open('gpurun_out/var/b$i.log').read().strip().splitlines()[-1]); print('$L', d['value'], d.get('value_one_batch_at_a_time'), d.get('launch_ms',{}).get('in_flight_mean'), d.get('launch_ms',{}).get('alone'), d['pcie_inclusive']['value'], d['pcie_inclusive'].get('pipelined'))"
   done
 done

@@ -519,6 +519,7 @@ int wvg_batch_upload(wvg_batch *b) {
 int wvg_batch_decode(wvg_batch *b, void *stream) {
     if (!b || !b->uploaded) return WVG_ERR_ARG;
     wvg_ctx *c = b->ctx;
+    HIPCHK(c, hipSetDevice(c->device));  // side streams and events belong to the batch's device, whatever the calling thread
     hipStream_t s = stream ? (hipStream_t)stream : b->stream;
     if (b->timing) {
         hipEvent_t e0, e1;
@@ -814,6 +815,7 @@ int wvg_format_samples(const int32_t *src, int64_t samcnt, int bps, uint8_t *pcm
 int wvg_batch_format(wvg_batch *b, int dsd, void *stream) {
     if (!b || !b->uploaded) return WVG_ERR_ARG;
     wvg_ctx *c = b->ctx;
+    HIPCHK(c, hipSetDevice(c->device));  // d_pcm is allocated on the batch's device
     hipStream_t s = stream ? (hipStream_t)stream : b->stream;
     HIPCHK(c, hipStreamWaitEvent(s, b->done, 0));
     if (!b->segs_uploaded) {  // once per upload (the file set may have changed)

@@ -354,6 +354,178 @@ __device__ __forceinline__ DsdResult dsd_high_vwave(const BlockDesc &d, const ui
     return res;
 }
 
+// One range-coder decision of decode_high (DsdUtils.cs:409-422) on the scalar
+// unit: split, compare, narrow; the outcome comes back as `lanes` (this
+// channel's lane mask) or 0, and as the next bit of the output byte.  In asm
+// so the compare's SCC feeds all four selects (the compiler re-derives it
+// from a saved mask after the split + 1 add).
+__device__ __forceinline__ uint64_t dsd_decide(uint32_t value, uint32_t s, uint32_t &high, uint32_t &low, uint32_t &b,
+                                               uint64_t lanes) {
+#ifdef WV_DSD_CDEC
+    const uint32_t split = low + ((high - low) >> 8) * s;
+    const bool z = value <= split;
+    high = z ? split : high;
+    low = z ? low : split + 1;
+    b = (b << 1) | (uint32_t)z;
+    return z ? lanes : 0ull;
+#else
+    uint64_t zm;
+    uint32_t t, t1;
+    asm("s_sub_u32 %[t], %[hi], %[lo]\n\t"
+        "s_lshr_b32 %[t], %[t], 8\n\t"
+        "s_mul_i32 %[t], %[t], %[s]\n\t"
+        "s_add_u32 %[t], %[t], %[lo]\n\t"
+        "s_add_u32 %[t1], %[t], 1\n\t"
+        "s_cmp_le_u32 %[v], %[t]\n\t"
+        "s_cselect_b32 %[hi], %[t], %[hi]\n\t"
+        "s_cselect_b32 %[lo], %[lo], %[t1]\n\t"
+        "s_cselect_b64 %[zm], %[ln], 0\n\t"
+        "s_addc_u32 %[b], %[b], %[b]"
+        : [hi] "+s"(high), [lo] "+s"(low), [b] "+s"(b), [zm] "=&s"(zm), [t] "=&s"(t), [t1] "=&s"(t1)
+        : [v] "s"(value), [s] "s"(s), [ln] "s"(lanes)
+        : "scc");
+    return zm;
+#endif
+}
+
+// Stereo mode 3, issue-count version of dsd_high_vwave.  A lone wave issues
+// about one instruction per four cycles, so a decision costs what it issues
+// plus whatever latency is left exposed.  Per bit:
+//  * the LDS read of both channels' ptable entries is issued first, and the
+//    parts of the filter update that do not depend on the decision (both
+//    outcomes of the factor step and of filter1/filter2's steps) are computed
+//    while it is in flight;
+//  * the two decisions stay scalar; their outcomes become one lane mask
+//    (inverse ballot), so each decision-dependent filter step is one select;
+//  * both channels' ptable updates are one per-lane LDS write (when both
+//    channels hit one entry, channel 1's update starts from channel 0's and
+//    channel 0's write goes to a spare slot, ptable[256]);
+//  * filter6 and factor stay far inside 24 bits (|filter6| <= 2^16,
+//    |factor| <= 2^15 + 8 for any stream: the filters are convex updates of
+//    0 / 2^20 and the factor decays by 1/1024 per byte), so their products
+//    are full-rate 24-bit multiplies with the same low 32 bits as C#'s
+//    wrapping int multiply;
+//  * the output bytes accumulate in scalar registers.
+// Same results and status bits as dsd_high_wave<2> (DsdUtils.cs:391-493).
+__device__ __forceinline__ DsdResult dsd_high_v2(const BlockDesc &d, const uint8_t *blob, const uint8_t *tables,
+                                                 int32_t *ptable, DevStoreWave &out) {
+    using namespace wvf;
+    constexpr int32_t kUp = 0x010000FE, kDown = 0x00010000;
+    constexpr uint64_t kEven = 0x5555555555555555ull;
+    const uint32_t dlen = d.dsd_data_len;
+    const int ch = threadIdx.x & 1;
+    ByteSrcWave src;
+    src.init(blob + d.bits_off);
+    uint32_t bp = 0;
+    int32_t crc = -1;
+    DsdResult res = {0, 0};
+    bool mute = false;
+    uint32_t low = 0, high = 0xFFFFFFFFu, value = 0;
+    for (int i = 0; i < 4; i++) value = (value << 8) | src.byte(bp++);
+    {
+        const int32_t *pt0 = (const int32_t *)(tables + d.dsd_table_off);
+        for (uint32_t i = threadIdx.x; i < 256; i += 64) ptable[i] = pt0[i];
+        __syncthreads();
+    }
+    uint8_t *lds = (uint8_t *)ptable;
+    int32_t q2 = d.dsd_filters[ch][0], q3 = d.dsd_filters[ch][1], q4 = d.dsd_filters[ch][2];
+    int32_t q5 = d.dsd_filters[ch][3], q6 = d.dsd_filters[ch][4], q8 = d.dsd_filters[ch][5];
+    int32_t q7 = 0;
+    uint32_t f = 0, chunk_len = d.first_chunk, ci = 0;
+    while (f < d.nframes) {
+        uint32_t n = chunk_len;
+        if (n > d.nframes - f) n = d.nframes - f;
+        if (!mute) {
+            for (uint32_t j = 0; j < n; j++) {
+                int32_t q0 = add32(sub32(q2, q6), __mul24(q7, q8) >> 2);
+                uint32_t b0 = 0, b1 = 0;
+#pragma unroll
+                for (int bit = 0; bit < 8; bit++) {
+                    const uint32_t addr = ((uint32_t)q0 >> 6) & 0x3FCu;
+                    int32_t pv = *(const int32_t *)(lds + addr);
+                    // decision-independent work, under the LDS latency
+                    const int32_t v = add32(q0, shl32(q7, 3));
+                    int32_t t;  // q0 - 8 * filter6, one 24-bit multiply-add
+                    asm("v_mad_i32_i24 %0, %1, -8, %2" : "=v"(t) : "v"(q7), "v"(q0));
+                    const int32_t sx = (v ^ t) >> 31;
+                    const int32_t w = v >> 31;
+                    const int32_t dz0 = sx & (w | 1), dz1 = sx & (~w | 1);  // factor step for filter0 = 0 / -1
+                    const int32_t a20 = sub32(0, q2) >> 6, a21 = sub32(1 << 20, q2) >> 6;
+                    const int32_t a30 = sub32(0, q3) >> 4, a31 = sub32(1 << 20, q3) >> 4;
+                    // computed before the first use of pv, i.e. while the read is in flight (the
+                    // compiler would otherwise sink them past the decisions and wait at once)
+                    asm volatile("" : "+v"(pv) : "v"(dz0), "v"(dz1), "v"(a20), "v"(a21), "v"(a30), "v"(a31));
+                    const uint32_t pa0 = (uint32_t)__builtin_amdgcn_readlane((int32_t)addr, 0);
+                    const uint32_t pa1 = (uint32_t)__builtin_amdgcn_readlane((int32_t)addr, 1);
+                    // channel 0's decision
+                    const uint32_t ps = (uint32_t)pv >> 16;
+                    const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane((int32_t)ps, 0);
+                    uint32_t s1 = (uint32_t)__builtin_amdgcn_readlane((int32_t)ps, 1);
+                    const uint64_t zm0 = dsd_decide(value, s0, high, low, b0, kEven);
+                    const bool z0 = zm0 != 0;
+                    int32_t pvl = pv;
+                    uint32_t wa = addr;
+                    if (__builtin_expect(pa0 == pa1, 0)) {  // channel 1 reads channel 0's updated entry
+                        const int32_t p0 = __builtin_amdgcn_readlane(pv, 0);
+                        const int32_t np0 = p0 + (((z0 ? kUp : kDown) - p0) >> 8);
+                        s1 = (uint32_t)np0 >> 16;
+                        pvl = ch ? np0 : pv;
+                        wa = ch ? addr : 1024u;
+                    }
+                    if (__builtin_expect((high ^ low) < 0x1000000u, 0)) {
+                        while ((high ^ low) < 0x1000000u && bp < dlen) {
+                            value = (value << 8) | src.byte(bp++);
+                            high = (high << 8) | 0xFF;
+                            low <<= 8;
+                        }
+                    }
+                    // channel 1's decision
+                    const uint64_t zm1 = dsd_decide(value, s1, high, low, b1, ~kEven);
+                    if (__builtin_expect((high ^ low) < 0x1000000u, 0)) {
+                        while ((high ^ low) < 0x1000000u && bp < dlen) {
+                            value = (value << 8) | src.byte(bp++);
+                            high = (high << 8) | 0xFF;
+                            low <<= 8;
+                        }
+                    }
+                    // this lane's channel's outcome
+                    const bool zl = __builtin_amdgcn_inverse_ballot_w64(zm0 | zm1);
+                    *(int32_t *)(lds + wa) = pvl + (((zl ? kUp : kDown) - pvl) >> 8);
+                    q8 = add32(q8, zl ? dz1 : dz0);
+                    q2 = add32(q2, zl ? a21 : a20);
+                    q3 = add32(q3, zl ? a31 : a30);
+                    q4 = add32(q4, sub32(q3, q4) >> 4);
+                    q5 = add32(q5, sub32(q4, q5) >> 4);
+                    const int32_t dd = sub32(q5, q6) >> 4;
+                    q6 = add32(q6, dd);
+                    q7 = add32(q7, sub32(dd, q7) >> 3);
+                    q0 = add32(sub32(q2, q6), __mul24(q7, q8) >> 2);
+                }
+                const int32_t v0 = (int32_t)(b0 & 0xFFu), v1 = (int32_t)(b1 & 0xFFu);
+                q8 = sub32(q8, add32(q8, 512) >> 10);
+                crc = add32(crc, add32(shl32(crc, 1), v0));
+                crc = add32(crc, add32(shl32(crc, 1), v1));
+                const uint64_t o = (uint64_t)(f + j) * 2u;
+                out.put(o, v0);
+                out.put(o + 1, v1);
+            }
+            if (f + n == d.block_samples && crc != d.crc) mute = true;
+        }
+        if (mute && !(res.status & ST_DSD_MUTE)) {
+            res.status |= ST_DSD_MUTE;
+            res.mute_chunk = ci;
+        }
+        f += n;
+        chunk_len = next_call_len(d, f);
+        ci++;
+    }
+    if (d.nframes == d.block_samples) {
+        res.status |= ST_CRC_CHECKED;
+        if (crc != d.crc) res.status |= ST_CRC_ERROR;
+    }
+    return res;
+}
+
 // DsdUtils mode 1's tables (prob u8, summed u16, lookup u8, value_lookup i32;
 // 16-B aligned by the framing) read through the scalar cache: a data-dependent
 // table read costs a scalar-cache hit, not a vector load's memory latency
@@ -506,7 +678,7 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_wave(const BlockD
                                                                     uint32_t *__restrict__ status,
                                                                     uint32_t *__restrict__ mute_chunk,
                                                                     uint32_t skip_fast) {
-    __shared__ int32_t pt_lds[256];  // mode 3's adaptive ptable, one per block
+    __shared__ int32_t pt_lds[260];  // mode 3's adaptive ptable, one per block (+ dsd_high_v2's spare slot)
     const uint32_t bi = list[blockIdx.x];
     const BlockDesc &d = descs[bi];
     if (skip_fast && d.kind == KIND_DSD_FAST) return;  // wv_decode_dsd_fast's
@@ -515,10 +687,12 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_wave(const BlockD
     DsdResult r;
     if (d.kind == KIND_DSD_HIGH)
         r = (d.flags & wvf::MONO_DATA) ? dsd_high_wave<1>(d, blob, tables, pt_lds, st)
-#ifdef WV_DSD_HIGH_SCALAR
+#if defined(WV_DSD_HIGH_SCALAR)
                                        : dsd_high_wave<2>(d, blob, tables, pt_lds, st);
-#else
+#elif defined(WV_DSD_HIGH_V1)
                                        : dsd_high_vwave(d, blob, tables, pt_lds, st);
+#else
+                                       : dsd_high_v2(d, blob, tables, pt_lds, st);
 #endif
     else if (d.kind == KIND_DSD_FAST)
         r = (d.flags & wvf::MONO_DATA) ? dsd_simple_wave<1, true>(d, blob, tables, st)

@@ -1224,6 +1224,32 @@ __device__ __forceinline__ bool hybrid_run_narrow(Entropy &w, SmemReader &rd, ui
 // lane mask running out (once per 8 stereo / 4 mono words), so no M0 counter.
 // Each VALU instruction reads at most one SGPR (gfx9 constant bus).
 // ---------------------------------------------------------------------------
+// the median updates on the VALU, the result read back into the median's SGPR
+// (stereo: a channel's medians are next read two words later, by which time
+// the v_readfirstlane has long completed)
+#ifdef WV2_SALU_MEDIANS
+#define WV2_FDEC NW_DEC
+#define WV2_FINC NW_INC
+#else
+#define WV2_FDEC FV_DEC
+#define WV2_FINC FV_INC
+#endif
+#define FV_DEC(M, ADD, SH1)                                         \
+    "v_mov_b32 %[vm], " M "\n"                                      \
+    "v_add_u32 %[vm], " ADD ", %[vm]\n"                             \
+    "v_ashrrev_i32 %[vm], " SH1 ", %[vm]\n"                         \
+    "v_and_b32 %[vm], -2, %[vm]\n"                                  \
+    "v_sub_u32 %[vm], " M ", %[vm]\n"                               \
+    "s_nop 0\n" /* VALU VGPR write -> v_readfirstlane: 1 wait state */ \
+    "v_readfirstlane_b32 " M ", %[vm]\n"
+#define FV_INC(M, ADD, SH)                                          \
+    "v_mov_b32 %[vm], " M "\n"                                      \
+    "v_add_u32 %[vm], " ADD ", %[vm]\n"                             \
+    "v_ashrrev_i32 %[vm], " SH ", %[vm]\n"                          \
+    "v_lshl_add_u32 %[vm], %[vm], 2, %[vm]\n"                       \
+    "v_add_u32 %[vm], " M ", %[vm]\n"                               \
+    "s_nop 0\n"                                                     \
+    "v_readfirstlane_b32 " M ", %[vm]\n"
 #define FW_TAIL(I, S, LOWOP, J)                                     \
     "s_or_b32 %[t0], %[mc], 1\n"                                    \
     "s_flbit_i32_b32 %[z], %[t0]\n"                                 \
@@ -1255,7 +1281,7 @@ __device__ __forceinline__ bool hybrid_run_narrow(Entropy &w, SmemReader &rd, ui
     "s_lshr_b64 vcc, vcc, %[n1]\n"                                  \
     "s_sub_u32 %[nb], %[nb], %[n1]\n" /* SCC: fewer than 32 left */ \
     "s_cbranch_scc1 FR" J "_%=\n"
-#define FW_WORD(I, MA, J)                                           \
+#define FW_WORD(I, MA, J, DEC)                                           \
     "FA" I "_%=:\n"                                                 \
     "s_lshl_b64 vcc, vcc, %[h0]\n"                                  \
     "s_add_u32 %[nb], %[nb], %[h0]\n"                               \
@@ -1269,7 +1295,7 @@ __device__ __forceinline__ bool hybrid_run_narrow(Entropy &w, SmemReader &rd, ui
     "s_lshr_b32 %[ones], %[t0], 1\n" /* SCC = ones != 0 */          \
     "s_cbranch_scc1 FG" I "_%=\n"                                   \
     "s_lshr_b32 %[mc], " MA ", 4\n"                                 \
-    NW_DEC(MA, "126", "6")                                          \
+    DEC(MA, "126", "6")                                             \
     FW_TAIL(I, "a", "", J)
 #define FW_REFILL(J, DEST)                                          \
     "FR" J "_%=:\n"                                                 \
@@ -1282,15 +1308,15 @@ __device__ __forceinline__ bool hybrid_run_narrow(Entropy &w, SmemReader &rd, ui
     "s_load_dwordx2 %[q], %[base], %[off]\n"                        \
     "s_add_u32 %[off], %[off], 4\n"                                 \
     "s_branch " DEST "_%=\n"
-#define FW_COLD(I, NEXT, MA, MB, MC, J)                             \
+#define FW_COLD(I, NEXT, MA, MB, MC, J, DEC, INC)                             \
     "FG" I "_%=:\n" /* ones == 1 */                                 \
     "s_cmp_eq_u32 %[ones], 1\n"                                     \
     "s_cbranch_scc0 FH" I "_%=\n"                                   \
     "s_lshr_b32 %[low], " MA ", 4\n"                                \
     "s_add_u32 %[low], %[low], 1\n"                                 \
     "s_lshr_b32 %[mc], " MB ", 4\n"                                 \
-    NW_INC(MA, "128", "7")                                          \
-    NW_DEC(MB, "62", "5")                                           \
+    INC(MA, "128", "7")                                          \
+    DEC(MB, "62", "5")                                           \
     FW_TAIL(I, "b", "v_add_u32 %[r], %[low], %[r]\n", J)            \
     "s_branch " NEXT "_%=\n"                                        \
     "FH" I "_%=:\n" /* ones >= 2 */                                 \
@@ -1302,11 +1328,11 @@ __device__ __forceinline__ bool hybrid_run_narrow(Entropy &w, SmemReader &rd, ui
     "s_lshr_b32 %[t0], " MB ", 4\n"                                 \
     "s_add_u32 %[low], %[low], %[t0]\n"                             \
     "s_add_u32 %[low], %[low], 2\n"                                 \
-    NW_INC(MA, "128", "7")                                          \
-    NW_INC(MB, "64", "6")                                           \
+    INC(MA, "128", "7")                                          \
+    INC(MB, "64", "6")                                           \
     "s_cmp_eq_u32 %[ones], 2\n"                                     \
     "s_cbranch_scc0 FM" I "_%=\n"                                   \
-    NW_DEC(MC, "30", "4")                                           \
+    DEC(MC, "30", "4")                                           \
     FW_TAIL(I, "c", "v_add_u32 %[r], %[low], %[r]\n", J)            \
     "s_branch " NEXT "_%=\n"                                        \
     "FM" I "_%=:\n" /* ones >= 3 */                                 \
@@ -1314,7 +1340,7 @@ __device__ __forceinline__ bool hybrid_run_narrow(Entropy &w, SmemReader &rd, ui
     "s_sub_u32 %[v], %[ones], 2\n"                                  \
     "s_mul_i32 %[t0], %[t0], %[v]\n"                                \
     "s_add_u32 %[low], %[low], %[t0]\n"                             \
-    NW_INC(MC, "32", "5")                                           \
+    INC(MC, "32", "5")                                           \
     FW_TAIL(I, "d", "v_add_u32 %[r], %[low], %[r]\n", J)            \
     "s_branch " NEXT "_%=\n"                                        \
     "FK" I "_%=:\n" /* 8..16 unary ones: escape, or test the bound */ \
@@ -1336,7 +1362,7 @@ __device__ __forceinline__ bool hybrid_run_narrow(Entropy &w, SmemReader &rd, ui
 template <bool MONO>
 __device__ __forceinline__ bool lossless_run_full(Entropy &w, SmemReader &rd, uint32_t &k, int32_t &resv) {
     uint32_t t0, t, u, ones, c1, mc, z, n1, low, ex, v;
-    int32_t r, rb, vt;
+    int32_t r, rb, vt, vm;
     uint64_t tq, lm = 1;
     uint32_t nb = (uint32_t)rd.nb;
     uint32_t off = 4u * (rd.rd + 1u);
@@ -1352,10 +1378,10 @@ __device__ __forceinline__ bool lossless_run_full(Entropy &w, SmemReader &rd, ui
             "s_sub_u32 %[nb], %[nb], 32\n"
             "s_cbranch_scc1 FR0_%=\n"
             "FL_%=:\n"
-            FW_WORD("0", "%[m00]", "1")
-            FW_WORD("1", "%[m00]", "2")
-            FW_WORD("2", "%[m00]", "3")
-            FW_WORD("3", "%[m00]", "0")
+            FW_WORD("0", "%[m00]", "1", NW_DEC)
+            FW_WORD("1", "%[m00]", "2", NW_DEC)
+            FW_WORD("2", "%[m00]", "3", NW_DEC)
+            FW_WORD("3", "%[m00]", "0", NW_DEC)
             "FC3_%=:\n"
             "s_cmp_lg_u64 %[lm], 0\n"
             "s_cbranch_scc1 FL_%=\n"
@@ -1364,10 +1390,10 @@ __device__ __forceinline__ bool lossless_run_full(Entropy &w, SmemReader &rd, ui
             FW_REFILL("1", "FA1")
             FW_REFILL("2", "FA2")
             FW_REFILL("3", "FA3")
-            FW_COLD("0", "FA1", "%[m00]", "%[m01]", "%[m02]", "1")
-            FW_COLD("1", "FA2", "%[m00]", "%[m01]", "%[m02]", "2")
-            FW_COLD("2", "FA3", "%[m00]", "%[m01]", "%[m02]", "3")
-            FW_COLD("3", "FC3", "%[m00]", "%[m01]", "%[m02]", "0")
+            FW_COLD("0", "FA1", "%[m00]", "%[m01]", "%[m02]", "1", NW_DEC, NW_INC)
+            FW_COLD("1", "FA2", "%[m00]", "%[m01]", "%[m02]", "2", NW_DEC, NW_INC)
+            FW_COLD("2", "FA3", "%[m00]", "%[m01]", "%[m02]", "3", NW_DEC, NW_INC)
+            FW_COLD("3", "FC3", "%[m00]", "%[m01]", "%[m02]", "0", NW_DEC, NW_INC)
             "FX_%=:\n"
             "FE_%=:\n"
             "s_add_u32 %[nb], %[nb], 32\n"
@@ -1375,7 +1401,7 @@ __device__ __forceinline__ bool lossless_run_full(Entropy &w, SmemReader &rd, ui
             "s_mov_b64 %[win], vcc\n"
             : [t0] "=&s"(t0), [t] "=&s"(t), [u] "=&s"(u), [ones] "=&s"(ones), [c1] "=&s"(c1), [mc] "=&s"(mc),
               [z] "=&s"(z), [n1] "=&s"(n1), [low] "=&s"(low), [ex] "=&s"(ex), [v] "=&s"(v), [tq] "=&s"(tq),
-              [r] "=&v"(r), [rb] "=&v"(rb), [vt] "=&v"(vt), [win] "+s"(win), [nb] "+s"(nb), [off] "+s"(off),
+              [r] "=&v"(r), [rb] "=&v"(rb), [vt] "=&v"(vt), [vm] "=&v"(vm), [win] "+s"(win), [nb] "+s"(nb), [off] "+s"(off),
               [q] "+s"(q), [m00] "+s"(m00), [m01] "+s"(m01), [m02] "+s"(m02), [h0] "+s"(h0), [h1] "+s"(h1),
               [lm] "+s"(lm), [resv] "+v"(resv)
             : [elim] "s"(elim), [base] "s"(rd.base), [k16] "s"(0x10000u), [k7f] "s"(0x7fffffffu),
@@ -1387,14 +1413,14 @@ __device__ __forceinline__ bool lossless_run_full(Entropy &w, SmemReader &rd, ui
             "s_sub_u32 %[nb], %[nb], 32\n"
             "s_cbranch_scc1 FR0_%=\n"
             "FL_%=:\n"
-            FW_WORD("0", "%[m00]", "1")
-            FW_WORD("1", "%[m10]", "2")
-            FW_WORD("2", "%[m00]", "3")
-            FW_WORD("3", "%[m10]", "4")
-            FW_WORD("4", "%[m00]", "5")
-            FW_WORD("5", "%[m10]", "6")
-            FW_WORD("6", "%[m00]", "7")
-            FW_WORD("7", "%[m10]", "0")
+            FW_WORD("0", "%[m00]", "1", WV2_FDEC)
+            FW_WORD("1", "%[m10]", "2", WV2_FDEC)
+            FW_WORD("2", "%[m00]", "3", WV2_FDEC)
+            FW_WORD("3", "%[m10]", "4", WV2_FDEC)
+            FW_WORD("4", "%[m00]", "5", WV2_FDEC)
+            FW_WORD("5", "%[m10]", "6", WV2_FDEC)
+            FW_WORD("6", "%[m00]", "7", WV2_FDEC)
+            FW_WORD("7", "%[m10]", "0", WV2_FDEC)
             "FC7_%=:\n"
             "s_cmp_lg_u64 %[lm], 0\n"
             "s_cbranch_scc1 FL_%=\n"
@@ -1407,14 +1433,14 @@ __device__ __forceinline__ bool lossless_run_full(Entropy &w, SmemReader &rd, ui
             FW_REFILL("5", "FA5")
             FW_REFILL("6", "FA6")
             FW_REFILL("7", "FA7")
-            FW_COLD("0", "FA1", "%[m00]", "%[m01]", "%[m02]", "1")
-            FW_COLD("1", "FA2", "%[m10]", "%[m11]", "%[m12]", "2")
-            FW_COLD("2", "FA3", "%[m00]", "%[m01]", "%[m02]", "3")
-            FW_COLD("3", "FA4", "%[m10]", "%[m11]", "%[m12]", "4")
-            FW_COLD("4", "FA5", "%[m00]", "%[m01]", "%[m02]", "5")
-            FW_COLD("5", "FA6", "%[m10]", "%[m11]", "%[m12]", "6")
-            FW_COLD("6", "FA7", "%[m00]", "%[m01]", "%[m02]", "7")
-            FW_COLD("7", "FC7", "%[m10]", "%[m11]", "%[m12]", "0")
+            FW_COLD("0", "FA1", "%[m00]", "%[m01]", "%[m02]", "1", WV2_FDEC, WV2_FINC)
+            FW_COLD("1", "FA2", "%[m10]", "%[m11]", "%[m12]", "2", WV2_FDEC, WV2_FINC)
+            FW_COLD("2", "FA3", "%[m00]", "%[m01]", "%[m02]", "3", WV2_FDEC, WV2_FINC)
+            FW_COLD("3", "FA4", "%[m10]", "%[m11]", "%[m12]", "4", WV2_FDEC, WV2_FINC)
+            FW_COLD("4", "FA5", "%[m00]", "%[m01]", "%[m02]", "5", WV2_FDEC, WV2_FINC)
+            FW_COLD("5", "FA6", "%[m10]", "%[m11]", "%[m12]", "6", WV2_FDEC, WV2_FINC)
+            FW_COLD("6", "FA7", "%[m00]", "%[m01]", "%[m02]", "7", WV2_FDEC, WV2_FINC)
+            FW_COLD("7", "FC7", "%[m10]", "%[m11]", "%[m12]", "0", WV2_FDEC, WV2_FINC)
             "FX_%=:\n"
             "FE_%=:\n"
             "s_add_u32 %[nb], %[nb], 32\n"
@@ -1422,7 +1448,7 @@ __device__ __forceinline__ bool lossless_run_full(Entropy &w, SmemReader &rd, ui
             "s_mov_b64 %[win], vcc\n"
             : [t0] "=&s"(t0), [t] "=&s"(t), [u] "=&s"(u), [ones] "=&s"(ones), [c1] "=&s"(c1), [mc] "=&s"(mc),
               [z] "=&s"(z), [n1] "=&s"(n1), [low] "=&s"(low), [ex] "=&s"(ex), [v] "=&s"(v), [tq] "=&s"(tq),
-              [r] "=&v"(r), [rb] "=&v"(rb), [vt] "=&v"(vt), [win] "+s"(win), [nb] "+s"(nb), [off] "+s"(off),
+              [r] "=&v"(r), [rb] "=&v"(rb), [vt] "=&v"(vt), [vm] "=&v"(vm), [win] "+s"(win), [nb] "+s"(nb), [off] "+s"(off),
               [q] "+s"(q), [m00] "+s"(m00), [m01] "+s"(m01), [m02] "+s"(m02), [m10] "+s"(m10), [m11] "+s"(m11),
               [m12] "+s"(m12), [h0] "+s"(h0), [h1] "+s"(h1), [lm] "+s"(lm), [resv] "+v"(resv)
             : [elim] "s"(elim), [base] "s"(rd.base), [k16] "s"(0x10000u), [k7f] "s"(0x7fffffffu),
@@ -1448,6 +1474,10 @@ __device__ __forceinline__ bool lossless_run_full(Entropy &w, SmemReader &rd, ui
 }
 #undef FW_TAIL
 #undef FW_WORD
+#undef FV_DEC
+#undef FV_INC
+#undef WV2_FDEC
+#undef WV2_FINC
 #undef FW_REFILL
 #undef FW_COLD
 #undef NW_DEC
