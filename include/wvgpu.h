@@ -189,7 +189,10 @@ int wvg_batch_format(wvg_batch *b, int dsd, void *stream);
 int64_t wvg_batch_pcm_bytes(const wvg_batch *b);
 int64_t wvg_batch_pcm_offset(const wvg_batch *b, int file);  /* -1: the file did not open */
 uint8_t *wvg_batch_device_pcm(wvg_batch *b);                 /* device pointer to the PCM image */
+/* host == NULL and cap == -1: into the batch's page-locked buffer (full PCIe
+ * rate), read through wvg_batch_host_pcm until the next such download. */
 int wvg_batch_download_pcm(wvg_batch *b, uint8_t *host, int64_t cap);
+uint8_t *wvg_batch_host_pcm(wvg_batch *b);
 
 /* WvDemo.Main (WvDemo.cs:15-168) for one file of a formatted batch built with
  * chunk_frames 4096: the .wav bytes it writes (stored RIFF header or the

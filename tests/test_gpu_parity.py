@@ -232,6 +232,7 @@ def test_format_epilogue_matches_oracle(gpu_batch_cls, dsd):
     b.decode()
     b.format(dsd=bool(dsd))
     pcm = b.download_pcm()
+    np.testing.assert_array_equal(b.download_pcm(pinned=True), pcm)  # the page-locked path, same bytes
     out = b.download()
     offs = [b.pcm_offset(i) for i in idx]
     infos = list(b.infos)

@@ -105,6 +105,7 @@ def lib():
         "wvg_batch_pcm_offset": (i64, [vp, i32]),
         "wvg_batch_device_pcm": (vp, [vp]),
         "wvg_batch_download_pcm": (i32, [vp, vp, i64]),
+        "wvg_batch_host_pcm": (vp, [vp]),
         "wvg_batch_wav": (i32, [vp, i32, vp, i64, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32)]),
     }
     for name, (res, args) in sig.items():
@@ -122,4 +123,4 @@ EXPORTED = ("wvg_open", "wvg_close", "wvg_last_error", "wvg_batch_new", "wvg_bat
             "wvg_batch_num_blocks", "wvg_batch_bytes_in", "wvg_batch_frames", "wvg_batch_download", "wvg_batch_host_out",
             "wvg_batch_file_result", "wvg_batch_block_status", "wvg_batch_file_blocks", "wvg_batch_time", "wvg_decode_file",
             "wvg_probe_file", "wvg_format_samples", "wvg_batch_format", "wvg_batch_pcm_bytes", "wvg_batch_pcm_offset",
-            "wvg_batch_device_pcm", "wvg_batch_download_pcm", "wvg_batch_wav")
+            "wvg_batch_device_pcm", "wvg_batch_download_pcm", "wvg_batch_host_pcm", "wvg_batch_wav")

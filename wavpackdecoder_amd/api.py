@@ -193,8 +193,16 @@ class DecodeBatch:
     def pcm_offset(self, i: int) -> int:
         return int(self._L.wvg_batch_pcm_offset(self._b, int(i)))
 
-    def download_pcm(self) -> np.ndarray:
+    def download_pcm(self, pinned: bool = False) -> np.ndarray:
+        """The formatted PCM bytes.  pinned=True: DMA into the batch's page-locked
+        buffer and return a view of it (valid until the next such download or close)."""
         n = int(self._L.wvg_batch_pcm_bytes(self._b))
+        if pinned:
+            self._check(self._L.wvg_batch_download_pcm(self._b, None, -1))
+            p = self._L.wvg_batch_host_pcm(self._b)
+            if not p or n == 0:
+                return np.zeros(0, dtype=np.uint8)
+            return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint8)), shape=(n,))
         out = np.empty(max(n, 1), dtype=np.uint8)
         self._check(self._L.wvg_batch_download_pcm(self._b, out.ctypes.data, out.size))
         return out[:n]

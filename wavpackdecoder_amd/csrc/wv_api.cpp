@@ -105,6 +105,9 @@ struct wvg_batch {
     bool segs_uploaded = false;
     PinnedBuf blob;                                     // every file's bytes, 16-B aligned
     PinnedBuf hout;                                     // wvg_batch_host_out: the output, downloaded
+    PinnedBuf stage;                                    // page-locked copies of an upload's small host arrays
+    PinnedBuf hst;                                      // page-locked landing area of the status download
+    PinnedBuf hpcm;                                     // wvg_batch_host_pcm: the formatted PCM, downloaded
     FramingOutput fo;
     std::vector<FileInfo> finfo;
     std::vector<wvg_file_info> infos;
@@ -459,19 +462,37 @@ int wvg_batch_upload(wvg_batch *b) {
     HIPCHK(c, hipMemsetAsync(b->d_blob + b->blob.size(), 0xFF, 64, s));
     if (!b->blob.empty()) HIPCHK(c, hipMemcpyAsync(b->d_blob, b->blob.data(), b->blob.size(), hipMemcpyHostToDevice, s));
     const size_t nd = b->fo.descs.size();
+    // The small host arrays go through one page-locked staging buffer: a
+    // pageable hipMemcpyAsync is staged synchronously inside the runtime, which
+    // serialises host threads serving other batches.  Sized up front (a grow
+    // would move the source of copies already queued); the synchronize above
+    // means no earlier copy still reads it.
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    size_t need = al(sizeof(BlockDesc) * nd) + al(sizeof(MetaItem) * b->fo.items.size()) +
+                  al(sizeof(MetaJob) * b->fo.jobs.size()) + al(b->fo.tables.size()) + al(sizeof(uint32_t) * (nd + 1)) +
+                  al(sizeof(uint32_t) * b->pcm_list.size()) + al(sizeof(uint32_t) * b->dsd_list.size());
+    for (int t = 0; t < kMaxTermSets; t++) need += al(sizeof(uint32_t) * b->ts_list[t].size());
+    if (!b->stage.resize(need)) return WVG_ERR_SPACE;
+    size_t soff = 0;
+    auto put = [&](void *dst, const void *src, size_t bytes) -> hipError_t {
+        if (!bytes) return hipSuccess;
+        uint8_t *h = b->stage.data() + soff;
+        memcpy(h, src, bytes);
+        soff += al(bytes);
+        return hipMemcpyAsync(dst, h, bytes, hipMemcpyHostToDevice, s);
+    };
     HIPCHK(c, ensure(b->d_descs, b->cap_descs, sizeof(BlockDesc) * (nd ? nd : 1)));
-    if (nd) HIPCHK(c, hipMemcpyAsync(b->d_descs, b->fo.descs.data(), sizeof(BlockDesc) * nd, hipMemcpyHostToDevice, s));
+    HIPCHK(c, put(b->d_descs, b->fo.descs.data(), sizeof(BlockDesc) * nd));
     if (!b->fo.jobs.empty()) {  // device-side metadata parse: finishes the descriptors in place
         const size_t ni = b->fo.items.size(), nj = b->fo.jobs.size();
         HIPCHK(c, ensure(b->d_items, b->cap_items, sizeof(MetaItem) * ni));
         HIPCHK(c, ensure(b->d_jobs, b->cap_jobs, sizeof(MetaJob) * nj));
-        HIPCHK(c, hipMemcpyAsync(b->d_items, b->fo.items.data(), sizeof(MetaItem) * ni, hipMemcpyHostToDevice, s));
-        HIPCHK(c, hipMemcpyAsync(b->d_jobs, b->fo.jobs.data(), sizeof(MetaJob) * nj, hipMemcpyHostToDevice, s));
+        HIPCHK(c, put(b->d_items, b->fo.items.data(), sizeof(MetaItem) * ni));
+        HIPCHK(c, put(b->d_jobs, b->fo.jobs.data(), sizeof(MetaJob) * nj));
         HIPCHK(c, launch_meta(b->d_descs, b->d_jobs, (uint32_t)nj, b->d_items, b->d_blob, s));
     }
     HIPCHK(c, ensure(b->d_tables, b->cap_tables, b->fo.tables.size() + 16));
-    if (!b->fo.tables.empty())
-        HIPCHK(c, hipMemcpyAsync(b->d_tables, b->fo.tables.data(), b->fo.tables.size(), hipMemcpyHostToDevice, s));
+    HIPCHK(c, put(b->d_tables, b->fo.tables.data(), b->fo.tables.size()));
     const size_t no = (size_t)(b->out_ints ? b->out_ints : 1);
     HIPCHK(c, ensure(b->d_out, b->cap_out, sizeof(int32_t) * no));
     HIPCHK(c, hipMemsetAsync(b->d_out, 0, sizeof(int32_t) * no, s));
@@ -480,7 +501,7 @@ int wvg_batch_upload(wvg_batch *b) {
     HIPCHK(c, ensure(b->d_mute, b->cap_st, sizeof(uint32_t) * (nd ? nd : 1)));
     b->h_status.assign(nd ? nd : 1, 0);
     for (size_t k = 0; k < nd; k++) b->h_status[k] = b->fo.descs[k].fstatus;
-    HIPCHK(c, hipMemcpyAsync(b->d_status, b->h_status.data(), sizeof(uint32_t) * b->h_status.size(), hipMemcpyHostToDevice, s));
+    HIPCHK(c, put(b->d_status, b->h_status.data(), sizeof(uint32_t) * b->h_status.size()));
     HIPCHK(c, hipMemsetAsync(b->d_mute, 0, sizeof(uint32_t) * (nd ? nd : 1), s));
     // longest blocks first within a kind, so the long tail starts early (order is
     // free: every block writes its own output range; DSD fills follow on the same stream)
@@ -500,16 +521,17 @@ int wvg_batch_upload(wvg_batch *b) {
     const size_t np = b->pcm_list.size(), ns = b->dsd_list.size();
     HIPCHK(c, ensure(b->d_pcml, b->cap_pcml, sizeof(uint32_t) * (np ? np : 1)));
     HIPCHK(c, ensure(b->d_dsd, b->cap_dsd, sizeof(uint32_t) * (ns ? ns : 1)));
-    if (np) HIPCHK(c, hipMemcpyAsync(b->d_pcml, b->pcm_list.data(), sizeof(uint32_t) * np, hipMemcpyHostToDevice, s));
-    if (ns) HIPCHK(c, hipMemcpyAsync(b->d_dsd, b->dsd_list.data(), sizeof(uint32_t) * ns, hipMemcpyHostToDevice, s));
+    HIPCHK(c, put(b->d_pcml, b->pcm_list.data(), sizeof(uint32_t) * np));
+    HIPCHK(c, put(b->d_dsd, b->dsd_list.data(), sizeof(uint32_t) * ns));
     for (int t = 0; t < kMaxTermSets; t++) {
         std::vector<uint32_t> &L = b->ts_list[t];
         if (L.empty()) continue;
         std::sort(L.begin(), L.end(), by_kind_len);
         HIPCHK(c, ensure(b->d_ts[t], b->cap_ts[t], sizeof(uint32_t) * L.size()));
-        HIPCHK(c, hipMemcpyAsync(b->d_ts[t], L.data(), sizeof(uint32_t) * L.size(), hipMemcpyHostToDevice, s));
+        HIPCHK(c, put(b->d_ts[t], L.data(), sizeof(uint32_t) * L.size()));
     }
-    HIPCHK(c, hipStreamSynchronize(s));  // the host vectors may change after this call
+    if (soff > need) return WVG_ERR_SPACE;  // (cannot happen: the sizes above cover every put)
+    HIPCHK(c, hipStreamSynchronize(s));  // the blob may change after this call
     b->uploaded = true;
     b->downloaded = false;
     b->segs_uploaded = false;
@@ -611,11 +633,15 @@ static int download_status(wvg_batch *b) {
     size_t nd = b->fo.descs.size();
     b->h_status.assign(nd, 0);
     b->h_aux.assign(nd, 0);
-    if (nd) {
+    if (nd) {  // through page-locked memory (a pageable copy blocks other host threads' HIP calls)
+        if (!b->hst.resize(2 * sizeof(uint32_t) * nd)) return WVG_ERR_SPACE;
+        uint32_t *h = (uint32_t *)b->hst.data();
         HIPCHK(c, hipStreamWaitEvent(b->stream, b->done, 0));
-        HIPCHK(c, hipMemcpyAsync(b->h_status.data(), b->d_status, sizeof(uint32_t) * nd, hipMemcpyDeviceToHost, b->stream));
-        HIPCHK(c, hipMemcpyAsync(b->h_aux.data(), b->d_mute, sizeof(uint32_t) * nd, hipMemcpyDeviceToHost, b->stream));
+        HIPCHK(c, hipMemcpyAsync(h, b->d_status, sizeof(uint32_t) * nd, hipMemcpyDeviceToHost, b->stream));
+        HIPCHK(c, hipMemcpyAsync(h + nd, b->d_mute, sizeof(uint32_t) * nd, hipMemcpyDeviceToHost, b->stream));
         HIPCHK(c, hipStreamSynchronize(b->stream));
+        memcpy(b->h_status.data(), h, sizeof(uint32_t) * nd);
+        memcpy(b->h_aux.data(), h + nd, sizeof(uint32_t) * nd);
     }
     b->downloaded = true;
     return WVG_OK;
@@ -843,11 +869,19 @@ int64_t wvg_batch_pcm_offset(const wvg_batch *b, int file) {
 }
 
 uint8_t *wvg_batch_device_pcm(wvg_batch *b) { return b ? b->d_pcm : nullptr; }
+uint8_t *wvg_batch_host_pcm(wvg_batch *b) { return b && !b->hpcm.empty() ? b->hpcm.data() : nullptr; }
 
 int wvg_batch_download_pcm(wvg_batch *b, uint8_t *host, int64_t cap) {
-    if (!b || !b->formatted || (!host && b->pcm_bytes)) return WVG_ERR_ARG;
-    if (cap < b->pcm_bytes) return WVG_ERR_SPACE;
+    if (!b || !b->formatted) return WVG_ERR_ARG;
     wvg_ctx *c = b->ctx;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!host && cap == -1) {  // into the batch's page-locked buffer (wvg_batch_host_pcm)
+        if (!b->hpcm.resize((size_t)(b->pcm_bytes ? b->pcm_bytes : 1))) return WVG_ERR_SPACE;
+        host = b->hpcm.data();
+        cap = b->pcm_bytes;
+    }
+    if (!host && b->pcm_bytes) return WVG_ERR_ARG;
+    if (cap < b->pcm_bytes) return WVG_ERR_SPACE;
     HIPCHK(c, hipStreamWaitEvent(b->stream, b->done, 0));
     if (b->pcm_bytes)
         HIPCHK(c, hipMemcpyAsync(host, b->d_pcm, (size_t)b->pcm_bytes, hipMemcpyDeviceToHost, b->stream));
