@@ -4,7 +4,7 @@
 cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && mkdir -p gpurun_out/prof_cfg
 TAG=${TAG:-r02}
 CFGS=${CFGS:-"c1 c3 c4 c5 dsd0 dsd1 dsd3"}
-timeout -k 10 900 python3 scripts/bench_configs.py $CFGS --cpu-threads 16 > gpurun_out/prof_cfg/rates.jsonl 2> gpurun_out/prof_cfg/rates.err
+timeout -k 10 900 python3 scripts/bench_configs.py $CFGS --cpu-threads 16 --inflight 3 > gpurun_out/prof_cfg/rates.jsonl 2> gpurun_out/prof_cfg/rates.err
 rc=$?; echo "rates rc=$rc"; cat gpurun_out/prof_cfg/rates.jsonl; [ $rc -ne 0 ] && { tail -5 gpurun_out/prof_cfg/rates.err; exit $rc; }
 for c in $CFGS; do
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_cfg/$c -o ${TAG}_$c --output-format csv -- python3 scripts/bench_configs.py $c > gpurun_out/prof_cfg/$c.log 2>&1

@@ -551,13 +551,16 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
         b->tev.push_back(e1);
         HIPCHK(c, hipEventRecord(e0, s));
     }
-    // one stream slot per non-empty launch group: term sets 0..7, generic PCM, DSD
+    // one stream slot per non-empty launch group: DSD, DSD mode 1, generic PCM,
+    // term sets 0..7.  DSD first (streams are created, and kernels submitted, in
+    // this order): its blocks are the longest serial chains, and streams beyond
+    // the hardware queues share a queue with the ones created before them.
     int used[kSide], n = 0;
-    for (int t = 0; t < kMaxTermSets; t++)
-        if (!b->ts_list[t].empty()) used[n++] = t;
-    if (!b->pcm_list.empty()) used[n++] = kMaxTermSets;
     if (!b->dsd_list.empty()) used[n++] = kMaxTermSets + 1;
     if (b->dsd_fast_n) used[n++] = kMaxTermSets + 2;
+    if (!b->pcm_list.empty()) used[n++] = kMaxTermSets;
+    for (int t = 0; t < kMaxTermSets; t++)
+        if (!b->ts_list[t].empty()) used[n++] = t;
     auto slot = [&](int g) -> hipStream_t { return n > 1 ? b->side[g] : s; };
     for (int i = 0; n > 1 && i < n; i++) {
         const int g = used[i];
@@ -570,13 +573,13 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
         HIPCHK(c, hipEventRecord(b->fork, s));
         for (int i = 0; i < n; i++) HIPCHK(c, hipStreamWaitEvent(b->side[used[i]], b->fork, 0));
     }
+    HIPCHK(c, launch_decode(b->d_descs, b->d_pcml, (uint32_t)b->pcm_list.size(), b->d_dsd, (uint32_t)b->dsd_list.size(),
+                            b->dsd_fast_lo, b->dsd_fast_n, b->d_blob, b->d_tables, b->d_out, b->d_status, b->d_mute,
+                            slot(kMaxTermSets), slot(kMaxTermSets + 1), slot(kMaxTermSets + 2)));
     for (int t = 0; t < kMaxTermSets; t++)
         if (!b->ts_list[t].empty())
             HIPCHK(c, launch_2wave(t, b->d_descs, b->d_ts[t], (uint32_t)b->ts_list[t].size(), b->d_blob, b->d_out,
                                    b->d_status, b->d_mute, slot(t)));
-    HIPCHK(c, launch_decode(b->d_descs, b->d_pcml, (uint32_t)b->pcm_list.size(), b->d_dsd, (uint32_t)b->dsd_list.size(),
-                            b->dsd_fast_lo, b->dsd_fast_n, b->d_blob, b->d_tables, b->d_out, b->d_status, b->d_mute,
-                            slot(kMaxTermSets), slot(kMaxTermSets + 1), slot(kMaxTermSets + 2)));
     if (n > 1) {
         for (int i = 0; i < n; i++) {
             HIPCHK(c, hipEventRecord(b->join[used[i]], b->side[used[i]]));

@@ -125,6 +125,50 @@ struct ByteSrcWave {
     }
 };
 
+// Payload bytes for the DSD range coders, read four at a time: the
+// big-endian 32 bits starting at a byte offset, from a cached aligned pair of
+// dwords (scalar loads).  Bytes past the payload are whatever follows it in
+// the blob; callers shift in only real ones.
+struct BeSrcWave {
+    const uint32_t *w;
+    uint32_t sh, win_i = 0xFFFFFFFFu, lo = 0, hi = 0;
+    __device__ __forceinline__ void init(const uint8_t *p) {
+        sh = (uint32_t)((uintptr_t)p & 3);
+        w = (const uint32_t *)(p - sh);
+    }
+    __device__ __forceinline__ uint32_t be32(uint32_t bp) {
+        const uint32_t a = bp + sh;
+        const uint32_t i = a >> 2;
+        if (i != win_i) {
+            win_i = i;
+            lo = __builtin_amdgcn_readfirstlane(w[i]);
+            hi = __builtin_amdgcn_readfirstlane(w[i + 1]);
+        }
+        const uint32_t le = (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * (a & 3u)));
+        return (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)__builtin_bswap32(le));
+    }
+};
+
+// The DSD coders' renormalisation (DsdUtils.cs:295-300, 424-429) in one step:
+// the byte loop shifts while the top bytes of high and low agree, and each
+// shift moves high ^ low left by a byte (filling 0xFF), so it runs once per
+// leading zero byte of high ^ low (4 when equal), capped by the bytes left.
+// Call when (high ^ low) < 2^24.
+__device__ __forceinline__ void dsd_renorm(BeSrcWave &src, uint32_t &bp, uint32_t dlen, uint32_t &value,
+                                           uint32_t &high, uint32_t &low) {
+    const uint32_t x = high ^ low;
+    uint32_t n = x ? (uint32_t)__clz(x) >> 3 : 4u;
+    const uint32_t left = dlen - bp;
+    n = n < left ? n : left;
+    if (n == 0) return;
+    const uint32_t s = 8u * n;
+    const uint32_t nb = src.be32(bp);
+    value = (uint32_t)(((uint64_t)value << s) | (nb >> (32u - s)));
+    high = (uint32_t)(((uint64_t)high << s) | ((1ull << s) - 1u));
+    low = (uint32_t)((uint64_t)low << s);
+    bp += n;
+}
+
 // DsdUtils.init_dsd_block_high + decode_high (DsdUtils.cs:343-493) for one
 // block, wave-uniform, with the channel count a compile-time constant so the
 // per-channel filter state (value, filter0..6, factor) lives in scalar
@@ -414,14 +458,15 @@ __device__ __forceinline__ DsdResult dsd_high_v2(const BlockDesc &d, const uint8
     constexpr uint64_t kEven = 0x5555555555555555ull;
     const uint32_t dlen = d.dsd_data_len;
     const int ch = threadIdx.x & 1;
-    ByteSrcWave src;
+    BeSrcWave src;
     src.init(blob + d.bits_off);
     uint32_t bp = 0;
     int32_t crc = -1;
     DsdResult res = {0, 0};
     bool mute = false;
     uint32_t low = 0, high = 0xFFFFFFFFu, value = 0;
-    for (int i = 0; i < 4; i++) value = (value << 8) | src.byte(bp++);
+    value = src.be32(0);  // init_dsd_block_high checked >= 4 payload bytes
+    bp = 4;
     {
         const int32_t *pt0 = (const int32_t *)(tables + d.dsd_table_off);
         for (uint32_t i = threadIdx.x; i < 256; i += 64) ptable[i] = pt0[i];
@@ -472,22 +517,10 @@ __device__ __forceinline__ DsdResult dsd_high_v2(const BlockDesc &d, const uint8
                         pvl = ch ? np0 : pv;
                         wa = ch ? addr : 1024u;
                     }
-                    if (__builtin_expect((high ^ low) < 0x1000000u, 0)) {
-                        while ((high ^ low) < 0x1000000u && bp < dlen) {
-                            value = (value << 8) | src.byte(bp++);
-                            high = (high << 8) | 0xFF;
-                            low <<= 8;
-                        }
-                    }
+                    if (__builtin_expect((high ^ low) < 0x1000000u, 0)) dsd_renorm(src, bp, dlen, value, high, low);
                     // channel 1's decision
                     const uint64_t zm1 = dsd_decide(value, s1, high, low, b1, ~kEven);
-                    if (__builtin_expect((high ^ low) < 0x1000000u, 0)) {
-                        while ((high ^ low) < 0x1000000u && bp < dlen) {
-                            value = (value << 8) | src.byte(bp++);
-                            high = (high << 8) | 0xFF;
-                            low <<= 8;
-                        }
-                    }
+                    if (__builtin_expect((high ^ low) < 0x1000000u, 0)) dsd_renorm(src, bp, dlen, value, high, low);
                     // this lane's channel's outcome
                     const bool zl = __builtin_amdgcn_inverse_ballot_w64(zm0 | zm1);
                     *(int32_t *)(lds + wa) = pvl + (((zl ? kUp : kDown) - pvl) >> 8);
@@ -708,10 +741,141 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_wave(const BlockD
     }
 }
 
-// DsdUtils mode 1 (decode_fast, DsdUtils.cs:149-304), one wave per block with
-// the block's prob / summed / lookup / value_lookup tables copied to LDS first
-// (at most 32 history bins: 65,664 B).  Launched over the mode-1 part of the
-// DSD list (the list is sorted by kind); wv_decode_dsd_wave skips those blocks.
+// DsdUtils mode 1 (decode_fast, DsdUtils.cs:244-304) without its two 32-bit
+// divisions per symbol.  The block's cumulative table (summed_probabilities,
+// widened to u32) sits in LDS, one 1-KiB row per history bin; lane L holds the
+// current bin's entries 4L..4L+3.  Per symbol:
+//  * mult = (high - low) / tot by an invariant-divisor reciprocal
+//    (Granlund-Montgomery: one mul_hi, four shifts/adds) whose constants lane b
+//    holds for bin b and the wave reads with v_readlane;
+//  * the decoded code is lookup[value_lookup[p0] + (value - low) / mult], i.e.
+//    the number of entries with summed[i] <= (value - low) / mult, i.e. with
+//    summed[i] * mult <= value - low (no product overflows: summed[i] <= tot
+//    and tot * mult <= high - low): four products and compares per lane and a
+//    popcount of the four ballots.  All 256 true <=> index >= tot (the C#
+//    `return 0`);
+//  * low and high move by summed[code - 1] * mult and summed[code] * mult, the
+//    products themselves, picked in the lane that holds entry `code` (entry
+//    code - 1 may be the previous lane's last one: a wave shift).
+// Stereo reads the next symbol's row (p1) a symbol ahead.  Same results and
+// status bits as dsd_simple_wave<WCH, true> (DsdUtils.cs:149-304).
+template <int WCH>
+__device__ __forceinline__ DsdResult dsd_fast_v2(const BlockDesc &d, const uint8_t *blob, const uint32_t *rows,
+                                                 uint32_t vtot, uint32_t vmag, uint32_t vsh1, uint32_t vsh2,
+                                                 DevStoreWave &out) {
+    using namespace wvf;
+    const bool fstereo = (d.flags & FALSE_STEREO) != 0;
+    const uint32_t och = (d.flags & MONO_FLAG) ? 1u : 2u;
+    const uint32_t dlen = d.dsd_data_len;
+    const uint32_t lane = threadIdx.x;
+    BeSrcWave src;
+    src.init(blob + d.bits_off);
+    const uint32_t bmask = (uint32_t)d.dsd_history_bins - 1u;
+    uint32_t bp = 0;
+    int32_t crc = -1;
+    DsdResult res = {0, 0};
+    bool mute = false;
+    uint32_t low = 0, high = 0xFFFFFFFFu, value = 0;
+    uint32_t p0 = 0, p1 = 0;
+    value = src.be32(0);  // init_dsd_block_fast checked >= 4 payload bytes
+    bp = 4;
+    uint4 row = *(const uint4 *)(rows + lane * 4u);  // bin 0
+    uint32_t f = 0, chunk_len = d.first_chunk, ci = 0;
+    while (f < d.nframes) {
+        uint32_t n = chunk_len;
+        if (n > d.nframes - f) n = d.nframes - f;
+        bool chunk_ok = true;
+        if (!mute) {
+            for (uint32_t j = 0; j < n && chunk_ok; j++) {
+                int32_t v[2] = {0, 0};
+#pragma unroll
+                for (int c = 0; c < WCH; c++) {
+                    // the next symbol's row, while this one decodes (stereo: its bin is known)
+                    uint4 nrow;
+                    if (WCH == 2) nrow = *(const uint4 *)(rows + p1 * 256u + lane * 4u);
+                    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int32_t)vtot, (int32_t)p0);
+                    if (tot == 0) { chunk_ok = false; break; }
+                    const uint32_t mag = (uint32_t)__builtin_amdgcn_readlane((int32_t)vmag, (int32_t)p0);
+                    const uint32_t s1 = (uint32_t)__builtin_amdgcn_readlane((int32_t)vsh1, (int32_t)p0);
+                    const uint32_t s2 = (uint32_t)__builtin_amdgcn_readlane((int32_t)vsh2, (int32_t)p0);
+                    uint32_t range = high - low;
+                    uint32_t t1 = __umulhi(mag, range);
+                    uint32_t mult = (t1 + ((range - t1) >> s1)) >> s2;
+                    if (__builtin_expect(mult == 0, 0)) {
+                        if (dlen - bp >= 4) {
+                            value = src.be32(bp);
+                            bp += 4;
+                        }
+                        low = 0;
+                        high = 0xFFFFFFFFu;
+                        t1 = __umulhi(mag, high);
+                        mult = (t1 + ((high - t1) >> s1)) >> s2;
+                        if (mult == 0) { chunk_ok = false; break; }
+                    }
+                    const uint32_t x = value - low;
+                    const uint32_t q0 = row.x * mult, q1 = row.y * mult, q2 = row.z * mult, q3 = row.w * mult;
+                    const bool c0 = q0 <= x, c1 = q1 <= x, c2 = q2 <= x, c3 = q3 <= x;
+                    const uint32_t code = (uint32_t)(__popcll(__ballot(c0)) + __popcll(__ballot(c1)) +
+                                                     __popcll(__ballot(c2)) + __popcll(__ballot(c3)));
+                    if (code >= 256u) { chunk_ok = false; break; }  // index >= tot
+                    const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int32_t)q3, 0x138, 0xf, 0xf, true);
+                    const uint32_t hi_l = c0 ? (c1 ? (c2 ? q3 : q2) : q1) : q0;
+                    const uint32_t lo_l = c3 ? q3 : (c2 ? q2 : (c1 ? q1 : (c0 ? q0 : prev)));
+                    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int32_t)hi_l, (int32_t)(code >> 2));
+                    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int32_t)lo_l, (int32_t)(code >> 2));
+                    high = low + hi - 1u;
+                    low = low + lo;
+                    if (WCH == 1) {
+                        p0 = code & bmask;
+                        row = *(const uint4 *)(rows + p0 * 256u + lane * 4u);
+                    } else {
+                        p0 = p1;
+                        p1 = code & bmask;
+                        row = nrow;
+                    }
+                    if ((high ^ low) < 0x1000000u) dsd_renorm(src, bp, dlen, value, high, low);
+                    v[c] = (int32_t)code;
+                }
+                if (!chunk_ok) break;
+#pragma unroll
+                for (int c = 0; c < WCH; c++) crc = add32(crc, add32(shl32(crc, 1), v[c]));
+                const uint64_t o = (uint64_t)(f + j) * och;
+                if (WCH == 1 && !fstereo) {
+                    out.put(o, v[0]);
+                } else if (fstereo) {
+                    out.put(o, v[0]);
+                    out.put(o + 1, v[0]);
+                } else {
+                    out.put(o, v[0]);
+                    out.put(o + 1, v[1]);
+                }
+            }
+            if (!chunk_ok) {
+                mute = true;
+                res.status |= ST_NONDET;  // the rest of this chunk's region keeps stale caller data
+            }
+            if (!mute && f + n == d.block_samples && crc != d.crc) mute = true;
+        }
+        if (mute && !(res.status & ST_DSD_MUTE)) {
+            res.status |= ST_DSD_MUTE;
+            res.mute_chunk = ci;
+        }
+        f += n;
+        chunk_len = next_call_len(d, f);
+        ci++;
+    }
+    if (d.nframes == d.block_samples) {
+        res.status |= ST_CRC_CHECKED;
+        if (crc != d.crc) res.status |= ST_CRC_ERROR;
+    }
+    return res;
+}
+
+// Mode 1: one wave per block, its tables staged in LDS first.  Launched over
+// the mode-1 part of the DSD list (the list is sorted by kind);
+// wv_decode_dsd_wave skips those blocks.  Default: dsd_fast_v2 (rows of u32
+// cumulative counts, 32 KiB at 32 bins); WV_DSD_FAST_V1: the division path over
+// the raw tables (65,664 B).
 constexpr uint32_t kDsdFastLds = 32u * 2052u;
 extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_fast(const BlockDesc *__restrict__ descs,
                                                                     const uint32_t *__restrict__ list,
@@ -725,18 +889,43 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_fast(const BlockD
     const BlockDesc &d = descs[bi];
     const bool lead = threadIdx.x == 0;
     const uint32_t bins = (uint32_t)d.dsd_history_bins;
+    DevStoreWave st{out + d.out_off, (uint64_t)d.pre_end * d.out_nch, lead};
+    DsdResult r;
+#ifdef WV_DSD_FAST_V1
     const uint32_t nw = bins <= 32u ? (bins * 2052u + 3u) / 4u : 0u;
     const uint32_t *src = (const uint32_t *)(tables + d.dsd_table_off);  // 16-B aligned by the framing
     for (uint32_t i = threadIdx.x; i < nw; i += 64) tab[i] = src[i];
     __syncthreads();
-    DevStoreWave st{out + d.out_off, (uint64_t)d.pre_end * d.out_nch, lead};
-    DsdResult r;
     if (bins > 32u)  // not produced by the framing (init_dsd_block_fast rejects > 5 history bits)
         r = decode_dsd_block(d, blob, tables, nullptr, st);
     else
         r = (d.flags & wvf::MONO_DATA)
                 ? dsd_simple_wave<1, true, DsdTablesLds>(d, blob, tables, st, (const uint8_t *)tab)
                 : dsd_simple_wave<2, true, DsdTablesLds>(d, blob, tables, st, (const uint8_t *)tab);
+#else
+    // summed_probabilities (u16, after the bins x 256 probability bytes) widened to u32 rows
+    const uint16_t *sum16 = (const uint16_t *)(tables + d.dsd_table_off + (size_t)bins * 256u);
+    const uint32_t ne = bins <= 32u ? bins * 256u : 0u;
+    for (uint32_t i = threadIdx.x; i < ne; i += 64) tab[i] = sum16[i];
+    // lane b: bin b's total and the reciprocal constants of dividing by it
+    uint32_t vtot = 0, vmag = 0, vsh1 = 0, vsh2 = 0;
+    if (threadIdx.x < bins && bins <= 32u) {
+        const uint32_t dv = sum16[threadIdx.x * 256u + 255u];
+        if (dv) {
+            const uint32_t l = dv > 1u ? 32u - (uint32_t)__clz(dv - 1u) : 0u;  // ceil(log2 dv)
+            vmag = (uint32_t)(((((uint64_t)1 << l) - dv) << 32) / dv) + 1u;
+            vsh1 = l ? 1u : 0u;
+            vsh2 = l ? l - 1u : 0u;
+        }
+        vtot = dv;
+    }
+    __syncthreads();
+    if (bins > 32u)  // not produced by the framing (init_dsd_block_fast rejects > 5 history bits)
+        r = decode_dsd_block(d, blob, tables, nullptr, st);
+    else
+        r = (d.flags & wvf::MONO_DATA) ? dsd_fast_v2<1>(d, blob, tab, vtot, vmag, vsh1, vsh2, st)
+                                       : dsd_fast_v2<2>(d, blob, tab, vtot, vmag, vsh1, vsh2, st);
+#endif
     if (lead) {
         status[bi] = d.fstatus | r.status;
         mute_chunk[bi] = r.mute_chunk;
@@ -915,8 +1104,7 @@ hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint3
                          uint32_t n_dsd, uint32_t fast_lo, uint32_t n_fast, const uint8_t *blob, const uint8_t *tables,
                          int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s_pcm, hipStream_t s_dsd,
                          hipStream_t s_fast) {
-    if (n_pcm)
-        hipLaunchKernelGGL(wv_decode_pcm_wave, dim3(n_pcm), dim3(64), 0, s_pcm, descs, pcm_list, blob, out, status, aux);
+    // the DSD kernels first: their blocks are the batch's longest serial chains
     const uint32_t skip = n_fast ? 1u : 0u;
     if (n_dsd > n_fast) {
         hipLaunchKernelGGL(wv_decode_dsd_wave, dim3(n_dsd), dim3(64), 0, s_dsd, descs, dsd_list, blob, tables, out,
@@ -931,6 +1119,8 @@ hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint3
         hipLaunchKernelGGL(wv_dsd_fill, dim3((n_fast + 63) / 64), dim3(64), 0, s_fast, descs, fl, n_fast, status, aux,
                            out, 0u);
     }
+    if (n_pcm)
+        hipLaunchKernelGGL(wv_decode_pcm_wave, dim3(n_pcm), dim3(64), 0, s_pcm, descs, pcm_list, blob, out, status, aux);
     return hipGetLastError();
 }
 
