@@ -718,6 +718,11 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_wave(const BlockD
     const bool lead = threadIdx.x == 0;
     DevStoreWave st{out + d.out_off, (uint64_t)d.pre_end * d.out_nch, lead};
     DsdResult r;
+#ifndef WV_NO_DSD_PRIO
+    // a mode-3 block is the batch's longest serial chain: its wave wins the
+    // issue arbitration against the PCM waves sharing its SIMD
+    if (d.kind == KIND_DSD_HIGH) __builtin_amdgcn_s_setprio(3);
+#endif
     if (d.kind == KIND_DSD_HIGH)
         r = (d.flags & wvf::MONO_DATA) ? dsd_high_wave<1>(d, blob, tables, pt_lds, st)
 #if defined(WV_DSD_HIGH_SCALAR)
