@@ -125,47 +125,60 @@ struct ByteSrcWave {
     }
 };
 
-// Payload bytes for the DSD range coders, read four at a time: the
-// big-endian 32 bits starting at a byte offset, from a cached aligned pair of
-// dwords (scalar loads).  Bytes past the payload are whatever follows it in
-// the blob; callers shift in only real ones.
-struct BeSrcWave {
+// Payload bytes for the DSD range coders: a 64-bit big-endian window of the
+// next bytes (byte bp in bits 63..56), refilled a dword at a time from a
+// dword loaded one refill ahead (scalar loads, so the load latency is off the
+// decode chain).  Reads run at most 12 bytes past the consumed position:
+// inside the blob's 64-byte 0xFF tail at worst; bytes past the payload are
+// never shifted in (callers cap n by the bytes left).
+struct DsdWin {
     const uint32_t *w;
-    uint32_t sh, win_i = 0xFFFFFFFFu, lo = 0, hi = 0;
-    __device__ __forceinline__ void init(const uint8_t *p) {
-        sh = (uint32_t)((uintptr_t)p & 3);
-        w = (const uint32_t *)(p - sh);
+    uint64_t win;
+    uint32_t avail;  // loaded bytes in win, >= 4 between calls
+    uint32_t ni;     // index of the dword in nxt
+    uint32_t nxt;
+    static __device__ __forceinline__ uint32_t bswap_u(uint32_t x) {
+        return (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)__builtin_bswap32(x));
     }
-    __device__ __forceinline__ uint32_t be32(uint32_t bp) {
-        const uint32_t a = bp + sh;
-        const uint32_t i = a >> 2;
-        if (i != win_i) {
-            win_i = i;
-            lo = __builtin_amdgcn_readfirstlane(w[i]);
-            hi = __builtin_amdgcn_readfirstlane(w[i + 1]);
-        }
-        const uint32_t le = (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * (a & 3u)));
-        return (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)__builtin_bswap32(le));
+    __device__ __forceinline__ void init(const uint8_t *p) {
+        const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
+        w = (const uint32_t *)(p - sh);
+        win = (uint64_t)bswap_u(__builtin_amdgcn_readfirstlane(w[0])) << (32u + 8u * sh);
+        avail = 4u - sh;
+        nxt = __builtin_amdgcn_readfirstlane(w[1]);
+        ni = 2;
+        refill();
+    }
+    __device__ __forceinline__ void refill() {  // avail <= 4
+        win |= (uint64_t)bswap_u(nxt) << (32u - 8u * avail);
+        avail += 4u;
+        nxt = __builtin_amdgcn_readfirstlane(w[ni]);
+        ni++;
+    }
+    // v shifted left by n bytes (s = 8n, n <= 4) with the next n bytes below it
+    __device__ __forceinline__ uint32_t shift_in(uint32_t v, uint32_t s, uint32_t n) {
+        const uint64_t t = ((((uint64_t)v << 32) | (win >> 32)) << s) >> 32;
+        win <<= s;
+        avail -= n;
+        if (avail < 4u) refill();
+        return (uint32_t)t;
     }
 };
 
 // The DSD coders' renormalisation (DsdUtils.cs:295-300, 424-429) in one step:
 // the byte loop shifts while the top bytes of high and low agree, and each
 // shift moves high ^ low left by a byte (filling 0xFF), so it runs once per
-// leading zero byte of high ^ low (4 when equal), capped by the bytes left.
-// Call when (high ^ low) < 2^24.
-__device__ __forceinline__ void dsd_renorm(BeSrcWave &src, uint32_t &bp, uint32_t dlen, uint32_t &value,
-                                           uint32_t &high, uint32_t &low) {
-    const uint32_t x = high ^ low;
-    uint32_t n = x ? (uint32_t)__clz(x) >> 3 : 4u;
+// leading zero byte of high ^ low (4 when equal; none when the top bytes
+// differ), capped by the payload bytes left.  Branch-free.
+__device__ __forceinline__ void dsd_renorm(DsdWin &src, uint32_t &bp, uint32_t dlen, uint32_t &value, uint32_t &high,
+                                           uint32_t &low) {
+    uint32_t n = (uint32_t)__clz(high ^ low) >> 3;
     const uint32_t left = dlen - bp;
     n = n < left ? n : left;
-    if (n == 0) return;
     const uint32_t s = 8u * n;
-    const uint32_t nb = src.be32(bp);
-    value = (uint32_t)(((uint64_t)value << s) | (nb >> (32u - s)));
-    high = (uint32_t)(((uint64_t)high << s) | ((1ull << s) - 1u));
-    low = (uint32_t)((uint64_t)low << s);
+    value = src.shift_in(value, s, n);
+    high = (uint32_t)(((((uint64_t)high << 32) | 0xFFFFFFFFu) << s) >> 32);
+    low = (uint32_t)((((uint64_t)low << 32) << s) >> 32);
     bp += n;
 }
 
@@ -458,14 +471,14 @@ __device__ __forceinline__ DsdResult dsd_high_v2(const BlockDesc &d, const uint8
     constexpr uint64_t kEven = 0x5555555555555555ull;
     const uint32_t dlen = d.dsd_data_len;
     const int ch = threadIdx.x & 1;
-    BeSrcWave src;
+    DsdWin src;
     src.init(blob + d.bits_off);
     uint32_t bp = 0;
     int32_t crc = -1;
     DsdResult res = {0, 0};
     bool mute = false;
     uint32_t low = 0, high = 0xFFFFFFFFu, value = 0;
-    value = src.be32(0);  // init_dsd_block_high checked >= 4 payload bytes
+    value = src.shift_in(0, 32, 4);  // init_dsd_block_high checked >= 4 payload bytes
     bp = 4;
     {
         const int32_t *pt0 = (const int32_t *)(tables + d.dsd_table_off);
@@ -766,14 +779,14 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_wave(const BlockD
 // status bits as dsd_simple_wave<WCH, true> (DsdUtils.cs:149-304).
 template <int WCH>
 __device__ __forceinline__ DsdResult dsd_fast_v2(const BlockDesc &d, const uint8_t *blob, const uint32_t *rows,
-                                                 uint32_t vtot, uint32_t vmag, uint32_t vsh1, uint32_t vsh2,
+                                                 uint32_t vmag, uint32_t vsh1, uint32_t vsh2,
                                                  DevStoreWave &out) {
     using namespace wvf;
     const bool fstereo = (d.flags & FALSE_STEREO) != 0;
     const uint32_t och = (d.flags & MONO_FLAG) ? 1u : 2u;
     const uint32_t dlen = d.dsd_data_len;
     const uint32_t lane = threadIdx.x;
-    BeSrcWave src;
+    DsdWin src;
     src.init(blob + d.bits_off);
     const uint32_t bmask = (uint32_t)d.dsd_history_bins - 1u;
     uint32_t bp = 0;
@@ -782,7 +795,7 @@ __device__ __forceinline__ DsdResult dsd_fast_v2(const BlockDesc &d, const uint8
     bool mute = false;
     uint32_t low = 0, high = 0xFFFFFFFFu, value = 0;
     uint32_t p0 = 0, p1 = 0;
-    value = src.be32(0);  // init_dsd_block_fast checked >= 4 payload bytes
+    value = src.shift_in(0, 32, 4);  // init_dsd_block_fast checked >= 4 payload bytes
     bp = 4;
     uint4 row = *(const uint4 *)(rows + lane * 4u);  // bin 0
     uint32_t f = 0, chunk_len = d.first_chunk, ci = 0;
@@ -798,8 +811,10 @@ __device__ __forceinline__ DsdResult dsd_fast_v2(const BlockDesc &d, const uint8
                     // the next symbol's row, while this one decodes (stereo: its bin is known)
                     uint4 nrow;
                     if (WCH == 2) nrow = *(const uint4 *)(rows + p1 * 256u + lane * 4u);
-                    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int32_t)vtot, (int32_t)p0);
-                    if (tot == 0) { chunk_ok = false; break; }
+                    // (a bin with no counts, the C#'s first `return 0`, has an all-zero row: every
+                    // product below is <= value - low, so code = 256 fails it; mult is then
+                    // range (zero constants) and a mult == 0 reload before that changes nothing
+                    // the failed chunk leaves behind)
                     const uint32_t mag = (uint32_t)__builtin_amdgcn_readlane((int32_t)vmag, (int32_t)p0);
                     const uint32_t s1 = (uint32_t)__builtin_amdgcn_readlane((int32_t)vsh1, (int32_t)p0);
                     const uint32_t s2 = (uint32_t)__builtin_amdgcn_readlane((int32_t)vsh2, (int32_t)p0);
@@ -808,7 +823,7 @@ __device__ __forceinline__ DsdResult dsd_fast_v2(const BlockDesc &d, const uint8
                     uint32_t mult = (t1 + ((range - t1) >> s1)) >> s2;
                     if (__builtin_expect(mult == 0, 0)) {
                         if (dlen - bp >= 4) {
-                            value = src.be32(bp);
+                            value = src.shift_in(value, 32, 4);
                             bp += 4;
                         }
                         low = 0;
@@ -838,7 +853,7 @@ __device__ __forceinline__ DsdResult dsd_fast_v2(const BlockDesc &d, const uint8
                         p1 = code & bmask;
                         row = nrow;
                     }
-                    if ((high ^ low) < 0x1000000u) dsd_renorm(src, bp, dlen, value, high, low);
+                    dsd_renorm(src, bp, dlen, value, high, low);  // branch-free: ~a byte per symbol
                     v[c] = (int32_t)code;
                 }
                 if (!chunk_ok) break;
@@ -913,7 +928,7 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_fast(const BlockD
     const uint32_t ne = bins <= 32u ? bins * 256u : 0u;
     for (uint32_t i = threadIdx.x; i < ne; i += 64) tab[i] = sum16[i];
     // lane b: bin b's total and the reciprocal constants of dividing by it
-    uint32_t vtot = 0, vmag = 0, vsh1 = 0, vsh2 = 0;
+    uint32_t vmag = 0, vsh1 = 0, vsh2 = 0;  // all zero for an empty bin (see dsd_fast_v2)
     if (threadIdx.x < bins && bins <= 32u) {
         const uint32_t dv = sum16[threadIdx.x * 256u + 255u];
         if (dv) {
@@ -922,14 +937,13 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_fast(const BlockD
             vsh1 = l ? 1u : 0u;
             vsh2 = l ? l - 1u : 0u;
         }
-        vtot = dv;
     }
     __syncthreads();
     if (bins > 32u)  // not produced by the framing (init_dsd_block_fast rejects > 5 history bits)
         r = decode_dsd_block(d, blob, tables, nullptr, st);
     else
-        r = (d.flags & wvf::MONO_DATA) ? dsd_fast_v2<1>(d, blob, tab, vtot, vmag, vsh1, vsh2, st)
-                                       : dsd_fast_v2<2>(d, blob, tab, vtot, vmag, vsh1, vsh2, st);
+        r = (d.flags & wvf::MONO_DATA) ? dsd_fast_v2<1>(d, blob, tab, vmag, vsh1, vsh2, st)
+                                       : dsd_fast_v2<2>(d, blob, tab, vmag, vsh1, vsh2, st);
 #endif
     if (lead) {
         status[bi] = d.fstatus | r.status;
