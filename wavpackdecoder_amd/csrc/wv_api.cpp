@@ -23,6 +23,8 @@ int term_set_of(const BlockDesc &d, int prefer_pipe);
 hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, uint32_t n, const uint8_t *blob,
                         int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s);
 hipError_t launch_format(const FormatSeg *segs, uint32_t nseg, const int32_t *in, uint8_t *out, int dsd, hipStream_t s);
+hipError_t launch_dsd_fill(const BlockDesc *descs, const uint32_t *dsd_list, uint32_t n_dsd, const uint32_t *status,
+                           const uint32_t *aux, int32_t *out, hipStream_t s);
 hipError_t launch_meta(BlockDesc *descs, const MetaJob *jobs, uint32_t njobs, const MetaItem *items, const uint8_t *blob,
                        hipStream_t s);
 constexpr int kMaxTermSets = 8;
@@ -586,6 +588,7 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
             HIPCHK(c, hipStreamWaitEvent(s, b->join[used[i]], 0));
         }
     }
+    HIPCHK(c, launch_dsd_fill(b->d_descs, b->d_dsd, (uint32_t)b->dsd_list.size(), b->d_status, b->d_mute, b->d_out, s));
     if (b->timing) HIPCHK(c, hipEventRecord(b->tev.back(), s));
     HIPCHK(c, hipEventRecord(b->done, s));
     b->downloaded = false;

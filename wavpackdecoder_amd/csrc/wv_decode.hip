@@ -956,12 +956,11 @@ extern "C" __global__ void __launch_bounds__(64) wv_dsd_fill(const BlockDesc *__
                                                              const uint32_t *__restrict__ list, uint32_t n,
                                                              const uint32_t *__restrict__ status,
                                                              const uint32_t *__restrict__ mute_chunk,
-                                                             int32_t *__restrict__ out, uint32_t skip_fast) {
+                                                             int32_t *__restrict__ out) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint32_t bi = list[i];
     const BlockDesc &d = descs[bi];
-    if (skip_fast && d.kind == KIND_DSD_FAST) return;  // filled on the mode-1 stream
     if (!(status[bi] & ST_DSD_MUTE)) return;
     uint32_t f = 0, cl = d.first_chunk, mc = mute_chunk[bi];
     for (uint32_t ci = 0; f < d.nframes; ci++) {
@@ -1115,10 +1114,9 @@ hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, ui
 namespace wvg {
 
 // PCM blocks without a two-wave instantiation (generic wave kernel) on s_pcm;
-// DSD blocks (decode, then the mute fills that depend on it) on s_dsd
 // DSD blocks: the mode-1 range [fast_lo, fast_lo + n_fast) of the kind-sorted
-// list by wv_decode_dsd_fast on its own stream (then its mute fills), every
-// other DSD block by one wv_decode_dsd_wave launch (then their fills)
+// list by wv_decode_dsd_fast on s_fast, every other DSD block by one
+// wv_decode_dsd_wave launch on s_dsd (mute fills: launch_dsd_fill, after the join)
 hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint32_t n_pcm, const uint32_t *dsd_list,
                          uint32_t n_dsd, uint32_t fast_lo, uint32_t n_fast, const uint8_t *blob, const uint8_t *tables,
                          int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s_pcm, hipStream_t s_dsd,
@@ -1128,18 +1126,25 @@ hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint3
     if (n_dsd > n_fast) {
         hipLaunchKernelGGL(wv_decode_dsd_wave, dim3(n_dsd), dim3(64), 0, s_dsd, descs, dsd_list, blob, tables, out,
                            status, aux, skip);
-        hipLaunchKernelGGL(wv_dsd_fill, dim3((n_dsd + 63) / 64), dim3(64), 0, s_dsd, descs, dsd_list, n_dsd, status,
-                           aux, out, skip);
     }
     if (n_fast) {
         const uint32_t *fl = dsd_list + fast_lo;
         hipLaunchKernelGGL(wv_decode_dsd_fast, dim3(n_fast), dim3(64), 0, s_fast, descs, fl, blob, tables, out, status,
                            aux);
-        hipLaunchKernelGGL(wv_dsd_fill, dim3((n_fast + 63) / 64), dim3(64), 0, s_fast, descs, fl, n_fast, status, aux,
-                           out, 0u);
     }
     if (n_pcm)
         hipLaunchKernelGGL(wv_decode_pcm_wave, dim3(n_pcm), dim3(64), 0, s_pcm, descs, pcm_list, blob, out, status, aux);
+    return hipGetLastError();
+}
+
+// the 0x55 mute fills of every DSD block (quirk B-9), on the batch stream after
+// every decode launch has joined it: a fill starts at its call's buffer start,
+// i.e. inside the output of earlier blocks of the same call, which may be PCM
+// or DSD blocks decoded on other streams
+hipError_t launch_dsd_fill(const BlockDesc *descs, const uint32_t *dsd_list, uint32_t n_dsd, const uint32_t *status,
+                           const uint32_t *aux, int32_t *out, hipStream_t s) {
+    if (!n_dsd) return hipSuccess;
+    hipLaunchKernelGGL(wv_dsd_fill, dim3((n_dsd + 63) / 64), dim3(64), 0, s, descs, dsd_list, n_dsd, status, aux, out);
     return hipGetLastError();
 }
 
