@@ -136,16 +136,59 @@ int64_t emu_frame_descs(const uint8_t *file, size_t len, int64_t seek_to, int ch
     return (int64_t)fo.descs.size();
 }
 
-// FileInfo fields of the host framing, for the WavpackGet* getters' tests.
-int emu_file_info(const uint8_t *file, size_t len, int64_t *vals, int nvals) {
-    FramingOutput fo;
-    FileInfo info;
-    frame_file(file, len, 0, 0, 0, 4096, fo, info);
+static int info_vals(const FileInfo &info, int64_t ndesc, int64_t *vals, int nvals) {
     int64_t v[] = {info.open_ok, info.total_samples, info.sample_rate, info.num_channels, info.bits_per_sample,
                    info.bytes_per_sample, info.reduced_channels, info.mode, info.version, info.is_float,
-                   info.out_frames, info.out_nch, (int64_t)fo.descs.size(), (int64_t)info.dsd_multiplier};
+                   info.out_frames, info.out_nch, ndesc, (int64_t)info.dsd_multiplier,
+                   info.lossy_blocks, info.is_five, info.file_format, info.header_off, info.header_len,
+                   info.trailer_off, info.trailer_len, info.first_call_frames, info.config_flags,
+                   info.sample_index0, info.exception, info.nondet};
     int n = (int)(sizeof(v) / sizeof(v[0]));
     for (int i = 0; i < n && i < nvals; i++) vals[i] = v[i];
     return n;
+}
+
+// FileInfo fields of the host framing, for the WavpackGet* getters' tests.
+int emu_file_info_chunk(const uint8_t *file, size_t len, int chunk, int64_t *vals, int nvals) {
+    FramingOutput fo;
+    FileInfo info;
+    frame_file(file, len, 0, 0, 0, chunk, fo, info);
+    return info_vals(info, (int64_t)fo.descs.size(), vals, nvals);
+}
+int emu_file_info(const uint8_t *file, size_t len, int64_t *vals, int nvals) {
+    return emu_file_info_chunk(file, len, 4096, vals, nvals);
+}
+
+// The device framing (wv_dframe.h) run on the host, one file: the walk, every
+// block's descriptor, the host-side FileInfo reduction.  Returns the block
+// count, or -(1 + why) when the file is left to the host framing (*why: the
+// DF_* reason, 9 = the blocks' records disagree).
+int64_t emu_dframe(const uint8_t *file, size_t len, int chunk, void *descs, int64_t cap_bytes, int64_t *vals,
+                   int nvals) {
+    DFile df;
+    memset(&df, 0, sizeof(df));
+    df.base = 0;
+    df.len = len;
+    df.slot = 0;
+    df.chunk = (uint32_t)chunk;
+    std::vector<uint64_t> slots(len / 32 + 1);
+    dframe_walk(df, file, slots.data());
+    if (!df.regular) return -1 - (int64_t)df.why;
+    std::vector<BlockDesc> d(df.nblocks);
+    std::vector<DBlock> r(df.nblocks);
+    df.out_base = 0;
+    df.first_desc = 0;
+    for (uint32_t k = 0; k < df.nblocks; k++) dframe_block(df, k, file, slots.data(), d[k], r[k]);
+    FileInfo fi;
+    if (!dframe_file_info(df, r.data(), fi)) {
+        for (uint32_t k = 0; k < df.nblocks; k++)
+            if (!r[k].regular) return -1 - (int64_t)r[k].why;
+        return -1 - (int64_t)DF_UNIFORM;
+    }
+    const int64_t nb = (int64_t)(d.size() * sizeof(BlockDesc));
+    if (nb > cap_bytes) return -100;
+    memcpy(descs, d.data(), (size_t)nb);
+    info_vals(fi, (int64_t)df.nblocks, vals, nvals);
+    return (int64_t)df.nblocks;
 }
 }

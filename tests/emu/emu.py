@@ -70,3 +70,47 @@ def file_info(data: bytes) -> dict:
     vals = np.zeros(len(INFO_FIELDS), dtype=np.int64)
     lib().emu_file_info(data, len(data), vals.ctypes.data, len(INFO_FIELDS))
     return dict(zip(INFO_FIELDS, (int(v) for v in vals)))
+
+
+INFO_FIELDS_FULL = INFO_FIELDS + ("lossy_blocks", "is_five", "file_format", "header_off", "header_len", "trailer_off",
+                                  "trailer_len", "first_call_frames", "config_flags", "sample_index0", "exception",
+                                  "nondet")
+DESC_BYTES = 1408  # sizeof(BlockDesc)
+
+
+def file_info_full(data: bytes, chunk: int = 4096) -> dict:
+    f = lib().emu_file_info_chunk
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    vals = np.zeros(len(INFO_FIELDS_FULL), dtype=np.int64)
+    f(data, len(data), chunk, vals.ctypes.data, len(vals))
+    return dict(zip(INFO_FIELDS_FULL, (int(v) for v in vals)))
+
+
+def frame_descs(data: bytes, chunk: int = 4096, seek: int = -1) -> bytes:
+    """host framing (deferred values applied) -> descriptor bytes"""
+    f = lib().emu_frame_descs
+    f.restype = ctypes.c_int64
+    f.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                  ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
+    cap = (len(data) // 32 + 16) * DESC_BYTES
+    out = np.zeros(cap, np.uint8)
+    nj = ctypes.c_int64(0)
+    n = f(data, len(data), seek, chunk, 1, out.ctypes.data, cap, ctypes.byref(nj))
+    assert n >= 0
+    return out[: n * DESC_BYTES].tobytes()
+
+
+def dframe(data: bytes, chunk: int = 4096):
+    """device framing run on the host -> (descriptor bytes, info dict) or (None, why)"""
+    f = lib().emu_dframe
+    f.restype = ctypes.c_int64
+    f.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                  ctypes.c_int]
+    cap = (len(data) // 32 + 16) * DESC_BYTES
+    out = np.zeros(cap, np.uint8)
+    vals = np.zeros(len(INFO_FIELDS_FULL), dtype=np.int64)
+    n = f(data, len(data), chunk, out.ctypes.data, cap, vals.ctypes.data, len(vals))
+    if n < 0:
+        return None, int(-n - 1)
+    return out[: n * DESC_BYTES].tobytes(), dict(zip(INFO_FIELDS_FULL, (int(v) for v in vals)))

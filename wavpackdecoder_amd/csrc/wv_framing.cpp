@@ -1042,6 +1042,55 @@ int64_t file_out_extent(const FramingOutput &out, const FileInfo &info, uint64_t
     return extent;
 }
 
+bool dframe_file_info(const DFile &df, const DBlock *r, FileInfo &info) {
+    if (!df.regular || df.nblocks == 0) return false;
+    // state the host would carry from block to block must be re-sent the same way in
+    // every block (INT32/FLOAT info), and the channel count must not change
+    const int32_t mask0 = r[0].info_mask;
+    bool lossy = false, five = false;
+    int32_t file_format = 0;
+    int64_t hoff = -1, hlen = 0, toff = -1, tlen = 0;
+    for (uint32_t k = 0; k < df.nblocks; k++) {
+        const DBlock &b = r[k];
+        if (!b.regular || b.info_mask != mask0 || (b.num_channels >= 0 && b.num_channels != df.num_channels))
+            return false;
+        lossy |= b.lossy != 0;
+        five |= b.five != 0;
+        if (b.file_format >= 0) file_format = b.file_format;
+        if (b.header_off >= 0) hoff = b.header_off, hlen = b.header_len;
+        if (b.trailer_off >= 0) toff = b.trailer_off, tlen = b.trailer_len;
+    }
+    const uint64_t blob_base = info.blob_base;
+    const int64_t first_desc = info.first_desc;
+    info = FileInfo();
+    info.blob_base = blob_base;
+    info.first_desc = first_desc;
+    info.num_desc = df.nblocks;
+    info.open_ok = 1;
+    info.num_channels = df.num_channels;
+    info.reduced_channels = 0;
+    info.bits_per_sample = df.bits_per_sample;
+    info.bytes_per_sample = df.bytes_per_sample;
+    info.version = df.version;
+    info.mode = df.mode;
+    info.is_float = df.is_float;
+    info.sample_rate = df.sample_rate;
+    info.total_samples = df.total_samples;
+    info.config_flags = df.config_flags;
+    info.out_nch = df.nch;
+    info.out_frames = df.total_samples;
+    info.first_call_frames = df.total_samples < (int64_t)df.chunk ? df.total_samples : (int64_t)df.chunk;
+    info.sample_index0 = 0;
+    info.lossy_blocks = lossy;
+    info.is_five = five;
+    info.file_format = file_format;
+    info.header_off = hoff;
+    info.header_len = hlen;
+    info.trailer_off = toff;
+    info.trailer_len = tlen;
+    return true;
+}
+
 int compute_mode(const FileInfo &info) {  // WavPackUtils.cs:133-167 (fields captured at open)
     return info.mode;
 }

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "wv_desc.h"
+#include "wv_dframe.h"
 #include "wv_meta.h"
 
 namespace wvg {
@@ -72,6 +73,12 @@ void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t ou
 // that raised the C# exception mid-call keeps the descriptor of that call,
 // whose writes must not reach the next file's range.
 int64_t file_out_extent(const FramingOutput &out, const FileInfo &info, uint64_t out_base_ints);
+
+// FileInfo of a file framed on the device (wv_dframe.h) from its walk and its
+// blocks' records (nblocks of them); false when a block left the device scope
+// or the blocks disagree on what they carry (the host frames the file instead).
+// first_desc / blob_base are the caller's.
+bool dframe_file_info(const DFile &df, const DBlock *blocks, FileInfo &fi);
 
 // WavpackGetMode (WavPackUtils.cs:133-167) from the framed context values
 int compute_mode(const FileInfo &info);
