@@ -123,6 +123,20 @@ int wvg_batch_add_files(wvg_batch *b, int n, const uint8_t *const *files, const 
 int wvg_batch_add_file_at(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open_flags, int64_t start_sample,
                           wvg_file_info *info);
 
+/* n files framed ON THE DEVICE at the next wvg_batch_upload (the
+ * WavpackOpenFileInput header + sub-block walk of WavPackUtils.cs:36-120,600-671,
+ * UnpackUtils.cs:24-68, MetadataUtils.cs:15-192 as kernels, open_flags 0).  The
+ * bytes are copied now and file slots reserved (indices[i]); a file outside the
+ * device framer's scope (DSD, wvx, sticky state, junk, damaged headers) is framed
+ * by the host at the same upload with the same result as wvg_batch_add_file.
+ * The files' infos are available after the upload (wvg_batch_file_info). */
+int wvg_batch_add_files_device(wvg_batch *b, int n, const uint8_t *const *files, const size_t *lens,
+                               int32_t *indices);
+/* A file's info (after the upload for device-framed files); WVG_ERR_OPEN if it did not open. */
+int wvg_batch_file_info(const wvg_batch *b, int file, wvg_file_info *info);
+/* Files of the batch framed on the device / by the host fallback at its uploads. */
+int wvg_batch_framing_stats(const wvg_batch *b, int64_t *device_files, int64_t *host_files);
+
 /* Drop every file of the batch but keep its device and page-locked host
  * buffers (a decode server refills one batch per request). */
 int wvg_batch_reset(wvg_batch *b);

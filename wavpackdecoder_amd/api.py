@@ -108,8 +108,35 @@ class DecodeBatch:
         self._uploaded = False
         return [int(idx[i]) for i in range(n)]
 
+    def add_files_device(self, files):
+        """Queue files for device-side framing at the next upload
+        (wvg_batch_add_files_device); returns their indices.  Their infos are
+        filled in by upload()."""
+        n = len(files)
+        if n == 0:
+            return []
+        bufs = [bytes(f) for f in files]
+        ptrs = (ctypes.c_char_p * n)(*bufs)
+        lens = (ctypes.c_size_t * n)(*[len(f) for f in bufs])
+        idx = (ctypes.c_int32 * n)()
+        rc = self._L.wvg_batch_add_files_device(self._b, n, ctypes.cast(ptrs, ctypes.c_void_p),
+                                                ctypes.cast(lens, ctypes.c_void_p), ctypes.cast(idx, ctypes.c_void_p))
+        if rc < 0:
+            self._check(rc)
+        self.infos.extend(_L.WvgFileInfo() for _ in range(n))
+        self._uploaded = False
+        return [int(idx[i]) for i in range(n)]
+
+    def framing_stats(self):
+        """(files framed on the device, files framed by the host fallback)"""
+        dev, host = ctypes.c_int64(), ctypes.c_int64()
+        self._check(self._L.wvg_batch_framing_stats(self._b, ctypes.byref(dev), ctypes.byref(host)))
+        return int(dev.value), int(host.value)
+
     def upload(self):
         self._check(self._L.wvg_batch_upload(self._b))
+        for i in range(len(self.infos)):  # device-framed files get their infos here
+            self._L.wvg_batch_file_info(self._b, i, ctypes.byref(self.infos[i]))
         self._uploaded = True
 
     def decode(self, stream=None):

@@ -25,6 +25,10 @@ hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, ui
 hipError_t launch_format(const FormatSeg *segs, uint32_t nseg, const int32_t *in, uint8_t *out, int dsd, hipStream_t s);
 hipError_t launch_dsd_fill(const BlockDesc *descs, const uint32_t *dsd_list, uint32_t n_dsd, const uint32_t *status,
                            const uint32_t *aux, int32_t *out, hipStream_t s);
+hipError_t launch_dframe_walk(DFile *files, uint32_t n, const uint8_t *blob, uint64_t *slots, hipStream_t s);
+hipError_t launch_dframe_block(const DFile *files, const uint32_t *blk_file, const uint32_t *blk_k, uint32_t n,
+                               const uint8_t *blob, const uint64_t *slots, BlockDesc *descs, DBlock *recs,
+                               hipStream_t s);
 hipError_t launch_meta(BlockDesc *descs, const MetaJob *jobs, uint32_t njobs, const MetaItem *items, const uint8_t *blob,
                        hipStream_t s);
 constexpr int kMaxTermSets = 8;
@@ -135,6 +139,21 @@ struct wvg_batch {
     int32_t *d_out = nullptr;
     uint32_t *d_status = nullptr, *d_mute = nullptr, *d_pcml = nullptr, *d_dsd = nullptr;
     bool uploaded = false, downloaded = false, formatted = false;
+    // device-side framing (wv_dframe.h): files added by wvg_batch_add_files_device
+    // are framed at upload, on the device, or by the host when outside its scope
+    struct PendingFile {
+        size_t base, len;
+        int idx;
+    };
+    std::vector<PendingFile> dfiles;
+    int64_t framed_dev = 0, framed_host = 0;
+    PinnedBuf dfst;  // page-locked staging of the framing passes
+    DFile *d_dfiles = nullptr;
+    uint64_t *d_slots = nullptr;
+    uint32_t *d_blkf = nullptr, *d_blkk = nullptr;
+    BlockDesc *d_ddescs = nullptr;
+    DBlock *d_drecs = nullptr;
+    size_t cap_dfiles = 0, cap_slots = 0, cap_blkf = 0, cap_blkk = 0, cap_ddescs = 0, cap_drecs = 0;
 };
 
 static int hip_fail(wvg_ctx *c, hipError_t e, const char *what) {
@@ -228,6 +247,18 @@ static void free_dev(wvg_batch *b) {
     hipFree(b->d_mute);
     hipFree(b->d_pcml);
     hipFree(b->d_dsd);
+    hipFree(b->d_dfiles);
+    hipFree(b->d_slots);
+    hipFree(b->d_blkf);
+    hipFree(b->d_blkk);
+    hipFree(b->d_ddescs);
+    hipFree(b->d_drecs);
+    b->d_dfiles = nullptr;
+    b->d_slots = nullptr;
+    b->d_blkf = b->d_blkk = nullptr;
+    b->d_ddescs = nullptr;
+    b->d_drecs = nullptr;
+    b->cap_dfiles = b->cap_slots = b->cap_blkf = b->cap_blkk = b->cap_ddescs = b->cap_drecs = 0;
     for (int t = 0; t < kMaxTermSets; t++) {
         hipFree(b->d_ts[t]);
         b->d_ts[t] = nullptr;
@@ -290,7 +321,8 @@ int wvg_probe_file(const uint8_t *file, size_t len, uint32_t open_flags, int chu
 // Record a framed file in the batch: the getters' view, its output range, its
 // WavpackFormatSamples segments and its blocks' launch groups.  `fi` refers to
 // descriptors already in b->fo.
-static int commit_file(wvg_batch *b, const FileInfo &fi, size_t len, wvg_file_info *info) {
+// `at` >= 0: the file's slot was reserved when it was added (device framing).
+static int commit_file(wvg_batch *b, const FileInfo &fi, size_t len, wvg_file_info *info, int at = -1) {
     wvg_file_info wi;
     fill_info(fi, wi);
     wi.out_offset = b->out_ints;
@@ -298,17 +330,21 @@ static int commit_file(wvg_batch *b, const FileInfo &fi, size_t len, wvg_file_in
     wi.header_len = fi.header_len;
     wi.trailer_off = fi.trailer_off;
     wi.trailer_len = fi.trailer_len;
-    b->finfo.push_back(fi);
-    b->infos.push_back(wi);
-    if (info) *info = wi;
-    if (!fi.open_ok) {
+    if (at < 0) {
+        at = (int)b->infos.size();
+        b->finfo.push_back(fi);
+        b->infos.push_back(wi);
         b->pcm_off.push_back(-1);
-        return WVG_ERR_OPEN;
+    } else {
+        b->finfo[(size_t)at] = fi;
+        b->infos[(size_t)at] = wi;
     }
+    if (info) *info = wi;
+    if (!fi.open_ok) return WVG_ERR_OPEN;
     // the file's WavpackFormatSamples image: frames x reduced channels x bytes per sample, 16-B aligned
     const int64_t nvals = fi.out_frames * fi.out_nch;
     b->pcm_bytes = (b->pcm_bytes + 15) & ~(int64_t)15;
-    b->pcm_off.push_back(b->pcm_bytes);
+    b->pcm_off[(size_t)at] = b->pcm_bytes;
     for (int64_t s = 0; s < nvals; s += kFormatSeg) {
         FormatSeg g;
         g.in_off = (uint64_t)(b->out_ints + s);
@@ -332,7 +368,7 @@ static int commit_file(wvg_batch *b, const FileInfo &fi, size_t len, wvg_file_in
     }
     // compressed bytes of the file's decoded blocks (whole file is a fine proxy)
     b->bytes_in += (int64_t)len;
-    return (int)b->infos.size() - 1;
+    return at;
 }
 
 static int add_file(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open_flags, int64_t seek_to,
@@ -370,6 +406,8 @@ int wvg_batch_reset(wvg_batch *b) {
     b->pcm_bytes = 0;
     b->segs.clear();
     b->uploaded = b->downloaded = b->formatted = b->segs_uploaded = false;
+    b->dfiles.clear();
+    b->framed_dev = b->framed_host = 0;
     return WVG_OK;
 }
 
@@ -451,6 +489,151 @@ int wvg_batch_add_file_at(wvg_batch *b, const uint8_t *file, size_t len, uint32_
     return add_file(b, file, len, open_flags, start_sample, info);
 }
 
+// Files whose framing waits for the upload: their bytes are copied into the
+// blob and their file slots reserved; wvg_batch_upload frames them on the device
+// (wv_dframe.h), or on the host when a file is outside the device scope.
+int wvg_batch_add_files_device(wvg_batch *b, int n, const uint8_t *const *files, const size_t *lens,
+                               int32_t *indices) {
+    if (!b || n < 0 || (n && (!files || !lens))) return WVG_ERR_ARG;
+    b->uploaded = b->formatted = false;
+    size_t end = b->blob.size();
+    std::vector<size_t> base((size_t)n);
+    for (int i = 0; i < n; i++) {
+        if (!files[i] && lens[i]) return WVG_ERR_ARG;
+        base[(size_t)i] = (end + 15) & ~(size_t)15;
+        end = base[(size_t)i] + lens[i];
+    }
+    if (!b->blob.resize(end)) {
+        b->ctx->err = "out of host memory";
+        return WVG_ERR_ARG;
+    }
+    for (int i = 0; i < n; i++) {
+        if (lens[i]) memcpy(b->blob.data() + base[(size_t)i], files[i], lens[i]);
+        const int idx = (int)b->infos.size();
+        FileInfo fi;
+        fi.error = "not framed yet (wvg_batch_upload frames it)";
+        wvg_file_info wi;
+        fill_info(fi, wi);
+        b->finfo.push_back(fi);
+        b->infos.push_back(wi);
+        b->pcm_off.push_back(-1);
+        b->dfiles.push_back({base[(size_t)i], lens[i], idx});
+        if (indices) indices[i] = idx;
+    }
+    return n;
+}
+
+// The framing passes of the pending files (the blob is on the device already):
+// the walk (one lane per file), the output range of every file it accepted, the
+// block pass (one lane per block), then, in file order, the accepted files'
+// descriptors committed and every other file framed by the host.
+static int device_frame(wvg_batch *b, hipStream_t s) {
+    wvg_ctx *c = b->ctx;
+    const size_t nf = b->dfiles.size();
+    std::vector<DFile> df(nf);
+    uint64_t nslots = 0;
+    for (size_t i = 0; i < nf; i++) {
+        memset(&df[i], 0, sizeof(DFile));
+        df[i].base = b->dfiles[i].base;
+        df[i].len = b->dfiles[i].len;
+        df[i].slot = nslots;
+        df[i].chunk = (uint32_t)b->chunk;
+        nslots += b->dfiles[i].len / 32 + 1;
+    }
+    HIPCHK(c, ensure(b->d_dfiles, b->cap_dfiles, sizeof(DFile) * (nf ? nf : 1)));
+    HIPCHK(c, ensure(b->d_slots, b->cap_slots, sizeof(uint64_t) * (nslots ? nslots : 1)));
+    if (!b->dfst.resize(sizeof(DFile) * nf)) return WVG_ERR_SPACE;
+    memcpy(b->dfst.data(), df.data(), sizeof(DFile) * nf);
+    HIPCHK(c, hipMemcpyAsync(b->d_dfiles, b->dfst.data(), sizeof(DFile) * nf, hipMemcpyHostToDevice, s));
+    HIPCHK(c, launch_dframe_walk(b->d_dfiles, (uint32_t)nf, b->d_blob, b->d_slots, s));
+    HIPCHK(c, hipMemcpyAsync(b->dfst.data(), b->d_dfiles, sizeof(DFile) * nf, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    memcpy(df.data(), b->dfst.data(), sizeof(DFile) * nf);
+    // output ranges and the block list of the accepted files, in file order
+    std::vector<uint32_t> bf, bk;
+    std::vector<size_t> blk0(nf, 0);
+    int64_t ob = b->out_ints;
+    for (size_t i = 0; i < nf; i++) {
+        if (!df[i].regular) continue;
+        df[i].out_base = (uint64_t)ob;
+        blk0[i] = bf.size();
+        for (uint32_t k = 0; k < df[i].nblocks; k++) {
+            bf.push_back((uint32_t)i);
+            bk.push_back(k);
+        }
+        ob += df[i].total_samples * df[i].nch;
+    }
+    const size_t nb = bf.size();
+    std::vector<DBlock> recs(nb);
+    std::vector<BlockDesc> dd(nb);
+    if (nb) {
+        HIPCHK(c, ensure(b->d_blkf, b->cap_blkf, sizeof(uint32_t) * nb));
+        HIPCHK(c, ensure(b->d_blkk, b->cap_blkk, sizeof(uint32_t) * nb));
+        HIPCHK(c, ensure(b->d_ddescs, b->cap_ddescs, sizeof(BlockDesc) * nb));
+        HIPCHK(c, ensure(b->d_drecs, b->cap_drecs, sizeof(DBlock) * nb));
+        const size_t up = sizeof(DFile) * nf + 2 * sizeof(uint32_t) * nb;
+        const size_t down = (sizeof(BlockDesc) + sizeof(DBlock)) * nb;
+        if (!b->dfst.resize(up > down ? up : down)) return WVG_ERR_SPACE;
+        uint8_t *h = b->dfst.data();
+        memcpy(h, df.data(), sizeof(DFile) * nf);
+        memcpy(h + sizeof(DFile) * nf, bf.data(), sizeof(uint32_t) * nb);
+        memcpy(h + sizeof(DFile) * nf + sizeof(uint32_t) * nb, bk.data(), sizeof(uint32_t) * nb);
+        HIPCHK(c, hipMemcpyAsync(b->d_dfiles, h, sizeof(DFile) * nf, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(b->d_blkf, h + sizeof(DFile) * nf, sizeof(uint32_t) * nb, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(b->d_blkk, h + sizeof(DFile) * nf + sizeof(uint32_t) * nb, sizeof(uint32_t) * nb,
+                                 hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipStreamSynchronize(s));  // the staging is reused for the results
+        HIPCHK(c, launch_dframe_block(b->d_dfiles, b->d_blkf, b->d_blkk, (uint32_t)nb, b->d_blob, b->d_slots,
+                                      b->d_ddescs, b->d_drecs, s));
+        HIPCHK(c, hipMemcpyAsync(h, b->d_ddescs, sizeof(BlockDesc) * nb, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(h + sizeof(BlockDesc) * nb, b->d_drecs, sizeof(DBlock) * nb, hipMemcpyDeviceToHost,
+                                 s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        memcpy(dd.data(), h, sizeof(BlockDesc) * nb);
+        memcpy(recs.data(), h + sizeof(BlockDesc) * nb, sizeof(DBlock) * nb);
+    }
+    // commit: the accepted files at their reserved output ranges, in file order
+    std::vector<size_t> host;
+    for (size_t i = 0; i < nf; i++) {
+        const auto &p = b->dfiles[i];
+        FileInfo fi;
+        fi.blob_base = p.base;
+        fi.first_desc = (int64_t)b->fo.descs.size();
+        if (df[i].regular && dframe_file_info(df[i], recs.data() + blk0[i], fi)) {
+            b->fo.descs.insert(b->fo.descs.end(), dd.begin() + (ptrdiff_t)blk0[i],
+                               dd.begin() + (ptrdiff_t)(blk0[i] + df[i].nblocks));
+            b->out_ints = (int64_t)df[i].out_base;
+            commit_file(b, fi, p.len, nullptr, p.idx);
+            b->framed_dev++;
+        } else {
+            host.push_back(i);
+        }
+    }
+    if (b->out_ints < ob) b->out_ints = ob;  // a range whose file fell back to the host stays unused
+    for (size_t i : host) {
+        const auto &p = b->dfiles[i];
+        FileInfo fi;
+        frame_file(b->blob.data() + p.base, p.len, p.base, (uint64_t)b->out_ints, 0, b->chunk, b->fo, fi, -1);
+        commit_file(b, fi, p.len, nullptr, p.idx);
+        b->framed_host++;
+    }
+    b->dfiles.clear();
+    return WVG_OK;
+}
+
+int wvg_batch_file_info(const wvg_batch *b, int file, wvg_file_info *info) {
+    if (!b || !info || file < 0 || file >= (int)b->infos.size()) return WVG_ERR_ARG;
+    *info = b->infos[(size_t)file];
+    return b->finfo[(size_t)file].open_ok ? WVG_OK : WVG_ERR_OPEN;
+}
+
+int wvg_batch_framing_stats(const wvg_batch *b, int64_t *device_files, int64_t *host_files) {
+    if (!b) return WVG_ERR_ARG;
+    if (device_files) *device_files = b->framed_dev;
+    if (host_files) *host_files = b->framed_host;
+    return WVG_OK;
+}
+
 int wvg_batch_upload(wvg_batch *b) {
     if (!b) return WVG_ERR_ARG;
     wvg_ctx *c = b->ctx;
@@ -463,6 +646,10 @@ int wvg_batch_upload(wvg_batch *b) {
     HIPCHK(c, ensure(b->d_blob, b->cap_blob, blob_n));
     HIPCHK(c, hipMemsetAsync(b->d_blob + b->blob.size(), 0xFF, 64, s));
     if (!b->blob.empty()) HIPCHK(c, hipMemcpyAsync(b->d_blob, b->blob.data(), b->blob.size(), hipMemcpyHostToDevice, s));
+    if (!b->dfiles.empty()) {
+        const int rc = device_frame(b, s);
+        if (rc != WVG_OK) return rc;
+    }
     const size_t nd = b->fo.descs.size();
     // The small host arrays go through one page-locked staging buffer: a
     // pageable hipMemcpyAsync is staged synchronously inside the runtime, which
