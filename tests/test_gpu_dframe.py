@@ -92,3 +92,78 @@ def test_c2_device_framed_roundtrip(gpu_batch_cls):
     assert r.crc_errors == 0 and r.exception == 0
     np.testing.assert_array_equal(out[: pcm.size], pcm.reshape(-1))
     b.close()
+
+
+def _fake_header(data: bytes, block: int, at: int, target: int) -> bytes:
+    """`data` with a header-shaped 32 bytes written inside block `block`'s payload (at
+    `at` bytes before its end, even offset) whose ckSize points at byte `target`"""
+    off, n = V.block_spans(data)[block]
+    p = off + n - at
+    p -= p & 1
+    hdr = bytearray(data[off:off + 32])
+    hdr[4:8] = (target - p - 8).to_bytes(4, "little")
+    b = bytearray(data)
+    b[p:p + 32] = hdr
+    return bytes(b)
+
+
+def _rank_all(gpu_batch_cls, files, chunk=4096):
+    """device framing with every file on the parallel header walk vs the host framing"""
+    import os
+    old = os.environ.get("WVG_DFRAME_RANK_MIN")
+    os.environ["WVG_DFRAME_RANK_MIN"] = "0"
+    try:
+        b = gpu_batch_cls(chunk)
+    finally:
+        if old is None:
+            os.environ.pop("WVG_DFRAME_RANK_MIN")
+        else:
+            os.environ["WVG_DFRAME_RANK_MIN"] = old
+    a = gpu_batch_cls(chunk)
+    a.add_files(files, threads=8)
+    a.decode()
+    a.format()
+    fa = _per_file(a, len(files))
+    b.add_files_device(files)
+    b.decode()
+    b.format()
+    fb = _per_file(b, len(files))
+    for k in range(len(files)):
+        assert (fa[k] is None) == (fb[k] is None), k
+        if fa[k] is not None:
+            np.testing.assert_array_equal(fa[k][0], fb[k][0], err_msg=str(k))
+            assert fa[k][1:5] == fb[k][1:5], k
+    stats = b.framing_stats()
+    a.close()
+    b.close()
+    return stats
+
+
+def test_parallel_header_walk_matches_host(gpu_batch_cls):
+    """the scan + list-ranking walk (forced for every file) against the host framing, incl.
+    files with header-shaped bytes inside a payload: a dead chain (ignored), a chain
+    merging into the true one (rank collision -> serial walk), junk at the head/tail"""
+    from synth import corpora
+    base = V.pcm_cases()[2][1]
+    spans = V.block_spans(base)
+    fakes = [_fake_header(base, 1, 200, spans[2][0]),             # merges into block 2
+             _fake_header(base, 1, 300, len(base) + 1000),         # points past the end
+             _fake_header(base, 0, 500, spans[0][0] + spans[0][1] + 6),  # points between headers
+             _fake_header(base, len(spans) - 1, 100, len(base))]   # a second chain end at the file end
+    files = [c[1] for c in V.pcm_cases()] + corpora.c5(30) + fakes + \
+        [b"\0" * 40 + base, base + b"\0" * 40, base[:len(base) - 100]]
+    dev, host = _rank_all(gpu_batch_cls, files)
+    assert dev >= 30, (dev, host)
+
+
+def test_parallel_header_walk_c2(gpu_batch_cls):
+    """the 1,024-block C2 file takes the parallel walk by default (over 256 KiB)"""
+    from synth import corpora
+    pcm, data = corpora.c2(return_pcm=True)
+    b = gpu_batch_cls(4096)
+    b.add_files_device([data])
+    b.decode()
+    assert b.framing_stats() == (1, 0) and b.num_blocks == 1024
+    out = b.download()
+    np.testing.assert_array_equal(out[: pcm.size], pcm.reshape(-1))
+    b.close()

@@ -25,6 +25,11 @@ hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, ui
 hipError_t launch_format(const FormatSeg *segs, uint32_t nseg, const int32_t *in, uint8_t *out, int dsd, hipStream_t s);
 hipError_t launch_dsd_fill(const BlockDesc *descs, const uint32_t *dsd_list, uint32_t n_dsd, const uint32_t *status,
                            const uint32_t *aux, int32_t *out, hipStream_t s);
+hipError_t launch_dframe_rank(DFile *files, const uint32_t *tile_file, uint32_t ntiles, const uint32_t *rank_files,
+                              uint32_t nrank, const uint8_t *blob, uint32_t *cand, uint32_t *cnt, uint64_t *slots,
+                              hipStream_t s);
+size_t dframe_tile_cap();
+size_t dframe_tile_bytes();
 hipError_t launch_dframe_walk(DFile *files, uint32_t n, const uint8_t *blob, uint64_t *slots, hipStream_t s);
 hipError_t launch_dframe_block(const DFile *files, const uint32_t *blk_file, const uint32_t *blk_k, uint32_t n,
                                const uint8_t *blob, const uint64_t *slots, BlockDesc *descs, DBlock *recs,
@@ -150,7 +155,10 @@ struct wvg_batch {
     PinnedBuf dfst;  // page-locked staging of the framing passes
     DFile *d_dfiles = nullptr;
     uint64_t *d_slots = nullptr;
-    uint32_t *d_blkf = nullptr, *d_blkk = nullptr;
+    uint32_t *d_blkf = nullptr, *d_blkk = nullptr, *d_tfile = nullptr, *d_rankf = nullptr, *d_cand = nullptr,
+             *d_cnt = nullptr;
+    size_t cap_tfile = 0, cap_rankf = 0, cap_cand = 0, cap_cnt = 0;
+    int64_t rank_min = 256 * 1024;  // files from this size on take the parallel header walk (WVG_DFRAME_RANK_MIN)
     BlockDesc *d_ddescs = nullptr;
     DBlock *d_drecs = nullptr;
     size_t cap_dfiles = 0, cap_slots = 0, cap_blkf = 0, cap_blkk = 0, cap_ddescs = 0, cap_drecs = 0;
@@ -229,6 +237,8 @@ wvg_batch *wvg_batch_new(wvg_ctx *c, int chunk_frames) {
     b->prefer_pipe = pp ? atoi(pp) : 0;
     // the decorr/entropy values of each block are parsed on the device (wv_meta_parse);
     // WVG_HOST_META=1 keeps them on the host framing (A/B comparisons)
+    const char *rm = getenv("WVG_DFRAME_RANK_MIN");
+    if (rm) b->rank_min = atoll(rm);
     const char *hm = getenv("WVG_HOST_META");
     b->fo.defer_values = !(hm && hm[0] == '1');
     return b;
@@ -251,6 +261,12 @@ static void free_dev(wvg_batch *b) {
     hipFree(b->d_slots);
     hipFree(b->d_blkf);
     hipFree(b->d_blkk);
+    hipFree(b->d_tfile);
+    hipFree(b->d_rankf);
+    hipFree(b->d_cand);
+    hipFree(b->d_cnt);
+    b->d_tfile = b->d_rankf = b->d_cand = b->d_cnt = nullptr;
+    b->cap_tfile = b->cap_rankf = b->cap_cand = b->cap_cnt = 0;
     hipFree(b->d_ddescs);
     hipFree(b->d_drecs);
     b->d_dfiles = nullptr;
@@ -415,6 +431,59 @@ int wvg_batch_add_file(wvg_batch *b, const uint8_t *file, size_t len, uint32_t o
     return add_file(b, file, len, open_flags, -1, info);
 }
 
+// Frame files already in the blob on host threads, each into its own
+// FramingOutput with out offsets relative to 0 (merge_framed moves them).
+static void frame_threaded(wvg_batch *b, const std::vector<size_t> &base, const std::vector<size_t> &lens,
+                           uint32_t open_flags, int threads, std::vector<FramingOutput> &fos,
+                           std::vector<FileInfo> &fis) {
+    const int n = (int)base.size();
+    if (threads <= 0) {
+        const char *e = getenv("WVG_FRAME_THREADS");
+        threads = e ? atoi(e) : (int)std::thread::hardware_concurrency();
+        if (threads > 16) threads = 16;  // the lease's CPU share on the GPU boxes
+    }
+    if (threads < 1) threads = 1;
+    if (threads > n) threads = n > 0 ? n : 1;
+    fos.assign((size_t)n, FramingOutput());
+    fis.assign((size_t)n, FileInfo());
+    for (auto &f : fos) f.defer_values = b->fo.defer_values;
+    std::atomic<int> next(0);
+    auto work = [&]() {
+        for (int i; (i = next.fetch_add(1)) < n;)
+            frame_file(b->blob.data() + base[(size_t)i], lens[(size_t)i], base[(size_t)i], 0, open_flags, b->chunk,
+                       fos[(size_t)i], fis[(size_t)i], -1);
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < threads; t++) pool.emplace_back(work);
+    work();
+    for (auto &t : pool) t.join();
+}
+
+// Append one file framed by frame_threaded to the batch at the current output
+// end and commit it (at: its reserved file slot, or -1 for a new one).
+static int merge_framed(wvg_batch *b, FramingOutput &f, FileInfo &fi, size_t len, wvg_file_info *info, int at) {
+    const uint64_t ob = (uint64_t)b->out_ints;
+    const uint32_t d0 = (uint32_t)b->fo.descs.size(), i0 = (uint32_t)b->fo.items.size();
+    const size_t t0 = (b->fo.tables.size() + 15) & ~(size_t)15;
+    for (BlockDesc &d : f.descs) {
+        d.out_off += ob;  // wrapping add: a seek's offsets may lie before the file's output
+        d.dsd_table_off += t0;
+    }
+    for (MetaJob &j : f.jobs) {
+        j.desc += d0;
+        j.first += i0;
+    }
+    b->fo.descs.insert(b->fo.descs.end(), f.descs.begin(), f.descs.end());
+    b->fo.items.insert(b->fo.items.end(), f.items.begin(), f.items.end());
+    b->fo.jobs.insert(b->fo.jobs.end(), f.jobs.begin(), f.jobs.end());
+    if (!f.tables.empty()) {
+        b->fo.tables.resize(t0);
+        b->fo.tables.insert(b->fo.tables.end(), f.tables.begin(), f.tables.end());
+    }
+    fi.first_desc += d0;
+    return commit_file(b, fi, len, info, at);
+}
+
 // Many files at once: the bytes are copied into the blob, the files are framed
 // on host threads (each into its own FramingOutput, out offsets relative to 0),
 // then merged in file order with their offsets moved to the batch's.
@@ -435,49 +504,12 @@ int wvg_batch_add_files(wvg_batch *b, int n, const uint8_t *const *files, const 
     }
     for (int i = 0; i < n; i++)
         if (lens[i]) memcpy(b->blob.data() + base[(size_t)i], files[i], lens[i]);
-    if (threads <= 0) {
-        const char *e = getenv("WVG_FRAME_THREADS");
-        threads = e ? atoi(e) : (int)std::thread::hardware_concurrency();
-        if (threads > 16) threads = 16;  // the lease's CPU share on the GPU boxes
-    }
-    if (threads < 1) threads = 1;
-    if (threads > n) threads = n > 0 ? n : 1;
-    std::vector<FramingOutput> fos((size_t)n);
-    std::vector<FileInfo> fis((size_t)n);
-    for (auto &f : fos) f.defer_values = b->fo.defer_values;
-    std::atomic<int> next(0);
-    auto work = [&]() {
-        for (int i; (i = next.fetch_add(1)) < n;)
-            frame_file(b->blob.data() + base[(size_t)i], lens[i], base[(size_t)i], 0, open_flags, b->chunk,
-                       fos[(size_t)i], fis[(size_t)i], -1);
-    };
-    std::vector<std::thread> pool;
-    for (int t = 1; t < threads; t++) pool.emplace_back(work);
-    work();
-    for (auto &t : pool) t.join();
+    std::vector<size_t> ln(lens, lens + n);
+    std::vector<FramingOutput> fos;
+    std::vector<FileInfo> fis;
+    frame_threaded(b, base, ln, open_flags, threads, fos, fis);
     for (int i = 0; i < n; i++) {
-        FramingOutput &f = fos[(size_t)i];
-        FileInfo &fi = fis[(size_t)i];
-        const uint64_t ob = (uint64_t)b->out_ints;
-        const uint32_t d0 = (uint32_t)b->fo.descs.size(), i0 = (uint32_t)b->fo.items.size();
-        const size_t t0 = (b->fo.tables.size() + 15) & ~(size_t)15;
-        for (BlockDesc &d : f.descs) {
-            d.out_off += ob;  // wrapping add: a seek's offsets may lie before the file's output
-            d.dsd_table_off += t0;
-        }
-        for (MetaJob &j : f.jobs) {
-            j.desc += d0;
-            j.first += i0;
-        }
-        b->fo.descs.insert(b->fo.descs.end(), f.descs.begin(), f.descs.end());
-        b->fo.items.insert(b->fo.items.end(), f.items.begin(), f.items.end());
-        b->fo.jobs.insert(b->fo.jobs.end(), f.jobs.begin(), f.jobs.end());
-        if (!f.tables.empty()) {
-            b->fo.tables.resize(t0);
-            b->fo.tables.insert(b->fo.tables.end(), f.tables.begin(), f.tables.end());
-        }
-        fi.first_desc += d0;
-        const int idx = commit_file(b, fi, lens[i], infos ? &infos[i] : nullptr);
+        const int idx = merge_framed(b, fos[(size_t)i], fis[(size_t)i], lens[i], infos ? &infos[i] : nullptr, -1);
         if (indices) indices[i] = idx;
     }
     return n;
@@ -532,6 +564,9 @@ static int device_frame(wvg_batch *b, hipStream_t s) {
     const size_t nf = b->dfiles.size();
     std::vector<DFile> df(nf);
     uint64_t nslots = 0;
+    // large files: the parallel header walk (candidate scan over 8 KiB tiles + list ranking)
+    std::vector<uint32_t> tfile, rankf;
+    const size_t tb = dframe_tile_bytes();
     for (size_t i = 0; i < nf; i++) {
         memset(&df[i], 0, sizeof(DFile));
         df[i].base = b->dfiles[i].base;
@@ -539,12 +574,32 @@ static int device_frame(wvg_batch *b, hipStream_t s) {
         df[i].slot = nslots;
         df[i].chunk = (uint32_t)b->chunk;
         nslots += b->dfiles[i].len / 32 + 1;
+        if (b->rank_min >= 0 && (int64_t)df[i].len >= b->rank_min && df[i].len >= 32) {
+            df[i].tile0 = (uint32_t)tfile.size();
+            df[i].ntiles = (uint32_t)((df[i].len + tb - 1) / tb);
+            tfile.insert(tfile.end(), df[i].ntiles, (uint32_t)i);
+            rankf.push_back((uint32_t)i);
+        }
     }
     HIPCHK(c, ensure(b->d_dfiles, b->cap_dfiles, sizeof(DFile) * (nf ? nf : 1)));
     HIPCHK(c, ensure(b->d_slots, b->cap_slots, sizeof(uint64_t) * (nslots ? nslots : 1)));
-    if (!b->dfst.resize(sizeof(DFile) * nf)) return WVG_ERR_SPACE;
+    const size_t nt = tfile.size(), nr = rankf.size();
+    if (!b->dfst.resize(sizeof(DFile) * nf + sizeof(uint32_t) * (nt + nr))) return WVG_ERR_SPACE;
     memcpy(b->dfst.data(), df.data(), sizeof(DFile) * nf);
     HIPCHK(c, hipMemcpyAsync(b->d_dfiles, b->dfst.data(), sizeof(DFile) * nf, hipMemcpyHostToDevice, s));
+    if (nr) {
+        uint32_t *h = reinterpret_cast<uint32_t *>(b->dfst.data() + sizeof(DFile) * nf);
+        memcpy(h, tfile.data(), sizeof(uint32_t) * nt);
+        memcpy(h + nt, rankf.data(), sizeof(uint32_t) * nr);
+        HIPCHK(c, ensure(b->d_tfile, b->cap_tfile, sizeof(uint32_t) * nt));
+        HIPCHK(c, ensure(b->d_rankf, b->cap_rankf, sizeof(uint32_t) * nr));
+        HIPCHK(c, ensure(b->d_cand, b->cap_cand, sizeof(uint32_t) * nt * dframe_tile_cap()));
+        HIPCHK(c, ensure(b->d_cnt, b->cap_cnt, sizeof(uint32_t) * nt));
+        HIPCHK(c, hipMemcpyAsync(b->d_tfile, h, sizeof(uint32_t) * nt, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(b->d_rankf, h + nt, sizeof(uint32_t) * nr, hipMemcpyHostToDevice, s));
+        HIPCHK(c, launch_dframe_rank(b->d_dfiles, b->d_tfile, (uint32_t)nt, b->d_rankf, (uint32_t)nr, b->d_blob,
+                                     b->d_cand, b->d_cnt, b->d_slots, s));
+    }
     HIPCHK(c, launch_dframe_walk(b->d_dfiles, (uint32_t)nf, b->d_blob, b->d_slots, s));
     HIPCHK(c, hipMemcpyAsync(b->dfst.data(), b->d_dfiles, sizeof(DFile) * nf, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
@@ -610,12 +665,19 @@ static int device_frame(wvg_batch *b, hipStream_t s) {
         }
     }
     if (b->out_ints < ob) b->out_ints = ob;  // a range whose file fell back to the host stays unused
-    for (size_t i : host) {
-        const auto &p = b->dfiles[i];
-        FileInfo fi;
-        frame_file(b->blob.data() + p.base, p.len, p.base, (uint64_t)b->out_ints, 0, b->chunk, b->fo, fi, -1);
-        commit_file(b, fi, p.len, nullptr, p.idx);
-        b->framed_host++;
+    if (!host.empty()) {  // the host framing of the rest, on host threads
+        std::vector<size_t> hb, hl;
+        for (size_t i : host) {
+            hb.push_back(b->dfiles[i].base);
+            hl.push_back(b->dfiles[i].len);
+        }
+        std::vector<FramingOutput> fos;
+        std::vector<FileInfo> fis;
+        frame_threaded(b, hb, hl, 0, 0, fos, fis);
+        for (size_t j = 0; j < host.size(); j++) {
+            merge_framed(b, fos[j], fis[j], hl[j], nullptr, b->dfiles[host[j]].idx);
+            b->framed_host++;
+        }
     }
     b->dfiles.clear();
     return WVG_OK;

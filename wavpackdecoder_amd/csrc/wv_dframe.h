@@ -50,6 +50,12 @@ struct DFile {
     uint32_t why;        // first reason it is not (DF_*), for diagnostics
     uint32_t nblocks;
     int32_t num_channels, bits_per_sample, bytes_per_sample, version, mode, is_float, nch;
+    // the parallel header walk of a large file (wv_dframe.hip: scan + rank) before
+    // dframe_walk: 1 the slots and nblocks are filled and every header checked,
+    // -1 the file is not regular (why set), 0 not ranked (dframe_walk walks it)
+    int32_t ranked;
+    uint32_t tile0, ntiles;  // the file's tiles in the candidate scan
+    uint32_t pad_;
     int64_t sample_rate, total_samples, config_flags;
 };
 
@@ -330,7 +336,8 @@ WVF_HD void dframe_walk(DFile &fi, const uint8_t *blob, uint64_t *slots) {
     const uint8_t *f = blob + fi.base;
     const uint64_t len = fi.len, cap = len / 32 + 1;
     fi.regular = 0;
-    fi.nblocks = 0;
+    if (fi.ranked < 0) return;  // the parallel walk found it irregular (why set)
+    if (fi.ranked == 0) fi.nblocks = 0;
     DHdr h;
     if (!dframe_header(f, len, 0, h)) {
         fi.why = DF_HEADER;
@@ -397,6 +404,15 @@ WVF_HD void dframe_walk(DFile &fi, const uint8_t *blob, uint64_t *slots) {
     fi.config_flags = cfg;
     // the header walk: every block starts where the previous one ends
     const uint32_t bch0 = (uint32_t)num_channels;
+    if (fi.ranked == 1) {  // walked in parallel: every header checked but against block 0's layout
+        if (((h.flags & MONO_FLAG) ? 1u : 2u) != bch0) {
+            fi.why = DF_WALK;
+            return;
+        }
+        fi.why = DF_OK;
+        fi.regular = 1;
+        return;
+    }
     uint64_t pos = 0;
     int64_t sum = 0;
     uint32_t n = 0;
