@@ -123,6 +123,14 @@ int wvg_batch_add_files(wvg_batch *b, int n, const uint8_t *const *files, const 
 int wvg_batch_add_file_at(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open_flags, int64_t start_sample,
                           wvg_file_info *info);
 
+/* A hybrid .wv file with its .wvc correction file: the hybrid blocks decode
+ * EXACTLY (lossless) instead of the reference's lossy output.  Beyond the
+ * reference (it opens ID_WVC_BITSTREAM, UnpackUtils.cs:96-106, but never reads
+ * it): parity is the round trip to the encoder's input.  Returns the
+ * file index or WVG_ERR_OPEN, as wvg_batch_add_file. */
+int wvg_batch_add_file_wvc(wvg_batch *b, const uint8_t *file, size_t len, const uint8_t *wvc, size_t wvc_len,
+                           uint32_t open_flags, wvg_file_info *info);
+
 /* n files framed ON THE DEVICE at the next wvg_batch_upload (the
  * WavpackOpenFileInput header + sub-block walk of WavPackUtils.cs:36-120,600-671,
  * UnpackUtils.cs:24-68, MetadataUtils.cs:15-192 as kernels, open_flags 0).  The

@@ -69,6 +69,7 @@ struct wvenc_params {
     int64_t total_override;    // > 0: header total_samples (a file encoded in parallel parts, then concatenated)
     int32_t sticky_passes;     // blocks after the first omit DECORR_TERMS/WEIGHTS/SAMPLES: the decoder
                                // continues the passes of the block before (sticky state, B-8)
+    int32_t wvc;               // hybrid only: also write a .wvc correction file (wvenc_encode_pcm_wvc)
 };
 
 struct wvenc_dsd_params {
@@ -122,6 +123,19 @@ struct BitWriter {
         return out;
     }
 };
+
+// read_code inverse (WordsUtils.cs:546-570): `code` in [0, maxcode]
+void put_code(BitWriter &bw, uint32_t code, uint32_t maxcode) {
+    int bitcount = count_bits_u32(maxcode);
+    if (!bitcount) return;
+    uint32_t extras = (uint32_t)((1ull << bitcount) - maxcode - 1);
+    if (code < extras)
+        bw.put(code, bitcount - 1);
+    else {
+        bw.put((code + extras) >> 1, bitcount - 1);
+        bw.bit((code + extras) & 1);
+    }
+}
 
 // Elias-gamma-like count (decoder: WordsUtils.cs:321-335 and 391-405)
 void put_gamma(BitWriter &bw, uint32_t v) {
@@ -215,6 +229,10 @@ void update_error_limit(EntropyState &w, uint32_t flags) {
 // -------------------------------------------------------------------------
 struct WordEncoder {
     BitWriter bw;
+    // .wvc correction stream: for every word the bisection left inexact, the exact
+    // magnitude as read_code(wvcbits, high - low) + low (WavPack 4 words.c get_word)
+    BitWriter cw;
+    bool wvc = false;
     EntropyState w;
     uint32_t flags;
     bool mono;
@@ -359,6 +377,7 @@ struct WordEncoder {
                     mid = (high + low + 1) >> 1;
                 }
             }
+            if (wvc) put_code(cw, (uint32_t)((int64_t)u - low), (uint32_t)(high - low));
         }
         tail.bit(sign);
         uint64_t tbits = tail.acc;
@@ -698,6 +717,12 @@ struct PcmEncoder {
     const wvenc_params &P;
     std::vector<Pass> passes;  // decoder order
     EntropyState ent;
+    // P.wvc: the correction file.  The passes stay closed-loop (the .wv alone
+    // decodes exactly as without it); word k's correction is the exact residual
+    // minus the lossy one, added by the decoder to the passes' output (before
+    // joint stereo).  That is exact when no pass reads the other channel's
+    // current output (stereo terms -1 / -2): checked per sample below.
+    std::vector<uint8_t> wvc_file;
     // previous block's final outputs per pass (for history metadata)
     explicit PcmEncoder(const wvenc_params &p) : P(p) {}
 
@@ -935,6 +960,8 @@ struct PcmEncoder {
             // ---- samples: pre-fixup domain values
             WordEncoder we(flags);
             we.w = ent;
+            we.wvc = P.wvc != 0;
+            int32_t crc_exact = -1;
             int32_t crc = -1;
             uint32_t maxabs = 0;
             std::vector<int32_t> inres(n + 1);
@@ -960,6 +987,13 @@ struct PcmEncoder {
                     int32_t r = we.word(t);
                     int32_t y = r;
                     for (int d = 0; d < n; d++) y = pass_fwd_mono(passes[d], y);
+                    if (P.wvc) {
+                        const int32_t ye = add32(y, sub32(t, r));
+                        if (ye != L) throw std::runtime_error("wvc: exact reconstruction mismatch");
+                        crc_exact = add32(mul32(crc_exact, 3), ye);
+                        uint32_t ae = ye < 0 ? (uint32_t)(-(int64_t)ye) : (uint32_t)ye;
+                        if (ae > maxabs) maxabs = ae;
+                    }
                     crc = add32(mul32(crc, 3), y);
                     wvx_value(y, vL);
                     uint32_t a = y < 0 ? (uint32_t)(-(int64_t)y) : (uint32_t)y;
@@ -986,6 +1020,20 @@ struct PcmEncoder {
                         pass_fwd_stereo(passes[d], yL, yR, oL, oR);
                         yL = oL;
                         yR = oR;
+                    }
+                    if (P.wvc) {
+                        int32_t eL = add32(yL, sub32(tL, rL)), eR = add32(yR, sub32(tR, rR));
+                        if (P.joint_stereo) {
+                            eR = sub32(eR, eL >> 1);
+                            eL = add32(eL, eR);
+                        }
+                        if (eL != L || eR != R)
+                            throw std::runtime_error("wvc: exact reconstruction mismatch (stereo terms -1/-2?)");
+                        crc_exact = add32(mul32(add32(mul32(crc_exact, 3), eL), 3), eR);
+                        uint32_t ae = eL < 0 ? (uint32_t)(-(int64_t)eL) : (uint32_t)eL;
+                        uint32_t be = eR < 0 ? (uint32_t)(-(int64_t)eR) : (uint32_t)eR;
+                        if (ae > maxabs) maxabs = ae;
+                        if (be > maxabs) maxabs = be;
                     }
                     if (P.joint_stereo) {
                         yR = sub32(yR, yL >> 1);
@@ -1029,6 +1077,17 @@ struct PcmEncoder {
             write_header(blk, P.version, P.total_override > 0 ? P.total_override : frames, P.block_index_start + f0,
                          (uint32_t)nf, flags, crc, P.total_unknown);
             file.insert(file.end(), blk.begin(), blk.end());
+            if (P.wvc) {  // the .wvc block: same header fields, the exact output's CRC, ID_WVC_BITSTREAM
+                std::vector<uint8_t> cb = we.cw.finish();
+                while (cb.size() < 2 || (cb.size() & 1)) cb.push_back(0);  // even (UnpackUtils.cs:100)
+                std::vector<uint8_t> cmd;
+                put_subblock(cmd, ID_WVC_BITSTREAM, cb);
+                std::vector<uint8_t> cblk(32);
+                cblk.insert(cblk.end(), cmd.begin(), cmd.end());
+                write_header(cblk, P.version, P.total_override > 0 ? P.total_override : frames,
+                             P.block_index_start + f0, (uint32_t)nf, flags, crc_exact, P.total_unknown);
+                wvc_file.insert(wvc_file.end(), cblk.begin(), cblk.end());
+            }
         }
         return file;
     }
@@ -1296,11 +1355,44 @@ int64_t wvenc_encode_pcm(const int32_t *samples, int64_t frames, const wvenc_par
             bool ok = (t >= 1 && t <= 8) || t == 17 || t == 18 || ((t >= -3 && t <= -1) && p->nch == 2 && !p->false_stereo);
             if (!ok) throw std::runtime_error("unsupported term for this channel layout");
         }
+        if (p->wvc) throw std::runtime_error("wvc: use wvenc_encode_pcm_wvc");
         PcmEncoder enc(*p);
         std::vector<uint8_t> f = enc.encode(samples, frames);
         if (!out) return (int64_t)f.size();
         if ((int64_t)f.size() > cap) return -(int64_t)f.size();
         memcpy(out, f.data(), f.size());
+        return (int64_t)f.size();
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
+// Hybrid PCM with its .wvc correction file: the .wv into `out`, the .wvc into
+// `wvc_out`; returns the .wv size (*wvc_n the .wvc size), or -1 (too small / error).
+// NULL outputs query both sizes.
+int64_t wvenc_encode_pcm_wvc(const int32_t *samples, int64_t frames, const wvenc_params *p, uint8_t *out, int64_t cap,
+                             uint8_t *wvc_out, int64_t wvc_cap, int64_t *wvc_n) {
+    try {
+        if (p->nch < 1 || p->nch > 2) throw std::runtime_error("nch must be 1 or 2");
+        if (p->num_terms < 0 || p->num_terms > 16) throw std::runtime_error("num_terms");
+        if (p->block_samples <= 0) throw std::runtime_error("block_samples");
+        if (!p->hybrid || !p->wvc) throw std::runtime_error("wvc needs hybrid");
+        if (p->wvx || p->int32_zeros || p->int32_sent_bits || p->int32_ones || p->int32_dups || p->sticky_passes)
+            throw std::runtime_error("wvc: plain PCM or float only");
+        for (int e = 0; e < p->num_terms; e++)
+            if (p->terms[e] == -1 || p->terms[e] == -2)
+                throw std::runtime_error("wvc: terms -1/-2 read the other channel's current output");
+        PcmEncoder enc(*p);
+        std::vector<uint8_t> f = enc.encode(samples, frames);
+        *wvc_n = (int64_t)enc.wvc_file.size();
+        if (!out || !wvc_out) return (int64_t)f.size();
+        if ((int64_t)f.size() > cap || (int64_t)enc.wvc_file.size() > wvc_cap) {
+            g_err = "output too small";
+            return -1;
+        }
+        memcpy(out, f.data(), f.size());
+        memcpy(wvc_out, enc.wvc_file.data(), enc.wvc_file.size());
         return (int64_t)f.size();
     } catch (const std::exception &e) {
         g_err = e.what();

@@ -39,7 +39,7 @@ class _Params(ctypes.Structure):
             "bitrate_x256", "float_data", "float_flags", "float_shift", "float_max_exp", "float_norm_exp",
             "int32_zeros", "write_riff", "config_flags", "write_history", "reset_state", "block_index_start",
             "total_unknown", "extras", "mag_override", "int32_sent_bits", "int32_ones", "int32_dups", "wvx",
-            "wvx_max_width", "wvx_short")] + [("total_override", ctypes.c_int64), ("sticky_passes", ctypes.c_int32)]
+            "wvx_max_width", "wvx_short")] + [("total_override", ctypes.c_int64), ("sticky_passes", ctypes.c_int32), ("wvc", ctypes.c_int32)]
 
 
 class _DsdParams(ctypes.Structure):
@@ -86,6 +86,7 @@ class EncParams:
     wvx_short: int = 0      # bytes dropped from every wvx payload (the reference then over-reads and throws)
     total_override: int = 0  # > 0: header total_samples (parts encoded in parallel, then concatenated)
     sticky_passes: bool = False  # blocks after the first continue the decoder's passes (no pass metadata)
+    wvc: bool = False            # hybrid: also write the .wvc correction file (encode_pcm_wvc)
 
     def to_c(self) -> _Params:
         p = _Params()
@@ -102,7 +103,7 @@ class EncParams:
                   "wvx_short", "total_override"):
             setattr(p, n, int(getattr(self, n)))
         for n in ("hybrid", "hybrid_bitrate", "hybrid_balance", "float_data", "write_riff", "write_history",
-                  "reset_state", "total_unknown", "sticky_passes"):
+                  "reset_state", "total_unknown", "sticky_passes", "wvc"):
             setattr(p, n, int(bool(getattr(self, n))))
         return p
 
@@ -152,6 +153,10 @@ def lib():
         L.wvenc_encode_pcm.restype = ctypes.c_int64
         L.wvenc_encode_pcm.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(_Params), ctypes.c_void_p,
                                        ctypes.c_int64]
+        L.wvenc_encode_pcm_wvc.restype = ctypes.c_int64
+        L.wvenc_encode_pcm_wvc.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(_Params), ctypes.c_void_p,
+                                           ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+                                           ctypes.POINTER(ctypes.c_int64)]
         L.wvenc_encode_dsd.restype = ctypes.c_int64
         L.wvenc_encode_dsd.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(_DsdParams),
                                        ctypes.c_void_p, ctypes.c_int64]
@@ -174,6 +179,28 @@ def encode_pcm(samples: np.ndarray, params: EncParams) -> bytes:
     if m != n:
         raise RuntimeError("wvenc: size mismatch " + L.wvenc_last_error().decode())
     return out.tobytes()
+
+
+def encode_pcm_wvc(samples: np.ndarray, params: EncParams):
+    """Hybrid PCM -> (.wv bytes, .wvc bytes): the .wv decodes lossy (the reference's
+    output); with the .wvc correction the residuals are exact and the decode is lossless."""
+    x = np.ascontiguousarray(samples, dtype=np.int32).reshape(-1)
+    frames = x.size // params.nch
+    params.hybrid = True
+    params.wvc = True
+    p = params.to_c()
+    L = lib()
+    nc = ctypes.c_int64(0)
+    n = L.wvenc_encode_pcm_wvc(x.ctypes.data, frames, ctypes.byref(p), None, 0, None, 0, ctypes.byref(nc))
+    if n < 0:
+        raise RuntimeError("wvenc: " + L.wvenc_last_error().decode())
+    out = np.empty(n, dtype=np.uint8)
+    cout = np.empty(max(nc.value, 1), dtype=np.uint8)
+    m = L.wvenc_encode_pcm_wvc(x.ctypes.data, frames, ctypes.byref(p), out.ctypes.data, n, cout.ctypes.data,
+                               cout.size, ctypes.byref(nc))
+    if m != n:
+        raise RuntimeError("wvenc: " + L.wvenc_last_error().decode())
+    return out.tobytes(), cout[: nc.value].tobytes()
 
 
 @dataclass

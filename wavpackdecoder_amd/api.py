@@ -70,11 +70,17 @@ class DecodeBatch:
         self._uploaded = False
         self._data: list = []
 
-    def add_file(self, data: bytes, open_flags: int = 0, start_sample: int | None = None):
+    def add_file(self, data: bytes, open_flags: int = 0, start_sample: int | None = None, wvc: bytes | None = None):
         """Frame one file; with start_sample, as a caller that calls SetSample(start_sample)
-        right after WavpackOpenFileInput (WavPackUtils.cs:509-594)."""
+        right after WavpackOpenFileInput (WavPackUtils.cs:509-594).  wvc: the hybrid file's
+        .wvc correction file -- its hybrid blocks then decode exactly (beyond the reference)."""
         info = _L.WvgFileInfo()
-        if start_sample is None:
+        if wvc is not None:
+            if start_sample is not None:
+                raise ValueError("wvc with start_sample is not supported")
+            idx = self._L.wvg_batch_add_file_wvc(self._b, data, len(data), wvc, len(wvc), int(open_flags),
+                                                 ctypes.byref(info))
+        elif start_sample is None:
             idx = self._L.wvg_batch_add_file(self._b, data, len(data), int(open_flags), ctypes.byref(info))
         else:
             idx = self._L.wvg_batch_add_file_at(self._b, data, len(data), int(open_flags), int(start_sample),

@@ -515,6 +515,27 @@ int wvg_batch_add_files(wvg_batch *b, int n, const uint8_t *const *files, const 
     return n;
 }
 
+// A hybrid file with its .wvc correction file (beyond the reference, which
+// never reads the correction stream: SURVEY §8f-4): both are copied into the blob
+// and the hybrid blocks decode exactly.
+int wvg_batch_add_file_wvc(wvg_batch *b, const uint8_t *file, size_t len, const uint8_t *wvc, size_t wvc_len,
+                           uint32_t open_flags, wvg_file_info *info) {
+    if (!b || (!file && len) || (!wvc && wvc_len)) return WVG_ERR_ARG;
+    b->uploaded = b->formatted = false;
+    const size_t base = (b->blob.size() + 15) & ~(size_t)15;
+    const size_t cbase = (base + len + 15) & ~(size_t)15;
+    if (!b->blob.resize(cbase + wvc_len)) {
+        b->ctx->err = "out of host memory";
+        return WVG_ERR_ARG;
+    }
+    if (len) memcpy(b->blob.data() + base, file, len);
+    if (wvc_len) memcpy(b->blob.data() + cbase, wvc, wvc_len);
+    FileInfo fi;
+    frame_file(b->blob.data() + base, len, base, (uint64_t)b->out_ints, open_flags, b->chunk, b->fo, fi, -1,
+               wvc_len ? b->blob.data() + cbase : nullptr, wvc_len, cbase);
+    return commit_file(b, fi, len + wvc_len, info);
+}
+
 int wvg_batch_add_file_at(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open_flags, int64_t start_sample,
                           wvg_file_info *info) {
     if (start_sample < 0) return WVG_ERR_ARG;

@@ -1069,6 +1069,7 @@ int term_set_of(const BlockDesc &d, int prefer_pipe) {
     if (d.kind != KIND_PCM) return -1;
     if (d.chain_len >= 2 || (d.inherit & INH_MEMBER)) return -1;  // sticky-state chain (wv_decode_pcm_wave)
     if (d.wvx_state & 0x100) return -1;  // int32 + wvx fixup reads a second stream
+    if (d.wvc_len) return -1;            // .wvc correction: a second stream read per hybrid word
     const bool mono = (d.flags & MONO_DATA) != 0;
     if (d.num_terms < 0 || d.num_terms > MAXP) return -1;
     bool neg12 = false;

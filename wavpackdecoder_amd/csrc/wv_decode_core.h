@@ -223,12 +223,37 @@ WVF_HD void update_error_limit(Entropy &w, uint32_t flags, int &exc, const TB &t
     }
 }
 
+// read_code (WordsUtils.cs:546-570) with count_bits (:513-537); false: the
+// nbits_table[] index is out of range (the C# throws)
+template <class BR>
+WVF_HD bool read_code(BR &bs, int64_t maxcode, int64_t &code) {
+    if (maxcode < 0 || maxcode >= (1LL << 32)) return false;
+    const uint32_t mc = (uint32_t)maxcode;
+    const int bitcount = mc ? 32 - __builtin_clz(mc) : 0;
+    code = 0;
+    if (bitcount != 0) {
+        const int64_t extras = (int64_t)wvf::shl32(1, bitcount) - maxcode - 1;
+        code = (int64_t)(bs.getbits(bitcount - 1) & (uint32_t)(wvf::shl32(1, bitcount - 1) - 1));
+        if (code >= extras) {
+            code = (code << 1) - extras;
+            if (bs.getbit()) ++code;
+        }
+    }
+    return true;
+}
+
 // One residual of get_words (WordsUtils.cs:290-503).  `c` is entidx, `even`
 // is ((csamples & 1) == 0).  Returns DEC_* and the value in `out`.
+// With a .wvc correction stream `cb` (beyond the reference, which never reads
+// it; WavPack 4's get_word): a word the error limit left inexact reads its exact
+// magnitude as read_code(wvcbits, high - low) + low, and *corr receives the
+// exact residual minus the lossy one (0 for every other word).
 template <class BR, class TB = MemTabs>
-WVF_HD int get_word(Entropy &w, BR &bs, uint32_t flags, int c, bool even, int32_t &out, const TB &tb = TB()) {
+WVF_HD int get_word(Entropy &w, BR &bs, uint32_t flags, int c, bool even, int32_t &out, const TB &tb = TB(),
+                    BR *cb = nullptr, int32_t *corr = nullptr) {
     using namespace wvf;
     int exc = 0;
+    if (corr) *corr = 0;
     const bool mono = (flags & MONO_DATA) != 0;
     if ((w.med[0][0] & ~1) == 0 && !w.h0 && !w.h1 && (w.med[1][0] & ~1) == 0) {
         // zero-run mode (:304-352)
@@ -312,20 +337,8 @@ WVF_HD int get_word(Entropy &w, BR &bs, uint32_t flags, int c, bool even, int32_
 
     int64_t mid;
     if (w.errlim[c] == 0) {
-        // read_code (:546-570) with count_bits (:513-537)
-        int64_t maxcode = high - low;
-        if (maxcode < 0 || maxcode >= (1LL << 32)) return DEC_EXCEPTION;  // nbits_table[] out of range
-        uint32_t mc = (uint32_t)maxcode;
-        int bitcount = mc ? 32 - __builtin_clz(mc) : 0;
-        int64_t code = 0;
-        if (bitcount != 0) {
-            int64_t extras = (int64_t)shl32(1, bitcount) - maxcode - 1;
-            code = (int64_t)(bs.getbits(bitcount - 1) & (uint32_t)(shl32(1, bitcount - 1) - 1));
-            if (code >= extras) {
-                code = (code << 1) - extras;
-                if (bs.getbit()) ++code;
-            }
-        }
+        int64_t code;
+        if (!read_code(bs, high - low, code)) return DEC_EXCEPTION;  // nbits_table[] out of range
         mid = code + low;
     } else if (w.errlim[c] >= 0 && low >= 0 && high >= low && high < ((int64_t)1 << 30)) {
         // The bisection (WordsUtils.cs:486-492) in 32 bits: with a non-negative
@@ -347,6 +360,8 @@ WVF_HD int get_word(Entropy &w, BR &bs, uint32_t flags, int c, bool even, int32_
         }
         bs.skip(used);
         mid = (int64_t)md;
+        low = (int64_t)lo;
+        high = (int64_t)hi;
     } else {
         mid = (high + low + 1) >> 1;
         // The C# loop (WordsUtils.cs:486-492) never ends for some negative error
@@ -367,7 +382,14 @@ WVF_HD int get_word(Entropy &w, BR &bs, uint32_t flags, int c, bool even, int32_
                 mid = ((high = mid - 1) + low + 1) >> 1;
         }
     }
-    out = bs.getbit() ? (int32_t)~(uint32_t)(uint64_t)mid : (int32_t)(uint32_t)(uint64_t)mid;
+    const int sign = bs.getbit();
+    out = sign ? (int32_t)~(uint32_t)(uint64_t)mid : (int32_t)(uint32_t)(uint64_t)mid;
+    if (cb && w.errlim[c] != 0) {
+        int64_t code;
+        if (!read_code(*cb, high - low, code)) return DEC_EXCEPTION;
+        const int64_t value = code + low;
+        *corr = (int32_t)(uint32_t)(uint64_t)(sign ? mid - value : value - mid);
+    }
     if (flags & HYBRID_BITRATE) {
         int lg = dev_mylog2(mid, exc, tb);
         w.slow[c] = add32(sub32(w.slow[c], add32(w.slow[c], SLO) >> SLS), lg);
@@ -628,6 +650,8 @@ WVF_HD int32_t fixup_wvx(const Fixup &f, BitReader &xb, uint32_t xlen, int32_t x
 // ---------------------------------------------------------------------------
 struct PcmState {
     BitReader bs, xb;
+    BitReader cb;         // .wvc correction stream (d.wvc_len > 0)
+    bool wvc;
     Entropy w;
     PassState ps[MAXP];
     int32_t crc, crc_x;   // wps.crc / wps.crc_x
@@ -668,6 +692,8 @@ WVF_HD uint32_t pcm_state_load(PcmState &s, const BlockDesc &d, const uint8_t *b
         // the rest of the current byte reads as zeros
         s.bs.win &= ~((1ull << (s.bs.nb & 7)) - 1ull);
     }
+    s.wvc = d.wvc_len > 0;
+    if (s.wvc) s.cb.init(blob, d.wvc_off, d.wvc_len);
     if (!(inh & INH_WVX)) {
         s.xb.init(blob, d.wvx_off, d.wvx_len);
         if (d.wvx_state & 0x100) {
@@ -774,9 +800,10 @@ WVF_HD uint32_t decode_pcm_run(PcmState &s, const BlockDesc &d, Store &out, uint
         bool words_short = false;
         for (uint32_t j = 0; j < n; j++) {
             uint32_t t = f + j;
-            int32_t L, R = 0;
-            int rc = get_word(w, bs, flags, 0, true, L);
-            if (rc == DEC_OK && !mono) rc = get_word(w, bs, flags, 1, false, R);
+            int32_t L, R = 0, cL = 0, cR = 0;
+            BitReader *cbp = s.wvc ? &s.cb : nullptr;
+            int rc = get_word(w, bs, flags, 0, true, L, MemTabs(), cbp, &cL);
+            if (rc == DEC_OK && !mono) rc = get_word(w, bs, flags, 1, false, R, MemTabs(), cbp, &cR);
             if (rc != DEC_OK) {
                 if (rc == DEC_EXCEPTION) {
                     if (exc_frame) *exc_frame = t;  // block frame of the word that threw
@@ -793,6 +820,7 @@ WVF_HD uint32_t decode_pcm_run(PcmState &s, const BlockDesc &d, Store &out, uint
             }
             if (mono) {
                 for (int i = 0; i < nt; i++) pass_mono(ps[i], t, L);
+                L = add32(L, cL);  // .wvc: the exact value (the passes keep the lossy history)
                 int32_t a = L < 0 ? (int32_t)(0u - (uint32_t)L) : L;
                 if (!crc_stop && a > ml) {
                     uint32_t q = bsp + j;  // absolute buffer index (quirk B-6)
@@ -805,6 +833,8 @@ WVF_HD uint32_t decode_pcm_run(PcmState &s, const BlockDesc &d, Store &out, uint
                 if (!crc_stop) s.crc = add32(mul32(s.crc, 3), L);
             } else {
                 for (int i = 0; i < nt; i++) pass_stereo(ps[i], t, L, R, n >= 16 && j >= 8);
+                L = add32(L, cL);  // .wvc: the exact values (the passes keep the lossy history)
+                R = add32(R, cR);
                 if (joint) {
                     R = sub32(R, L >> 1);
                     L = add32(L, R);

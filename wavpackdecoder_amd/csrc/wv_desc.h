@@ -89,6 +89,12 @@ struct alignas(16) BlockDesc {
     uint32_t inherit;         // InheritBits (0: everything comes from the descriptor)
     uint32_t inherit_passes;  // bit i: pass i's weights, bit 16 + i: its samples continue
     uint32_t chain_len;       // first block of a chain: blocks decoded in sequence from it (>= 2)
+    // --- .wvc correction (beyond the reference): the hybrid block's
+    // ID_WVC_BITSTREAM in the correction file; crc then holds the .wvc header's
+    // crc (of the exact output) and crc_lossy the .wv header's
+    uint64_t wvc_off;
+    uint32_t wvc_len;         // 0: no correction stream (the reference's decode)
+    int32_t crc_lossy;
 };
 
 // A block that starts from state an earlier decode left behind: a block without

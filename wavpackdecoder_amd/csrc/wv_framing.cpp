@@ -135,6 +135,11 @@ class Framer {
     // computes; until materialize() the host copies of those values are stale
     bool defer = false;
     std::vector<MetaItem> pending;  // file offsets, stream order
+    // the .wvc correction file (beyond the reference): its blocks are
+    // matched to the main stream's by block_index, walked forward from wvc_pos
+    const uint8_t *wvc = nullptr;
+    int64_t wvc_len = 0, wvc_pos = 0;
+    uint64_t wvc_base = 0;
 
     Framer() {
         memset(read_buffer, 0, sizeof(read_buffer));
@@ -873,6 +878,7 @@ class Framer {
         if (d.kind == KIND_PCM) {
             d.inherit = inh;
             d.inherit_passes = inhp;
+            if (!inh && !inhp && !(d.wvx_state & 1)) attach_wvc(d);
         } else if (inh & INH_NOINIT) {
             status |= ST_UNSUPPORTED;  // a DSD block continuing the crc / mute state
         }
@@ -883,6 +889,48 @@ class Framer {
         // the framing reports its verdicts through the same status word
         d.fstatus = status;
         return d;
+    }
+
+    // The correction stream of the hybrid block being snapshotted: the .wvc block
+    // with the same block_index (its headers back to back, as WavPack writes
+    // them), its ID_WVC_BITSTREAM sub-block (even length, UnpackUtils.cs:96-106).
+    // d.crc becomes the .wvc header's crc (of the exact output).
+    void attach_wvc(BlockDesc &d) {
+        if (!wvc || !(wphdr.flags & HYBRID_FLAG) || (wphdr.flags & HYBRID_SHAPE)) return;
+        while (wvc_pos + 32 <= wvc_len) {
+            const uint8_t *b = wvc + wvc_pos;
+            if (!(b[0] == 'w' && b[1] == 'v' && b[2] == 'p' && b[3] == 'k')) return;
+            const uint32_t ck = (uint32_t)b[4] | ((uint32_t)b[5] << 8) | ((uint32_t)b[6] << 16) | ((uint32_t)b[7] << 24);
+            const int64_t bi = (int64_t)(((uint64_t)b[10] << 32) | ((uint64_t)b[19] << 24) | ((uint64_t)b[18] << 16) |
+                                         ((uint64_t)b[17] << 8) | b[16]);
+            if (bi > wphdr.block_index) return;
+            const int64_t end = wvc_pos + (int64_t)ck + 8;
+            if (end > wvc_len) return;
+            if (bi == wphdr.block_index) {
+                for (int64_t p = wvc_pos + 32; p + 2 <= end;) {
+                    uint8_t id = wvc[p];
+                    int64_t bl = (int64_t)wvc[p + 1] << 1, hl = 2;
+                    if (id & ID_LARGE) {
+                        if (p + 4 > end) return;
+                        bl += ((int64_t)wvc[p + 2] << 9) + ((int64_t)wvc[p + 3] << 17);
+                        hl = 4;
+                    }
+                    const int64_t real = (id & ID_ODD_SIZE) ? bl - 1 : bl;
+                    if ((id & 0x3f) == ID_WVC_BITSTREAM && real > 0 && !(real & 1) && p + hl + bl <= end) {
+                        d.wvc_off = wvc_base + (uint64_t)(p + hl);
+                        d.wvc_len = (uint32_t)real;
+                        d.crc_lossy = d.crc;
+                        d.crc = (int32_t)((uint32_t)b[28] | ((uint32_t)b[29] << 8) | ((uint32_t)b[30] << 16) |
+                                          ((uint32_t)b[31] << 24));
+                        break;
+                    }
+                    p += hl + bl;
+                }
+                wvc_pos = end;
+                return;
+            }
+            wvc_pos = end;
+        }
     }
 
     // decoding changes the passes, the entropy state and the bitstreams
@@ -1121,10 +1169,14 @@ static void chain_blocks(FramingOutput &out, int64_t first, int64_t count) {
 }
 
 void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t out_base_ints, uint32_t open_flags,
-                int chunk, FramingOutput &out, FileInfo &info, int64_t seek_to) {
+                int chunk, FramingOutput &out, FileInfo &info, int64_t seek_to, const uint8_t *wvc, size_t wvc_len,
+                uint64_t wvc_base) {
     std::unique_ptr<Framer> FP(new Framer());
     Framer &F = *FP;
     F.defer = out.defer_values;
+    F.wvc = wvc;
+    F.wvc_len = wvc ? (int64_t)wvc_len : 0;
+    F.wvc_base = wvc_base;
     F.in.d = file;
     F.in.len = (int64_t)len;
     info = FileInfo();
@@ -1301,6 +1353,15 @@ void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t ou
     info.num_desc = (int64_t)out.descs.size() - info.first_desc;
     (void)cur;
     chain_blocks(out, info.first_desc, info.num_desc);
+    for (int64_t k = info.first_desc; k < info.first_desc + info.num_desc; k++) {
+        BlockDesc &d = out.descs[(size_t)k];
+        if (d.wvc_len && (d.kind != KIND_PCM || d.chain_len || (d.inherit & INH_MEMBER))) {
+            d.crc = d.crc_lossy;  // a chain continues the lossy state: decoded as the reference does
+            d.wvc_len = 0;
+            d.wvc_off = 0;
+            d.crc_lossy = 0;
+        }
+    }
 }
 
 }  // namespace wvg

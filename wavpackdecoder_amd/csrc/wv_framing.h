@@ -65,8 +65,11 @@ void apply_meta_jobs(FramingOutput &out, const uint8_t *blob);
 // appended to `out` with out_off relative to `out_base_ints`.
 // seek_to >= 0: the caller calls SetSample(seek_to) (WavPackUtils.cs:509-594)
 // right after opening, and its calls return the frames from there on.
+// wvc (optional): the file's .wvc correction file, whose bytes start at blob
+// offset wvc_base; hybrid blocks then decode exactly (beyond the reference).
 void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t out_base_ints, uint32_t open_flags,
-                int chunk, FramingOutput &out, FileInfo &info, int64_t seek_to = -1);
+                int chunk, FramingOutput &out, FileInfo &info, int64_t seek_to = -1, const uint8_t *wvc = nullptr,
+                size_t wvc_len = 0, uint64_t wvc_base = 0);
 
 // Output ints a batch reserves for a framed file: its reported values
 // (out_frames x out_nch) or more when a descriptor writes past them -- a file
