@@ -1670,11 +1670,15 @@ __device__ __forceinline__ int32_t iabs(int32_t x) { return x < 0 ? (int32_t)(0u
 // both sample and input are non-zero; negative terms clamp to +-1024
 // (:808-818), and |w| <= 1024 holds for them throughout (restore_weight
 // range, clamped updates), so the clamp is a plain med3.
+// As sign(s) * sign(x) * delta: two v_med3_i32 and two full-rate 24-bit multiplies
+// (delta <= 7) instead of a compare/select per condition.
+__device__ __forceinline__ int32_t vsgn(int32_t v) {  // (the compiler lowers min/max of it to compare + selects)
+    int32_t r;
+    asm("v_med3_i32 %0, %1, -1, 1" : "=v"(r) : "v"(v));
+    return r;
+}
 __device__ __forceinline__ int32_t vupd(int32_t w, int32_t s, int32_t x, int32_t delta) {
-    int32_t dd = (s ^ x) < 0 ? -delta : delta;
-    dd = s != 0 ? dd : 0;
-    dd = x != 0 ? dd : 0;
-    return wvf::add32(w, dd);
+    return wvf::add32(w, __mul24(__mul24(vsgn(s), vsgn(x)), delta));
 }
 __device__ __forceinline__ int32_t vupdc(int32_t w, int32_t s, int32_t x, int32_t delta) {
     return max(-1024, min(1024, vupd(w, s, x, delta)));
