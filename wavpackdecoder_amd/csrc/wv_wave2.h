@@ -1677,8 +1677,13 @@ __device__ __forceinline__ int32_t vsgn(int32_t v) {  // (the compiler lowers mi
     asm("v_med3_i32 %0, %1, -1, 1" : "=v"(r) : "v"(v));
     return r;
 }
+__device__ __forceinline__ int32_t vmul24(int32_t a, int32_t b) {  // (else a v_mul_lo_u32, quarter rate)
+    int32_t r;
+    asm("v_mul_i32_i24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 __device__ __forceinline__ int32_t vupd(int32_t w, int32_t s, int32_t x, int32_t delta) {
-    return wvf::add32(w, __mul24(__mul24(vsgn(s), vsgn(x)), delta));
+    return wvf::add32(w, __mul24(vmul24(vsgn(s), vsgn(x)), delta));
 }
 __device__ __forceinline__ int32_t vupdc(int32_t w, int32_t s, int32_t x, int32_t delta) {
     return max(-1024, min(1024, vupd(w, s, x, delta)));
@@ -1863,8 +1868,15 @@ __device__ __forceinline__ void recon_batch(CH &ch, const Fixup &fx, const int32
     constexpr uint32_t BF = MONO ? 64 : 32;
     const bool isB = !MONO && (lane & 1);
     const int pair = lane >> 1;
+    // LEAN && IDENT: the mute test of 8 frames is one ballot at the group's end
+    // (the running max of |value|); a group that mutes is replayed from the staged
+    // outputs (o0/o1 hold the values themselves) for the muting frame and the crc
+    // before it -- the passes' state past it no longer matters (the block ends muted)
+    constexpr bool BATCH_MUTE = LEAN && IDENT;
     for (uint32_t g = 0; g < BF / 8; g++) {
         if (!LEAN && t0 + g * 8 >= tvalid) break;
+        const int32_t crc_g = crc;
+        int32_t vmx = 0;
         int32_t xr[8];
 #pragma unroll
         for (int u = 0; u < 8; u++)
@@ -1878,7 +1890,10 @@ __device__ __forceinline__ void recon_batch(CH &ch, const Fixup &fx, const int32
             int32_t fl;                                                                        \
             if (MONO) {                                                                        \
                 ch.template mono<U>(x);                                                        \
-                if (LEAN) {                                                                    \
+                if (BATCH_MUTE) {                                                              \
+                    vmx = max(vmx, iabs(x));                                                   \
+                    crc = add32(mul32(crc, 3), x);                                             \
+                } else if (LEAN) {                                                             \
                     if (__builtin_expect(any_lane(iabs(x) > ml), 0)) {                         \
                         mute_at = (int)t;                                                      \
                         break;                                                                 \
@@ -1904,12 +1919,15 @@ __device__ __forceinline__ void recon_batch(CH &ch, const Fixup &fx, const int32
                     Rv = sub32(Rv, Lv >> 1);                                                   \
                     Lv = add32(Lv, Rv);                                                        \
                 }                                                                              \
-                if (__builtin_expect(any_lane(max(iabs(Lv), iabs(Rv)) > ml), 0)) {             \
+                fl = isB ? Rv : Lv;                                                            \
+                /* even lanes test L, odd lanes R: one wave-wide ballot covers both */         \
+                if (BATCH_MUTE) {                                                              \
+                    vmx = max(vmx, iabs(fl));                                                  \
+                } else if (__builtin_expect(any_lane(iabs(fl) > ml), 0)) {                     \
                     mute_at = (int)t;                                                          \
                     break;                                                                     \
                 }                                                                              \
                 crc = add32(mul32(crc, 9), add32(mul32(Lv, 3), Rv));                           \
-                fl = isB ? Rv : Lv;                                                            \
             }                                                                                  \
             if (!LEAN && (t == sm.seam8 || t == sm.chunk_end - 1)) ch.trunc();                 \
             if (!IDENT) fl = fixup_tail(fx, fl);                                               \
@@ -1937,6 +1955,29 @@ __device__ __forceinline__ void recon_batch(CH &ch, const Fixup &fx, const int32
             WV2_VFRAME(7)
         } while (0);
 #undef WV2_VFRAME
+        if (BATCH_MUTE && __builtin_expect(any_lane(vmx > ml), 0)) {
+            crc = crc_g;
+            for (uint32_t u = 0; u < 8; u++) {
+                const uint32_t j = g * 8 + u;
+                bool mute;
+                if (MONO) {
+                    const int32_t v = (LAYOUT == 1) ? __builtin_amdgcn_readlane(o0, (int)j)
+                                                    : (j < 32 ? __builtin_amdgcn_readlane(o0, 2 * (int)j)
+                                                              : __builtin_amdgcn_readlane(o1, 2 * (int)j - 64));
+                    mute = iabs(v) > ml;
+                    if (!mute) crc = add32(mul32(crc, 3), v);
+                } else {
+                    const int32_t Lv = __builtin_amdgcn_readlane(o0, 2 * (int)j);
+                    const int32_t Rv = __builtin_amdgcn_readlane(o0, 2 * (int)j + 1);
+                    mute = iabs(Lv) > ml || iabs(Rv) > ml;
+                    if (!mute) crc = add32(mul32(crc, 9), add32(mul32(Lv, 3), Rv));
+                }
+                if (mute) {
+                    mute_at = (int)(t0 + j);
+                    break;
+                }
+            }
+        }
         if (mute_at >= 0) break;
     }
 }
