@@ -377,6 +377,18 @@ def run_rank(args) -> None:
         t_runs.append(time.perf_counter() - t_e2e)
     t_e2e = float(np.median(t_runs))
     e2e = frames_rank / t_e2e / 1e6
+    # the same request with the framing on the device (wvg_batch_add_files_device)
+    t_runs = []
+    for _ in range(3):
+        t_d = time.perf_counter()
+        be.reset()
+        be.add_files_device(files)
+        be.upload()
+        be.decode()
+        be.download(pinned=True)
+        t_runs.append(time.perf_counter() - t_d)
+    t_e2e_dev = float(np.median(t_runs))
+    dev_framed = be.framing_stats()
     # the same request stream served by one host thread per batch copy, so one
     # batch's framing, upload, decode and download overlap the others' (ctypes
     # drops the GIL inside the library; each batch has its own stream)
@@ -456,6 +468,11 @@ def run_rank(args) -> None:
             "pcie_inclusive": {"value": round(e2e, 2), "unit": "Msamples/s", "ms": round(t_e2e * 1e3, 3),
                                "what": "warm batch: host framing + upload of the compressed batch (page-locked) + "
                                        "decode + download of int32 PCM into page-locked memory, rank 0, median of 3",
+                               "device_framing": {"value": round(frames_rank / t_e2e_dev / 1e6, 2),
+                                                  "ms": round(t_e2e_dev * 1e3, 3),
+                                                  "files_device_host": list(dev_framed),
+                                                  "what": "the same warm request with the header/sub-block walk "
+                                                          "on the GPU (wvg_batch_add_files_device)"},
                                "pipelined": None if e2e_pipe is None else round(e2e_pipe, 2),
                                "pipelined_pcm": None if e2e_pcm is None else round(e2e_pcm, 2),
                                "pipelined_what": "the same request served by one host thread per batch copy "

@@ -68,7 +68,7 @@ struct DBlock {
     int32_t file_format;  // ID_NEW_CONFIG_BLOCK's value, -1 none
     int32_t info_mask;    // bit 0 INT32_INFO, bit 1 FLOAT_INFO seen
     int32_t num_channels; // ID_CHANNEL_INFO's count, -1 none
-    int32_t pad_;
+    int32_t dsd_mult_log2;  // ID_DSD_BLOCK's rate multiplier (log2), -1 none
     int64_t header_off, header_len, trailer_off, trailer_len;  // file-relative, -1 none
 };
 
@@ -126,6 +126,11 @@ struct DState {
     int32_t i32[4];     // sent_bits, zeros, ones, dups
     int32_t fl[4];      // float flags, shift, max_exp, norm_exp
     bool terms, entropy, bits, has_i32, has_fl;
+    // ID_DSD_BLOCK, mode 0 only (DsdUtils.cs:17-54): the raw bytes after mult/mode
+    bool dsd;
+    int32_t dsd_mult_log2;  // data[0] & 31
+    int64_t dsd_off;        // file offset of data[2]
+    int32_t dsd_len;        // C# data.Length - 2
     // context (file-level) values, updated in place
     int64_t cfg_flags;
     int32_t xmode;
@@ -144,6 +149,10 @@ WVF_HD void dstate_init(DState &s) {
     s.bits_len = 0;
     for (int i = 0; i < 4; i++) s.i32[i] = s.fl[i] = 0;
     s.terms = s.entropy = s.bits = s.has_i32 = s.has_fl = false;
+    s.dsd = false;
+    s.dsd_mult_log2 = 0;
+    s.dsd_off = 0;
+    s.dsd_len = 0;
     s.cfg_flags = 0;
     s.xmode = 0;
     s.num_channels = -1;
@@ -317,13 +326,25 @@ WVF_HD uint32_t dframe_subblocks(const uint8_t *f, uint64_t len, uint64_t hpos, 
         case ID_WVC_BITSTREAM:
         case ID_WVX_BITSTREAM:
         case ID_WVX_NEW_BITSTREAM:
-        case ID_DSD_BLOCK: return DF_KIND;
+        case ID_DSD_BLOCK: {  // init_dsd_block (DsdUtils.cs:17-54); modes 1/3 build tables: the host's
+            if (byte_length < 2 || d[0] > 31 || d[1] != 0) return DF_KIND;
+            // copy_data's length: the read buffer's fill for a small sub-block, the bytes read for a large one
+            const int32_t dl = to_read > BITSTREAM_BUFFER_SIZE ? to_read : byte_length;
+            if ((int64_t)(dl - 2) != (int64_t)h.block_samples * (mono ? 1 : 2)) return DF_READER;
+            s.dsd = true;
+            s.dsd_mult_log2 = d[0] & 31;
+            s.dsd_off = (int64_t)doff + 2;
+            s.dsd_len = dl - 2;
+            break;
+        }
         default:
             if (!(id & ID_OPTIONAL_DATA)) return DF_READER;  // "invalid metadata id": the host reports it
             break;
         }
     }
     if (bytecount != (int64_t)h.ckSize) return DF_SUBBLOCK;
+    if (h.flags & DSD_FLAG) return s.dsd ? DF_OK : DF_STATE;  // unpack_init: dsd.ready (a block without
+                                                              // ID_DSD_BLOCK continues the consumed DSD state)
     if (!s.bits || s.bits_len == 0) return DF_READER;  // "invalid WavPack file"
     if (!s.terms || !s.entropy) return DF_STATE;       // passes / words_data continue the previous decode
     return DF_OK;
@@ -343,7 +364,8 @@ WVF_HD void dframe_walk(DFile &fi, const uint8_t *blob, uint64_t *slots) {
         fi.why = DF_HEADER;
         return;
     }
-    if (h.block_samples == 0 || h.block_index != 0 || (h.flags & DSD_FLAG)) {
+    if (h.block_samples == 0 || h.block_index != 0 ||
+        ((h.flags & DSD_FLAG) && (h.flags & FALSE_STEREO))) {  // DSD mode 0 + FALSE_STEREO overruns (DsdUtils.cs:81)
         fi.why = DF_OPEN;
         return;
     }
@@ -392,6 +414,11 @@ WVF_HD void dframe_walk(DFile &fi, const uint8_t *blob, uint64_t *slots) {
     }
     if (cfg & CONFIG_FAST_FLAG) mode |= 0x40;
     if (cfg & CONFIG_EXTRA_MODE) mode |= 0x80 | ((s.xmode << 12) & 0x7000);
+    if (h.flags & DSD_FLAG) {  // dsd_multiplier > 0 (open_input, WavPackUtils.cs:116-119)
+        mode |= 0x10000;
+        bytes_per_sample = 1;
+        bits_per_sample = 8;
+    }
     fi.num_channels = num_channels;
     fi.nch = num_channels;
     fi.bits_per_sample = bits_per_sample;
@@ -404,6 +431,7 @@ WVF_HD void dframe_walk(DFile &fi, const uint8_t *blob, uint64_t *slots) {
     fi.config_flags = cfg;
     // the header walk: every block starts where the previous one ends
     const uint32_t bch0 = (uint32_t)num_channels;
+    const uint32_t h0flags = h.flags;
     if (fi.ranked == 1) {  // walked in parallel: every header checked but against block 0's layout
         if (((h.flags & MONO_FLAG) ? 1u : 2u) != bch0) {
             fi.why = DF_WALK;
@@ -419,7 +447,8 @@ WVF_HD void dframe_walk(DFile &fi, const uint8_t *blob, uint64_t *slots) {
     for (;;) {
         const uint32_t bch = (h.flags & MONO_FLAG) ? 1u : 2u;
         if (h.block_samples == 0 || !(h.flags & INITIAL_BLOCK) || h.block_index != sum || bch != bch0 ||
-            (h.flags & DSD_FLAG) || ((h.flags & FALSE_STEREO) && (h.flags & MONO_FLAG))) {
+            ((h.flags ^ h0flags) & DSD_FLAG) || ((h.flags & DSD_FLAG) && (h.flags & FALSE_STEREO)) ||
+            ((h.flags & FALSE_STEREO) && (h.flags & MONO_FLAG))) {
             fi.why = DF_WALK;
             return;
         }
@@ -465,7 +494,7 @@ WVF_HD void dframe_block(const DFile &fi, uint32_t k, const uint8_t *blob, const
     r.file_format = -1;
     r.info_mask = 0;
     r.num_channels = -1;
-    r.pad_ = 0;
+    r.dsd_mult_log2 = -1;
     r.header_off = r.header_len = r.trailer_off = r.trailer_len = -1;
     DHdr h;
     if (!dframe_header(f, fi.len, hpos, h)) {
@@ -493,6 +522,7 @@ WVF_HD void dframe_block(const DFile &fi, uint32_t k, const uint8_t *blob, const
     r.file_format = s.file_format;
     r.info_mask = (s.has_i32 ? 1 : 0) | (s.has_fl ? 2 : 0);
     r.num_channels = s.num_channels;
+    r.dsd_mult_log2 = s.dsd ? s.dsd_mult_log2 : -1;
     r.header_off = s.header_off;
     r.header_len = s.header_len;
     r.trailer_off = s.trailer_off;
@@ -512,15 +542,21 @@ WVF_HD void dframe_block(const DFile &fi, uint32_t k, const uint8_t *blob, const
     d.int32_zeros = s.i32[1];
     d.int32_ones = s.i32[2];
     d.int32_dups = s.i32[3];
-    d.kind = KIND_PCM;
-    d.bits_off = fi.base + (uint64_t)s.bits_off;
-    d.bits_len = (uint32_t)s.bits_len;
-    d.num_terms = s.num_terms;
-    for (int i = 0; i < s.num_terms; i++) {
-        d.term[i] = s.term[i];
-        d.delta[i] = s.delta[i];
+    if (flags & DSD_FLAG) {  // DSD mode 0 (DsdUtils.cs:60-147): the raw bytes
+        d.kind = KIND_DSD_RAW;
+        d.bits_off = fi.base + (uint64_t)s.dsd_off;
+        d.dsd_data_len = (uint32_t)s.dsd_len;
+    } else {
+        d.kind = KIND_PCM;
+        d.bits_off = fi.base + (uint64_t)s.bits_off;
+        d.bits_len = (uint32_t)s.bits_len;
+        d.num_terms = s.num_terms;
+        for (int i = 0; i < s.num_terms; i++) {
+            d.term[i] = s.term[i];
+            d.delta[i] = s.delta[i];
+        }
+        for (int i = 0; i < s.nitems; i++) meta_apply(d, s.items[i], f);
     }
-    for (int i = 0; i < s.nitems; i++) meta_apply(d, s.items[i], f);
     // the caller's chunk schedule: block k starts at file frame block_index
     const uint64_t nch = (uint64_t)fi.nch, chunk = fi.chunk, at = (uint64_t)h.block_index;
     const uint64_t into = at % chunk;

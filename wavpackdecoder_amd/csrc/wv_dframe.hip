@@ -243,8 +243,8 @@ extern "C" __global__ void __launch_bounds__(1024) wv_dframe_rank(DFile *__restr
             DHdr h;
             dframe_header(f, len, slots[F.slot + r], h);
             const uint32_t fl = h.flags;
-            if (h.block_samples == 0 || !(fl & INITIAL_BLOCK) || (fl & DSD_FLAG) ||
-                ((fl & FALSE_STEREO) && (fl & MONO_FLAG)) || ((fl ^ h0.flags) & MONO_FLAG))
+            if (h.block_samples == 0 || !(fl & INITIAL_BLOCK) || ((fl ^ h0.flags) & (DSD_FLAG | MONO_FLAG)) ||
+                ((fl & FALSE_STEREO) && (fl & (MONO_FLAG | DSD_FLAG))))
                 bad = DF_WALK;
             bs[q] = h.block_samples;
         }

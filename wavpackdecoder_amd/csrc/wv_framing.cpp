@@ -1096,7 +1096,7 @@ bool dframe_file_info(const DFile &df, const DBlock *r, FileInfo &info) {
     // every block (INT32/FLOAT info), and the channel count must not change
     const int32_t mask0 = r[0].info_mask;
     bool lossy = false, five = false;
-    int32_t file_format = 0;
+    int32_t file_format = 0, dsd_log2 = -1;
     int64_t hoff = -1, hlen = 0, toff = -1, tlen = 0;
     for (uint32_t k = 0; k < df.nblocks; k++) {
         const DBlock &b = r[k];
@@ -1105,6 +1105,7 @@ bool dframe_file_info(const DFile &df, const DBlock *r, FileInfo &info) {
         lossy |= b.lossy != 0;
         five |= b.five != 0;
         if (b.file_format >= 0) file_format = b.file_format;
+        if (b.dsd_mult_log2 >= 0) dsd_log2 = b.dsd_mult_log2;
         if (b.header_off >= 0) hoff = b.header_off, hlen = b.header_len;
         if (b.trailer_off >= 0) toff = b.trailer_off, tlen = b.trailer_len;
     }
@@ -1132,6 +1133,7 @@ bool dframe_file_info(const DFile &df, const DBlock *r, FileInfo &info) {
     info.lossy_blocks = lossy;
     info.is_five = five;
     info.file_format = file_format;
+    info.dsd_multiplier = dsd_log2 >= 0 ? 1u << dsd_log2 : 0u;
     info.header_off = hoff;
     info.header_len = hlen;
     info.trailer_off = toff;
