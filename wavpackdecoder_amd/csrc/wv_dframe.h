@@ -19,9 +19,11 @@
 //   * headers back to back from byte 0 to the file's end, every one passing
 //     read_next_header's test where the previous block ends, block_index
 //     running from 0 without gaps, total_samples known and equal to the sum;
-//   * every block PCM (no DSD), mono or stereo as the file opened, INITIAL_BLOCK
+//   * every block PCM, or every block DSD mode 0 (raw bytes; modes 1/3 build
+//     tables on the host), mono or stereo as the file opened, INITIAL_BLOCK
 //     set, block_samples > 0, and its unpack_init succeeds with the decorr
-//     terms, entropy variables and bitstream re-sent (no sticky state, B-8),
+//     terms, entropy variables and bitstream (or ID_DSD_BLOCK) re-sent (no
+//     sticky state, B-8),
 //     every deferred read inside its sub-block (wv_meta.h's conditions), no
 //     wvx/wvc stream, INT32_INFO / FLOAT_INFO / CHANNEL_INFO the same way in
 //     every block.
