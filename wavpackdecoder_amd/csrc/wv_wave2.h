@@ -1856,27 +1856,72 @@ struct Seams {
     bool crc_stop;
 };
 
+// The lean batch's CRC in one wave sum (wv_pipe.h does the same per group):
+// crc * base^n + sum base^(n-1-j) v_j over the staged values, base 9 per stereo
+// frame (3 L + R) or 3 per mono value; w0/w1 are this lane's weights for o0/o1.
+struct CrcBatch {
+    uint32_t w0, w1, pw;
+};
+__device__ __forceinline__ uint32_t upow_u32(uint32_t b, uint32_t e) {
+    uint32_t r = 1;
+    while (e) {
+        if (e & 1) r *= b;
+        b *= b;
+        e >>= 1;
+    }
+    return r;
+}
+template <int LAYOUT>
+__device__ __forceinline__ CrcBatch crc_batch_weights(int lane) {
+    CrcBatch c;
+    const uint32_t j = (uint32_t)lane >> 1;
+    if (LAYOUT == 0) {
+        c.w0 = upow_u32(9u, 31u - j) * ((lane & 1) ? 1u : 3u);
+        c.w1 = 0;
+        c.pw = upow_u32(9u, 32u);
+    } else if (LAYOUT == 1) {
+        c.w0 = upow_u32(3u, 63u - (uint32_t)lane);
+        c.w1 = 0;
+        c.pw = upow_u32(3u, 64u);
+    } else {  // two lanes per value: the even one counts
+        c.w0 = (lane & 1) ? 0u : upow_u32(3u, 63u - j);
+        c.w1 = (lane & 1) ? 0u : upow_u32(3u, 31u - j);
+        c.pw = upow_u32(3u, 64u);
+    }
+    return c;
+}
+__device__ __forceinline__ uint32_t wave_sum64(uint32_t x) {  // DPP row shifts + row broadcasts, lane 63
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int32_t)x, 0x111, 0xF, 0xF, true);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int32_t)x, 0x112, 0xF, 0xF, true);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int32_t)x, 0x114, 0xF, 0xF, true);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int32_t)x, 0x118, 0xF, 0xF, true);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int32_t)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int32_t)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int32_t)x, 63);
+}
+
 // One residual batch (32 stereo / 64 mono frames from t0).  LEAN: full batch,
 // no chunk-seam event inside, so no per-frame seam or validity tests.  The
 // steps per frame are those of decode_pcm_block in wv_decode_core.h.
 template <int LAYOUT, bool LEAN, bool JOINT, bool IDENT, class CH>
 __device__ __forceinline__ void recon_batch(CH &ch, const Fixup &fx, const int32_t *res, uint32_t rbase, int32_t &o0,
                                             int32_t &o1, int32_t &crc, int32_t ml, uint32_t t0, uint32_t tvalid,
-                                            Seams &sm, int &mute_at, int lane) {
+                                            Seams &sm, int &mute_at, int lane, const CrcBatch &cb) {
     using namespace wvf;
     constexpr bool MONO = LAYOUT != 0;
     constexpr uint32_t BF = MONO ? 64 : 32;
     const bool isB = !MONO && (lane & 1);
     const int pair = lane >> 1;
-    // LEAN && IDENT: the mute test of 8 frames is one ballot at the group's end
-    // (the running max of |value|); a group that mutes is replayed from the staged
-    // outputs (o0/o1 hold the values themselves) for the muting frame and the crc
-    // before it -- the passes' state past it no longer matters (the block ends muted)
+    // LEAN && IDENT: the staged outputs o0/o1 hold the values themselves, so the
+    // batch's CRC is one weighted wave sum at its end (CrcBatch) and the mute test
+    // of 8 frames one ballot on the running max |value|; a group that mutes is
+    // replayed from the staged values for the muting frame and the crc before it
+    // (the passes' state past it no longer matters: the block ends muted)
     constexpr bool BATCH_MUTE = LEAN && IDENT;
+    const int32_t crc_b = crc;
     for (uint32_t g = 0; g < BF / 8; g++) {
         if (!LEAN && t0 + g * 8 >= tvalid) break;
-        const int32_t crc_g = crc;
-        int32_t vmx = 0;
+        int32_t vmx = 0;  // the group's largest |value| (iabs: INT_MIN stays negative, as the per-frame test)
         int32_t xr[8];
 #pragma unroll
         for (int u = 0; u < 8; u++)
@@ -1892,7 +1937,6 @@ __device__ __forceinline__ void recon_batch(CH &ch, const Fixup &fx, const int32
                 ch.template mono<U>(x);                                                        \
                 if (BATCH_MUTE) {                                                              \
                     vmx = max(vmx, iabs(x));                                                   \
-                    crc = add32(mul32(crc, 3), x);                                             \
                 } else if (LEAN) {                                                             \
                     if (__builtin_expect(any_lane(iabs(x) > ml), 0)) {                         \
                         mute_at = (int)t;                                                      \
@@ -1927,7 +1971,7 @@ __device__ __forceinline__ void recon_batch(CH &ch, const Fixup &fx, const int32
                     mute_at = (int)t;                                                          \
                     break;                                                                     \
                 }                                                                              \
-                crc = add32(mul32(crc, 9), add32(mul32(Lv, 3), Rv));                           \
+                if (!BATCH_MUTE) crc = add32(mul32(crc, 9), add32(mul32(Lv, 3), Rv));          \
             }                                                                                  \
             if (!LEAN && (t == sm.seam8 || t == sm.chunk_end - 1)) ch.trunc();                 \
             if (!IDENT) fl = fixup_tail(fx, fl);                                               \
@@ -1955,21 +1999,21 @@ __device__ __forceinline__ void recon_batch(CH &ch, const Fixup &fx, const int32
             WV2_VFRAME(7)
         } while (0);
 #undef WV2_VFRAME
+        // max |v| > ml <=> some |v| > ml; the replay finds the first one
         if (BATCH_MUTE && __builtin_expect(any_lane(vmx > ml), 0)) {
-            crc = crc_g;
-            for (uint32_t u = 0; u < 8; u++) {
-                const uint32_t j = g * 8 + u;
+            crc = crc_b;
+            for (uint32_t j = 0; j < g * 8 + 8; j++) {
                 bool mute;
                 if (MONO) {
                     const int32_t v = (LAYOUT == 1) ? __builtin_amdgcn_readlane(o0, (int)j)
                                                     : (j < 32 ? __builtin_amdgcn_readlane(o0, 2 * (int)j)
                                                               : __builtin_amdgcn_readlane(o1, 2 * (int)j - 64));
-                    mute = iabs(v) > ml;
+                    mute = j >= g * 8 && iabs(v) > ml;
                     if (!mute) crc = add32(mul32(crc, 3), v);
                 } else {
                     const int32_t Lv = __builtin_amdgcn_readlane(o0, 2 * (int)j);
                     const int32_t Rv = __builtin_amdgcn_readlane(o0, 2 * (int)j + 1);
-                    mute = iabs(Lv) > ml || iabs(Rv) > ml;
+                    mute = j >= g * 8 && (iabs(Lv) > ml || iabs(Rv) > ml);
                     if (!mute) crc = add32(mul32(crc, 9), add32(mul32(Lv, 3), Rv));
                 }
                 if (mute) {
@@ -1977,8 +2021,13 @@ __device__ __forceinline__ void recon_batch(CH &ch, const Fixup &fx, const int32
                     break;
                 }
             }
+            if (mute_at < 0) crc = crc_b;  // no value of the group mutes: the batch sum below
         }
         if (mute_at >= 0) break;
+    }
+    if (BATCH_MUTE && mute_at < 0) {
+        const uint32_t sum = wave_sum64((uint32_t)o0 * cb.w0 + (LAYOUT == 2 ? (uint32_t)o1 * cb.w1 : 0u));
+        crc = (int32_t)((uint32_t)crc_b * cb.pw + sum);
     }
 }
 
@@ -2026,6 +2075,7 @@ __device__ __forceinline__ void recon_impl(const BlockDesc &d, const uint8_t *bl
     Fixup fx;
     fixup_init(fx, d);
     const bool ident = fx.mode == 3 && fx.shift == 0 && !fx.lossy;  // fixup is the identity
+    const CrcBatch cb = crc_batch_weights<LAYOUT>(lane);
 
     uint32_t status = 0;
     int32_t crc = -1;  // identical in every lane
@@ -2087,15 +2137,15 @@ __device__ __forceinline__ void recon_impl(const BlockDesc &d, const uint8_t *bl
             MONO && (sm.crc_stop || (sm.bsp > 0 && sm.chunk_end - sm.bsp >= t0 && sm.chunk_end - sm.bsp <= tlast));
         if (tvalid == t0 + BF && !seam_in && !quirk_in) {
             if (joint) {
-                if (ident) recon_batch<LAYOUT, true, true, true>(ch, fx, sh.res, rbase, o0, o1, crc, ml, t0, tvalid, sm, mute_at, lane);
-                else recon_batch<LAYOUT, true, true, false>(ch, fx, sh.res, rbase, o0, o1, crc, ml, t0, tvalid, sm, mute_at, lane);
+                if (ident) recon_batch<LAYOUT, true, true, true>(ch, fx, sh.res, rbase, o0, o1, crc, ml, t0, tvalid, sm, mute_at, lane, cb);
+                else recon_batch<LAYOUT, true, true, false>(ch, fx, sh.res, rbase, o0, o1, crc, ml, t0, tvalid, sm, mute_at, lane, cb);
             } else {
-                if (ident) recon_batch<LAYOUT, true, false, true>(ch, fx, sh.res, rbase, o0, o1, crc, ml, t0, tvalid, sm, mute_at, lane);
-                else recon_batch<LAYOUT, true, false, false>(ch, fx, sh.res, rbase, o0, o1, crc, ml, t0, tvalid, sm, mute_at, lane);
+                if (ident) recon_batch<LAYOUT, true, false, true>(ch, fx, sh.res, rbase, o0, o1, crc, ml, t0, tvalid, sm, mute_at, lane, cb);
+                else recon_batch<LAYOUT, true, false, false>(ch, fx, sh.res, rbase, o0, o1, crc, ml, t0, tvalid, sm, mute_at, lane, cb);
             }
         } else {
-            if (joint) recon_batch<LAYOUT, false, true, false>(ch, fx, sh.res, rbase, o0, o1, crc, ml, t0, tvalid, sm, mute_at, lane);
-            else recon_batch<LAYOUT, false, false, false>(ch, fx, sh.res, rbase, o0, o1, crc, ml, t0, tvalid, sm, mute_at, lane);
+            if (joint) recon_batch<LAYOUT, false, true, false>(ch, fx, sh.res, rbase, o0, o1, crc, ml, t0, tvalid, sm, mute_at, lane, cb);
+            else recon_batch<LAYOUT, false, false, false>(ch, fx, sh.res, rbase, o0, o1, crc, ml, t0, tvalid, sm, mute_at, lane, cb);
         }
         // the batch's residuals have been read: release the ring space
         lds_publish(&sh.consumed, tend * WPF);
