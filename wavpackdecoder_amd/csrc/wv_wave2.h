@@ -1912,13 +1912,15 @@ __device__ __forceinline__ void recon_batch(CH &ch, const Fixup &fx, const int32
     constexpr uint32_t BF = MONO ? 64 : 32;
     const bool isB = !MONO && (lane & 1);
     const int pair = lane >> 1;
-    // LEAN && IDENT: the staged outputs o0/o1 hold the values themselves, so the
-    // batch's CRC is one weighted wave sum at its end (CrcBatch) and the mute test
-    // of 8 frames one ballot on the running max |value|; a group that mutes is
-    // replayed from the staged values for the muting frame and the crc before it
-    // (the passes' state past it no longer matters: the block ends muted)
-    constexpr bool BATCH_MUTE = LEAN && IDENT;
+    // LEAN: the values before fixup are staged like the outputs (in o0/o1 when the
+    // fixup is the identity, else in q0/q1), so the batch's CRC is one weighted
+    // wave sum at its end (CrcBatch) and the mute test of 8 frames one ballot on
+    // the running max |value|; a group that mutes is replayed from the staged
+    // values for the muting frame and the crc before it (the passes' state past it
+    // no longer matters: the block ends muted; fixup_tail reads no stream here)
+    constexpr bool BATCH_MUTE = LEAN;
     const int32_t crc_b = crc;
+    int32_t q0 = 0, q1 = 0;
     for (uint32_t g = 0; g < BF / 8; g++) {
         if (!LEAN && t0 + g * 8 >= tvalid) break;
         int32_t vmx = 0;  // the group's largest |value| (iabs: INT_MIN stays negative, as the per-frame test)
@@ -1974,14 +1976,23 @@ __device__ __forceinline__ void recon_batch(CH &ch, const Fixup &fx, const int32
                 if (!BATCH_MUTE) crc = add32(mul32(crc, 9), add32(mul32(Lv, 3), Rv));          \
             }                                                                                  \
             if (!LEAN && (t == sm.seam8 || t == sm.chunk_end - 1)) ch.trunc();                 \
+            const int32_t pre = fl;                                                            \
             if (!IDENT) fl = fixup_tail(fx, fl);                                               \
+            constexpr bool STAGE_PRE = LEAN && !IDENT;                                         \
             if (LAYOUT == 1) {                                                                 \
                 o0 = lane == (int)j ? fl : o0;                                                 \
+                if (STAGE_PRE) q0 = lane == (int)j ? pre : q0;                                 \
             } else if (LAYOUT == 2) {                                                          \
-                if (j < 32) o0 = pair == (int)j ? fl : o0;                                     \
-                else o1 = pair == (int)j - 32 ? fl : o1;                                       \
+                if (j < 32) {                                                                  \
+                    o0 = pair == (int)j ? fl : o0;                                             \
+                    if (STAGE_PRE) q0 = pair == (int)j ? pre : q0;                             \
+                } else {                                                                       \
+                    o1 = pair == (int)j - 32 ? fl : o1;                                        \
+                    if (STAGE_PRE) q1 = pair == (int)j - 32 ? pre : q1;                        \
+                }                                                                              \
             } else {                                                                           \
                 o0 = pair == (int)j ? fl : o0;                                                 \
+                if (STAGE_PRE) q0 = pair == (int)j ? pre : q0;                                 \
             }                                                                                  \
             if (!LEAN && t == sm.chunk_end - 1) {                                              \
                 sm.chunk_start = t + 1;                                                        \
@@ -2001,18 +2012,19 @@ __device__ __forceinline__ void recon_batch(CH &ch, const Fixup &fx, const int32
 #undef WV2_VFRAME
         // max |v| > ml <=> some |v| > ml; the replay finds the first one
         if (BATCH_MUTE && __builtin_expect(any_lane(vmx > ml), 0)) {
+            const int32_t s0 = IDENT ? o0 : q0, s1 = IDENT ? o1 : q1;
             crc = crc_b;
             for (uint32_t j = 0; j < g * 8 + 8; j++) {
                 bool mute;
                 if (MONO) {
-                    const int32_t v = (LAYOUT == 1) ? __builtin_amdgcn_readlane(o0, (int)j)
-                                                    : (j < 32 ? __builtin_amdgcn_readlane(o0, 2 * (int)j)
-                                                              : __builtin_amdgcn_readlane(o1, 2 * (int)j - 64));
+                    const int32_t v = (LAYOUT == 1) ? __builtin_amdgcn_readlane(s0, (int)j)
+                                                    : (j < 32 ? __builtin_amdgcn_readlane(s0, 2 * (int)j)
+                                                              : __builtin_amdgcn_readlane(s1, 2 * (int)j - 64));
                     mute = j >= g * 8 && iabs(v) > ml;
                     if (!mute) crc = add32(mul32(crc, 3), v);
                 } else {
-                    const int32_t Lv = __builtin_amdgcn_readlane(o0, 2 * (int)j);
-                    const int32_t Rv = __builtin_amdgcn_readlane(o0, 2 * (int)j + 1);
+                    const int32_t Lv = __builtin_amdgcn_readlane(s0, 2 * (int)j);
+                    const int32_t Rv = __builtin_amdgcn_readlane(s0, 2 * (int)j + 1);
                     mute = j >= g * 8 && (iabs(Lv) > ml || iabs(Rv) > ml);
                     if (!mute) crc = add32(mul32(crc, 9), add32(mul32(Lv, 3), Rv));
                 }
@@ -2026,7 +2038,8 @@ __device__ __forceinline__ void recon_batch(CH &ch, const Fixup &fx, const int32
         if (mute_at >= 0) break;
     }
     if (BATCH_MUTE && mute_at < 0) {
-        const uint32_t sum = wave_sum64((uint32_t)o0 * cb.w0 + (LAYOUT == 2 ? (uint32_t)o1 * cb.w1 : 0u));
+        const int32_t s0 = IDENT ? o0 : q0, s1 = IDENT ? o1 : q1;
+        const uint32_t sum = wave_sum64((uint32_t)s0 * cb.w0 + (LAYOUT == 2 ? (uint32_t)s1 * cb.w1 : 0u));
         crc = (int32_t)((uint32_t)crc_b * cb.pw + sum);
     }
 }
