@@ -67,7 +67,7 @@ constexpr int kTile = 8192;
 constexpr int kTileCap = kTile / 6 + 2;  // two accepted headers are >= 6 B apart ('w' != 'p', b[4] even)
 constexpr int kRankMax = 8192;           // candidates one workgroup ranks in LDS
 
-WVF_HD inline bool hdr_ok(const uint8_t *b) {
+__device__ __forceinline__ bool hdr_ok(const uint8_t *b) {
     return b[0] == 'w' && b[1] == 'v' && b[2] == 'p' && b[3] == 'k' && (b[4] & 1) == 0 && b[6] < 16 && b[7] == 0 &&
            b[9] == 4 && b[8] >= (wvf::MIN_STREAM_VERS & 0xff) && b[8] <= (wvf::MAX_STREAM_VERS & 0xff);
 }
