@@ -26,8 +26,8 @@ hipError_t launch_format(const FormatSeg *segs, uint32_t nseg, const int32_t *in
 hipError_t launch_dsd_fill(const BlockDesc *descs, const uint32_t *dsd_list, uint32_t n_dsd, const uint32_t *status,
                            const uint32_t *aux, int32_t *out, hipStream_t s);
 hipError_t launch_dframe_rank(DFile *files, const uint32_t *tile_file, uint32_t ntiles, const uint32_t *rank_files,
-                              uint32_t nrank, const uint8_t *blob, uint32_t *cand, uint32_t *cnt, uint64_t *slots,
-                              hipStream_t s);
+                              uint32_t nrank, const uint8_t *blob, uint32_t *cand, uint32_t cand_cap, uint32_t *cnt,
+                              uint64_t *slots, hipStream_t s);
 size_t dframe_tile_cap();
 size_t dframe_tile_bytes();
 hipError_t launch_dframe_walk(DFile *files, uint32_t n, const uint8_t *blob, uint64_t *slots, hipStream_t s);
@@ -614,12 +614,13 @@ static int device_frame(wvg_batch *b, hipStream_t s) {
         memcpy(h + nt, rankf.data(), sizeof(uint32_t) * nr);
         HIPCHK(c, ensure(b->d_tfile, b->cap_tfile, sizeof(uint32_t) * nt));
         HIPCHK(c, ensure(b->d_rankf, b->cap_rankf, sizeof(uint32_t) * nr));
-        HIPCHK(c, ensure(b->d_cand, b->cap_cand, sizeof(uint32_t) * nt * dframe_tile_cap()));
-        HIPCHK(c, ensure(b->d_cnt, b->cap_cnt, sizeof(uint32_t) * nt));
+        const size_t ncand = nt * dframe_tile_cap() + 1024;
+        HIPCHK(c, ensure(b->d_cand, b->cap_cand, sizeof(uint32_t) * ncand));
+        HIPCHK(c, ensure(b->d_cnt, b->cap_cnt, sizeof(uint32_t) * (2 * nt + 1)));
         HIPCHK(c, hipMemcpyAsync(b->d_tfile, h, sizeof(uint32_t) * nt, hipMemcpyHostToDevice, s));
         HIPCHK(c, hipMemcpyAsync(b->d_rankf, h + nt, sizeof(uint32_t) * nr, hipMemcpyHostToDevice, s));
         HIPCHK(c, launch_dframe_rank(b->d_dfiles, b->d_tfile, (uint32_t)nt, b->d_rankf, (uint32_t)nr, b->d_blob,
-                                     b->d_cand, b->d_cnt, b->d_slots, s));
+                                     b->d_cand, (uint32_t)ncand, b->d_cnt, b->d_slots, s));
     }
     HIPCHK(c, launch_dframe_walk(b->d_dfiles, (uint32_t)nf, b->d_blob, b->d_slots, s));
     HIPCHK(c, hipMemcpyAsync(b->dfst.data(), b->d_dfiles, sizeof(DFile) * nf, hipMemcpyDeviceToHost, s));

@@ -63,22 +63,30 @@ extern "C" __global__ void __launch_bounds__(64) wv_dframe_block(const DFile *__
 // A candidate inside a payload that happens to pass the test either heads a chain
 // that dies (ignored) or merges with the true chain and collides with a true
 // block's rank: the file then falls back to the serial walk (ranked = 0).
+// Candidates are stored compactly (each tile takes its range with one atomic
+// add); the store is sized for one header per 32 bytes (a block is a 32-byte
+// header plus its sub-blocks) and a file whose tiles overflow it is walked
+// serially instead.
 constexpr int kTile = 8192;
-constexpr int kTileCap = kTile / 6 + 2;  // two accepted headers are >= 6 B apart ('w' != 'p', b[4] even)
 constexpr int kRankMax = 8192;           // candidates one workgroup ranks in LDS
+constexpr uint32_t kNoRange = 0xFFFFFFFFu;
 
 __device__ __forceinline__ bool hdr_ok(const uint8_t *b) {
     return b[0] == 'w' && b[1] == 'v' && b[2] == 'p' && b[3] == 'k' && (b[4] & 1) == 0 && b[6] < 16 && b[7] == 0 &&
            b[9] == 4 && b[8] >= (wvf::MIN_STREAM_VERS & 0xff) && b[8] <= (wvf::MAX_STREAM_VERS & 0xff);
 }
 
+// cnt[t]: tile t's candidates, cnt[ntiles + t]: their first index in `cand`
+// (kNoRange: the store overflowed), cnt[2 ntiles]: the store's fill (zeroed first)
 extern "C" __global__ void __launch_bounds__(256) wv_dframe_scan(const DFile *__restrict__ files,
                                                                  const uint32_t *__restrict__ tile_file,
+                                                                 uint32_t ntiles,
                                                                  const uint8_t *__restrict__ blob,
-                                                                 uint32_t *__restrict__ cand,
+                                                                 uint32_t *__restrict__ cand, uint32_t cand_cap,
                                                                  uint32_t *__restrict__ cnt) {
     __shared__ uint32_t buf[(kTile + 64) / 4];
     __shared__ uint32_t part[256];
+    __shared__ uint32_t range0;
     const uint32_t t = blockIdx.x, tid = threadIdx.x;
     const DFile &F = files[tile_file[t]];
     const uint64_t start = (uint64_t)(t - F.tile0) * kTile;
@@ -103,13 +111,22 @@ extern "C" __global__ void __launch_bounds__(256) wv_dframe_scan(const DFile *__
         part[tid] += v;
         __syncthreads();
     }
-    const uint32_t at = part[tid] - mine;
-    for (uint32_t j = 0; j < mine; j++) cand[(uint64_t)t * kTileCap + at + j] = found[j];
-    if (tid == 255) cnt[t] = part[255];
+    const uint32_t at = part[tid] - mine, total = part[255];
+    if (tid == 255) {
+        uint32_t r = total ? atomicAdd(&cnt[2 * ntiles], total) : 0u;
+        if (total && r + total > cand_cap) r = kNoRange;
+        range0 = r;
+        cnt[t] = total;
+        cnt[ntiles + t] = r;
+    }
+    __syncthreads();
+    if (range0 != kNoRange)
+        for (uint32_t j = 0; j < mine; j++) cand[range0 + at + j] = found[j];
 }
 
 extern "C" __global__ void __launch_bounds__(1024) wv_dframe_rank(DFile *__restrict__ files,
                                                                   const uint32_t *__restrict__ rank_files,
+                                                                  uint32_t ntiles,
                                                                   const uint8_t *__restrict__ blob,
                                                                   const uint32_t *__restrict__ cand,
                                                                   const uint32_t *__restrict__ cnt,
@@ -134,6 +151,13 @@ extern "C" __global__ void __launch_bounds__(1024) wv_dframe_rank(DFile *__restr
         ntot = 0;
     }
     __syncthreads();
+    for (uint32_t t = tid; t < F.ntiles; t += 1024)
+        if (cnt[ntiles + F.tile0 + t] == kNoRange) verdict = 0;  // a tile overflowed the candidate store
+    __syncthreads();
+    if (verdict == 0) {
+        if (tid == 0) F.ranked = 0;  // the serial walk
+        return;
+    }
     // gather the tiles' candidates in order (1,024 tiles per round)
     for (uint32_t t0 = 0; t0 < F.ntiles; t0 += 1024) {
         const uint32_t t = t0 + tid;
@@ -148,7 +172,7 @@ extern "C" __global__ void __launch_bounds__(1024) wv_dframe_rank(DFile *__restr
         }
         const uint32_t base = ntot + tsum[tid] - c, tot = ntot + tsum[1023];
         if (tot <= kRankMax)
-            for (uint32_t j = 0; j < c; j++) pos[base + j] = cand[(uint64_t)(F.tile0 + t) * kTileCap + j];
+            for (uint32_t j = 0; j < c; j++) pos[base + j] = cand[cnt[ntiles + F.tile0 + t] + j];
         __syncthreads();
         if (tid == 0) ntot = tot;
         __syncthreads();
@@ -293,16 +317,21 @@ extern "C" __global__ void __launch_bounds__(1024) wv_dframe_rank(DFile *__restr
     }
 }
 
+// cnt: 2 ntiles + 1 words; cand: cand_cap words
 hipError_t launch_dframe_rank(DFile *files, const uint32_t *tile_file, uint32_t ntiles, const uint32_t *rank_files,
-                              uint32_t nrank, const uint8_t *blob, uint32_t *cand, uint32_t *cnt, uint64_t *slots,
-                              hipStream_t s) {
+                              uint32_t nrank, const uint8_t *blob, uint32_t *cand, uint32_t cand_cap, uint32_t *cnt,
+                              uint64_t *slots, hipStream_t s) {
     if (!nrank) return hipSuccess;
-    hipLaunchKernelGGL(wv_dframe_scan, dim3(ntiles), dim3(256), 0, s, files, tile_file, blob, cand, cnt);
-    hipLaunchKernelGGL(wv_dframe_rank, dim3(nrank), dim3(1024), 0, s, files, rank_files, blob, cand, cnt, slots);
+    hipError_t e = hipMemsetAsync(cnt + 2 * (size_t)ntiles, 0, sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(wv_dframe_scan, dim3(ntiles), dim3(256), 0, s, files, tile_file, ntiles, blob, cand, cand_cap,
+                       cnt);
+    hipLaunchKernelGGL(wv_dframe_rank, dim3(nrank), dim3(1024), 0, s, files, rank_files, ntiles, blob, cand, cnt,
+                       slots);
     return hipGetLastError();
 }
 
-size_t dframe_tile_cap() { return kTileCap; }
+size_t dframe_tile_cap() { return kTile / 32; }  // candidate store per tile
 size_t dframe_tile_bytes() { return kTile; }
 
 hipError_t launch_dframe_walk(DFile *files, uint32_t n, const uint8_t *blob, uint64_t *slots, hipStream_t s) {
