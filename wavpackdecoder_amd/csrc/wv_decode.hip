@@ -296,121 +296,6 @@ __device__ __forceinline__ DsdResult dsd_high_wave(const BlockDesc &d, const uin
     return res;
 }
 
-// Stereo mode 3 with the two channels' filter chains on the VALU: lane 0
-// holds channel 0's filter state (filter1..6, factor, value, the output byte)
-// and lane 1 channel 1's, so one instruction updates both channels (the chains
-// are independent; only the range coder is shared).  The range coder and the
-// adaptive ptable stay scalar.  Per bit: both channels' ptable entries are
-// read from LDS at once (channel 1's is forwarded from channel 0's update when
-// they share an entry), the two binary decisions run back to back on the
-// scalar unit, then one VALU pass updates both filters (DsdUtils.cs:401-489).
-// Both entries come from one per-lane LDS read addressed by the filter lanes.
-// Same results and status bits as dsd_high_wave<2>.
-__device__ __forceinline__ DsdResult dsd_high_vwave(const BlockDesc &d, const uint8_t *blob, const uint8_t *tables,
-                                                    int32_t *ptable, DevStoreWave &out) {
-    using namespace wvf;
-    const uint32_t dlen = d.dsd_data_len;
-    const int ch = threadIdx.x & 1;
-    ByteSrcWave src;
-    src.init(blob + d.bits_off);
-    uint32_t bp = 0;
-    int32_t crc = -1;
-    DsdResult res = {0, 0};
-    bool mute = false;
-    uint32_t low = 0, high = 0xFFFFFFFFu, value = 0;
-    for (int i = 0; i < 4; i++) value = (value << 8) | src.byte(bp++);
-    {
-        const int32_t *pt0 = (const int32_t *)(tables + d.dsd_table_off);
-        for (uint32_t i = threadIdx.x; i < 256; i += 64) ptable[i] = pt0[i];
-        __syncthreads();
-    }
-    // per-lane (VGPR) filter state: lane & 1 = channel
-    int32_t q2 = d.dsd_filters[ch][0], q3 = d.dsd_filters[ch][1], q4 = d.dsd_filters[ch][2];
-    int32_t q5 = d.dsd_filters[ch][3], q6 = d.dsd_filters[ch][4], q8 = d.dsd_filters[ch][5];
-    int32_t q7 = 0, bytei = 0, q0;
-    uint32_t f = 0, chunk_len = d.first_chunk, ci = 0;
-    while (f < d.nframes) {
-        uint32_t n = chunk_len;
-        if (n > d.nframes - f) n = d.nframes - f;
-        if (!mute) {
-            for (uint32_t j = 0; j < n; j++) {
-                q0 = add32(sub32(q2, q6), mul32(q7, q8) >> 2);
-                for (int bit = 0; bit < 8; bit++) {
-                    // each lane reads its channel's ptable entry (one LDS read for both)
-                    const uint32_t ppv = ((uint32_t)q0 >> 8) & 255u;
-                    const int32_t pvv = ptable[ppv];
-                    const uint32_t pp0 = (uint32_t)__builtin_amdgcn_readlane((int32_t)ppv, 0);
-                    const uint32_t pp1 = (uint32_t)__builtin_amdgcn_readlane((int32_t)ppv, 1);
-                    const int32_t p0 = __builtin_amdgcn_readlane(pvv, 0);
-                    int32_t pv1 = __builtin_amdgcn_readlane(pvv, 1);
-                    // channel 0's decision
-                    uint32_t split = low + ((high - low) >> 8) * ((uint32_t)p0 >> 16);
-                    const bool z0 = value <= split;
-                    high = z0 ? split : high;
-                    low = z0 ? low : split + 1;
-                    const int32_t np0 = p0 + (((z0 ? 0x010000FE : 0x00010000) - p0) >> 8);
-                    ptable[pp0] = np0;
-                    pv1 = pp1 == pp0 ? np0 : pv1;
-                    if (__builtin_expect((high ^ low) < 0x1000000u, 0)) {  // renormalise (rare)
-                        while ((high ^ low) < 0x1000000u && bp < dlen) {
-                            value = (value << 8) | src.byte(bp++);
-                            high = (high << 8) | 0xFF;
-                            low <<= 8;
-                        }
-                    }
-                    // channel 1's decision
-                    split = low + ((high - low) >> 8) * ((uint32_t)pv1 >> 16);
-                    const bool z1 = value <= split;
-                    high = z1 ? split : high;
-                    low = z1 ? low : split + 1;
-                    ptable[pp1] = pv1 + (((z1 ? 0x010000FE : 0x00010000) - pv1) >> 8);
-                    if (__builtin_expect((high ^ low) < 0x1000000u, 0)) {  // renormalise (rare)
-                        while ((high ^ low) < 0x1000000u && bp < dlen) {
-                            value = (value << 8) | src.byte(bp++);
-                            high = (high << 8) | 0xFF;
-                            low <<= 8;
-                        }
-                    }
-                    // both channels' filters, one lane each
-                    const int32_t q1 = (ch ? z1 : z0) ? -1 : 0;
-                    q0 = add32(q0, mul32(q7, 8));
-                    bytei = shl32(bytei, 1) | (q1 & 1);
-                    q8 = add32(q8, (((q0 ^ q1) >> 31) | 1) & ((q0 ^ sub32(q0, mul32(q7, 16))) >> 31));
-                    q2 = add32(q2, sub32(q1 & (1 << 20), q2) >> 6);
-                    q3 = add32(q3, sub32(q1 & (1 << 20), q3) >> 4);
-                    q4 = add32(q4, sub32(q3, q4) >> 4);
-                    q5 = add32(q5, sub32(q4, q5) >> 4);
-                    q0 = sub32(q5, q6) >> 4;
-                    q6 = add32(q6, q0);
-                    q7 = add32(q7, sub32(q0, q7) >> 3);
-                    q0 = add32(sub32(q2, q6), mul32(q7, q8) >> 2);
-                }
-                const int32_t v0 = __builtin_amdgcn_readlane(bytei, 0) & 0xFF;
-                const int32_t v1 = __builtin_amdgcn_readlane(bytei, 1) & 0xFF;
-                q8 = sub32(q8, add32(q8, 512) >> 10);
-                crc = add32(crc, add32(shl32(crc, 1), v0));
-                crc = add32(crc, add32(shl32(crc, 1), v1));
-                const uint64_t o = (uint64_t)(f + j) * 2u;
-                out.put(o, v0);
-                out.put(o + 1, v1);
-            }
-            if (f + n == d.block_samples && crc != d.crc) mute = true;
-        }
-        if (mute && !(res.status & ST_DSD_MUTE)) {
-            res.status |= ST_DSD_MUTE;
-            res.mute_chunk = ci;
-        }
-        f += n;
-        chunk_len = next_call_len(d, f);
-        ci++;
-    }
-    if (d.nframes == d.block_samples) {
-        res.status |= ST_CRC_CHECKED;
-        if (crc != d.crc) res.status |= ST_CRC_ERROR;
-    }
-    return res;
-}
-
 // One range-coder decision of decode_high (DsdUtils.cs:409-422) on the scalar
 // unit: split, compare, narrow; the outcome comes back as `lanes` (this
 // channel's lane mask) or 0, and as the next bit of the output byte.  In asm
@@ -418,14 +303,6 @@ __device__ __forceinline__ DsdResult dsd_high_vwave(const BlockDesc &d, const ui
 // from a saved mask after the split + 1 add).
 __device__ __forceinline__ uint64_t dsd_decide(uint32_t value, uint32_t s, uint32_t &high, uint32_t &low, uint32_t &b,
                                                uint64_t lanes) {
-#ifdef WV_DSD_CDEC
-    const uint32_t split = low + ((high - low) >> 8) * s;
-    const bool z = value <= split;
-    high = z ? split : high;
-    low = z ? low : split + 1;
-    b = (b << 1) | (uint32_t)z;
-    return z ? lanes : 0ull;
-#else
     uint64_t zm;
     uint32_t t, t1;
     asm("s_sub_u32 %[t], %[hi], %[lo]\n\t"
@@ -442,10 +319,11 @@ __device__ __forceinline__ uint64_t dsd_decide(uint32_t value, uint32_t s, uint3
         : [v] "s"(value), [s] "s"(s), [ln] "s"(lanes)
         : "scc");
     return zm;
-#endif
 }
 
-// Stereo mode 3, issue-count version of dsd_high_vwave.  A lone wave issues
+// Stereo mode 3: lane 0 holds channel 0's filter state and lane 1 channel
+// 1's, so one VALU instruction updates both channels (the chains are
+// independent; only the range coder and the ptable are shared).  A lone wave issues
 // about one instruction per four cycles, so a decision costs what it issues
 // plus whatever latency is left exposed.  Per bit:
 //  * the LDS read of both channels' ptable entries is issued first, and the
@@ -591,39 +469,17 @@ struct DsdTablesWave {
 // DsdUtils modes 0 (raw bytes) and 1 (init_dsd_block_fast + decode_fast,
 // DsdUtils.cs:149-304), wave-uniform, channel count a template parameter.
 // Same results and status bits as decode_dsd_block (wv_decode_core.h).
-// the same tables staged in LDS by the mode-1 kernel (wv_decode_dsd_fast):
-// a data-dependent read then costs an LDS round trip instead of a scalar-cache
-// miss (up to 32 bins x 2,052 B exceed the scalar cache)
-struct DsdTablesLds {
-    const uint8_t *t;  // LDS
-    int bins;
-    __device__ __forceinline__ uint32_t prob(uint32_t i) const { return __builtin_amdgcn_readfirstlane(t[i]); }
-    __device__ __forceinline__ uint32_t summed(uint32_t i) const {
-        return __builtin_amdgcn_readfirstlane(((const uint16_t *)(t + (uint32_t)bins * 256u))[i]);
-    }
-    __device__ __forceinline__ uint32_t lookup(uint32_t i) const {
-        return __builtin_amdgcn_readfirstlane(t[(uint32_t)bins * 768u + i]);
-    }
-    __device__ __forceinline__ int32_t vlook(uint32_t i) const {
-        return __builtin_amdgcn_readfirstlane(((const int32_t *)(t + (uint32_t)bins * 2048u))[i]);
-    }
-};
-
-template <int WCH, bool FAST, class TT = DsdTablesWave>
+template <int WCH, bool FAST>
 __device__ __forceinline__ DsdResult dsd_simple_wave(const BlockDesc &d, const uint8_t *blob, const uint8_t *tables,
-                                                     DevStoreWave &out, const uint8_t *lds_tables = nullptr) {
+                                                     DevStoreWave &out) {
     using namespace wvf;
     const bool fstereo = (d.flags & FALSE_STEREO) != 0;
     const uint32_t och = (d.flags & MONO_FLAG) ? 1u : 2u;
     const uint32_t dlen = d.dsd_data_len;
     ByteSrcWave src;
     src.init(blob + d.bits_off);
-    TT tb;
-    if constexpr (__is_same(TT, DsdTablesLds)) {
-        tb.t = lds_tables;
-    } else {
-        tb.t = (w2::cdw_ptr)(tables + d.dsd_table_off);
-    }
+    DsdTablesWave tb;
+    tb.t = (w2::cdw_ptr)(tables + d.dsd_table_off);
     tb.bins = d.dsd_history_bins;
     const uint32_t bmask = (uint32_t)d.dsd_history_bins - 1u;
     uint32_t bp = 0;
@@ -731,20 +587,12 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_wave(const BlockD
     const bool lead = threadIdx.x == 0;
     DevStoreWave st{out + d.out_off, (uint64_t)d.pre_end * d.out_nch, lead};
     DsdResult r;
-#ifndef WV_NO_DSD_PRIO
     // a mode-3 block is the batch's longest serial chain: its wave wins the
     // issue arbitration against the PCM waves sharing its SIMD
     if (d.kind == KIND_DSD_HIGH) __builtin_amdgcn_s_setprio(3);
-#endif
     if (d.kind == KIND_DSD_HIGH)
         r = (d.flags & wvf::MONO_DATA) ? dsd_high_wave<1>(d, blob, tables, pt_lds, st)
-#if defined(WV_DSD_HIGH_SCALAR)
-                                       : dsd_high_wave<2>(d, blob, tables, pt_lds, st);
-#elif defined(WV_DSD_HIGH_V1)
-                                       : dsd_high_vwave(d, blob, tables, pt_lds, st);
-#else
                                        : dsd_high_v2(d, blob, tables, pt_lds, st);
-#endif
     else if (d.kind == KIND_DSD_FAST)
         r = (d.flags & wvf::MONO_DATA) ? dsd_simple_wave<1, true>(d, blob, tables, st)
                                        : dsd_simple_wave<2, true>(d, blob, tables, st);
@@ -893,10 +741,9 @@ __device__ __forceinline__ DsdResult dsd_fast_v2(const BlockDesc &d, const uint8
 
 // Mode 1: one wave per block, its tables staged in LDS first.  Launched over
 // the mode-1 part of the DSD list (the list is sorted by kind);
-// wv_decode_dsd_wave skips those blocks.  Default: dsd_fast_v2 (rows of u32
-// cumulative counts, 32 KiB at 32 bins); WV_DSD_FAST_V1: the division path over
-// the raw tables (65,664 B).
-constexpr uint32_t kDsdFastLds = 32u * 2052u;
+// wv_decode_dsd_wave skips those blocks.  dsd_fast_v2 reads rows of u32
+// cumulative counts (32 KiB at the framing's maximum of 32 bins).
+constexpr uint32_t kDsdFastLds = 32u * 256u * 4u;
 extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_fast(const BlockDesc *__restrict__ descs,
                                                                     const uint32_t *__restrict__ list,
                                                                     const uint8_t *__restrict__ blob,
@@ -911,18 +758,6 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_fast(const BlockD
     const uint32_t bins = (uint32_t)d.dsd_history_bins;
     DevStoreWave st{out + d.out_off, (uint64_t)d.pre_end * d.out_nch, lead};
     DsdResult r;
-#ifdef WV_DSD_FAST_V1
-    const uint32_t nw = bins <= 32u ? (bins * 2052u + 3u) / 4u : 0u;
-    const uint32_t *src = (const uint32_t *)(tables + d.dsd_table_off);  // 16-B aligned by the framing
-    for (uint32_t i = threadIdx.x; i < nw; i += 64) tab[i] = src[i];
-    __syncthreads();
-    if (bins > 32u)  // not produced by the framing (init_dsd_block_fast rejects > 5 history bits)
-        r = decode_dsd_block(d, blob, tables, nullptr, st);
-    else
-        r = (d.flags & wvf::MONO_DATA)
-                ? dsd_simple_wave<1, true, DsdTablesLds>(d, blob, tables, st, (const uint8_t *)tab)
-                : dsd_simple_wave<2, true, DsdTablesLds>(d, blob, tables, st, (const uint8_t *)tab);
-#else
     // summed_probabilities (u16, after the bins x 256 probability bytes) widened to u32 rows
     const uint16_t *sum16 = (const uint16_t *)(tables + d.dsd_table_off + (size_t)bins * 256u);
     const uint32_t ne = bins <= 32u ? bins * 256u : 0u;
@@ -944,7 +779,6 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_fast(const BlockD
     else
         r = (d.flags & wvf::MONO_DATA) ? dsd_fast_v2<1>(d, blob, tab, vmag, vsh1, vsh2, st)
                                        : dsd_fast_v2<2>(d, blob, tab, vmag, vsh1, vsh2, st);
-#endif
     if (lead) {
         status[bi] = d.fstatus | r.status;
         mute_chunk[bi] = r.mute_chunk;

@@ -31,9 +31,7 @@ constexpr int RES_RING = 2048;  // residual words in flight (8 KiB: 2 waves x 8 
 constexpr uint32_t SPIN_LIMIT = 1u << 26;  // bounded waits: a bug ends the kernel, never hangs the GPU
 // the reconstruction wave's poll interval (s_sleep units of 64 cycles): its
 // polls issue scalar instructions on the SIMD the parser waves are bound on
-#ifndef WV2_RECON_SLEEP
-#define WV2_RECON_SLEEP 64
-#endif
+constexpr int WV2_RECON_SLEEP = 64;
 // the reconstruction wave's wait bound in polls: about the same wall time
 // (~4 s) as SPIN_LIMIT polls of s_sleep 2
 constexpr uint32_t RECON_SPIN_LIMIT = SPIN_LIMIT / (WV2_RECON_SLEEP > 2 ? WV2_RECON_SLEEP / 2 : 1);
@@ -1227,13 +1225,8 @@ __device__ __forceinline__ bool hybrid_run_narrow(Entropy &w, SmemReader &rd, ui
 // the median updates on the VALU, the result read back into the median's SGPR
 // (stereo: a channel's medians are next read two words later, by which time
 // the v_readfirstlane has long completed)
-#ifdef WV2_SALU_MEDIANS
-#define WV2_FDEC NW_DEC
-#define WV2_FINC NW_INC
-#else
 #define WV2_FDEC FV_DEC
 #define WV2_FINC FV_INC
-#endif
 #define FV_DEC(M, ADD, SH1)                                         \
     "v_mov_b32 %[vm], " M "\n"                                      \
     "v_add_u32 %[vm], " ADD ", %[vm]\n"                             \
@@ -1555,22 +1548,17 @@ __device__ __forceinline__ void parse_loop(const BlockDesc &d, Reader &rd, Entro
             }
             if (LOSSLESS && (MONO || (k & 1) == 0)) {
                 if (narrow_ok<MONO>(w, rd)) {
-#ifndef WV2_NO_FULL_BATCH
                     if ((k & 63u) == 0 && kend - k == 64u) {
                         // false: the word at k (the run stopped there) takes the general path
                         if (lossless_run_full<MONO>(w, rd, k, resv)) break;
-                    } else
-#endif
-                    if (lossless_run_narrow<MONO>(w, rd, k, kend, resv)) break;
+                    } else if (lossless_run_narrow<MONO>(w, rd, k, kend, resv)) break;
                 } else if (lossless_run<MONO>(w, rd, k, kend, resv)) {
                     break;
                 }
             }
-#ifndef WV2_NO_HYBRID_NARROW
             if (!LOSSLESS && (MONO || (k & 1) == 0) && hybrid_ok<MONO>(w, rd, flags)) {
                 if (hybrid_run_narrow<MONO>(w, rd, k, kend, resv, tb)) break;
             }
-#endif
 
             // the word at k (and, in stereo, its pair) through the general path
             int32_t v = 0;
