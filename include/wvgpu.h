@@ -123,6 +123,15 @@ int wvg_batch_add_files(wvg_batch *b, int n, const uint8_t *const *files, const 
 int wvg_batch_add_file_at(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open_flags, int64_t start_sample,
                           wvg_file_info *info);
 
+/* open_flags bit beyond the reference (whose only flag is OPEN_2CH_MAX = 0x8,
+ * Defines.cs:26): FLOAT_DATA blocks decode to IEEE-754 float32 bit patterns by
+ * WavPack 4's float_values -- exact when the block carries its classic
+ * ID_WVX_BITSTREAM (in the .wv, or in the .wvc for a hybrid file) -- instead of
+ * FloatUtils.cs:32-56's scaling to 24-bit integers.  Blocks with a wvx stream
+ * check its crc (WVG_ST_CRC_ERROR); a NEW-format float wvx stream is
+ * WVG_ST_UNSUPPORTED.  Parity: round trip to the encoder's float input. */
+#define WVG_OPEN_EXACT_FLOAT 0x40000000u
+
 /* A hybrid .wv file with its .wvc correction file: the hybrid blocks decode
  * EXACTLY (lossless) instead of the reference's lossy output.  Beyond the
  * reference (it opens ID_WVC_BITSTREAM, UnpackUtils.cs:96-106, but never reads

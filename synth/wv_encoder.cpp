@@ -70,6 +70,9 @@ struct wvenc_params {
     int32_t sticky_passes;     // blocks after the first omit DECORR_TERMS/WEIGHTS/SAMPLES: the decoder
                                // continues the passes of the block before (sticky state, B-8)
     int32_t wvc;               // hybrid only: also write a .wvc correction file (wvenc_encode_pcm_wvc)
+    int32_t float_exact;       // float_data: the input ints are float32 bit patterns, split per block into
+                               // the integers and a classic wvx stream (float_split); with wvc the wvx
+                               // stream goes into the .wvc block
 };
 
 struct wvenc_dsd_params {
@@ -713,6 +716,104 @@ int32_t replay_wvx(const Int32Map &im, bool fresh_new, const std::vector<uint8_t
     return crc;
 }
 
+// float32 bit patterns -> the integers a FLOAT_DATA block carries and its wvx
+// stream: the inverse of WavPack 4's float_values (fixup_xfloat in the decoder
+// core; the reference's FloatUtils.cs:32-56 reads neither).  The integer is the
+// mantissa (implicit bit included) shifted right by max_exp - exponent; the
+// shifted-out bits go to the wvx stream as FLOAT_SHIFT_ONES (none sent),
+// FLOAT_SHIFT_SAME (one bit) or FLOAT_SHIFT_SENT (the bits); floats the shift
+// takes to 0 are sent whole (FLOAT_ZEROS_SENT), -0.0 as a sign (FLOAT_NEG_ZEROS),
+// inf/nan as integer +-2^24 and their mantissa (FLOAT_EXCEPTIONS).  `vals` are the
+// block's values in the decoder's order.
+struct FloatSplit {
+    std::vector<int32_t> ints;
+    BitWriter xw;
+    int flags = 0, max_exp = 0;
+    int32_t crc_x = -1;
+    bool need_wvx = false;
+};
+static void float_split(const std::vector<uint32_t> &vals, FloatSplit &fs) {
+    int me = 0;
+    for (uint32_t b : vals) {
+        const int e = (int)((b >> 23) & 0xff);
+        if (e != 255 && e > me) me = e;
+    }
+    fs.max_exp = me;
+    auto shift_of = [&](int e) { return e ? me - e : (me ? me - 1 : 0); };
+    bool any_lost = false, all_ones = true, all_same = true, zeros = false, negz = false, exc = false;
+    for (uint32_t b : vals) {
+        const int e = (int)((b >> 23) & 0xff);
+        const uint32_t m = b & 0x7fffffu;
+        if (e == 255) {
+            exc = true;
+            continue;
+        }
+        if (e == 0 && m == 0) {
+            negz |= (b >> 31) != 0;
+            continue;
+        }
+        const uint32_t M = e ? (m | 0x800000u) : m;
+        const int sc = shift_of(e);
+        const uint32_t v = sc >= 24 ? 0u : M >> sc;
+        if (!v) {
+            zeros = true;
+            continue;
+        }
+        if (sc) {
+            const uint32_t full = (1u << sc) - 1u, lost = M & full;
+            any_lost |= lost != 0;
+            all_ones &= lost == full;
+            all_same &= lost == 0 || lost == full;
+        }
+    }
+    int fl = 0;
+    if (any_lost) fl |= all_ones ? FLOAT_SHIFT_ONES : all_same ? FLOAT_SHIFT_SAME : FLOAT_SHIFT_SENT;
+    if (zeros) fl |= FLOAT_ZEROS_SENT;
+    if (negz) fl |= FLOAT_NEG_ZEROS;
+    if (exc) fl |= FLOAT_EXCEPTIONS;
+    fs.flags = fl;
+    fs.need_wvx = (fl & (FLOAT_SHIFT_SAME | FLOAT_SHIFT_SENT | FLOAT_ZEROS_SENT | FLOAT_NEG_ZEROS | FLOAT_EXCEPTIONS)) != 0;
+    fs.ints.clear();
+    int32_t crc = -1;
+    for (uint32_t b : vals) {
+        const uint32_t sign = b >> 31;
+        const int e = (int)((b >> 23) & 0xff);
+        const uint32_t m = b & 0x7fffffu;
+        int32_t x;
+        if (e == 255) {
+            x = sign ? -0x1000000 : 0x1000000;
+            fs.xw.bit(m != 0);
+            if (m) fs.xw.put(m, 23);
+        } else if (e == 0 && m == 0) {
+            x = 0;
+            if (fl & FLOAT_ZEROS_SENT) fs.xw.bit(0);
+            if (fl & FLOAT_NEG_ZEROS) fs.xw.bit((int)sign);
+        } else {
+            const uint32_t M = e ? (m | 0x800000u) : m;
+            const int sc = shift_of(e);
+            const uint32_t v = sc >= 24 ? 0u : M >> sc;
+            if (!v) {
+                if (me < 25 && e != 0) throw std::runtime_error("float_split: exponent not representable");
+                x = 0;
+                fs.xw.bit(1);
+                fs.xw.put(m, 23);
+                if (me >= 25) fs.xw.put((uint32_t)e, 8);
+                fs.xw.bit((int)sign);
+            } else {
+                x = sign ? -(int32_t)v : (int32_t)v;
+                if (sc) {
+                    const uint32_t lost = M & ((1u << sc) - 1u);
+                    if (fl & FLOAT_SHIFT_SAME) fs.xw.bit(lost != 0);
+                    else if (fl & FLOAT_SHIFT_SENT) fs.xw.put(lost, sc);
+                }
+            }
+        }
+        fs.ints.push_back(x);
+        crc = add32(add32(add32(mul32(crc, 27), mul32((int32_t)m, 9)), mul32(e, 3)), (int32_t)sign);
+    }
+    fs.crc_x = crc;
+}
+
 struct PcmEncoder {
     const wvenc_params &P;
     std::vector<Pass> passes;  // decoder order
@@ -745,6 +846,25 @@ struct PcmEncoder {
         for (int64_t bi = 0; bi < nblocks; bi++) {
             int64_t f0 = bi * B;
             int64_t nf = std::min<int64_t>(B, frames - f0);
+            // exact float: the block's floats -> integers (+ the wvx stream); the
+            // frame loop reads the integers (channel 1 = channel 0 for FALSE_STEREO)
+            FloatSplit fsplit;
+            std::vector<int32_t> fconv;
+            if (P.float_exact) {
+                std::vector<uint32_t> vals;
+                for (int64_t f = 0; f < nf; f++) {
+                    const int32_t *xf = x + (f0 + f) * P.nch;
+                    vals.push_back((uint32_t)xf[0]);
+                    if (!mono_block) vals.push_back((uint32_t)xf[1]);
+                }
+                float_split(vals, fsplit);
+                fconv.assign((size_t)nf * P.nch, 0);
+                for (int64_t f = 0, k = 0; f < nf; f++) {
+                    fconv[(size_t)(f * P.nch)] = fsplit.ints[(size_t)k++];
+                    if (P.nch == 2) fconv[(size_t)(f * P.nch + 1)] = mono_block ? fconv[(size_t)(f * P.nch)]
+                                                                                 : fsplit.ints[(size_t)k++];
+                }
+            }
             if (P.reset_state) {
                 for (auto &p : passes) {
                     p.wA = p.wB = 0;
@@ -919,7 +1039,10 @@ struct PcmEncoder {
                 ent.bitrate_delta[0] = ent.bitrate_delta[1] = 0;
                 ent.error_limit[0] = ent.error_limit[1] = 0;
             }
-            if (P.float_data) {
+            if (P.float_data && P.float_exact) {
+                std::vector<uint8_t> fi = {(uint8_t)fsplit.flags, 0, (uint8_t)fsplit.max_exp, (uint8_t)P.float_norm_exp};
+                put_subblock(md, ID_FLOAT_INFO, fi);
+            } else if (P.float_data) {
                 std::vector<uint8_t> fi = {(uint8_t)P.float_flags, (uint8_t)P.float_shift, (uint8_t)P.float_max_exp,
                                            (uint8_t)P.float_norm_exp};
                 put_subblock(md, ID_FLOAT_INFO, fi);
@@ -966,7 +1089,7 @@ struct PcmEncoder {
             uint32_t maxabs = 0;
             std::vector<int32_t> inres(n + 1);
             for (int64_t f = 0; f < nf; f++) {
-                const int32_t *xf = x + (f0 + f) * P.nch;
+                const int32_t *xf = P.float_exact ? fconv.data() + f * P.nch : x + (f0 + f) * P.nch;
                 int32_t L = xf[0], R = P.nch == 2 ? xf[1] : 0;
                 int32_t vL = 0, vR = 0;  // pre-shift (post-zod) values: the crc_x input
                 if (im.mode == 2) {
@@ -1056,6 +1179,15 @@ struct PcmEncoder {
             ent = we.w;
             if (bits.empty()) bits.push_back(0);
             put_subblock(md, ID_WV_BITSTREAM, bits);
+            std::vector<uint8_t> xfloat_sub;  // the exact-float wvx sub-block payload
+            if (P.float_exact && fsplit.need_wvx) {
+                std::vector<uint8_t> xb = fsplit.xw.finish();
+                const int32_t cm = fsplit.crc_x;
+                xfloat_sub = {(uint8_t)cm, (uint8_t)(cm >> 8), (uint8_t)(cm >> 16), (uint8_t)(cm >> 24)};
+                xfloat_sub.insert(xfloat_sub.end(), xb.begin(), xb.end());
+                while (xfloat_sub.size() < 6 || (xfloat_sub.size() & 1)) xfloat_sub.push_back(0);  // > 4, even
+                if (!P.wvc) put_subblock(md, ID_WVX_BITSTREAM, xfloat_sub);
+            }
             if (P.wvx) {
                 std::vector<uint8_t> xb = xw.finish();
                 if (im.mode == 2) crc_x = replay_wvx(im, P.wvx == 2, xb, wvx_y, wvx_v, !P.hybrid);
@@ -1082,6 +1214,7 @@ struct PcmEncoder {
                 while (cb.size() < 2 || (cb.size() & 1)) cb.push_back(0);  // even (UnpackUtils.cs:100)
                 std::vector<uint8_t> cmd;
                 put_subblock(cmd, ID_WVC_BITSTREAM, cb);
+                if (!xfloat_sub.empty()) put_subblock(cmd, ID_WVX_BITSTREAM, xfloat_sub);
                 std::vector<uint8_t> cblk(32);
                 cblk.insert(cblk.end(), cmd.begin(), cmd.end());
                 write_header(cblk, P.version, P.total_override > 0 ? P.total_override : frames,
@@ -1356,6 +1489,7 @@ int64_t wvenc_encode_pcm(const int32_t *samples, int64_t frames, const wvenc_par
             if (!ok) throw std::runtime_error("unsupported term for this channel layout");
         }
         if (p->wvc) throw std::runtime_error("wvc: use wvenc_encode_pcm_wvc");
+        if (p->float_exact && (!p->float_data || p->wvx)) throw std::runtime_error("float_exact: float_data, no wvx param");
         PcmEncoder enc(*p);
         std::vector<uint8_t> f = enc.encode(samples, frames);
         if (!out) return (int64_t)f.size();
@@ -1380,6 +1514,7 @@ int64_t wvenc_encode_pcm_wvc(const int32_t *samples, int64_t frames, const wvenc
         if (!p->hybrid || !p->wvc) throw std::runtime_error("wvc needs hybrid");
         if (p->wvx || p->int32_zeros || p->int32_sent_bits || p->int32_ones || p->int32_dups || p->sticky_passes)
             throw std::runtime_error("wvc: plain PCM or float only");
+        if (p->float_exact && !p->float_data) throw std::runtime_error("float_exact: float_data");
         for (int e = 0; e < p->num_terms; e++)
             if (p->terms[e] == -1 || p->terms[e] == -2)
                 throw std::runtime_error("wvc: terms -1/-2 read the other channel's current output");

@@ -39,7 +39,8 @@ class _Params(ctypes.Structure):
             "bitrate_x256", "float_data", "float_flags", "float_shift", "float_max_exp", "float_norm_exp",
             "int32_zeros", "write_riff", "config_flags", "write_history", "reset_state", "block_index_start",
             "total_unknown", "extras", "mag_override", "int32_sent_bits", "int32_ones", "int32_dups", "wvx",
-            "wvx_max_width", "wvx_short")] + [("total_override", ctypes.c_int64), ("sticky_passes", ctypes.c_int32), ("wvc", ctypes.c_int32)]
+            "wvx_max_width", "wvx_short")] + [("total_override", ctypes.c_int64), ("sticky_passes", ctypes.c_int32), ("wvc", ctypes.c_int32),
+                                                          ("float_exact", ctypes.c_int32)]
 
 
 class _DsdParams(ctypes.Structure):
@@ -87,6 +88,7 @@ class EncParams:
     total_override: int = 0  # > 0: header total_samples (parts encoded in parallel, then concatenated)
     sticky_passes: bool = False  # blocks after the first continue the decoder's passes (no pass metadata)
     wvc: bool = False            # hybrid: also write the .wvc correction file (encode_pcm_wvc)
+    float_exact: bool = False    # float_data: samples are float32 bit patterns (encode_float_exact)
 
     def to_c(self) -> _Params:
         p = _Params()
@@ -103,7 +105,7 @@ class EncParams:
                   "wvx_short", "total_override"):
             setattr(p, n, int(getattr(self, n)))
         for n in ("hybrid", "hybrid_bitrate", "hybrid_balance", "float_data", "write_riff", "write_history",
-                  "reset_state", "total_unknown", "sticky_passes", "wvc"):
+                  "reset_state", "total_unknown", "sticky_passes", "wvc", "float_exact"):
             setattr(p, n, int(bool(getattr(self, n))))
         return p
 
@@ -201,6 +203,20 @@ def encode_pcm_wvc(samples: np.ndarray, params: EncParams):
     if m != n:
         raise RuntimeError("wvenc: " + L.wvenc_last_error().decode())
     return out.tobytes(), cout[: nc.value].tobytes()
+
+
+def encode_float_exact(x: np.ndarray, params: EncParams, wvc: bool = False):
+    """float32 samples (frames, nch) -> a FLOAT_DATA .wv whose integers are the
+    mantissas shifted to each block's largest exponent, with a classic wvx stream
+    holding what the shift dropped, the floats it took to 0, -0.0 and inf/nan
+    (beyond the reference, which scales the integers to 24-bit PCM and never
+    reads the stream).  wvc: hybrid .wv + .wvc, the wvx stream in the .wvc.
+    Returns the .wv bytes, or (.wv, .wvc) with wvc."""
+    bits = np.ascontiguousarray(x, dtype=np.float32).view(np.int32)
+    params.float_data = True
+    params.float_exact = True
+    params.bytes_per_sample = 4
+    return encode_pcm_wvc(bits, params) if wvc else encode_pcm(bits, params)
 
 
 @dataclass

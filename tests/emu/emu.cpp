@@ -113,17 +113,20 @@ int64_t emu_decode_from(const uint8_t *file, size_t len, int64_t seek_to, int ch
     return info.out_frames;
 }
 
-// A hybrid file with its .wvc correction file, decoded by the device core on the
-// host (blocks in order, no chains): frames or -2/-3, as emu_decode.
-int64_t emu_decode_wvc(const uint8_t *file, size_t len, const uint8_t *wvc, size_t wvc_len, int chunk, int32_t *out,
-                       int64_t cap, int64_t *crc_errors, int *nch, uint32_t *status_or) {
+// A hybrid file with its .wvc correction file (wvc_len 0: none), opened with
+// open_flags, decoded by the device core on the host (blocks in order, no
+// chains): frames or -2/-3, as emu_decode.
+int64_t emu_decode_wvc(const uint8_t *file, size_t len, const uint8_t *wvc, size_t wvc_len, int chunk,
+                       uint32_t open_flags, int32_t *out, int64_t cap, int64_t *crc_errors, int *nch,
+                       uint32_t *status_or) {
     std::vector<uint8_t> blob(len + wvc_len + 64, 0xFF);
     memcpy(blob.data(), file, len);
-    memcpy(blob.data() + len, wvc, wvc_len);
+    if (wvc_len) memcpy(blob.data() + len, wvc, wvc_len);
     FramingOutput fo;
     FileInfo info;
     fo.defer_values = true;
-    frame_file(blob.data(), len, 0, 0, 0, chunk, fo, info, -1, blob.data() + len, wvc_len, len);
+    frame_file(blob.data(), len, 0, 0, open_flags, chunk, fo, info, -1, wvc_len ? blob.data() + len : nullptr,
+               wvc_len, len);
     apply_meta_jobs(fo, blob.data());
     *crc_errors = 0;
     *status_or = 0;
@@ -136,7 +139,8 @@ int64_t emu_decode_wvc(const uint8_t *file, size_t len, const uint8_t *wvc, size
         if (d.kind != KIND_PCM || d.chain_len || (d.inherit & INH_MEMBER)) return -5;
         HostStore hs{out, d.out_off, (uint64_t)d.pre_end * d.out_nch};
         uint32_t st = d.fstatus | decode_pcm_block(d, blob.data(), hs);
-        *status_or |= st | (d.wvc_len ? 0x10000u : 0u);  // bit 16: a block read its correction stream
+        // bit 16: a block read its correction stream; bit 17: an exact-float block read a wvx stream
+        *status_or |= st | (d.wvc_len ? 0x10000u : 0u) | ((d.xfloat && (d.wvx_state & 1)) ? 0x20000u : 0u);
         if (st & ST_CRC_ERROR) (*crc_errors)++;
         if (st & ST_EXCEPTION) return -3;
     }

@@ -75,7 +75,7 @@ def file_info(data: bytes) -> dict:
 INFO_FIELDS_FULL = INFO_FIELDS + ("lossy_blocks", "is_five", "file_format", "header_off", "header_len", "trailer_off",
                                   "trailer_len", "first_call_frames", "config_flags", "sample_index0", "exception",
                                   "nondet")
-DESC_BYTES = 1424  # sizeof(BlockDesc)
+DESC_BYTES = 1440  # sizeof(BlockDesc)
 
 
 def file_info_full(data: bytes, chunk: int = 4096) -> dict:
@@ -116,18 +116,19 @@ def dframe(data: bytes, chunk: int = 4096):
     return out[: n * DESC_BYTES].tobytes(), dict(zip(INFO_FIELDS_FULL, (int(v) for v in vals)))
 
 
-def decode_wvc(data: bytes, wvc: bytes, chunk: int = 4096):
-    """.wv + .wvc through the device core on the host -> (frames, samples, crc_errors, status_or)"""
+def decode_wvc(data: bytes, wvc: bytes | None, chunk: int = 4096, open_flags: int = 0):
+    """.wv (+ .wvc) through the device core on the host -> (frames, samples, crc_errors, status_or)"""
     f = lib().emu_decode_wvc
     f.restype = ctypes.c_int64
-    f.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p,
-                  ctypes.c_int64, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int),
+    f.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint32,
+                  ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int),
                   ctypes.POINTER(ctypes.c_uint32)]
     cap = max(len(data) * 32, 1 << 16)
     out = np.zeros(cap, dtype=np.int32)
     crc, nch, st = ctypes.c_int64(0), ctypes.c_int(0), ctypes.c_uint32(0)
-    n = f(data, len(data), wvc, len(wvc), chunk, out.ctypes.data, cap, ctypes.byref(crc), ctypes.byref(nch),
-          ctypes.byref(st))
+    wvc = wvc or b""
+    n = f(data, len(data), wvc, len(wvc), chunk, open_flags, out.ctypes.data, cap, ctypes.byref(crc),
+          ctypes.byref(nch), ctypes.byref(st))
     if n < 0:
         return int(n), np.zeros(0, np.int32), crc.value, st.value
     return int(n), out[: n * nch.value].copy(), crc.value, st.value

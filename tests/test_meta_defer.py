@@ -21,7 +21,7 @@ from synth import wvsynth as S
 from tests import vectors as V
 from tests.emu import emu as E
 
-DESC_BYTES = 1424
+DESC_BYTES = 1440
 
 
 def frame(data: bytes, defer: bool, seek: int = -1, chunk: int = 4096):

@@ -34,6 +34,9 @@ from . import _lib as _L
 
 SAMPLE_BUFFER_SIZE = 4096  # Defines.cs:18
 OPEN_2CH_MAX = 0x8         # Defines.cs:26
+# beyond the reference: float files decode to float32 bit patterns, exact via the wvx stream
+# (WVG_OPEN_EXACT_FLOAT, include/wvgpu.h)
+OPEN_EXACT_FLOAT = 0x40000000
 
 
 class WavpackException(RuntimeError):

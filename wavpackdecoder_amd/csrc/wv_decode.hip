@@ -896,7 +896,7 @@ constexpr int kPipe = 3;
 static_assert(kNumTermSets <= kPipe, "term-set slots");
 
 // which two-wave kernel decodes this block (-1: the generic wave kernel, for
-// int32 + wvx blocks).  prefer_pipe 2: every list goes to the pipelined kernel
+// int32 + wvx, .wvc, exact-float and chained blocks).  prefer_pipe 2: every list goes to the pipelined kernel
 // (A/B tests)
 int term_set_of(const BlockDesc &d, int prefer_pipe) {
     using namespace wvf;
@@ -904,6 +904,7 @@ int term_set_of(const BlockDesc &d, int prefer_pipe) {
     if (d.chain_len >= 2 || (d.inherit & INH_MEMBER)) return -1;  // sticky-state chain (wv_decode_pcm_wave)
     if (d.wvx_state & 0x100) return -1;  // int32 + wvx fixup reads a second stream
     if (d.wvc_len) return -1;            // .wvc correction: a second stream read per hybrid word
+    if (d.xfloat) return -1;             // exact float: WavPack 4's float_values over the wvx stream
     const bool mono = (d.flags & MONO_DATA) != 0;
     if (d.num_terms < 0 || d.num_terms > MAXP) return -1;
     bool neg12 = false;

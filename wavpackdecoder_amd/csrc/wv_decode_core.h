@@ -536,8 +536,10 @@ WVF_HD void pass_mono(PassState &p, uint32_t t, int32_t &X) {
 // per-value map prepared once per block.
 // ---------------------------------------------------------------------------
 struct Fixup {
-    int mode;  // 0 float, 1 int32 per-value (zeros/ones/dups), 2 int32+wvx, 3 plain
+    int mode;  // 0 float, 1 int32 per-value (zeros/ones/dups), 2 int32+wvx, 3 plain, 4 exact float
     int32_t fshift;
+    int32_t xflags, xmax_exp, xshift;  // mode 4: ID_FLOAT_INFO's flags, max_exp, shift
+    bool xwvx;                         // mode 4: the block carries a wvx stream
     int32_t zeros, ones, dups, sent_bits, max_width;
     uint32_t mask;
     bool lossy;
@@ -587,6 +589,20 @@ WVF_HD void fixup_init(Fixup &f, const BlockDesc &d) {
     }
     f.min_shifted = shl32(f.min_value, f.shift);
     f.max_shifted = shl32(f.max_value, f.shift);
+}
+
+// exact float output (OPEN_EXACT_FLOAT): mode 4 for a FLOAT_DATA block whose
+// descriptor asks for it.  Only the generic kernel's decode_pcm_run calls this
+// (the two-wave and pipelined kernels never receive such blocks).
+WVF_HD void fixup_init_exact_float(Fixup &f, const BlockDesc &d) {
+    f.xflags = f.xmax_exp = f.xshift = 0;
+    f.xwvx = false;
+    if (!(d.flags & wvf::FLOAT_DATA) || !(d.xfloat & XF_ON)) return;
+    f.mode = 4;
+    f.xflags = (int32_t)(d.xfloat & 0xffu);
+    f.xmax_exp = (int32_t)((d.xfloat >> 8) & 0xffu);
+    f.xshift = (int32_t)((d.xfloat >> 16) & 0xffu);
+    f.xwvx = (d.wvx_state & 1) != 0;
 }
 
 WVF_HD int32_t zod(const Fixup &f, int32_t x) {  // zeros / ones / dups (UnpackUtils.cs:1300-1305)
@@ -643,6 +659,74 @@ WVF_HD int32_t fixup_wvx(const Fixup &f, BitReader &xb, uint32_t xlen, int32_t x
     return fixup_tail(f, x);
 }
 
+// Exact float output (OPEN_EXACT_FLOAT; beyond the reference):
+// WavPack 4's float_values, where FloatUtils.cs:32-56 scales to 24-bit
+// integers instead.  A nonzero integer is the float's mantissa (implicit bit
+// included) shifted right by float_max_exp - exponent; the wvx stream, when
+// the block carries one, holds the bits that shift dropped (FLOAT_SHIFT_*),
+// the floats that became 0 (FLOAT_ZEROS_SENT / FLOAT_NEG_ZEROS) and inf/nan
+// mantissas (FLOAT_EXCEPTIONS: integer +-2^24).  Returns the float's bits;
+// crc_x takes crc * 27 + mantissa * 9 + exponent * 3 + sign per value (the wvx
+// header's crc).  A read past the wvx payload, or a shift no encoder makes,
+// sets `bad` (the block's CRC verdict then fails).
+WVF_HD int32_t fixup_xfloat(const Fixup &f, BitReader &xb, uint32_t xlen, int32_t x, int32_t &crc_x, int &bad) {
+    using namespace wvf;
+    const bool wx = f.xwvx;
+    uint32_t sign = 0, exp = (uint32_t)f.xmax_exp, mant = 0;
+    if (x == 0) {
+        exp = 0;
+        if (wx && (f.xflags & FLOAT_ZEROS_SENT)) {
+            if (xb.getbit()) {  // a float the shift took to 0: sent whole
+                mant = xb.getbits(23);
+                if (f.xmax_exp >= 25) exp = xb.getbits(8);
+                sign = (uint32_t)xb.getbit();
+            } else if (f.xflags & FLOAT_NEG_ZEROS) {
+                sign = (uint32_t)xb.getbit();
+            }
+        } else if (wx && (f.xflags & FLOAT_NEG_ZEROS)) {
+            sign = (uint32_t)xb.getbit();
+        }
+    } else {
+        uint32_t v = (uint32_t)shl32(x, f.xshift);
+        if ((int32_t)v < 0) {
+            v = 0u - v;
+            sign = 1;
+        }
+        if (wx && v == 0x1000000u) {  // inf / nan
+            if (xb.getbit()) mant = xb.getbits(23);
+            exp = 255;
+        } else if (!wx && v >= 0x1000000u) {
+            while (v & 0xf000000u) {
+                v >>= 1;
+                ++exp;
+            }
+            mant = v;
+        } else {
+            int sc = 0;
+            if (exp)
+                while (!(v & 0x800000u) && --exp) {
+                    sc++;
+                    v <<= 1;
+                }
+            if (sc > 23) {
+                bad = 1;
+            } else if (sc) {
+                const uint32_t m = (1u << sc) - 1u;
+                if ((f.xflags & FLOAT_SHIFT_ONES) || (wx && (f.xflags & FLOAT_SHIFT_SAME) && xb.getbit()))
+                    v |= m;
+                else if (wx && (f.xflags & FLOAT_SHIFT_SENT))
+                    v |= xb.getbits(sc) & m;
+            }
+            mant = v;
+        }
+    }
+    mant &= 0x7fffffu;
+    exp &= 0xffu;
+    if (wx && xb.consumed() > 8ull * xlen) bad = 1;
+    crc_x = add32(add32(add32(mul32(crc_x, 27), mul32((int32_t)mant, 9)), mul32((int32_t)exp, 3)), (int32_t)sign);
+    return (int32_t)((sign << 31) | (exp << 23) | mant);
+}
+
 // ---------------------------------------------------------------------------
 // one PCM block.  PcmState is the part of the WavpackStream a decode adapts:
 // pcm_state_load fills it from the descriptor and, inside a chain, keeps what
@@ -658,6 +742,7 @@ struct PcmState {
     bool muted;           // wps.mute_error
     bool crc_garbage;     // the running crc went over stale buffer contents
     bool pass_garbage;    // a pass ran over stale residuals (get_words stopped short)
+    bool xbad;            // exact float: the wvx stream ran out or held an impossible value
 };
 
 // Every reference pass call leaves its ring rotated so that slot 0 is the
@@ -745,6 +830,7 @@ WVF_HD uint32_t pcm_state_load(PcmState &s, const BlockDesc &d, const uint8_t *b
         s.crc = s.crc_x = -1;
         s.muted = false;
         s.crc_garbage = false;
+        s.xbad = false;
     }
     return status;
 }
@@ -772,6 +858,7 @@ WVF_HD uint32_t decode_pcm_run(PcmState &s, const BlockDesc &d, Store &out, uint
 
     Fixup fx;
     fixup_init(fx, d);
+    fixup_init_exact_float(fx, d);
 
     uint32_t status = 0;
     if (fstereo && fx.mode == 2) status |= ST_NONDET;  // fixup reads wvx bits for 2n values (n stale)
@@ -864,6 +951,11 @@ WVF_HD uint32_t decode_pcm_run(PcmState &s, const BlockDesc &d, Store &out, uint
                     if (exc_frame) *exc_frame = t;
                     return status | ST_EXCEPTION;
                 }
+            } else if (fx.mode == 4) {
+                int bad = 0;
+                oL = fixup_xfloat(fx, xb, d.wvx_len, L, s.crc_x, bad);
+                oR = mono ? 0 : fixup_xfloat(fx, xb, d.wvx_len, R, s.crc_x, bad);
+                if (bad) s.xbad = true;
             } else {
                 oL = fixup_tail(fx, L);
                 oR = mono ? 0 : fixup_tail(fx, R);
@@ -932,6 +1024,8 @@ WVF_HD uint32_t decode_pcm_run(PcmState &s, const BlockDesc &d, Store &out, uint
                         if (exc_frame) *exc_frame = f + j;
                         return status | ST_EXCEPTION;
                     }
+                } else if (fx.mode == 4) {
+                    z0 = 0;  // +0.0f; the wvx stream is not read past a mute
                 } else {
                     z0 = fixup_tail(fx, 0);
                     z1 = mono ? 0 : fixup_tail(fx, 0);
@@ -960,6 +1054,7 @@ WVF_HD uint32_t decode_pcm_run(PcmState &s, const BlockDesc &d, Store &out, uint
         status |= ST_CRC_CHECKED;
         bool err = s.crc_garbage || s.crc != d.crc;
         if (!(flags & FLOAT_DATA) && (d.wvx_state & 1) && s.crc_x != d.crc_mvx) err = true;
+        if (fx.mode == 4 && (s.xbad || ((d.wvx_state & 1) && s.crc_x != d.crc_mvx))) err = true;
         if (err) status |= ST_CRC_ERROR;
     }
     return status;

@@ -95,7 +95,13 @@ struct alignas(16) BlockDesc {
     uint64_t wvc_off;
     uint32_t wvc_len;         // 0: no correction stream (the reference's decode)
     int32_t crc_lossy;
+    // --- exact float output (OPEN_EXACT_FLOAT, beyond the reference): 0 = the
+    // reference's float_values; else XF_ON | float_flags | float_max_exp << 8 |
+    // ID_FLOAT_INFO's float_shift << 16 (the wvx stream, if any, in wvx_off/len)
+    uint32_t xfloat;
+    uint32_t xfloat_pad_[3];
 };
+constexpr uint32_t XF_ON = 1u << 31;
 
 // A block that starts from state an earlier decode left behind: a block without
 // one of the metadata sub-blocks that reset it, or one read without unpack_init

@@ -140,6 +140,7 @@ class Framer {
     const uint8_t *wvc = nullptr;
     int64_t wvc_len = 0, wvc_pos = 0;
     uint64_t wvc_base = 0;
+    bool exact_float = false;  // OPEN_EXACT_FLOAT (beyond the reference)
 
     Framer() {
         memset(read_buffer, 0, sizeof(read_buffer));
@@ -834,6 +835,20 @@ class Framer {
                     d.wvx_state |= 0x100;
                 }
             }
+            if (exact_float && (flags & FLOAT_DATA)) {
+                // WavPack 4's float_values instead of FloatUtils.cs:32-56 (fixup_xfloat):
+                // the block's own classic ID_WVX_BITSTREAM, if any (WavPack opens the
+                // stream per block; a NEW-format stream is not decoded)
+                d.xfloat = XF_ON | ((uint32_t)float_flags & 0xffu) | (((uint32_t)float_max_exp & 0xffu) << 8) |
+                           (((uint32_t)float_shift & 0xffu) << 16);
+                if (wvxbits.valid && !wvxbits.fresh) {
+                    d.wvx_state = 0;
+                    d.wvx_off = 0;
+                    d.wvx_len = 0;
+                } else if (wvxbits.valid && wvx_skip_bits) {
+                    status |= ST_UNSUPPORTED;
+                }
+            }
             if (!w.known) {
                 inh |= INH_ENTROPY;
                 for (int c = 0; c < 2; c++) {
@@ -916,13 +931,22 @@ class Framer {
                         hl = 4;
                     }
                     const int64_t real = (id & ID_ODD_SIZE) ? bl - 1 : bl;
-                    if ((id & 0x3f) == ID_WVC_BITSTREAM && real > 0 && !(real & 1) && p + hl + bl <= end) {
+                    if ((id & 0x3f) == ID_WVC_BITSTREAM && real > 0 && !(real & 1) && p + hl + bl <= end &&
+                        !d.wvc_len) {
                         d.wvc_off = wvc_base + (uint64_t)(p + hl);
                         d.wvc_len = (uint32_t)real;
                         d.crc_lossy = d.crc;
                         d.crc = (int32_t)((uint32_t)b[28] | ((uint32_t)b[29] << 8) | ((uint32_t)b[30] << 16) |
                                           ((uint32_t)b[31] << 24));
-                        break;
+                    } else if ((id & 0x3f) == ID_WVX_BITSTREAM && !(id & ID_OPTIONAL_DATA) && (d.xfloat & XF_ON) &&
+                               real > 4 && !(real & 1) && p + hl + bl <= end && !(d.wvx_state & 1)) {
+                        // exact float of a hybrid float file: its wvx stream sits in the .wvc block
+                        const uint8_t *x = wvc + p + hl;
+                        d.crc_mvx = (int32_t)((uint32_t)x[0] | ((uint32_t)x[1] << 8) | ((uint32_t)x[2] << 16) |
+                                              ((uint32_t)x[3] << 24));
+                        d.wvx_off = wvc_base + (uint64_t)(p + hl + 4);
+                        d.wvx_len = (uint32_t)(real - 4);
+                        d.wvx_state = 1;
                     }
                     p += hl + bl;
                 }
@@ -1179,6 +1203,7 @@ void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t ou
     F.wvc = wvc;
     F.wvc_len = wvc ? (int64_t)wvc_len : 0;
     F.wvc_base = wvc_base;
+    F.exact_float = (open_flags & OPEN_EXACT_FLOAT) != 0;
     F.in.d = file;
     F.in.len = (int64_t)len;
     info = FileInfo();
