@@ -144,7 +144,7 @@ int wvg_batch_add_file_wvc(wvg_batch *b, const uint8_t *file, size_t len, const 
  * WavpackOpenFileInput header + sub-block walk of WavPackUtils.cs:36-120,600-671,
  * UnpackUtils.cs:24-68, MetadataUtils.cs:15-192 as kernels, open_flags 0).  The
  * bytes are copied now and file slots reserved (indices[i]); a file outside the
- * device framer's scope (DSD, wvx, sticky state, junk, damaged headers) is framed
+ * device framer's scope (DSD mode 1, wvx, sticky state, junk, damaged headers) is framed
  * by the host at the same upload with the same result as wvg_batch_add_file.
  * The files' infos are available after the upload (wvg_batch_file_info). */
 int wvg_batch_add_files_device(wvg_batch *b, int n, const uint8_t *const *files, const size_t *lens,

@@ -203,11 +203,8 @@ __device__ __forceinline__ DsdResult dsd_high_wave(const BlockDesc &d, const uin
     bool mute = false;
     uint32_t low = 0, high = 0xFFFFFFFFu, value = 0;
     for (int i = 0; i < 4; i++) value = (value << 8) | src.byte(bp++);
-    {  // the block's initial probability table, 4 entries per lane
-        const int32_t *pt0 = (const int32_t *)(tables + d.dsd_table_off);
-        for (uint32_t i = threadIdx.x; i < 256; i += 64) ptable[i] = pt0[i];
-        __syncthreads();
-    }
+    dsd_ptable_init(d.dsd_rate_i, ptable, threadIdx.x, 64);  // the block's initial probability table
+    __syncthreads();
     int32_t q0[WCH], q1[WCH], q2[WCH], q3[WCH], q4[WCH], q5[WCH], q6[WCH], q7[WCH], q8[WCH], bytei[WCH];
 #pragma unroll
     for (int c = 0; c < WCH; c++) {
@@ -358,11 +355,8 @@ __device__ __forceinline__ DsdResult dsd_high_v2(const BlockDesc &d, const uint8
     uint32_t low = 0, high = 0xFFFFFFFFu, value = 0;
     value = src.shift_in(0, 32, 4);  // init_dsd_block_high checked >= 4 payload bytes
     bp = 4;
-    {
-        const int32_t *pt0 = (const int32_t *)(tables + d.dsd_table_off);
-        for (uint32_t i = threadIdx.x; i < 256; i += 64) ptable[i] = pt0[i];
-        __syncthreads();
-    }
+    dsd_ptable_init(d.dsd_rate_i, ptable, threadIdx.x, 64);
+    __syncthreads();
     uint8_t *lds = (uint8_t *)ptable;
     int32_t q2 = d.dsd_filters[ch][0], q3 = d.dsd_filters[ch][1], q4 = d.dsd_filters[ch][2];
     int32_t q5 = d.dsd_filters[ch][3], q6 = d.dsd_filters[ch][4], q8 = d.dsd_filters[ch][5];

@@ -1080,6 +1080,26 @@ struct DsdResult {
     uint32_t mute_chunk;  // first muted chunk (valid with ST_DSD_MUTE)
 };
 
+// init_ptable (DsdUtils.cs:321-341; rate_s is 20, the framing rejects any
+// other): mode 3's starting probability table from the block's rate_i.  A
+// uniform serial recurrence of at most 3,469 steps over all 256 rate_i (value
+// reaches 0x10000 and stops moving, which ends the rate growth); of `nl` lanes,
+// lane `lane` stores entries i and 255 - i for i == lane (mod nl).
+WVF_HD void dsd_ptable_init(int32_t rate_i, int32_t *pt, uint32_t lane, uint32_t nl) {
+    int32_t value = 0x808000, rate = rate_i << 8;
+    for (int32_t c = (rate + 128) >> 8; c > 0; c--) value += (0x00010000 - value) >> 8;
+    for (uint32_t i = 0; i < 128; ++i) {
+        if (i % nl == lane) {
+            pt[i] = value;
+            pt[255 - i] = 0x100ffff - value;
+        }
+        if (value > 0x010000) {
+            rate += (rate * 20 + 128) >> 8;
+            for (int32_t c = (rate + 64) >> 7; c > 0; c--) value += (0x00010000 - value) >> 8;
+        }
+    }
+}
+
 template <class Store>
 WVF_HD DsdResult decode_dsd_block(const BlockDesc &d, const uint8_t *blob, const uint8_t *tables, int32_t *ptable,
                                   Store &out) {
@@ -1111,8 +1131,7 @@ WVF_HD DsdResult decode_dsd_block(const BlockDesc &d, const uint8_t *blob, const
         for (int i = 0; i < 4; i++) value = (value << 8) | data[bp++];
     }
     if (d.kind == KIND_DSD_HIGH) {
-        const int32_t *pt0 = (const int32_t *)(tables + d.dsd_table_off);
-        for (int i = 0; i < 256; i++) ptable[i] = pt0[i];
+        dsd_ptable_init(d.dsd_rate_i, ptable, 0, 1);
         for (int c = 0; c < 2; c++) {
             F[c][0] = 0;
             F[c][1] = 0;

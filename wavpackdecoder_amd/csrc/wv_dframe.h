@@ -19,8 +19,9 @@
 //   * headers back to back from byte 0 to the file's end, every one passing
 //     read_next_header's test where the previous block ends, block_index
 //     running from 0 without gaps, total_samples known and equal to the sum;
-//   * every block PCM, or every block DSD mode 0 (raw bytes; modes 1/3 build
-//     tables on the host), mono or stereo as the file opened, INITIAL_BLOCK
+//   * every block PCM, or every block DSD mode 0 (raw bytes) or 3 (the high
+//     coder: rate and filter bytes; mode 1's tables are built on the host),
+//     mono or stereo as the file opened, INITIAL_BLOCK
 //     set, block_samples > 0, and its unpack_init succeeds with the decorr
 //     terms, entropy variables and bitstream (or ID_DSD_BLOCK) re-sent (no
 //     sticky state, B-8),
@@ -128,11 +129,15 @@ struct DState {
     int32_t i32[4];     // sent_bits, zeros, ones, dups
     int32_t fl[4];      // float flags, shift, max_exp, norm_exp
     bool terms, entropy, bits, has_i32, has_fl;
-    // ID_DSD_BLOCK, mode 0 only (DsdUtils.cs:17-54): the raw bytes after mult/mode
+    // ID_DSD_BLOCK, modes 0 and 3 (DsdUtils.cs:17-54, 343-389): the payload after
+    // mult/mode (and mode 3's rate and filter bytes)
     bool dsd;
+    int32_t dsd_mode;
     int32_t dsd_mult_log2;  // data[0] & 31
-    int64_t dsd_off;        // file offset of data[2]
-    int32_t dsd_len;        // C# data.Length - 2
+    int64_t dsd_off;        // file offset of the payload (data[byteptr])
+    int32_t dsd_len;        // C# data.Length - byteptr
+    int32_t dsd_rate_i;     // mode 3: init_ptable's rate index
+    int32_t dsd_filt[2][6]; // mode 3: filter1..5 << 12, factor
     // context (file-level) values, updated in place
     int64_t cfg_flags;
     int32_t xmode;
@@ -152,9 +157,13 @@ WVF_HD void dstate_init(DState &s) {
     for (int i = 0; i < 4; i++) s.i32[i] = s.fl[i] = 0;
     s.terms = s.entropy = s.bits = s.has_i32 = s.has_fl = false;
     s.dsd = false;
+    s.dsd_mode = 0;
     s.dsd_mult_log2 = 0;
     s.dsd_off = 0;
     s.dsd_len = 0;
+    s.dsd_rate_i = 0;
+    for (int c = 0; c < 2; c++)
+        for (int k = 0; k < 6; k++) s.dsd_filt[c][k] = 0;
     s.cfg_flags = 0;
     s.xmode = 0;
     s.num_channels = -1;
@@ -327,16 +336,30 @@ WVF_HD uint32_t dframe_subblocks(const uint8_t *f, uint64_t len, uint64_t hpos, 
         case ID_BLOCK_CHECKSUM: s.five = true; break;
         case ID_WVC_BITSTREAM:
         case ID_WVX_BITSTREAM:
-        case ID_WVX_NEW_BITSTREAM:
-        case ID_DSD_BLOCK: {  // init_dsd_block (DsdUtils.cs:17-54); modes 1/3 build tables: the host's
-            if (byte_length < 2 || d[0] > 31 || d[1] != 0) return DF_KIND;
+        case ID_WVX_NEW_BITSTREAM: return DF_KIND;  // a second stream: the host frames the file
+        case ID_DSD_BLOCK: {  // init_dsd_block (DsdUtils.cs:17-54); mode 1 builds tables: the host's
+            if (byte_length < 2 || d[0] > 31 || (d[1] != 0 && d[1] != 3)) return DF_KIND;
             // copy_data's length: the read buffer's fill for a small sub-block, the bytes read for a large one
             const int32_t dl = to_read > BITSTREAM_BUFFER_SIZE ? to_read : byte_length;
-            if ((int64_t)(dl - 2) != (int64_t)h.block_samples * (mono ? 1 : 2)) return DF_READER;
+            int32_t p = 2;
+            if (d[1] == 0) {
+                if ((int64_t)(dl - 2) != (int64_t)h.block_samples * (mono ? 1 : 2)) return DF_READER;
+            } else {  // init_dsd_block_high (:343-389); its ptable is built by the decode kernel
+                if (dl - 2 < (mono ? 13 : 20) || d[3] != 20) return DF_READER;
+                s.dsd_rate_i = d[2];
+                p = 4;
+                for (int c = 0; c < (mono ? 1 : 2); c++) {
+                    for (int k = 0; k < 5; k++) s.dsd_filt[c][k] = (int32_t)d[p++] << 12;
+                    const uint32_t fv = (uint32_t)d[p] | ((uint32_t)d[p + 1] << 8);
+                    p += 2;
+                    s.dsd_filt[c][5] = (int32_t)(fv << 16) >> 16;
+                }
+            }
             s.dsd = true;
+            s.dsd_mode = d[1];
             s.dsd_mult_log2 = d[0] & 31;
-            s.dsd_off = (int64_t)doff + 2;
-            s.dsd_len = dl - 2;
+            s.dsd_off = (int64_t)doff + p;
+            s.dsd_len = dl - p;
             break;
         }
         default:
@@ -544,10 +567,13 @@ WVF_HD void dframe_block(const DFile &fi, uint32_t k, const uint8_t *blob, const
     d.int32_zeros = s.i32[1];
     d.int32_ones = s.i32[2];
     d.int32_dups = s.i32[3];
-    if (flags & DSD_FLAG) {  // DSD mode 0 (DsdUtils.cs:60-147): the raw bytes
-        d.kind = KIND_DSD_RAW;
+    if (flags & DSD_FLAG) {  // DSD mode 0 (DsdUtils.cs:60-147: the raw bytes) or 3 (:391-493)
+        d.kind = s.dsd_mode == 3 ? KIND_DSD_HIGH : KIND_DSD_RAW;
         d.bits_off = fi.base + (uint64_t)s.dsd_off;
         d.dsd_data_len = (uint32_t)s.dsd_len;
+        d.dsd_rate_i = s.dsd_rate_i;
+        for (int c = 0; c < 2; c++)
+            for (int k = 0; k < 6; k++) d.dsd_filters[c][k] = s.dsd_filt[c][k];
     } else {
         d.kind = KIND_PCM;
         d.bits_off = fi.base + (uint64_t)s.bits_off;

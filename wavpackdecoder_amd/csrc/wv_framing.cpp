@@ -61,7 +61,6 @@ struct DsdState {  // WavpackStream.dsds
     std::vector<uint16_t> summed;
     std::vector<uint8_t> lookup;
     std::vector<int32_t> value_lookup;
-    int32_t ptable[256];
     int32_t filt[2][7];
     int rate_i = 0;
 };
@@ -673,17 +672,7 @@ class Framer {
         d.rate_i = data[d.byteptr++];
         int rate_s = data[d.byteptr++];
         if (rate_s != 20) return false;
-        // init_ptable (:321-341)
-        int value = 0x808000, rate = d.rate_i << 8;
-        for (int c = (rate + 128) >> 8; c > 0; c--) value += (0x00010000 - value) >> 8;
-        for (int i = 0; i < 128; ++i) {
-            d.ptable[i] = value;
-            d.ptable[255 - i] = 0x100ffff - value;
-            if (value > 0x010000) {
-                rate += (rate * rate_s + 128) >> 8;
-                for (int c = (rate + 64) >> 7; c > 0; c--) value += (0x00010000 - value) >> 8;
-            }
-        }
+        // init_ptable (:321-341) runs on the device from rate_i (dsd_ptable_init)
         memset(d.filt, 0, sizeof(d.filt));
         for (int ch = 0; ch < (mono ? 1 : 2); ch++) {
             for (int k = 0; k < 5; k++) d.filt[ch][k] = data[d.byteptr++] << 12;
@@ -812,11 +801,7 @@ class Framer {
                 memcpy(t + bins * 768, dsd.lookup.data(), bins * 1280);
                 memcpy(t + bins * 2048, dsd.value_lookup.data(), bins * 4);
                 d.dsd_table_off = off;
-            } else if (dsd.mode == 3) {
-                size_t off = (out.tables.size() + 15) & ~(size_t)15;
-                out.tables.resize(off + 1024, 0);
-                memcpy(out.tables.data() + off, dsd.ptable, 1024);
-                d.dsd_table_off = off;
+            } else if (dsd.mode == 3) {  // the kernel builds the ptable from dsd_rate_i (dsd_ptable_init)
                 memcpy(d.dsd_filters, dsd.filt, sizeof(d.dsd_filters));
             }
         } else {
