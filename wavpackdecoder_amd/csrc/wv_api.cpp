@@ -23,6 +23,7 @@ int term_set_of(const BlockDesc &d, int prefer_pipe);
 hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, uint32_t n, const uint8_t *blob,
                         int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s);
 hipError_t launch_format(const FormatSeg *segs, uint32_t nseg, const int32_t *in, uint8_t *out, int dsd, hipStream_t s);
+hipError_t upload_dsd_ptables();
 hipError_t launch_dsd_fill(const BlockDesc *descs, const uint32_t *dsd_list, uint32_t n_dsd, const uint32_t *status,
                            const uint32_t *aux, int32_t *out, hipStream_t s);
 hipError_t launch_dframe_rank(DFile *files, const uint32_t *tile_file, uint32_t ntiles, const uint32_t *rank_files,
@@ -193,6 +194,7 @@ wvg_ctx *wvg_open(int device) {
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return nullptr;
     if (device < 0) hipGetDevice(&device);
     if (device >= n || hipSetDevice(device) != hipSuccess) return nullptr;
+    if (upload_dsd_ptables() != hipSuccess) return nullptr;  // DSD mode 3's starting tables, per device
     wvg_ctx *c = new wvg_ctx();
     c->device = device;
     return c;

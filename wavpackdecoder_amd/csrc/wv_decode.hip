@@ -33,6 +33,7 @@
 // blocks the block frame of the residual whose decode raised the reference's
 // C# exception (with ST_EXCEPTION).
 #include <hip/hip_runtime.h>
+#include <vector>
 
 #include "wv_decode_core.h"
 #include "wv_meta.h"
@@ -98,6 +99,19 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_pcm_wave(const BlockD
         status[bi] = s;
         aux[bi] = exc;
     }
+}
+
+// Mode 3's starting probability table for every rate_i (init_ptable,
+// DsdUtils.cs:321-341; dsd_ptable_init), 256 KiB, filled once per device at
+// wvg_open (upload_dsd_ptables): a block copies its row into LDS rather than
+// running the up-to-3,469-step recurrence on its serial path (measured: 1.8 ms
+// more per 22,050-frame block when each block built its own)
+__device__ int32_t g_dsd_ptables[256 * 256];
+
+hipError_t upload_dsd_ptables() {
+    std::vector<int32_t> t(256 * 256);
+    for (int r = 0; r < 256; r++) dsd_ptable_init(r, t.data() + (size_t)r * 256, 0, 1);
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_dsd_ptables), t.data(), t.size() * sizeof(int32_t));
 }
 
 // Payload bytes for a wave-uniform decoder: aligned dwords through the scalar
@@ -203,8 +217,11 @@ __device__ __forceinline__ DsdResult dsd_high_wave(const BlockDesc &d, const uin
     bool mute = false;
     uint32_t low = 0, high = 0xFFFFFFFFu, value = 0;
     for (int i = 0; i < 4; i++) value = (value << 8) | src.byte(bp++);
-    dsd_ptable_init(d.dsd_rate_i, ptable, threadIdx.x, 64);  // the block's initial probability table
-    __syncthreads();
+    {  // the block's initial probability table, 4 entries per lane
+        const int32_t *pt0 = g_dsd_ptables + (uint32_t)(d.dsd_rate_i & 255) * 256u;
+        for (uint32_t i = threadIdx.x; i < 256; i += 64) ptable[i] = pt0[i];
+        __syncthreads();
+    }
     int32_t q0[WCH], q1[WCH], q2[WCH], q3[WCH], q4[WCH], q5[WCH], q6[WCH], q7[WCH], q8[WCH], bytei[WCH];
 #pragma unroll
     for (int c = 0; c < WCH; c++) {
@@ -355,8 +372,11 @@ __device__ __forceinline__ DsdResult dsd_high_v2(const BlockDesc &d, const uint8
     uint32_t low = 0, high = 0xFFFFFFFFu, value = 0;
     value = src.shift_in(0, 32, 4);  // init_dsd_block_high checked >= 4 payload bytes
     bp = 4;
-    dsd_ptable_init(d.dsd_rate_i, ptable, threadIdx.x, 64);
-    __syncthreads();
+    {
+        const int32_t *pt0 = g_dsd_ptables + (uint32_t)(d.dsd_rate_i & 255) * 256u;
+        for (uint32_t i = threadIdx.x; i < 256; i += 64) ptable[i] = pt0[i];
+        __syncthreads();
+    }
     uint8_t *lds = (uint8_t *)ptable;
     int32_t q2 = d.dsd_filters[ch][0], q3 = d.dsd_filters[ch][1], q4 = d.dsd_filters[ch][2];
     int32_t q5 = d.dsd_filters[ch][3], q6 = d.dsd_filters[ch][4], q8 = d.dsd_filters[ch][5];
@@ -594,7 +614,7 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_wave(const BlockD
         r = (d.flags & wvf::MONO_DATA) ? dsd_simple_wave<1, false>(d, blob, tables, st)
                                        : dsd_simple_wave<2, false>(d, blob, tables, st);
     else
-        r = decode_dsd_block(d, blob, tables, pt_lds, st);
+        r = decode_dsd_block(d, blob, tables, pt_lds, st, g_dsd_ptables);
     if (lead) {
         status[bi] = d.fstatus | r.status;
         mute_chunk[bi] = r.mute_chunk;
@@ -769,7 +789,7 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_fast(const BlockD
     }
     __syncthreads();
     if (bins > 32u)  // not produced by the framing (init_dsd_block_fast rejects > 5 history bits)
-        r = decode_dsd_block(d, blob, tables, nullptr, st);
+        r = decode_dsd_block(d, blob, tables, nullptr, st, g_dsd_ptables);
     else
         r = (d.flags & wvf::MONO_DATA) ? dsd_fast_v2<1>(d, blob, tab, vmag, vsh1, vsh2, st)
                                        : dsd_fast_v2<2>(d, blob, tab, vmag, vsh1, vsh2, st);

@@ -536,10 +536,8 @@ WVF_HD void pass_mono(PassState &p, uint32_t t, int32_t &X) {
 // per-value map prepared once per block.
 // ---------------------------------------------------------------------------
 struct Fixup {
-    int mode;  // 0 float, 1 int32 per-value (zeros/ones/dups), 2 int32+wvx, 3 plain, 4 exact float
+    int mode;  // 0 float, 1 int32 per-value (zeros/ones/dups), 2 int32+wvx, 3 plain
     int32_t fshift;
-    int32_t xflags, xmax_exp, xshift;  // mode 4: ID_FLOAT_INFO's flags, max_exp, shift
-    bool xwvx;                         // mode 4: the block carries a wvx stream
     int32_t zeros, ones, dups, sent_bits, max_width;
     uint32_t mask;
     bool lossy;
@@ -591,18 +589,21 @@ WVF_HD void fixup_init(Fixup &f, const BlockDesc &d) {
     f.max_shifted = shl32(f.max_value, f.shift);
 }
 
-// exact float output (OPEN_EXACT_FLOAT): mode 4 for a FLOAT_DATA block whose
-// descriptor asks for it.  Only the generic kernel's decode_pcm_run calls this
-// (the two-wave and pipelined kernels never receive such blocks).
-WVF_HD void fixup_init_exact_float(Fixup &f, const BlockDesc &d) {
-    f.xflags = f.xmax_exp = f.xshift = 0;
-    f.xwvx = false;
-    if (!(d.flags & wvf::FLOAT_DATA) || !(d.xfloat & XF_ON)) return;
-    f.mode = 4;
-    f.xflags = (int32_t)(d.xfloat & 0xffu);
-    f.xmax_exp = (int32_t)((d.xfloat >> 8) & 0xffu);
-    f.xshift = (int32_t)((d.xfloat >> 16) & 0xffu);
-    f.xwvx = (d.wvx_state & 1) != 0;
+// exact float output (OPEN_EXACT_FLOAT) of a FLOAT_DATA block whose descriptor
+// asks for it.  Kept apart from Fixup: only the generic kernel's
+// decode_pcm_run uses it (the two-wave and pipelined kernels never receive
+// such blocks, and their Fixup stays as small as before).
+struct XFloat {
+    bool on;
+    bool wvx;                     // the block carries a wvx stream
+    int32_t flags, max_exp, shift;  // ID_FLOAT_INFO's flags, max_exp, shift
+};
+WVF_HD void xfloat_init(XFloat &x, const BlockDesc &d) {
+    x.on = (d.flags & wvf::FLOAT_DATA) && (d.xfloat & XF_ON);
+    x.flags = (int32_t)(d.xfloat & 0xffu);
+    x.max_exp = (int32_t)((d.xfloat >> 8) & 0xffu);
+    x.shift = (int32_t)((d.xfloat >> 16) & 0xffu);
+    x.wvx = (d.wvx_state & 1) != 0;
 }
 
 WVF_HD int32_t zod(const Fixup &f, int32_t x) {  // zeros / ones / dups (UnpackUtils.cs:1300-1305)
@@ -669,25 +670,25 @@ WVF_HD int32_t fixup_wvx(const Fixup &f, BitReader &xb, uint32_t xlen, int32_t x
 // crc_x takes crc * 27 + mantissa * 9 + exponent * 3 + sign per value (the wvx
 // header's crc).  A read past the wvx payload, or a shift no encoder makes,
 // sets `bad` (the block's CRC verdict then fails).
-WVF_HD int32_t fixup_xfloat(const Fixup &f, BitReader &xb, uint32_t xlen, int32_t x, int32_t &crc_x, int &bad) {
+WVF_HD int32_t fixup_xfloat(const XFloat &f, BitReader &xb, uint32_t xlen, int32_t x, int32_t &crc_x, int &bad) {
     using namespace wvf;
-    const bool wx = f.xwvx;
-    uint32_t sign = 0, exp = (uint32_t)f.xmax_exp, mant = 0;
+    const bool wx = f.wvx;
+    uint32_t sign = 0, exp = (uint32_t)f.max_exp, mant = 0;
     if (x == 0) {
         exp = 0;
-        if (wx && (f.xflags & FLOAT_ZEROS_SENT)) {
+        if (wx && (f.flags & FLOAT_ZEROS_SENT)) {
             if (xb.getbit()) {  // a float the shift took to 0: sent whole
                 mant = xb.getbits(23);
-                if (f.xmax_exp >= 25) exp = xb.getbits(8);
+                if (f.max_exp >= 25) exp = xb.getbits(8);
                 sign = (uint32_t)xb.getbit();
-            } else if (f.xflags & FLOAT_NEG_ZEROS) {
+            } else if (f.flags & FLOAT_NEG_ZEROS) {
                 sign = (uint32_t)xb.getbit();
             }
-        } else if (wx && (f.xflags & FLOAT_NEG_ZEROS)) {
+        } else if (wx && (f.flags & FLOAT_NEG_ZEROS)) {
             sign = (uint32_t)xb.getbit();
         }
     } else {
-        uint32_t v = (uint32_t)shl32(x, f.xshift);
+        uint32_t v = (uint32_t)shl32(x, f.shift);
         if ((int32_t)v < 0) {
             v = 0u - v;
             sign = 1;
@@ -712,9 +713,9 @@ WVF_HD int32_t fixup_xfloat(const Fixup &f, BitReader &xb, uint32_t xlen, int32_
                 bad = 1;
             } else if (sc) {
                 const uint32_t m = (1u << sc) - 1u;
-                if ((f.xflags & FLOAT_SHIFT_ONES) || (wx && (f.xflags & FLOAT_SHIFT_SAME) && xb.getbit()))
+                if ((f.flags & FLOAT_SHIFT_ONES) || (wx && (f.flags & FLOAT_SHIFT_SAME) && xb.getbit()))
                     v |= m;
-                else if (wx && (f.xflags & FLOAT_SHIFT_SENT))
+                else if (wx && (f.flags & FLOAT_SHIFT_SENT))
                     v |= xb.getbits(sc) & m;
             }
             mant = v;
@@ -858,7 +859,8 @@ WVF_HD uint32_t decode_pcm_run(PcmState &s, const BlockDesc &d, Store &out, uint
 
     Fixup fx;
     fixup_init(fx, d);
-    fixup_init_exact_float(fx, d);
+    XFloat xf;
+    xfloat_init(xf, d);
 
     uint32_t status = 0;
     if (fstereo && fx.mode == 2) status |= ST_NONDET;  // fixup reads wvx bits for 2n values (n stale)
@@ -951,10 +953,10 @@ WVF_HD uint32_t decode_pcm_run(PcmState &s, const BlockDesc &d, Store &out, uint
                     if (exc_frame) *exc_frame = t;
                     return status | ST_EXCEPTION;
                 }
-            } else if (fx.mode == 4) {
+            } else if (xf.on) {
                 int bad = 0;
-                oL = fixup_xfloat(fx, xb, d.wvx_len, L, s.crc_x, bad);
-                oR = mono ? 0 : fixup_xfloat(fx, xb, d.wvx_len, R, s.crc_x, bad);
+                oL = fixup_xfloat(xf, xb, d.wvx_len, L, s.crc_x, bad);
+                oR = mono ? 0 : fixup_xfloat(xf, xb, d.wvx_len, R, s.crc_x, bad);
                 if (bad) s.xbad = true;
             } else {
                 oL = fixup_tail(fx, L);
@@ -1024,7 +1026,7 @@ WVF_HD uint32_t decode_pcm_run(PcmState &s, const BlockDesc &d, Store &out, uint
                         if (exc_frame) *exc_frame = f + j;
                         return status | ST_EXCEPTION;
                     }
-                } else if (fx.mode == 4) {
+                } else if (xf.on) {
                     z0 = 0;  // +0.0f; the wvx stream is not read past a mute
                 } else {
                     z0 = fixup_tail(fx, 0);
@@ -1054,7 +1056,7 @@ WVF_HD uint32_t decode_pcm_run(PcmState &s, const BlockDesc &d, Store &out, uint
         status |= ST_CRC_CHECKED;
         bool err = s.crc_garbage || s.crc != d.crc;
         if (!(flags & FLOAT_DATA) && (d.wvx_state & 1) && s.crc_x != d.crc_mvx) err = true;
-        if (fx.mode == 4 && (s.xbad || ((d.wvx_state & 1) && s.crc_x != d.crc_mvx))) err = true;
+        if (xf.on && (s.xbad || ((d.wvx_state & 1) && s.crc_x != d.crc_mvx))) err = true;
         if (err) status |= ST_CRC_ERROR;
     }
     return status;
@@ -1102,7 +1104,7 @@ WVF_HD void dsd_ptable_init(int32_t rate_i, int32_t *pt, uint32_t lane, uint32_t
 
 template <class Store>
 WVF_HD DsdResult decode_dsd_block(const BlockDesc &d, const uint8_t *blob, const uint8_t *tables, int32_t *ptable,
-                                  Store &out) {
+                                  Store &out, const int32_t *ptables_all = nullptr) {
     using namespace wvf;
     const uint32_t flags = d.flags;
     const bool mono = (flags & MONO_DATA) != 0;
@@ -1131,7 +1133,12 @@ WVF_HD DsdResult decode_dsd_block(const BlockDesc &d, const uint8_t *blob, const
         for (int i = 0; i < 4; i++) value = (value << 8) | data[bp++];
     }
     if (d.kind == KIND_DSD_HIGH) {
-        dsd_ptable_init(d.dsd_rate_i, ptable, 0, 1);
+        if (ptables_all) {  // the device's precomputed rows (g_dsd_ptables)
+            const int32_t *pt0 = ptables_all + (uint32_t)(d.dsd_rate_i & 255) * 256u;
+            for (int i = 0; i < 256; i++) ptable[i] = pt0[i];
+        } else {
+            dsd_ptable_init(d.dsd_rate_i, ptable, 0, 1);
+        }
         for (int c = 0; c < 2; c++) {
             F[c][0] = 0;
             F[c][1] = 0;
