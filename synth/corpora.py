@@ -85,6 +85,20 @@ def c4(nblocks: int = 1024, block: int = 22050):
     return _cached(f"c4-{nblocks}-{block}", make)["wv"].tobytes()
 
 
+def c4_wvc(nblocks: int = 1024, block: int = 22050):
+    """C4 with its .wvc correction file -> (wv, wvc, the same mantissas encoded lossless)."""
+    def make():
+        pcm = c2_pcm(nblocks, block, seed0=0xC4)
+        mant = S.float_mantissas(pcm.astype(np.float32) / 32768.0)
+        common = dict(terms=S.TERMS_DEFAULT, bytes_per_sample=4, float_data=True, block_samples=block)
+        wv, wvc = S.encode_pcm_wvc(mant, S.EncParams(hybrid_bitrate=True, bitrate_x256=896, config_flags=0x8 | 0x80,
+                                                     **common))
+        lossless = S.encode_pcm(mant, S.EncParams(**common))
+        return {k: np.frombuffer(v, dtype=np.uint8) for k, v in (("wv", wv), ("wvc", wvc), ("ll", lossless))}
+    d = _cached(f"c4wvc-{nblocks}-{block}", make)
+    return d["wv"].tobytes(), d["wvc"].tobytes(), d["ll"].tobytes()
+
+
 def c1(seconds: float = 20.0):
     frames = int(44100 * seconds)
     def make():

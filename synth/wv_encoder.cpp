@@ -1138,20 +1138,29 @@ struct PcmEncoder {
                     int32_t rL = we.word(tL);
                     int32_t rR = we.word(tR);
                     int32_t yL = rL, yR = rR;
+                    // .wvc: the exact-minus-lossy difference of each channel through the
+                    // passes; terms -1/-2 predict from the other channel's output of the
+                    // same pass, which the inverse above took exact
+                    int32_t dL = sub32(tL, rL), dR = sub32(tR, rR);
                     for (int d = 0; d < n; d++) {
                         int32_t oL, oR;
+                        const int32_t wA0 = passes[d].wA, wB0 = passes[d].wB;
                         pass_fwd_stereo(passes[d], yL, yR, oL, oR);
+                        if (passes[d].term == -1)
+                            dR = add32(dR, sub32(apply_weight(wB0, add32(oL, dL)), apply_weight(wB0, oL)));
+                        else if (passes[d].term == -2)
+                            dL = add32(dL, sub32(apply_weight(wA0, add32(oR, dR)), apply_weight(wA0, oR)));
                         yL = oL;
                         yR = oR;
                     }
                     if (P.wvc) {
-                        int32_t eL = add32(yL, sub32(tL, rL)), eR = add32(yR, sub32(tR, rR));
+                        int32_t eL = add32(yL, dL), eR = add32(yR, dR);
                         if (P.joint_stereo) {
                             eR = sub32(eR, eL >> 1);
                             eL = add32(eL, eR);
                         }
                         if (eL != L || eR != R)
-                            throw std::runtime_error("wvc: exact reconstruction mismatch (stereo terms -1/-2?)");
+                            throw std::runtime_error("wvc: exact reconstruction mismatch");
                         crc_exact = add32(mul32(add32(mul32(crc_exact, 3), eL), 3), eR);
                         uint32_t ae = eL < 0 ? (uint32_t)(-(int64_t)eL) : (uint32_t)eL;
                         uint32_t be = eR < 0 ? (uint32_t)(-(int64_t)eR) : (uint32_t)eR;
@@ -1515,9 +1524,6 @@ int64_t wvenc_encode_pcm_wvc(const int32_t *samples, int64_t frames, const wvenc
         if (p->wvx || p->int32_zeros || p->int32_sent_bits || p->int32_ones || p->int32_dups || p->sticky_passes)
             throw std::runtime_error("wvc: plain PCM or float only");
         if (p->float_exact && !p->float_data) throw std::runtime_error("float_exact: float_data");
-        for (int e = 0; e < p->num_terms; e++)
-            if (p->terms[e] == -1 || p->terms[e] == -2)
-                throw std::runtime_error("wvc: terms -1/-2 read the other channel's current output");
         PcmEncoder enc(*p);
         std::vector<uint8_t> f = enc.encode(samples, frames);
         *wvc_n = (int64_t)enc.wvc_file.size();

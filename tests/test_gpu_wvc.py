@@ -27,3 +27,22 @@ def test_gpu_wvc_roundtrip(gpu_batch_cls, name, wv, wvc, exact, chunk):
     assert rj.crc_errors == ref.crc_errors
     np.testing.assert_array_equal(out[oj: oj + ref.samples.size], ref.samples, err_msg=name)
     b.close()
+
+
+def test_gpu_wvc_c4_corpus():
+    """C4's own corpus layout (float32, hybrid + bitrate, default terms {18,18,2,3,-2},
+    22,050-frame blocks) with its .wvc: the exact decode equals the oracle's decode of
+    the same mantissas encoded losslessly, on every block."""
+    from synth import corpora
+    from wavpackdecoder_amd.api import DecodeBatch
+    wv, wvc, lossless = corpora.c4_wvc(nblocks=24)
+    ref = O.decode_file(lossless)
+    assert ref.crc_errors == 0
+    b = DecodeBatch(4096)
+    i = b.add_file(wv, wvc=wvc)
+    b.decode()
+    out = b.download()
+    r = b.result(i)
+    assert r.crc_errors == 0 and r.exception == 0 and r.frames == 24 * 22050
+    np.testing.assert_array_equal(out[: ref.samples.size], ref.samples)
+    b.close()

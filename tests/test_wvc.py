@@ -6,7 +6,8 @@ decode here is exact: every word the error limit left inexact reads its exact
 magnitude from the correction stream (WavPack 4 get_word: read_code(wvcbits,
 high - low) + low), and the difference to the lossy residual is added to the
 passes' output (the passes keep the lossy history the encoder decorrelated
-against).  No reference behaviour exists, so parity is unpinned and pinned
+against); stereo terms -1/-2, which predict one channel from the other's output
+of the same pass, predict the exact value from the other channel's exact output.  No reference behaviour exists, so parity is unpinned and pinned
 instead by the round trip to the encoder's input PCM, plus the .wvc headers'
 CRC of the exact output; the .wv alone still decodes exactly as the oracle.
 
@@ -37,7 +38,17 @@ def wvc_cases():
                                        bitrate_x256=1280), 4096),
             ("mono16_high_br3", m, dict(nch=1, terms=S.TERMS_MONO_HIGH, hybrid_bitrate=True, bitrate_x256=768), 1000),
             ("nojoint_br2", x, dict(terms=S.TERMS_FAST, joint_stereo=False, hybrid_bitrate=True, bitrate_x256=512),
-             4096)):
+             4096),
+            # stereo terms -1/-2: a pass predicts one channel from the other's output of
+            # the same pass (the exact value from the exact output: pass_stereo_wvc)
+            ("stereo16_default_br3", x, dict(terms=S.TERMS_DEFAULT, hybrid_bitrate=True, bitrate_x256=768), 4096),
+            ("stereo16_neg1_br2_chunk13", x, dict(terms=[18, -1, 2, 17, -1], hybrid_bitrate=True, bitrate_x256=512),
+             13),
+            ("stereo16_neg12_nobitrate", x, dict(terms=[-2, 18, -1, 3, -3, -2, 2], bitrate_x256=1024), 4096),
+            ("stereo24_high_br4", x24, dict(terms=S.TERMS_HIGH, bytes_per_sample=3, hybrid_bitrate=True,
+                                            bitrate_x256=1024), 4096),
+            ("nojoint_default_balance", x, dict(terms=S.TERMS_DEFAULT, joint_stereo=False, hybrid_bitrate=True,
+                                                hybrid_balance=True, bitrate_x256=640), 4096)):
         p = S.EncParams(block_samples=6000, **kw)
         wv, wvc = S.encode_pcm_wvc(pcm, p)
         out.append((name, wv, wvc, pcm.reshape(-1), chunk))
@@ -48,6 +59,12 @@ def wvc_cases():
     lossless = S.encode_pcm(mant, S.EncParams(terms=S.TERMS_FAST, bytes_per_sample=4, float_data=True,
                                               block_samples=5000))
     out.append(("float_hybrid_br3", wv, wvc, E.decode(lossless)[1], 4096))
+    # C4's own layout: float hybrid + bitrate with the default terms (-2 included)
+    wv, wvc = S.encode_pcm_wvc(mant, S.EncParams(terms=S.TERMS_DEFAULT, bytes_per_sample=4, float_data=True,
+                                                 hybrid_bitrate=True, bitrate_x256=896, block_samples=5000))
+    lossless = S.encode_pcm(mant, S.EncParams(terms=S.TERMS_DEFAULT, bytes_per_sample=4, float_data=True,
+                                              block_samples=5000))
+    out.append(("float_hybrid_default_br3", wv, wvc, E.decode(lossless)[1], 4096))
     return out
 
 
@@ -76,9 +93,8 @@ def test_wvc_wrong_correction_file_fails_crc():
     assert crc_errors > 0 or n < 0
 
 
-def test_wvc_encoder_rejects_current_cross_terms():
-    """stereo terms -1/-2 read the other channel's current output: not exact with a
-    correction added after the passes, so the generator refuses them"""
-    x = S.audio_like(4000, 2, 16, seed=74)
-    with pytest.raises(RuntimeError):
-        S.encode_pcm_wvc(x, S.EncParams(terms=S.TERMS_DEFAULT, hybrid_bitrate=True, bitrate_x256=768))
+def test_wvc_cases_cover_cross_terms():
+    """the correction rule for stereo terms -1/-2 (pass_stereo_wvc) is exercised"""
+    names = [c[0] for c in CASES]
+    assert "stereo16_default_br3" in names and "stereo16_neg1_br2_chunk13" in names
+    assert "float_hybrid_default_br3" in names

@@ -22,6 +22,8 @@ WVG_ST_UNSUPPORTED = 0x20
 WVG_ST_DSD_MUTE = 0x40
 WVG_ST_NONDET = 0x80
 WVG_ST_TIMEOUT = 0x100
+WVG_ERR_ARG = -2
+WVG_ERR_OPEN = -3
 WVG_ERR_TIMEOUT = -5
 
 

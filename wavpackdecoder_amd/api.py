@@ -88,6 +88,11 @@ class DecodeBatch:
         else:
             idx = self._L.wvg_batch_add_file_at(self._b, data, len(data), int(open_flags), int(start_sample),
                                                 ctypes.byref(info))
+        # the C side reserves a file slot on success and on WVG_ERR_OPEN (an input that
+        # does not open); any other negative code reserved nothing, so infos[i] must
+        # not grow either (it mirrors the C file index i)
+        if idx < 0 and idx != _L.WVG_ERR_OPEN:
+            self._check(idx)
         self.infos.append(info)
         self._uploaded = False
         return idx

@@ -49,6 +49,7 @@ using namespace wvg;
 // Every batch owns its streams, so batches of one context (or of several host
 // threads) run concurrently on the device; nothing synchronises the whole device.
 constexpr int kSide = kMaxTermSets + 3;  // term sets, generic PCM, DSD, DSD mode 1
+constexpr size_t kTimingPending = 64;  // timing pairs left pending before the oldest is folded
 
 struct wvg_ctx {
     int device = 0;
@@ -110,7 +111,10 @@ struct wvg_batch {
     hipEvent_t fork = nullptr, join[kSide] = {nullptr};
     hipEvent_t done = nullptr;             // end of the last decode/format, on whatever stream it ran
     bool timing = false;                   // wvg_batch_set_timing: an event pair around every decode
-    std::vector<hipEvent_t> tev;
+    std::vector<hipEvent_t> tev;           // pending (start, end) pairs, folded into t_sum/t_cnt
+    std::vector<hipEvent_t> tfree;         // event objects of folded pairs, reused
+    double t_sum = 0;
+    int t_cnt = 0;
     // device buffers are kept across uploads and only grown (capacities in bytes)
     size_t cap_blob = 0, cap_descs = 0, cap_items = 0, cap_jobs = 0, cap_tables = 0, cap_out = 0, cap_st = 0,
            cap_pcml = 0, cap_dsd = 0, cap_pcm = 0, cap_segs = 0, cap_ts[kMaxTermSets] = {0};
@@ -213,7 +217,9 @@ static void free_streams(wvg_batch *b) {
     if (b->done) hipEventDestroy(b->done);
     if (b->stream) hipStreamDestroy(b->stream);
     for (auto &e : b->tev) hipEventDestroy(e);
+    for (auto &e : b->tfree) hipEventDestroy(e);
     b->tev.clear();
+    b->tfree.clear();
 }
 
 wvg_batch *wvg_batch_new(wvg_ctx *c, int chunk_frames) {
@@ -294,10 +300,24 @@ static void free_dev(wvg_batch *b) {
     b->uploaded = b->formatted = b->segs_uploaded = false;
 }
 
+// Wait for everything that may still read or write the batch's device buffers:
+// its own stream, and the last decode/format, which may have run on a caller's
+// stream (`done` is recorded there).  The buffers are grow-only and reused, so
+// a reset/re-upload must not overwrite them under a running kernel.
+static hipError_t quiesce(wvg_batch *b) {
+    hipError_t e = hipSuccess;
+    if (b->done) e = hipEventSynchronize(b->done);
+    if (b->stream) {
+        hipError_t e2 = hipStreamSynchronize(b->stream);
+        if (e == hipSuccess) e = e2;
+    }
+    return e;
+}
+
 void wvg_batch_free(wvg_batch *b) {
     if (!b) return;
     hipSetDevice(b->ctx->device);
-    if (b->stream) hipStreamSynchronize(b->stream);
+    quiesce(b);
     free_dev(b);
     free_streams(b);
     delete b;
@@ -406,7 +426,8 @@ static int add_file(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open
 
 int wvg_batch_reset(wvg_batch *b) {
     if (!b) return WVG_ERR_ARG;
-    if (b->stream) hipStreamSynchronize(b->stream);  // nothing in flight reads the old contents
+    hipSetDevice(b->ctx->device);
+    quiesce(b);  // nothing in flight reads the old contents (on the batch's or a caller's stream)
     b->blob.resize(0);
     const bool defer = b->fo.defer_values;
     b->fo = FramingOutput();
@@ -725,7 +746,7 @@ int wvg_batch_upload(wvg_batch *b) {
     wvg_ctx *c = b->ctx;
     hipStream_t s = b->stream;
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(s));  // earlier work on these buffers
+    HIPCHK(c, quiesce(b));  // earlier work on these buffers, on the batch's or a caller's stream
     b->formatted = false;
     // the blob is followed by 64 B of 0xFF (the reader's past-end fill)
     const size_t blob_n = b->blob.size() + 64;
@@ -813,15 +834,43 @@ int wvg_batch_upload(wvg_batch *b) {
     return WVG_OK;
 }
 
+static hipError_t take_event(wvg_batch *b, hipEvent_t *e) {
+    if (!b->tfree.empty()) {
+        *e = b->tfree.back();
+        b->tfree.pop_back();
+        return hipSuccess;
+    }
+    return hipEventCreate(e);
+}
+
+// Fold the oldest `pairs` pending timing pairs into t_sum/t_cnt (waits for them).
+static hipError_t fold_timing(wvg_batch *b, int pairs) {
+    for (int i = 0; i < pairs; i++) {
+        float t = 0;
+        hipError_t e = hipEventSynchronize(b->tev[2 * i + 1]);
+        if (e == hipSuccess) e = hipEventElapsedTime(&t, b->tev[2 * i], b->tev[2 * i + 1]);
+        if (e != hipSuccess) return e;
+        b->t_sum += t;
+        b->t_cnt++;
+        b->tfree.push_back(b->tev[2 * i]);
+        b->tfree.push_back(b->tev[2 * i + 1]);
+    }
+    b->tev.erase(b->tev.begin(), b->tev.begin() + 2 * pairs);
+    return hipSuccess;
+}
+
 int wvg_batch_decode(wvg_batch *b, void *stream) {
     if (!b || !b->uploaded) return WVG_ERR_ARG;
     wvg_ctx *c = b->ctx;
     HIPCHK(c, hipSetDevice(c->device));  // side streams and events belong to the batch's device, whatever the calling thread
     hipStream_t s = stream ? (hipStream_t)stream : b->stream;
     if (b->timing) {
+        // a bounded number of pairs stays pending: the oldest is folded into the
+        // running sum (it finished long ago) and its events are reused
+        if (b->tev.size() >= 2 * kTimingPending) HIPCHK(c, fold_timing(b, 1));
         hipEvent_t e0, e1;
-        HIPCHK(c, hipEventCreate(&e0));
-        HIPCHK(c, hipEventCreate(&e1));
+        HIPCHK(c, take_event(b, &e0));
+        HIPCHK(c, take_event(b, &e1));
         b->tev.push_back(e0);
         b->tev.push_back(e1);
         HIPCHK(c, hipEventRecord(e0, s));
@@ -880,24 +929,20 @@ void *wvg_batch_stream(wvg_batch *b) { return b ? (void *)b->stream : nullptr; }
 
 int wvg_batch_set_timing(wvg_batch *b, int on) {
     if (!b) return WVG_ERR_ARG;
-    for (auto &e : b->tev) hipEventDestroy(e);
+    // pending pairs are dropped; their events are reused (re-recording an event is allowed)
+    b->tfree.insert(b->tfree.end(), b->tev.begin(), b->tev.end());
     b->tev.clear();
+    b->t_sum = 0;
+    b->t_cnt = 0;
     b->timing = on != 0;
     return WVG_OK;
 }
 
 int wvg_batch_timed(wvg_batch *b, float *avg_ms, int *count) {
     if (!b || !avg_ms || !count) return WVG_ERR_ARG;
-    const int n = (int)(b->tev.size() / 2);
-    double tot = 0;
-    for (int i = 0; i < n; i++) {
-        float t = 0;
-        HIPCHK(b->ctx, hipEventSynchronize(b->tev[2 * i + 1]));
-        HIPCHK(b->ctx, hipEventElapsedTime(&t, b->tev[2 * i], b->tev[2 * i + 1]));
-        tot += t;
-    }
-    *avg_ms = n ? (float)(tot / n) : 0.f;
-    *count = n;
+    HIPCHK(b->ctx, fold_timing(b, (int)(b->tev.size() / 2)));
+    *avg_ms = b->t_cnt ? (float)(b->t_sum / b->t_cnt) : 0.f;
+    *count = b->t_cnt;
     return WVG_OK;
 }
 

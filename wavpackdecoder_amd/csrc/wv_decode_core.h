@@ -511,6 +511,26 @@ WVF_HD void pass_stereo(PassState &p, uint32_t t, int32_t &L, int32_t &R, bool c
     }
 }
 
+// .wvc (beyond the reference): one stereo frame through one pass, carrying the
+// exact-minus-lossy differences cL/cR of the frame along.  The passes keep the
+// lossy history and weights (what the encoder decorrelated against); a pass
+// whose prediction reads only history moves both channels' exact values by the
+// same prediction, so the differences pass through.  Terms -1 and -2 predict
+// one channel from the OTHER channel's output of this same pass: the exact
+// value predicts from the other channel's exact output, with the same (lossy,
+// not yet updated) weight -- the difference changes by the two predictions'
+// difference.
+WVF_HD void pass_stereo_wvc(PassState &p, uint32_t t, int32_t &L, int32_t &R, int32_t &cL, int32_t &cR,
+                            bool cont = false) {
+    using namespace wvf;
+    const int32_t wA0 = p.wA, wB0 = p.wB;
+    pass_stereo(p, t, L, R, cont);
+    if (p.term == -1)  // R predicted from this pass's L output
+        cR = add32(cR, sub32(apply_weight(wB0, add32(L, cL)), apply_weight(wB0, L)));
+    else if (p.term == -2)  // L predicted from this pass's R output
+        cL = add32(cL, sub32(apply_weight(wA0, add32(R, cR)), apply_weight(wA0, R)));
+}
+
 // one mono value through one pass (UnpackUtils.cs:1156-1240)
 WVF_HD void pass_mono(PassState &p, uint32_t t, int32_t &X) {
     using namespace wvf;
@@ -921,9 +941,13 @@ WVF_HD uint32_t decode_pcm_run(PcmState &s, const BlockDesc &d, Store &out, uint
                 }
                 if (!crc_stop) s.crc = add32(mul32(s.crc, 3), L);
             } else {
-                for (int i = 0; i < nt; i++) pass_stereo(ps[i], t, L, R, n >= 16 && j >= 8);
-                L = add32(L, cL);  // .wvc: the exact values (the passes keep the lossy history)
-                R = add32(R, cR);
+                if (s.wvc) {  // .wvc: the exact values (pass_stereo_wvc)
+                    for (int i = 0; i < nt; i++) pass_stereo_wvc(ps[i], t, L, R, cL, cR, n >= 16 && j >= 8);
+                    L = add32(L, cL);
+                    R = add32(R, cR);
+                } else {
+                    for (int i = 0; i < nt; i++) pass_stereo(ps[i], t, L, R, n >= 16 && j >= 8);
+                }
                 if (joint) {
                     R = sub32(R, L >> 1);
                     L = add32(L, R);

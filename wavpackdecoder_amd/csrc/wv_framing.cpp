@@ -454,11 +454,15 @@ class Framer {
         }
         w.known_acc[0] = true;
         if (!mono) w.known_acc[1] = true;
+        // bitrate_delta: read per channel when bytes remain (WordsUtils.cs:164-178:
+        // a mono block writes only channel 0, channel 1 keeps its old value),
+        // otherwise both channels are zeroed (:183-184) -- so both become known
         if (bc < byte_length) {
             w.known_dlt[0] = true;
             if (!mono) w.known_dlt[1] = true;
-        } else
+        } else {
             w.known_dlt[0] = w.known_dlt[1] = true;
+        }
     }
     bool read_hybrid_profile(Md &m) {  // WordsUtils.cs:124-187
         bool mono = (wphdr.flags & MONO_DATA) != 0;

@@ -1601,12 +1601,16 @@ __device__ __forceinline__ void parse_loop(const BlockDesc &d, Reader &rd, Entro
         uint32_t base = k & ~63u;
         if ((k & 63) && err != DEC_TIMEOUT) {
             uint32_t spins = 0;
-            while (base + 64 - consumed > (uint32_t)RES_RING && ++spins < SPIN_LIMIT) {
+            while (base + 64 - consumed > (uint32_t)RES_RING) {
                 __builtin_amdgcn_s_sleep(2);
                 consumed = uni(lds_load_acq(&sh.consumed));
                 if (uni(lds_load_acq(&sh.stop))) return;
+                if (++spins > SPIN_LIMIT) break;
             }
-            sh.res[(base % RES_RING) + lane] = resv;
+            // no ring space: the slots still hold unread words, so report the
+            // timeout (as the main loop does) instead of overwriting them
+            if (base + 64 - consumed > (uint32_t)RES_RING) err = DEC_TIMEOUT;
+            else sh.res[(base % RES_RING) + lane] = resv;
         }
         lds_store_rel(&sh.produced, k);
         lds_store_rel(&sh.err, err);
