@@ -113,8 +113,8 @@ def cpu_rate(files):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("configs", nargs="*", default=["c1", "c3", "c4", "c5"])
-    ap.add_argument("--c3-blocks", type=int, default=1024)
-    ap.add_argument("--c3-copies", type=int, default=4)
+    ap.add_argument("--c3-blocks", type=int, default=4096)
+    ap.add_argument("--c3-copies", type=int, default=1)
     ap.add_argument("--c5-files", type=int, default=4000)
     ap.add_argument("--cpu-threads", type=int, default=0, help="also time the oracle on this many host threads")
     ap.add_argument("--inflight", type=int, default=1, help="also time this many copies of each batch in flight")
@@ -130,9 +130,8 @@ def main():
             pcm, data = corpora.c1()
             run("C1 WvDemo file 20 s 16-bit stereo default", [data], pcm, fmt=True)
         elif c == "c3":
-            # generating 4,096 distinct 44,100-frame blocks takes ~3 min on one core, so the
-            # batch is C3_COPIES files of c3_blocks distinct blocks each (every block is still
-            # decoded independently; the copies only share content)
+            # BASELINE config 3 at full size: 4,096 distinct 44,100-frame blocks (encoded on
+            # every host core; --c3-copies > 1 repeats a smaller set instead)
             pcm, data = corpora.c3(nblocks=a.c3_blocks, return_pcm=True)
             run(f"C3 {a.c3_copies} x {a.c3_blocks} x 44100 24-bit stereo high (16 terms)", [data] * a.c3_copies,
                 np.concatenate([pcm.reshape(-1)] * a.c3_copies))

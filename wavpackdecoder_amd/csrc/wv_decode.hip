@@ -586,6 +586,80 @@ __device__ __forceinline__ DsdResult dsd_simple_wave(const BlockDesc &d, const u
     return res;
 }
 
+// DsdUtils mode 0 (DsdUtils.cs:73-82): the payload bytes ARE the output
+// values, in order, and crc = 3 crc + v over them -- lane-parallel instead of a
+// serial byte loop.  Value i (of N = nframes x channels read) is handled by
+// lane i % 64, kDsdRawU values per lane per step (one byte load each, all in
+// flight together; each load and each store instruction covers 64 consecutive
+// values).  The CRC is a power-of-3 weighted sum: lane l keeps
+// acc_l = sum_j v(l + 64 j) 3^(64 (J-1-j)) by Horner (acc = acc 3^64 + v), so
+// with the values padded by zeros to Npad = 64 J
+//   sum_i 3^(Npad-1-i) v_i = sum_l 3^(63-l) acc_l,
+// the padding multiplies the true sum by 3^(Npad-N) (undone with 3's inverse
+// mod 2^32), and crc = 3^N (-1) + sum.  Same outputs, status bits and mute
+// chunk as dsd_simple_wave<WCH, false>: the only mute of mode 0 is the final
+// chunk's CRC test (DsdUtils.cs:99-101); wv_dsd_fill writes its 0x55.
+constexpr uint32_t kDsdRawU = 16;
+template <int WCH>
+__device__ __forceinline__ DsdResult dsd_raw_lanes(const BlockDesc &d, const uint8_t *blob, int32_t *out) {
+    const bool fstereo = (d.flags & wvf::FALSE_STEREO) != 0;
+    const uint32_t N = d.nframes * (uint32_t)WCH;  // values read (one byte each)
+    const uint32_t dlen = d.dsd_data_len;          // (init_dsd_block: == block_samples x channels)
+    const uint64_t skip = (uint64_t)d.pre_end * d.out_nch;  // a seek's discarded values
+    const uint8_t *src = blob + d.bits_off;
+    const uint32_t lane = threadIdx.x;
+    constexpr uint32_t C64 = 0x797EBD01u;  // 3^64 mod 2^32
+    uint32_t acc = 0;
+    const uint32_t steps = (N + 64u * kDsdRawU - 1u) / (64u * kDsdRawU);
+    for (uint32_t st = 0; st < steps; st++) {
+        const uint32_t base = st * 64u * kDsdRawU + lane;
+        uint32_t v[kDsdRawU];
+#pragma unroll
+        for (uint32_t u = 0; u < kDsdRawU; u++) {
+            const uint32_t i = base + 64u * u;
+            v[u] = (i < N && i < dlen) ? (uint32_t)src[i] : 0u;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kDsdRawU; u++) {
+            const uint32_t i = base + 64u * u;
+            acc = acc * C64 + v[u];
+            if (i < N) {
+                if (!fstereo) {
+                    if (i >= skip) out[i] = (int32_t)v[u];
+                } else {
+                    const uint64_t o = 2ull * i;
+                    if (o >= skip) out[o] = (int32_t)v[u];
+                    if (o + 1 >= skip) out[o + 1] = (int32_t)v[u];
+                }
+            }
+        }
+    }
+    uint32_t part = acc * w2::upow_u32(3u, 63u - lane);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) part += (uint32_t)__shfl_xor((int)part, o);
+    const uint32_t npad = steps * 64u * kDsdRawU;
+    const uint32_t sum = part * w2::upow_u32(0xAAAAAAABu, npad - N);  // 3 * 0xAAAAAAAB == 1 mod 2^32
+    const int32_t crc = (int32_t)(sum - w2::upow_u32(3u, N));
+    DsdResult res = {0, 0};
+    if (d.nframes == d.block_samples) {
+        res.status |= ST_CRC_CHECKED;
+        if (crc != d.crc) {
+            res.status |= ST_CRC_ERROR;
+            if (d.nframes) {  // the final call mutes: its index in the call schedule
+                uint32_t f = 0, n = d.first_chunk, ci = 0;
+                while (n && f + (n < d.nframes - f ? n : d.nframes - f) < d.nframes) {
+                    f += n;
+                    n = next_call_len(d, f);
+                    ci++;
+                }
+                res.status |= ST_DSD_MUTE;
+                res.mute_chunk = ci;
+            }
+        }
+    }
+    return res;
+}
+
 extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_wave(const BlockDesc *__restrict__ descs,
                                                                     const uint32_t *__restrict__ list,
                                                                     const uint8_t *__restrict__ blob,
@@ -611,8 +685,8 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_wave(const BlockD
         r = (d.flags & wvf::MONO_DATA) ? dsd_simple_wave<1, true>(d, blob, tables, st)
                                        : dsd_simple_wave<2, true>(d, blob, tables, st);
     else if (d.kind == KIND_DSD_RAW)
-        r = (d.flags & wvf::MONO_DATA) ? dsd_simple_wave<1, false>(d, blob, tables, st)
-                                       : dsd_simple_wave<2, false>(d, blob, tables, st);
+        r = (d.flags & wvf::MONO_DATA) ? dsd_raw_lanes<1>(d, blob, out + d.out_off)
+                                       : dsd_raw_lanes<2>(d, blob, out + d.out_off);
     else
         r = decode_dsd_block(d, blob, tables, pt_lds, st, g_dsd_ptables);
     if (lead) {
