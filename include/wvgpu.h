@@ -39,6 +39,7 @@ extern "C" {
 #define WVG_ERR_OPEN (-3)     /* WavpackOpenFileInput failed (info.error holds the message) */
 #define WVG_ERR_SPACE (-4)    /* caller buffer too small */
 #define WVG_ERR_TIMEOUT (-5)  /* a kernel's bounded wait ran out (a decoder bug, never a property of the stream) */
+#define WVG_ERR_EXCEPTION (-6) /* wvg_stream_*: the reference raises a C# exception in this call */
 
 /* per-block status bits (wvg_file_result.status_or) */
 #define WVG_ST_CRC_CHECKED 0x01u
@@ -173,6 +174,10 @@ void *wvg_batch_stream(wvg_batch *b);  /* the batch's own hipStream_t */
  * stream); wvg_batch_timed waits for them and returns the mean and the count. */
 int wvg_batch_set_timing(wvg_batch *b, int on);
 int wvg_batch_timed(wvg_batch *b, float *avg_ms, int *count);
+/* With timing on: for the last decode, the time from its start to the end of
+ * each launch group on its own stream, ms[g] for g = term set 0..7, 8 generic
+ * PCM, 9 DSD, 10 DSD mode 1 (-1: not launched); cap >= 11. */
+int wvg_batch_group_times(wvg_batch *b, float *ms, int cap);
 
 int64_t wvg_batch_out_ints(const wvg_batch *b);
 int32_t *wvg_batch_device_out(wvg_batch *b);      /* device pointer to the int32 output */
@@ -230,6 +235,31 @@ uint8_t *wvg_batch_host_pcm(wvg_batch *b);
  * synthesized RIFF/fmt/data headers, the PCM, the stored trailer) and its exit
  * code.  out == NULL queries the length only. */
 int wvg_batch_wav(wvg_batch *b, int file, uint8_t *out, int64_t cap, int64_t *wav_len, int32_t *exit_code);
+
+/* ---- Streaming WavpackUnpackSamples (WavPackUtils.cs:200-282) --------------
+ * One file opened like WavpackOpenFileInput (WavPackUtils.cs:36-120; NULL when
+ * it does not open -- info->error holds the message), then served call by call.
+ * The first wvg_stream_unpack decodes the file on the device, its calls
+ * scheduled at that call's `samples` (the reference's seams follow the caller's
+ * request size; a different size before any frame went out re-decodes, a later
+ * one is served from the first schedule and flagged).  Host memory holds the
+ * compressed file and two staged windows of `window_frames` frames (0: 262,144);
+ * the int32 output stays in HBM.  wvg_stream_unpack returns the frames written
+ * to `buffer` (samples x reduced channels ints), 0 at the end, or
+ * WVG_ERR_EXCEPTION on the call the reference throws in (the calls before it
+ * returned their frames).  wvg_stream_set_sample is SetSample
+ * (WavPackUtils.cs:509-594): 1, 0 (false) or WVG_ERR_EXCEPTION.
+ * wvg_stream_state: WavpackGetSampleIndex (:355-358), WavpackGetNumErrors
+ * (:363-366, counted as each block's last frame is handed out, :273-275),
+ * WavpackLossy (:371-374). */
+typedef struct wvg_stream wvg_stream;
+wvg_stream *wvg_stream_open(wvg_ctx *ctx, const uint8_t *file, size_t len, uint32_t open_flags, int64_t window_frames,
+                            wvg_file_info *info);
+int64_t wvg_stream_unpack(wvg_stream *s, int32_t *buffer, int64_t samples);
+int wvg_stream_set_sample(wvg_stream *s, int64_t sample);
+int wvg_stream_state(const wvg_stream *s, int64_t *sample_index, int64_t *crc_errors, int32_t *lossy,
+                     int32_t *schedule_changed);
+void wvg_stream_close(wvg_stream *s);
 
 #ifdef __cplusplus
 }

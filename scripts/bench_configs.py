@@ -38,6 +38,16 @@ def run(name, files, pcm=None, iters=5, fmt=False):
     b.decode()
     b.sync()
     ms = b.time(iters)
+    # per launch group: end time of each group's kernels from the decode's start
+    # (each group on its own stream), median of 3 single decodes
+    b.set_timing(True)
+    gts = []
+    for _ in range(3):
+        b.decode()
+        b.sync()
+        gts.append(b.group_times())
+    b.set_timing(False)
+    group_ms = {g: round(float(np.median([t[g] for t in gts])), 3) for g in gts[0]}
     out = b.download()
     crc = sum(b.result(i).crc_errors for i in range(len(files)) if b.infos[i].open_ok)
     ok = None
@@ -53,7 +63,7 @@ def run(name, files, pcm=None, iters=5, fmt=False):
     line = {"config": name, "files": len(files), "blocks": b.num_blocks, "frames": b.frames,
             "compressed_bytes": b.bytes_in, "kernel_ms": round(ms, 3),
             "Mframes_per_s": round(b.frames / ms / 1e3, 1), "crc_errors": int(crc),
-            "lossless_roundtrip": ok, "host_framing_s": round(t_frame, 3)}
+            "lossless_roundtrip": ok, "host_framing_s": round(t_frame, 3), "group_end_ms": group_ms}
     if INFLIGHT > 1:
         # the same batch as INFLIGHT copies on their own streams, decodes issued
         # round-robin (bench.py's --inflight): throughput with launches overlapping
@@ -84,6 +94,22 @@ def run(name, files, pcm=None, iters=5, fmt=False):
         line["cpu_baseline_Mframes_per_s"] = round(cpu_rate(files), 1)
         line["cpu_threads"] = CPU_THREADS
     print(json.dumps(line), flush=True)
+    b.close()
+
+
+def run_wvc(name, wv, wvc, iters=5):
+    """A hybrid file with its .wvc: device time of the exact decode."""
+    b = DecodeBatch(4096)
+    b.add_file(wv, wvc=wvc)
+    b.upload()
+    b.decode()
+    b.sync()
+    ms = b.time(iters)
+    b.download()
+    r = b.result(0)
+    print(json.dumps({"config": name, "files": 1, "blocks": b.num_blocks, "frames": b.frames,
+                      "compressed_bytes": b.bytes_in, "kernel_ms": round(ms, 3),
+                      "Mframes_per_s": round(b.frames / ms / 1e3, 1), "crc_errors": int(r.crc_errors)}), flush=True)
     b.close()
 
 
@@ -138,6 +164,9 @@ def main():
             del pcm, data
         elif c == "c4":
             run("C4 1024 x 22050 float32 hybrid+bitrate", [corpora.c4()])
+        elif c == "c4wvc":  # C4 with its .wvc correction files: the exact decode (generic kernel)
+            wv, wvc, _ = corpora.c4_wvc()
+            run_wvc("C4 1024 x 22050 float32 hybrid+bitrate + .wvc (exact)", wv, wvc)
         elif c == "c5":
             run(f"C5 mixed corpus, files 0..{a.c5_files - 1}", corpora.c5(a.c5_files))
         elif c.startswith("dsd"):  # dsd0 / dsd1 / dsd3: 64 stereo files of one 22,050-frame block in one mode

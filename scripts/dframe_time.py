@@ -17,7 +17,7 @@ def run(name, files, reps=5):
     res = {"workload": name, "files": len(files)}
     for mode in ("host", "device"):
         b = api.DecodeBatch(4096)
-        ts = []
+        ts, tf = [], []
         for r in range(reps + 1):
             b.reset()
             t = time.perf_counter()
@@ -25,8 +25,11 @@ def run(name, files, reps=5):
                 b.add_files(files, threads=16)
             else:
                 b.add_files_device(files)
+            t1 = time.perf_counter()
             b.upload()
             ts.append(time.perf_counter() - t)
+            tf.append(t1 - t)
+        res[f"{mode}_add_ms"] = round(sorted(tf[1:])[len(tf[1:]) // 2] * 1e3, 3)
         b.decode()
         b.sync()
         if mode == "device":

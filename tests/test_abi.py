@@ -47,7 +47,7 @@ def test_library_exports_every_declared_symbol(lib):
 def test_binding_loads_and_types(lib):
     L = _lib.lib()  # loads and sets argtypes; no device call
     for name in _lib.EXPORTED:
-        assert getattr(L, name).restype is not None or name in ("wvg_close", "wvg_batch_free")
+        assert getattr(L, name).restype is not None or name in ("wvg_close", "wvg_batch_free", "wvg_stream_close")
 
 
 def _fmt(fn, src, samcnt, bps, cap, offset=0, dsd=0):

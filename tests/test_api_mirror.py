@@ -39,9 +39,9 @@ def _oracle_calls(data, samples, seek=None):
     return calls
 
 
-def _mirror_calls(data, samples, seek=None):
+def _mirror_calls(data, samples, seek=None, window=0):
     from wavpackdecoder_amd import api
-    wpc = api.WavpackOpenFileInput(data)
+    wpc = api.WavpackOpenFileInput(data, window_frames=window)
     calls = []
     if seek is not None:
         calls.append(("seek", int(api.SetSample(wpc, seek)), api.WavpackGetSampleIndex(wpc),
@@ -57,6 +57,7 @@ def _mirror_calls(data, samples, seek=None):
         calls.append((int(n), buf[: n * nch].copy(), api.WavpackGetSampleIndex(wpc), api.WavpackGetNumErrors(wpc)))
         if n == 0:
             break
+    wpc.close()
     return calls
 
 
@@ -94,3 +95,18 @@ def test_seek_then_calls_match_oracle():
     for name, data in _files()[:4] + _files()[-3:]:
         for target in (0, 5000, 12345):
             _same(_oracle_calls(data, 4096, seek=target), _mirror_calls(data, 4096, seek=target), f"{name}@{target}")
+
+
+@pytest.mark.parametrize("window", [1, 999, 4096, 10007])
+def test_stream_windows_match_oracle(window):
+    """The stream serves the calls from staged windows of `window` frames (wvg_stream,
+    host memory bounded by two windows): window edges inside calls, at call edges,
+    a window of one frame, over C1 (20 s, 40 blocks), a corrupted file and a file
+    whose reference decode throws."""
+    from synth import corpora
+    cases = [("config1", corpora.c1()[1])] + [f for f in _files() if f[0] in ("corrupt#3", "int32_wvx_short")]
+    for name, data in cases:
+        if window == 1 and name == "config1":
+            continue  # 882,000 one-frame DMAs: covered by the shorter files
+        for samples in (4096, 777):
+            _same(_oracle_calls(data, samples), _mirror_calls(data, samples, window=window), f"{name}/{window}/{samples}")

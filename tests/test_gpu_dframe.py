@@ -167,3 +167,29 @@ def test_parallel_header_walk_c2(gpu_batch_cls):
     out = b.download()
     np.testing.assert_array_equal(out[: pcm.size], pcm.reshape(-1))
     b.close()
+
+
+def test_device_framing_twice_without_reset(gpu_batch_cls):
+    """Files added after an upload (device- and host-framed, no reset): the earlier
+    device-framed descriptors, kept on the device, survive the second device pass."""
+    from synth import corpora
+    first = corpora.c5(30)
+    second = corpora.c5(20, start=30)
+    extra = [c[1] for c in V.pcm_cases()[:3]]
+    b = gpu_batch_cls(4096)
+    b.add_files_device(first)
+    b.upload()
+    b.add_files(extra)
+    b.add_files_device(second)
+    b.decode()
+    out = b.download()
+    files = first + extra + second
+    assert b.framing_stats()[0] >= 30
+    for k, f in enumerate(files):
+        ref = O.decode_file(f, chunk=4096)
+        info = b.infos[k]
+        r = b.result(k)
+        assert r.exception == 0 and r.frames == ref.frames and r.crc_errors == ref.crc_errors, k
+        np.testing.assert_array_equal(out[info.out_offset: info.out_offset + ref.frames * ref.nch], ref.samples,
+                                      err_msg=str(k))
+    b.close()

@@ -25,6 +25,7 @@ WVG_ST_TIMEOUT = 0x100
 WVG_ERR_ARG = -2
 WVG_ERR_OPEN = -3
 WVG_ERR_TIMEOUT = -5
+WVG_ERR_EXCEPTION = -6
 
 
 class WvgFileInfo(ctypes.Structure):
@@ -92,6 +93,7 @@ def lib():
         "wvg_batch_stream": (vp, [vp]),
         "wvg_batch_set_timing": (i32, [vp, i32]),
         "wvg_batch_timed": (i32, [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]),
+        "wvg_batch_group_times": (i32, [vp, vp, i32]),
         "wvg_batch_out_ints": (i64, [vp]),
         "wvg_batch_device_out": (vp, [vp]),
         "wvg_batch_num_blocks": (i64, [vp]),
@@ -114,6 +116,12 @@ def lib():
         "wvg_batch_download_pcm": (i32, [vp, vp, i64]),
         "wvg_batch_host_pcm": (vp, [vp]),
         "wvg_batch_wav": (i32, [vp, i32, vp, i64, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32)]),
+        "wvg_stream_open": (vp, [vp, ctypes.c_char_p, ctypes.c_size_t, u32, i64, ctypes.POINTER(WvgFileInfo)]),
+        "wvg_stream_unpack": (i64, [vp, vp, i64]),
+        "wvg_stream_set_sample": (i32, [vp, i64]),
+        "wvg_stream_state": (i32, [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
+                                   ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
+        "wvg_stream_close": (None, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -127,8 +135,9 @@ EXPORTED = ("wvg_open", "wvg_close", "wvg_last_error", "wvg_batch_new", "wvg_bat
             "wvg_batch_add_file_at", "wvg_batch_add_files", "wvg_batch_add_files_device", "wvg_batch_file_info", "wvg_batch_add_file_wvc",
             "wvg_batch_framing_stats",
             "wvg_batch_upload", "wvg_batch_reset", "wvg_batch_decode", "wvg_batch_sync", "wvg_batch_stream", "wvg_batch_set_timing",
-            "wvg_batch_timed", "wvg_batch_out_ints", "wvg_batch_device_out",
+            "wvg_batch_timed", "wvg_batch_group_times", "wvg_batch_out_ints", "wvg_batch_device_out",
             "wvg_batch_num_blocks", "wvg_batch_bytes_in", "wvg_batch_frames", "wvg_batch_download", "wvg_batch_host_out",
             "wvg_batch_file_result", "wvg_batch_block_status", "wvg_batch_file_blocks", "wvg_batch_time", "wvg_decode_file",
             "wvg_probe_file", "wvg_format_samples", "wvg_batch_format", "wvg_batch_pcm_bytes", "wvg_batch_pcm_offset",
-            "wvg_batch_device_pcm", "wvg_batch_download_pcm", "wvg_batch_host_pcm", "wvg_batch_wav")
+            "wvg_batch_device_pcm", "wvg_batch_download_pcm", "wvg_batch_host_pcm", "wvg_batch_wav",
+            "wvg_stream_open", "wvg_stream_unpack", "wvg_stream_set_sample", "wvg_stream_state", "wvg_stream_close")

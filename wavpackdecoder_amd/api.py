@@ -171,6 +171,16 @@ class DecodeBatch:
         self._check(self._L.wvg_batch_timed(self._b, ctypes.byref(ms), ctypes.byref(n)))
         return float(ms.value), int(n.value)
 
+    def group_times(self):
+        """With timing on: {group: ms from the last decode's start to the group's end}
+        (groups: 'ts0'..'ts7' term sets, 'pcm' generic, 'dsd', 'dsd1')."""
+        ms = (ctypes.c_float * 11)()
+        rc = self._L.wvg_batch_group_times(self._b, ms, 11)
+        if rc < 0:
+            self._check(rc)
+        names = [f"ts{i}" for i in range(8)] + ["pcm", "dsd", "dsd1"]
+        return {n: round(float(v), 3) for n, v in zip(names, ms) if v >= 0}
+
     def time(self, iters: int) -> float:
         ms = ctypes.c_float()
         self._check(self._L.wvg_batch_time(self._b, int(iters), ctypes.byref(ms)))
@@ -280,63 +290,54 @@ class DecodeBatch:
 
 
 class WavpackContext:
-    """Opaque context (WavpackContext.cs:13-35)."""
+    """Opaque context (WavpackContext.cs:13-35) over a wvg_stream: the file is decoded
+    on the device by the first WavpackUnpackSamples call and served a window at a
+    time, so host memory holds the compressed file and two windows, not the output."""
 
-    def __init__(self, data: bytes, open_flags: int):
+    def __init__(self, data: bytes, open_flags: int, window_frames: int = 0):
         self._data = data
         self._flags = open_flags
+        self._window = int(window_frames)
         self._info = _L.WvgFileInfo()
-        self._decoded = None
-        self._result = None
-        self._pos = 0            # frames handed out since the decode's start
-        self._limit = 0          # frames the calls return before the end (or before the throwing call)
-        self._throws = False     # the call starting at _limit raises
-        self._block_end = None   # per block: frames handed out when its last frame is unpacked
-        self._block_err = None   # per block: check_crc_error verdict
-        self._errors_before = 0  # crc_errors of calls made before a SetSample
-        self._index0 = 0         # stream.sample_index when the decode's first call starts
-        self._chunk = None
-        self._seek = None  # SetSample target, applied when the file is decoded
-        self.schedule_changed = False
+        self._s = None
         self.error_message = None
 
-    def _decode(self, chunk: int):
-        b = DecodeBatch(chunk)
+    def _stream(self):
+        if self._s is None:
+            self._s = _L.lib().wvg_stream_open(_context(), self._data, len(self._data), int(self._flags),
+                                               self._window, ctypes.byref(self._info))
+            if not self._s:
+                raise RuntimeError("wvg_stream_open failed: " + _L.lib().wvg_last_error(_context()).decode())
+        return self._s
+
+    def _state(self):
+        idx, err = ctypes.c_int64(), ctypes.c_int64()
+        lossy, changed = ctypes.c_int32(), ctypes.c_int32()
+        _L.lib().wvg_stream_state(self._stream(), ctypes.byref(idx), ctypes.byref(err), ctypes.byref(lossy),
+                                  ctypes.byref(changed))
+        return int(idx.value), int(err.value), bool(lossy.value), bool(changed.value)
+
+    @property
+    def schedule_changed(self) -> bool:
+        return self._state()[3] if self._s else False
+
+    def close(self):
+        if self._s:
+            _L.lib().wvg_stream_close(self._s)
+            self._s = None
+
+    def __del__(self):
         try:
-            idx = b.add_file(self._data, self._flags, self._seek)
-            if idx < 0:
-                raise RuntimeError("file cannot be opened: " + self._info.error.decode())
-            b.decode()
-            out = b.download()
-            res = b.result(idx)
-            info = b.infos[idx]
-            ends, sts = b.file_blocks(idx)
-        finally:
-            b.close()
-        nch = max(int(info.reduced_channels), 1)
-        self._result = res
-        self._throws = bool(res.exception)
-        self._limit = int(res.exception_frame) if res.exception else int(info.out_frames)
-        lo = int(info.out_offset)
-        self._decoded = out[lo: lo + self._limit * nch].reshape(-1, nch)
-        self._block_end = ends
-        self._block_err = (sts & _L.WVG_ST_CRC_ERROR) != 0
-        self._index0 = int(info.sample_index0)
-        self._chunk = chunk
-        self._pos = 0
-
-    def _crc_errors(self) -> int:
-        if self._block_end is None:
-            return self._errors_before
-        done = self._block_end <= self._pos
-        return self._errors_before + int(np.count_nonzero(self._block_err & done))
+            self.close()
+        except Exception:
+            pass
 
 
-def WavpackOpenFileInput(reader, flags: int = 0) -> WavpackContext:
+def WavpackOpenFileInput(reader, flags: int = 0, window_frames: int = 0) -> WavpackContext:
     """WavPackUtils.cs:36-120.  `reader` is bytes or a binary file object."""
     data = reader if isinstance(reader, (bytes, bytearray, memoryview)) else reader.read()
     data = bytes(data)
-    wpc = WavpackContext(data, flags)
+    wpc = WavpackContext(data, flags, window_frames)
     L = _L.lib()
     rc = L.wvg_probe_file(data, len(data), int(flags), SAMPLE_BUFFER_SIZE, ctypes.byref(wpc._info))  # host only
     if rc < 0 or not wpc._info.open_ok:
@@ -348,54 +349,34 @@ def WavpackUnpackSamples(wpc: WavpackContext, buffer: np.ndarray, samples: int) 
     """WavPackUtils.cs:200-282: fill `buffer` (int32, >= samples * reduced channels)."""
     if wpc.error_message:
         return 0
-    if wpc._decoded is None or (int(samples) != wpc._chunk and wpc._pos == 0):
-        wpc._decode(int(samples))  # (re)decode scheduled at this request size: nothing handed out yet
-    elif int(samples) != wpc._chunk:
-        wpc.schedule_changed = True
-    if wpc._pos >= wpc._limit:
-        if wpc._throws:
-            raise WavpackException("the reference decoder raises an exception in this call")
-        return 0
-    n = min(int(samples), wpc._limit - wpc._pos)
-    if n <= 0:
-        return 0
-    nch = wpc._decoded.shape[1]
-    buffer[: n * nch] = wpc._decoded[wpc._pos:wpc._pos + n].reshape(-1)
-    wpc._pos += n
-    return n
+    nch = max(int(wpc._info.reduced_channels), 1)
+    if buffer.dtype != np.int32 or not buffer.flags.c_contiguous or buffer.size < int(samples) * nch:
+        raise ValueError("buffer: contiguous int32 of samples x reduced channels")
+    n = _L.lib().wvg_stream_unpack(wpc._stream(), buffer.ctypes.data, int(samples))
+    if n == _L.WVG_ERR_EXCEPTION:
+        raise WavpackException("the reference decoder raises an exception in this call")
+    if n == _L.WVG_ERR_TIMEOUT:
+        raise DecoderTimeout(_L.lib().wvg_last_error(_context()).decode())
+    if n < 0:
+        raise RuntimeError(f"libwvgpu error {n}: {_L.lib().wvg_last_error(_context()).decode()}")
+    return int(n)
 
 
 def SetSample(wpc: WavpackContext, sample: int) -> bool:
-    """WavPackUtils.cs:509-594.  The decode happens on the next WavpackUnpackSamples
-    call, from the block the reference's search lands on; the result is the C#
-    return value.  (After samples were already handed out, the block search of
-    the reference starts from the current block; for well-formed files it ends
-    on the same block, which is what this mirror decodes from.)"""
+    """WavPackUtils.cs:509-594.  The block search runs on the host framing; the file
+    is then decoded from the block the reference's search lands on (its discard
+    calls included), and the result is the C# return value.  (After samples were
+    already handed out, the block search of the reference starts from the current
+    block; for well-formed files it ends on the same block, which is what this
+    mirror decodes from.)"""
     if wpc.error_message:
         return False
-    # the block search runs in the host framing (no device work until the decode)
-    b = DecodeBatch(SAMPLE_BUFFER_SIZE)
-    try:
-        idx = b.add_file(wpc._data, wpc._flags, int(sample))
-        if idx < 0:
-            return False
-        info = b.infos[idx]
-    finally:
-        b.close()
-    if info.seek_result < 0:
+    rc = _L.lib().wvg_stream_set_sample(wpc._stream(), int(sample))
+    if rc == _L.WVG_ERR_EXCEPTION:
         raise WavpackException("the reference's SetSample raises an exception on this file")
-    if info.seek_result == 1:
-        wpc._errors_before = wpc._crc_errors()
-        wpc._seek = int(sample)
-        wpc._decoded = None
-        wpc._block_end = wpc._block_err = None
-        wpc._pos = 0
-        wpc._limit = 0
-        wpc._index0 = int(sample)
-        wpc._result = None
-        # decode now: the discard calls' block ends count towards GetNumErrors at once
-        wpc._decode(wpc._chunk or SAMPLE_BUFFER_SIZE)
-    return info.seek_result == 1
+    if rc < 0:
+        raise RuntimeError(f"libwvgpu error {rc}: {_L.lib().wvg_last_error(_context()).decode()}")
+    return rc == 1
 
 
 def SetTime(wpc: WavpackContext, milliseconds: int) -> bool:
@@ -442,21 +423,23 @@ def WavpackGetNumSamples(wpc, native: bool = False) -> int:
 
 def WavpackGetSampleIndex(wpc) -> int:
     """stream.sample_index (WavPackUtils.cs:355-358): where the next call starts."""
-    if wpc._decoded is None and wpc._seek is None:
+    if wpc.error_message:
         return int(wpc._info.sample_index0)
-    return wpc._index0 + wpc._pos
+    return wpc._state()[0]
 
 
 def WavpackGetNumErrors(wpc) -> int:
     """crc_errors: blocks whose last frame a call has unpacked and whose check failed
     (WavPackUtils.cs:273-275), SetSample's discard calls included."""
-    return wpc._crc_errors()
+    if wpc.error_message:
+        return 0
+    return wpc._state()[1]
 
 
 def WavpackLossy(wpc) -> bool:
-    if wpc._result is not None:
-        return bool(wpc._result.lossy)
-    return bool(wpc._info.lossy)
+    if wpc.error_message:
+        return bool(wpc._info.lossy)
+    return wpc._state()[2]
 
 
 # wvg_file_info carries the getters' results (wv_api.cpp fill_info applies

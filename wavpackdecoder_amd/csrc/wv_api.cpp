@@ -5,6 +5,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstddef>
+#include <chrono>
+#include <cstdio>
 #include <string>
 #include <thread>
 #include <vector>
@@ -49,6 +52,12 @@ using namespace wvg;
 // Every batch owns its streams, so batches of one context (or of several host
 // threads) run concurrently on the device; nothing synchronises the whole device.
 constexpr int kSide = kMaxTermSets + 3;  // term sets, generic PCM, DSD, DSD mode 1
+// The part of a device-framed descriptor the host reads (kind, flags, frames, the
+// call schedule, status, terms): everything up to and including term[].  The rest
+// (weights, histories, DSD, seek, sticky, .wvc, exact float) is zero or unused on
+// the host for the files the device framer accepts.
+constexpr size_t kDescHead = offsetof(BlockDesc, term) + sizeof(((BlockDesc *)nullptr)->term);
+constexpr int SAMPLE_BUFFER_SIZE = 4096;  // Defines.cs:18, the request size WvDemo uses
 constexpr size_t kTimingPending = 64;  // timing pairs left pending before the oldest is folded
 
 struct wvg_ctx {
@@ -113,6 +122,11 @@ struct wvg_batch {
     bool timing = false;                   // wvg_batch_set_timing: an event pair around every decode
     std::vector<hipEvent_t> tev;           // pending (start, end) pairs, folded into t_sum/t_cnt
     std::vector<hipEvent_t> tfree;         // event objects of folded pairs, reused
+    // timing on: the end of each launch group of the last decode, on its own
+    // stream (wvg_batch_group_times), against that decode's start event
+    hipEvent_t gev[kSide] = {nullptr};
+    hipEvent_t gstart = nullptr;
+    uint32_t gmask = 0;                    // groups the last timed decode launched
     double t_sum = 0;
     int t_cnt = 0;
     // device buffers are kept across uploads and only grown (capacities in bytes)
@@ -166,6 +180,13 @@ struct wvg_batch {
     int64_t rank_min = 256 * 1024;  // files from this size on take the parallel header walk (WVG_DFRAME_RANK_MIN)
     BlockDesc *d_ddescs = nullptr;
     DBlock *d_drecs = nullptr;
+    // descriptors the device framing left in d_ddescs: descriptors [dst, dst + n)
+    // of the batch are d_ddescs[src, src + n) (the host keeps only their head,
+    // kDescHead bytes); the upload copies them into d_descs on the device
+    struct DevRun {
+        size_t dst, src, n;
+    };
+    std::vector<DevRun> dev_runs;
     size_t cap_dfiles = 0, cap_slots = 0, cap_blkf = 0, cap_blkk = 0, cap_ddescs = 0, cap_drecs = 0;
 };
 
@@ -220,6 +241,8 @@ static void free_streams(wvg_batch *b) {
     for (auto &e : b->tfree) hipEventDestroy(e);
     b->tev.clear();
     b->tfree.clear();
+    for (auto &e : b->gev)
+        if (e) hipEventDestroy(e);
 }
 
 wvg_batch *wvg_batch_new(wvg_ctx *c, int chunk_frames) {
@@ -446,6 +469,7 @@ int wvg_batch_reset(wvg_batch *b) {
     b->segs.clear();
     b->uploaded = b->downloaded = b->formatted = b->segs_uploaded = false;
     b->dfiles.clear();
+    b->dev_runs.clear();
     b->framed_dev = b->framed_host = 0;
     return WVG_OK;
 }
@@ -603,8 +627,15 @@ int wvg_batch_add_files_device(wvg_batch *b, int n, const uint8_t *const *files,
 // the walk (one lane per file), the output range of every file it accepted, the
 // block pass (one lane per block), then, in file order, the accepted files'
 // descriptors committed and every other file framed by the host.
+// WVG_DFRAME_TRACE=1 (diagnostic): the host-side phases of each device framing on stderr
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 static int device_frame(wvg_batch *b, hipStream_t s) {
     wvg_ctx *c = b->ctx;
+    static const bool trace = getenv("WVG_DFRAME_TRACE") && getenv("WVG_DFRAME_TRACE")[0] == '1';
+    double tp[6] = {now_ms(), 0, 0, 0, 0, 0};
     const size_t nf = b->dfiles.size();
     std::vector<DFile> df(nf);
     uint64_t nslots = 0;
@@ -648,6 +679,7 @@ static int device_frame(wvg_batch *b, hipStream_t s) {
     HIPCHK(c, launch_dframe_walk(b->d_dfiles, (uint32_t)nf, b->d_blob, b->d_slots, s));
     HIPCHK(c, hipMemcpyAsync(b->dfst.data(), b->d_dfiles, sizeof(DFile) * nf, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
+    tp[1] = now_ms();
     memcpy(df.data(), b->dfst.data(), sizeof(DFile) * nf);
     // output ranges and the block list of the accepted files, in file order
     std::vector<uint32_t> bf, bk;
@@ -666,14 +698,26 @@ static int device_frame(wvg_batch *b, hipStream_t s) {
     const size_t nb = bf.size();
     std::vector<DBlock> recs(nb);
     std::vector<BlockDesc> dd(nb);
+    if (nb && !b->dev_runs.empty()) {
+        // an earlier device framing of this batch left descriptors in d_ddescs, which
+        // this pass reuses: bring them to the host first (files added after an upload
+        // without a reset -- not the common path)
+        for (const auto &r : b->dev_runs)
+            HIPCHK(c, hipMemcpyAsync(b->fo.descs.data() + r.dst, b->d_ddescs + r.src, sizeof(BlockDesc) * r.n,
+                                     hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        b->dev_runs.clear();
+    }
     if (nb) {
         HIPCHK(c, ensure(b->d_blkf, b->cap_blkf, sizeof(uint32_t) * nb));
         HIPCHK(c, ensure(b->d_blkk, b->cap_blkk, sizeof(uint32_t) * nb));
         HIPCHK(c, ensure(b->d_ddescs, b->cap_ddescs, sizeof(BlockDesc) * nb));
         HIPCHK(c, ensure(b->d_drecs, b->cap_drecs, sizeof(DBlock) * nb));
+        // up and down in separate parts of the staging: no wait between the copies and the pass
         const size_t up = sizeof(DFile) * nf + 2 * sizeof(uint32_t) * nb;
-        const size_t down = (sizeof(BlockDesc) + sizeof(DBlock)) * nb;
-        if (!b->dfst.resize(up > down ? up : down)) return WVG_ERR_SPACE;
+        const size_t up_al = (up + 255) & ~(size_t)255;
+        const size_t down = (kDescHead + sizeof(DBlock)) * nb;
+        if (!b->dfst.resize(up_al + down)) return WVG_ERR_SPACE;
         uint8_t *h = b->dfst.data();
         memcpy(h, df.data(), sizeof(DFile) * nf);
         memcpy(h + sizeof(DFile) * nf, bf.data(), sizeof(uint32_t) * nb);
@@ -682,15 +726,22 @@ static int device_frame(wvg_batch *b, hipStream_t s) {
         HIPCHK(c, hipMemcpyAsync(b->d_blkf, h + sizeof(DFile) * nf, sizeof(uint32_t) * nb, hipMemcpyHostToDevice, s));
         HIPCHK(c, hipMemcpyAsync(b->d_blkk, h + sizeof(DFile) * nf + sizeof(uint32_t) * nb, sizeof(uint32_t) * nb,
                                  hipMemcpyHostToDevice, s));
-        HIPCHK(c, hipStreamSynchronize(s));  // the staging is reused for the results
+        tp[2] = now_ms();
         HIPCHK(c, launch_dframe_block(b->d_dfiles, b->d_blkf, b->d_blkk, (uint32_t)nb, b->d_blob, b->d_slots,
                                       b->d_ddescs, b->d_drecs, s));
-        HIPCHK(c, hipMemcpyAsync(h, b->d_ddescs, sizeof(BlockDesc) * nb, hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipMemcpyAsync(h + sizeof(BlockDesc) * nb, b->d_drecs, sizeof(DBlock) * nb, hipMemcpyDeviceToHost,
-                                 s));
+        // the descriptors stay on the device; the host takes each one's head (a strided
+        // copy) and the per-block records it reduces into the FileInfo
+        uint8_t *hd = h + up_al;
+        HIPCHK(c, hipMemcpy2DAsync(hd, kDescHead, b->d_ddescs, sizeof(BlockDesc), kDescHead, nb, hipMemcpyDeviceToHost,
+                                   s));
+        HIPCHK(c, hipMemcpyAsync(hd + kDescHead * nb, b->d_drecs, sizeof(DBlock) * nb, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
-        memcpy(dd.data(), h, sizeof(BlockDesc) * nb);
-        memcpy(recs.data(), h + sizeof(BlockDesc) * nb, sizeof(DBlock) * nb);
+        tp[3] = now_ms();
+        for (size_t k = 0; k < nb; k++) {
+            memset(&dd[k], 0, sizeof(BlockDesc));
+            memcpy(&dd[k], hd + kDescHead * k, kDescHead);
+        }
+        memcpy(recs.data(), hd + kDescHead * nb, sizeof(DBlock) * nb);
     }
     // commit: the accepted files at their reserved output ranges, in file order
     std::vector<size_t> host;
@@ -700,8 +751,14 @@ static int device_frame(wvg_batch *b, hipStream_t s) {
         fi.blob_base = p.base;
         fi.first_desc = (int64_t)b->fo.descs.size();
         if (df[i].regular && dframe_file_info(df[i], recs.data() + blk0[i], fi)) {
+            const size_t dst = b->fo.descs.size();
             b->fo.descs.insert(b->fo.descs.end(), dd.begin() + (ptrdiff_t)blk0[i],
                                dd.begin() + (ptrdiff_t)(blk0[i] + df[i].nblocks));
+            if (!b->dev_runs.empty() && b->dev_runs.back().dst + b->dev_runs.back().n == dst &&
+                b->dev_runs.back().src + b->dev_runs.back().n == blk0[i])
+                b->dev_runs.back().n += df[i].nblocks;  // contiguous with the previous file's
+            else
+                b->dev_runs.push_back({dst, blk0[i], (size_t)df[i].nblocks});
             b->out_ints = (int64_t)df[i].out_base;
             commit_file(b, fi, p.len, nullptr, p.idx);
             b->framed_dev++;
@@ -725,6 +782,11 @@ static int device_frame(wvg_batch *b, hipStream_t s) {
         }
     }
     b->dfiles.clear();
+    if (trace) {
+        tp[4] = now_ms();
+        fprintf(stderr, "dframe: walk+sync %.3f  lists+sync %.3f  block+D2H %.3f  commit+host %.3f ms (%zu files)\n",
+                tp[1] - tp[0], tp[2] - tp[1], tp[3] - tp[2], tp[4] - tp[3], nf);
+    }
     return WVG_OK;
 }
 
@@ -747,6 +809,8 @@ int wvg_batch_upload(wvg_batch *b) {
     hipStream_t s = b->stream;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, quiesce(b));  // earlier work on these buffers, on the batch's or a caller's stream
+    static const bool trace = getenv("WVG_DFRAME_TRACE") && getenv("WVG_DFRAME_TRACE")[0] == '1';
+    const double t_up0 = now_ms();
     b->formatted = false;
     // the blob is followed by 64 B of 0xFF (the reader's past-end fill)
     const size_t blob_n = b->blob.size() + 64;
@@ -778,7 +842,16 @@ int wvg_batch_upload(wvg_batch *b) {
         return hipMemcpyAsync(dst, h, bytes, hipMemcpyHostToDevice, s);
     };
     HIPCHK(c, ensure(b->d_descs, b->cap_descs, sizeof(BlockDesc) * (nd ? nd : 1)));
-    HIPCHK(c, put(b->d_descs, b->fo.descs.data(), sizeof(BlockDesc) * nd));
+    {   // the host-framed descriptors, around the device-framed runs, which are copied on the device
+        size_t k = 0;
+        for (const auto &r : b->dev_runs) {
+            HIPCHK(c, put(b->d_descs + k, b->fo.descs.data() + k, sizeof(BlockDesc) * (r.dst - k)));
+            HIPCHK(c, hipMemcpyAsync(b->d_descs + r.dst, b->d_ddescs + r.src, sizeof(BlockDesc) * r.n,
+                                     hipMemcpyDeviceToDevice, s));
+            k = r.dst + r.n;
+        }
+        HIPCHK(c, put(b->d_descs + k, b->fo.descs.data() + k, sizeof(BlockDesc) * (nd - k)));
+    }
     if (!b->fo.jobs.empty()) {  // device-side metadata parse: finishes the descriptors in place
         const size_t ni = b->fo.items.size(), nj = b->fo.jobs.size();
         HIPCHK(c, ensure(b->d_items, b->cap_items, sizeof(MetaItem) * ni));
@@ -828,6 +901,7 @@ int wvg_batch_upload(wvg_batch *b) {
     }
     if (soff > need) return WVG_ERR_SPACE;  // (cannot happen: the sizes above cover every put)
     HIPCHK(c, hipStreamSynchronize(s));  // the blob may change after this call
+    if (trace) fprintf(stderr, "upload: %.3f ms (%zu blocks)\n", now_ms() - t_up0, nd);
     b->uploaded = true;
     b->downloaded = false;
     b->segs_uploaded = false;
@@ -904,6 +978,16 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
         if (!b->ts_list[t].empty())
             HIPCHK(c, launch_2wave(t, b->d_descs, b->d_ts[t], (uint32_t)b->ts_list[t].size(), b->d_blob, b->d_out,
                                    b->d_status, b->d_mute, slot(t)));
+    if (b->timing) {  // per-group end times of this decode (one group: it ran on s)
+        b->gstart = b->tev[b->tev.size() - 2];
+        b->gmask = 0;
+        for (int i = 0; i < n; i++) {
+            const int g = used[i];
+            if (!b->gev[g]) HIPCHK(c, hipEventCreate(&b->gev[g]));
+            HIPCHK(c, hipEventRecord(b->gev[g], slot(g)));
+            b->gmask |= 1u << g;
+        }
+    }
     if (n > 1) {
         for (int i = 0; i < n; i++) {
             HIPCHK(c, hipEventRecord(b->join[used[i]], b->side[used[i]]));
@@ -944,6 +1028,17 @@ int wvg_batch_timed(wvg_batch *b, float *avg_ms, int *count) {
     *avg_ms = b->t_cnt ? (float)(b->t_sum / b->t_cnt) : 0.f;
     *count = b->t_cnt;
     return WVG_OK;
+}
+
+int wvg_batch_group_times(wvg_batch *b, float *ms, int cap) {
+    if (!b || !ms || cap < kSide) return WVG_ERR_ARG;
+    for (int g = 0; g < kSide; g++) {
+        ms[g] = -1.f;
+        if (!(b->gmask & (1u << g)) || !b->gstart) continue;
+        HIPCHK(b->ctx, hipEventSynchronize(b->gev[g]));
+        HIPCHK(b->ctx, hipEventElapsedTime(&ms[g], b->gstart, b->gev[g]));
+    }
+    return kSide;
 }
 
 int64_t wvg_batch_out_ints(const wvg_batch *b) { return b ? b->out_ints : 0; }
@@ -1308,6 +1403,206 @@ int wvg_batch_wav(wvg_batch *b, int file, uint8_t *out, int64_t cap, int64_t *wa
         HIPCHK(c, hipStreamSynchronize(b->stream));
     }
     if (tlen) memcpy(out + hlen + pcm, b->blob.data() + (size_t)(fi.blob_base + fi.trailer_off), (size_t)tlen);
+    return WVG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Streaming WavpackUnpackSamples (WavPackUtils.cs:200-282): the caller's calls
+// are served a window at a time.  The file is decoded on the device on the
+// first call (the blocks are independent: one launch decodes them all, and
+// 288 GB of HBM holds any file's int32 output); the host only ever holds the
+// compressed file and two windows of `window` frames in page-locked staging,
+// the next window's DMA running while the caller consumes the current one.
+// crc_errors are counted as each block's last frame is handed out (:273-275),
+// and the call that the reference throws in returns WVG_ERR_EXCEPTION after
+// the calls before it returned their frames.
+// ---------------------------------------------------------------------------
+struct wvg_stream {
+    wvg_ctx *ctx = nullptr;
+    wvg_batch *b = nullptr;
+    std::vector<uint8_t> file;
+    uint32_t flags = 0;
+    int64_t seek = -1;            // SetSample target (-1: none)
+    int chunk = 0;                // the request size the decode was scheduled at (0: not decoded)
+    int64_t window = 0;           // frames per staged window
+    wvg_file_info info;
+    wvg_file_result res;
+    int nch = 1;
+    bool throws = false;
+    int schedule_changed = 0;
+    int64_t pos = 0, limit = 0;   // frames handed out since the decode's start / before the end or the throw
+    int64_t errors_before = 0;    // crc_errors of calls made before a SetSample
+    int64_t index0 = 0;           // stream.sample_index when the decode's first call starts
+    std::vector<int64_t> blk_end;
+    std::vector<uint32_t> blk_st;
+    size_t blk_next = 0;          // blocks counted so far (their last frame was handed out)
+    int64_t errors = 0;
+    PinnedBuf stage[2];
+    int64_t lo[2] = {0, 0}, hi[2] = {0, 0};  // frames staged in stage[k] (hi == lo: none)
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    int cur = 0;
+};
+
+static int stream_fetch(wvg_stream *s, int k, int64_t from) {
+    wvg_ctx *c = s->ctx;
+    const int64_t to = std::min(from + s->window, s->limit);
+    s->lo[k] = from;
+    s->hi[k] = to;
+    if (to <= from) return WVG_OK;
+    if (!s->stage[k].resize(sizeof(int32_t) * (size_t)((to - from) * s->nch))) return WVG_ERR_SPACE;
+    const int32_t *src = s->b->d_out + s->info.out_offset + from * s->nch;
+    HIPCHK(c, hipMemcpyAsync(s->stage[k].data(), src, sizeof(int32_t) * (size_t)((to - from) * s->nch),
+                             hipMemcpyDeviceToHost, s->b->stream));
+    HIPCHK(c, hipEventRecord(s->ev[k], s->b->stream));
+    return WVG_OK;
+}
+
+// (re)decode the file with the calls scheduled at `chunk` frames
+static int stream_decode(wvg_stream *s, int chunk) {
+    wvg_ctx *c = s->ctx;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (s->b && s->b->chunk != chunk) {
+        wvg_batch_free(s->b);
+        s->b = nullptr;
+    }
+    if (!s->b) {
+        s->b = wvg_batch_new(c, chunk);
+        if (!s->b) return WVG_ERR_HIP;
+    } else {
+        wvg_batch_reset(s->b);
+    }
+    wvg_batch *b = s->b;
+    const int idx = s->seek >= 0 ? wvg_batch_add_file_at(b, s->file.data(), s->file.size(), s->flags, s->seek, &s->info)
+                                 : wvg_batch_add_file(b, s->file.data(), s->file.size(), s->flags, &s->info);
+    if (idx != 0) return idx < 0 ? idx : WVG_ERR_ARG;
+    int rc = wvg_batch_upload(b);
+    if (rc == WVG_OK) rc = wvg_batch_decode(b, nullptr);
+    if (rc == WVG_OK) rc = wvg_batch_download(b, nullptr, 0);  // statuses only
+    if (rc == WVG_OK) rc = wvg_batch_file_result(b, 0, &s->res);
+    if (rc != WVG_OK) return rc;
+    s->info.out_offset = b->infos[0].out_offset;
+    s->nch = s->info.reduced_channels > 0 ? s->info.reduced_channels : 1;
+    s->throws = s->res.exception != 0;
+    s->limit = s->throws ? s->res.exception_frame : s->info.out_frames;
+    s->blk_end.assign((size_t)s->res.num_blocks, 0);
+    s->blk_st.assign((size_t)s->res.num_blocks, 0);
+    if (s->res.num_blocks > 0) {
+        rc = wvg_batch_file_blocks(b, 0, s->blk_end.data(), s->blk_st.data(), s->res.num_blocks);
+        if (rc < 0) return rc;
+    }
+    s->blk_next = 0;
+    s->errors = 0;
+    s->pos = 0;
+    s->index0 = s->info.sample_index0;
+    s->chunk = chunk;
+    s->lo[0] = s->hi[0] = s->lo[1] = s->hi[1] = 0;
+    return stream_fetch(s, s->cur, 0);
+}
+
+static void stream_count_blocks(wvg_stream *s) {
+    while (s->blk_next < s->blk_end.size() && s->blk_end[s->blk_next] <= s->pos) {
+        if (s->blk_st[s->blk_next] & ST_CRC_ERROR) s->errors++;
+        s->blk_next++;
+    }
+}
+
+wvg_stream *wvg_stream_open(wvg_ctx *ctx, const uint8_t *file, size_t len, uint32_t open_flags, int64_t window_frames,
+                            wvg_file_info *info) {
+    if (!ctx || (!file && len)) return nullptr;
+    if (hipSetDevice(ctx->device) != hipSuccess) return nullptr;
+    wvg_stream *s = new wvg_stream();
+    s->ctx = ctx;
+    s->file.assign(file, file + len);
+    s->flags = open_flags;
+    s->window = window_frames > 0 ? window_frames : ((int64_t)1 << 18);
+    memset(&s->res, 0, sizeof(s->res));
+    const int rc = wvg_probe_file(s->file.data(), s->file.size(), open_flags, SAMPLE_BUFFER_SIZE, &s->info);
+    if (info) *info = s->info;
+    if (rc != WVG_OK || hipEventCreateWithFlags(&s->ev[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&s->ev[1], hipEventDisableTiming) != hipSuccess) {
+        wvg_stream_close(s);
+        return nullptr;
+    }
+    s->index0 = s->info.sample_index0;
+    return s;
+}
+
+void wvg_stream_close(wvg_stream *s) {
+    if (!s) return;
+    hipSetDevice(s->ctx->device);
+    if (s->b) wvg_batch_free(s->b);  // waits for the staged DMAs on its stream
+    for (auto &e : s->ev)
+        if (e) hipEventDestroy(e);
+    delete s;
+}
+
+int64_t wvg_stream_unpack(wvg_stream *s, int32_t *buffer, int64_t samples) {
+    if (!s || samples < 0 || (!buffer && samples)) return WVG_ERR_ARG;
+    if (samples > INT32_MAX) return WVG_ERR_ARG;
+    if (!s->chunk || ((int)samples != s->chunk && s->pos == 0 && samples > 0)) {
+        // the first call (or a new request size before any frame went out): the decode is
+        // scheduled at this request size, as the reference's seams follow the caller's calls
+        const int rc = stream_decode(s, samples > 0 ? (int)samples : SAMPLE_BUFFER_SIZE);
+        if (rc != WVG_OK) return rc;
+    } else if ((int)samples != s->chunk) {
+        s->schedule_changed = 1;  // later calls of another size: served from the first schedule
+    }
+    if (s->pos >= s->limit) return s->throws ? WVG_ERR_EXCEPTION : 0;
+    const int64_t n = std::min(samples, s->limit - s->pos);
+    wvg_ctx *c = s->ctx;
+    int64_t done = 0;
+    while (done < n) {
+        const int64_t f = s->pos + done;
+        int k = s->cur;
+        if (!(f >= s->lo[k] && f < s->hi[k])) {
+            k ^= 1;
+            if (!(f >= s->lo[k] && f < s->hi[k])) {  // not staged (the first call, or a skipped window)
+                const int rc = stream_fetch(s, k, f);
+                if (rc != WVG_OK) return rc;
+            }
+            s->cur = k;
+            // the next window's DMA runs while this one is served
+            const int rc = stream_fetch(s, k ^ 1, s->hi[k]);
+            if (rc != WVG_OK) return rc;
+        }
+        HIPCHK(c, hipEventSynchronize(s->ev[k]));
+        const int64_t m = std::min(n - done, s->hi[k] - f);
+        memcpy(buffer + done * s->nch, s->stage[k].data() + sizeof(int32_t) * (size_t)((f - s->lo[k]) * s->nch),
+               sizeof(int32_t) * (size_t)(m * s->nch));
+        done += m;
+    }
+    s->pos += n;
+    stream_count_blocks(s);
+    return n;
+}
+
+int wvg_stream_set_sample(wvg_stream *s, int64_t sample) {
+    if (!s || sample < 0) return WVG_ERR_ARG;
+    // the block search runs on the host framing (WavPackUtils.cs:521-594)
+    FramingOutput fo;
+    FileInfo fi;
+    frame_file(s->file.data(), s->file.size(), 0, 0, s->flags, s->chunk ? s->chunk : SAMPLE_BUFFER_SIZE, fo, fi,
+               sample);
+    if (!fi.open_ok) return 0;
+    if (fi.seek_result < 0) return WVG_ERR_EXCEPTION;
+    if (fi.seek_result == 0) return 0;
+    s->errors_before += s->errors;
+    s->seek = sample;
+    // decode now: the discard calls' block ends count towards the errors at once
+    const int rc = stream_decode(s, s->chunk ? s->chunk : SAMPLE_BUFFER_SIZE);
+    if (rc != WVG_OK) return rc;
+    s->index0 = sample;
+    stream_count_blocks(s);
+    return 1;
+}
+
+int wvg_stream_state(const wvg_stream *s, int64_t *sample_index, int64_t *crc_errors, int32_t *lossy,
+                     int32_t *schedule_changed) {
+    if (!s) return WVG_ERR_ARG;
+    if (sample_index) *sample_index = s->chunk ? s->index0 + s->pos : s->info.sample_index0;
+    if (crc_errors) *crc_errors = s->errors_before + s->errors;
+    if (lossy) *lossy = s->chunk ? s->res.lossy : s->info.lossy;
+    if (schedule_changed) *schedule_changed = s->schedule_changed;
     return WVG_OK;
 }
 

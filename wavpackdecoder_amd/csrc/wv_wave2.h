@@ -955,25 +955,32 @@ struct VTabs {
 // (:494-497), residual into lane M0, slow_level += mylog2(mid) - ((slow +
 // 128) >> 8) (:501-502), window advance; the advance's borrow is the next
 // word's refill test
+// The bisection runs on (low, n = high - low + 1): mid = low + (n >> 1), a 1
+// bit keeps the upper ceil(n / 2) values from mid, a 0 bit the lower n >> 1
+// (the reference's mid = (high + (low = mid) + 1) >> 1 / ((high = mid - 1) +
+// low + 1) >> 1), and the loop runs while n > errlim + 1.  Seven scalar
+// instructions and the test per bit, unrolled four bits per backward branch.
+#define HW_STEP(I, S)                                               \
+    "s_cmp_le_u32 %[hi], %[c1]\n"                                   \
+    "s_cbranch_scc1 HD" I S "_%=\n"                                 \
+    "s_lshr_b32 %[md], %[hi], 1\n"                                  \
+    "s_add_u32 %[x], %[lo], %[md]\n"                                \
+    "s_sub_u32 %[b], %[hi], %[md]\n"                                \
+    "s_bitcmp1_b32 vcc_lo, %[kb]\n"                                 \
+    "s_cselect_b32 %[lo], %[x], %[lo]\n"                            \
+    "s_cselect_b32 %[hi], %[b], %[md]\n"                            \
+    "s_add_u32 %[kb], %[kb], 1\n"
 #define HW_TAIL(I, S, SLOW, EL, J)                                  \
     "s_mov_b32 %[kb], %[k16]\n" /* bit index, s_bfe width 1 */      \
-    "s_add_u32 %[md], %[hi], %[lo]\n"                               \
-    "s_add_u32 %[md], %[md], 1\n"                                   \
-    "s_lshr_b32 %[md], %[md], 1\n"                                  \
+    "s_sub_u32 %[hi], %[hi], %[lo]\n"                               \
+    "s_add_u32 %[hi], %[hi], 1\n" /* n */                           \
+    "s_add_u32 %[c1], " EL ", 1\n"                                  \
     "HB" I S "_%=:\n"                                               \
-    "s_sub_u32 %[x], %[hi], %[lo]\n"                                \
-    "s_cmp_le_i32 %[x], " EL "\n"                                   \
-    "s_cbranch_scc1 HD" I S "_%=\n"                                 \
-    "s_add_u32 %[x], %[md], -1\n"                                   \
-    "s_bitcmp1_b32 vcc_lo, %[kb]\n"                                 \
-    "s_cselect_b32 %[lo], %[md], %[lo]\n"                           \
-    "s_cselect_b32 %[hi], %[hi], %[x]\n"                            \
-    "s_add_u32 %[kb], %[kb], 1\n"                                   \
-    "s_add_u32 %[md], %[hi], %[lo]\n"                               \
-    "s_add_u32 %[md], %[md], 1\n"                                   \
-    "s_lshr_b32 %[md], %[md], 1\n"                                  \
+    HW_STEP(I, S) HW_STEP(I, S) HW_STEP(I, S) HW_STEP(I, S)         \
     "s_branch HB" I S "_%=\n"                                       \
     "HD" I S "_%=:\n"                                               \
+    "s_lshr_b32 %[md], %[hi], 1\n"                                  \
+    "s_add_u32 %[md], %[md], %[lo]\n" /* mid */                     \
     "s_bfe_i32 %[x], vcc_lo, %[kb]\n"                               \
     "s_xor_b32 %[b], %[md], %[x]\n"                                 \
     "v_writelane_b32 %[resv], %[b], m0\n"                           \
@@ -1204,6 +1211,7 @@ __device__ __forceinline__ bool hybrid_run_narrow(Entropy &w, SmemReader &rd, ui
 }
 #undef HW_EL
 #undef HW_TAIL
+#undef HW_STEP
 #undef HW_WORD
 #undef HW_REFILL
 #undef HW_COLD
