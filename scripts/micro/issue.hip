@@ -6,9 +6,9 @@
 #define REP100(x) x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x x
 #define BENCH(name, setup, body)                                               \
     __global__ void name(long long *out) {                                    \
-        asm volatile(setup ::: "s20", "s21", "s22", "s23", "s24", "s25", "s26", "s27", "v20", "v21", "scc", "vcc"); \
+        asm volatile(setup ::: "s20", "s21", "s22", "s23", "s24", "s25", "s26", "s27", "v20", "v21", "v22", "v23", "v24", "v25", "scc", "vcc"); \
         long long t0 = clock64();                                              \
-        asm volatile(REP100(body) ::: "s20", "s21", "s22", "s23", "s24", "s25", "s26", "s27", "v20", "v21", "scc", "vcc"); \
+        asm volatile(REP100(body) ::: "s20", "s21", "s22", "s23", "s24", "s25", "s26", "s27", "v20", "v21", "v22", "v23", "v24", "v25", "scc", "vcc"); \
         long long t1 = clock64();                                              \
         if (threadIdx.x == 0) out[blockIdx.x] = t1 - t0;                       \
     }
@@ -28,6 +28,14 @@ BENCH(k_valu_dep, "v_mov_b32 v20, 0\n", "v_add_u32 v20, v20, 1\n")
 BENCH(k_rfl, "v_mov_b32 v20, 0\n", "v_add_u32 v20, 1, v20\n v_readfirstlane_b32 s20, v20\n s_add_u32 s21, s20, 1\n")
 BENCH(k_wl, "s_mov_b32 s20, 7\n s_mov_b32 m0, 3\n", "v_writelane_b32 v20, s20, m0\n s_add_u32 s20, s20, 1\n")
 BENCH(k_mix, "s_mov_b32 s20, 0\n v_mov_b32 v20, 0\n", "s_add_u32 s20, s20, 1\n v_add_u32 v20, v20, 1\n")
+// VALU multiplies: 64-bit mad (apply_weight), 32-bit mul_lo, 24-bit mul, dependent and independent
+BENCH(k_mad64_dep, "v_mov_b32 v20, 3\n v_mov_b32 v21, 5\n s_mov_b64 s[20:21], 0x200\n",
+      "v_mad_i64_i32 v[20:21], s[22:23], v20, v21, s[20:21]\n")
+BENCH(k_mad64_ind, "v_mov_b32 v20, 3\n v_mov_b32 v21, 5\n s_mov_b64 s[20:21], 0x200\n",
+      "v_mad_i64_i32 v[22:23], s[24:25], v20, v21, s[20:21]\n v_mad_i64_i32 v[24:25], s[26:27], v20, v21, s[20:21]\n")
+BENCH(k_mullo_dep, "v_mov_b32 v20, 3\n v_mov_b32 v21, 5\n", "v_mul_lo_u32 v20, v20, v21\n")
+BENCH(k_mul24_dep, "v_mov_b32 v20, 3\n v_mov_b32 v21, 5\n", "v_mul_i32_i24 v20, v20, v21\n")
+BENCH(k_mad24_dep, "v_mov_b32 v20, 3\n v_mov_b32 v21, 5\n", "v_mad_i32_i24 v20, v20, v21, v21\n")
 
 int main() {
     long long *d;
@@ -37,7 +45,9 @@ int main() {
         {"nop", k_nop}, {"sadd_dep", k_sadd_dep}, {"sadd_ind(x4)", k_sadd_ind}, {"smul_dep", k_smul_dep},
         {"shr64_dep", k_shr64_dep}, {"cmp+cselect", k_cmp_csel}, {"ff1_dep", k_ff1_dep},
         {"s_branch", k_branch_taken}, {"cbranch_not_taken", k_cbranch_nt}, {"cbranch_taken", k_cbranch_t},
-        {"valu_dep", k_valu_dep}, {"valu+rfl+salu", k_rfl}, {"writelane+sadd", k_wl}, {"salu+valu", k_mix}};
+        {"valu_dep", k_valu_dep}, {"valu+rfl+salu", k_rfl}, {"writelane+sadd", k_wl}, {"salu+valu", k_mix},
+        {"v_mad_i64_dep", k_mad64_dep}, {"v_mad_i64_ind(x2)", k_mad64_ind}, {"v_mul_lo_u32_dep", k_mullo_dep},
+        {"v_mul_i32_i24_dep", k_mul24_dep}, {"v_mad_i32_i24_dep", k_mad24_dep}};
     for (auto &k : ks) {
         for (int nb : {1, 1024, 2048}) {
             for (int rep = 0; rep < 2; rep++) hipLaunchKernelGGL(k.k, dim3(nb), dim3(64), 0, 0, d);

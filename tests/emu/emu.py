@@ -76,6 +76,9 @@ INFO_FIELDS_FULL = INFO_FIELDS + ("lossy_blocks", "is_five", "file_format", "hea
                                   "trailer_len", "first_call_frames", "config_flags", "sample_index0", "exception",
                                   "nondet")
 DESC_BYTES = 1440  # sizeof(BlockDesc)
+DESC_KIND = 32           # offsetof(BlockDesc, kind)
+DESC_DSD_TABLE_OFF = 1312  # offsetof(BlockDesc, dsd_table_off)
+KIND_DSD_FAST = 2
 
 
 def file_info_full(data: bytes, chunk: int = 4096) -> dict:

@@ -1590,8 +1590,7 @@ int wvg_stream_set_sample(wvg_stream *s, int64_t sample) {
     s->seek = sample;
     // decode now: the discard calls' block ends count towards the errors at once
     const int rc = stream_decode(s, s->chunk ? s->chunk : SAMPLE_BUFFER_SIZE);
-    if (rc != WVG_OK) return rc;
-    s->index0 = sample;
+    if (rc != WVG_OK) return rc;  // (the index is where the decode's first call starts: info.sample_index0)
     stream_count_blocks(s);
     return 1;
 }

@@ -883,6 +883,67 @@ __device__ __forceinline__ DsdResult dsd_fast_v2(const BlockDesc &d, const uint8
     return res;
 }
 
+// inclusive prefix sum over the wave's 64 lanes
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    const int lane = (int)threadIdx.x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+        if (lane >= o) x += y;
+    }
+    return x;
+}
+
+// init_dsd_block_fast's tables (DsdUtils.cs:169-229) in LDS, from the block's
+// probability data: the probabilities (run-length coded unless max_probability
+// is 0xFF: a code above max_probability is a run of code - max_probability
+// zeros, a code 1..max_probability one probability, 0 the end) into tab[bin *
+// 256 + i], then each bin's running sums (summed_probabilities, ushort) in place.
+// The framing ran the reference's checks on the same bytes (the data fills
+// exactly bins x 256 entries, the totals are in range), so the wave decodes 64
+// codes per step: a prefix sum of their run lengths gives each value its entry.
+// Codes read past the terminating one (at most 63 bytes) stay inside the blob.
+__device__ __forceinline__ void dsd_fast_tables(const BlockDesc &d, const uint8_t *blob, uint32_t bins, uint32_t *tab) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t ne = bins * 256u;
+    const uint8_t *pd = blob + d.dsd_prob_off;
+    if (d.dsd_max_prob < 0xFF) {
+        const uint32_t maxp = (uint32_t)d.dsd_max_prob;
+        for (uint32_t i = lane; i < ne; i += 64) tab[i] = 0;
+        __syncthreads();
+        uint32_t outptr = 0, p = 0;
+        while (outptr < ne) {
+            const uint32_t c = pd[p + lane];
+            const uint32_t len = c > maxp ? c - maxp : (c != 0 ? 1u : 0u);
+            const uint32_t incl = wave_incl_scan(len);
+            // the loop ends at the first 0 code, or once the entries are all filled
+            const uint64_t ev = __ballot(c == 0 || outptr + incl >= ne);
+            const uint32_t last = ev ? (uint32_t)__builtin_ctzll(ev) : 63u;
+            if (lane <= last && c != 0 && c <= maxp) tab[outptr + incl - 1u] = c;
+            outptr += (uint32_t)__builtin_amdgcn_readlane((int)incl, (int)last);
+            p += last + 1u;
+            if (ev) break;
+        }
+    } else {
+        for (uint32_t i = lane; i < ne; i += 64) tab[i] = pd[i];
+    }
+    __syncthreads();
+    // running sums per bin: lane l holds entries 4l .. 4l + 3 of the row
+    for (uint32_t b = 0; b < bins; b++) {
+        uint4 v = *(uint4 *)(tab + b * 256u + lane * 4u);
+        v.y += v.x;
+        v.z += v.y;
+        v.w += v.z;
+        const uint32_t before = wave_incl_scan(v.w) - v.w;
+        v.x = (v.x + before) & 0xFFFFu;
+        v.y = (v.y + before) & 0xFFFFu;
+        v.z = (v.z + before) & 0xFFFFu;
+        v.w = (v.w + before) & 0xFFFFu;
+        *(uint4 *)(tab + b * 256u + lane * 4u) = v;
+    }
+    __syncthreads();
+}
+
 // Mode 1: one wave per block, its tables staged in LDS first.  Launched over
 // the mode-1 part of the DSD list (the list is sorted by kind);
 // wv_decode_dsd_wave skips those blocks.  dsd_fast_v2 reads rows of u32
@@ -902,14 +963,11 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_fast(const BlockD
     const uint32_t bins = (uint32_t)d.dsd_history_bins;
     DevStoreWave st{out + d.out_off, (uint64_t)d.pre_end * d.out_nch, lead};
     DsdResult r;
-    // summed_probabilities (u16, after the bins x 256 probability bytes) widened to u32 rows
-    const uint16_t *sum16 = (const uint16_t *)(tables + d.dsd_table_off + (size_t)bins * 256u);
-    const uint32_t ne = bins <= 32u ? bins * 256u : 0u;
-    for (uint32_t i = threadIdx.x; i < ne; i += 64) tab[i] = sum16[i];
+    if (bins <= 32u) dsd_fast_tables(d, blob, bins, tab);
     // lane b: bin b's total and the reciprocal constants of dividing by it
     uint32_t vmag = 0, vsh1 = 0, vsh2 = 0;  // all zero for an empty bin (see dsd_fast_v2)
     if (threadIdx.x < bins && bins <= 32u) {
-        const uint32_t dv = sum16[threadIdx.x * 256u + 255u];
+        const uint32_t dv = tab[threadIdx.x * 256u + 255u];
         if (dv) {
             const uint32_t l = dv > 1u ? 32u - (uint32_t)__clz(dv - 1u) : 0u;  // ceil(log2 dv)
             vmag = (uint32_t)(((((uint64_t)1 << l) - dv) << 32) / dv) + 1u;

@@ -99,7 +99,12 @@ struct alignas(16) BlockDesc {
     // reference's float_values; else XF_ON | float_flags | float_max_exp << 8 |
     // ID_FLOAT_INFO's float_shift << 16 (the wvx stream, if any, in wvx_off/len)
     uint32_t xfloat;
-    uint32_t xfloat_pad_[3];
+    // --- DSD mode 1 (DsdUtils.cs:149-242): the probability data after the
+    // history-bits and max_probability bytes (run-length coded unless
+    // max_probability is 0xFF), from which the decode kernel builds its
+    // cumulative tables in LDS; bits_off is the first of the 4 value bytes
+    int32_t dsd_max_prob;
+    uint64_t dsd_prob_off;
 };
 constexpr uint32_t XF_ON = 1u << 31;
 

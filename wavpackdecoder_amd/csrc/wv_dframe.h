@@ -138,6 +138,9 @@ struct DState {
     int32_t dsd_len;        // C# data.Length - byteptr
     int32_t dsd_rate_i;     // mode 3: init_ptable's rate index
     int32_t dsd_filt[2][6]; // mode 3: filter1..5 << 12, factor
+    int32_t dsd_bins;       // mode 1: history bins
+    int32_t dsd_maxp;       // mode 1: max_probability
+    int64_t dsd_prob;       // mode 1: file offset of the probability data
     // context (file-level) values, updated in place
     int64_t cfg_flags;
     int32_t xmode;
@@ -162,6 +165,8 @@ WVF_HD void dstate_init(DState &s) {
     s.dsd_off = 0;
     s.dsd_len = 0;
     s.dsd_rate_i = 0;
+    s.dsd_bins = s.dsd_maxp = 0;
+    s.dsd_prob = 0;
     for (int c = 0; c < 2; c++)
         for (int k = 0; k < 6; k++) s.dsd_filt[c][k] = 0;
     s.cfg_flags = 0;
@@ -337,13 +342,62 @@ WVF_HD uint32_t dframe_subblocks(const uint8_t *f, uint64_t len, uint64_t hpos, 
         case ID_WVC_BITSTREAM:
         case ID_WVX_BITSTREAM:
         case ID_WVX_NEW_BITSTREAM: return DF_KIND;  // a second stream: the host frames the file
-        case ID_DSD_BLOCK: {  // init_dsd_block (DsdUtils.cs:17-54); mode 1 builds tables: the host's
-            if (byte_length < 2 || d[0] > 31 || (d[1] != 0 && d[1] != 3)) return DF_KIND;
+        case ID_DSD_BLOCK: {  // init_dsd_block (DsdUtils.cs:17-54)
+            if (byte_length < 2 || d[0] > 31 || (d[1] != 0 && d[1] != 1 && d[1] != 3)) return DF_KIND;
             // copy_data's length: the read buffer's fill for a small sub-block, the bytes read for a large one
             const int32_t dl = to_read > BITSTREAM_BUFFER_SIZE ? to_read : byte_length;
             int32_t p = 2;
             if (d[1] == 0) {
                 if ((int64_t)(dl - 2) != (int64_t)h.block_samples * (mono ? 1 : 2)) return DF_READER;
+            } else if (d[1] == 1) {
+                // init_dsd_block_fast (:149-242), its checks only: the decode kernel builds the
+                // cumulative tables from the probability data itself
+                if (p == dl) return DF_READER;
+                const int hbits = d[p++];
+                if (p == dl || hbits > 5) return DF_READER;
+                const int bins = 1 << hbits, outend = bins * 256;
+                const int maxp = d[p++];
+                s.dsd_bins = bins;
+                s.dsd_maxp = maxp;
+                s.dsd_prob = (int64_t)doff + p;
+                // the per-bin sums are ushort (wrapping); bins fill in order, so one running sum
+                int total = 0, cur = 0;
+                uint32_t sum = 0;
+                if (maxp < 0xFF) {
+                    int outptr = 0;
+                    while (outptr < outend && p < dl) {
+                        const int code = d[p++];
+                        if (code > maxp) {
+                            const int z = code - maxp;
+                            outptr += z < outend - outptr ? z : outend - outptr;
+                        } else if (code != 0) {
+                            if ((outptr >> 8) != cur) {
+                                total += (int)(sum & 0xFFFFu);
+                                sum = 0;
+                                cur = outptr >> 8;
+                            }
+                            sum += (uint32_t)code;
+                            outptr++;
+                        } else {
+                            break;
+                        }
+                    }
+                    if (outptr < outend || (p < dl && d[p++] > 0)) return DF_READER;
+                } else if (dl - p > outend) {
+                    for (int i = 0; i < outend; i++) {
+                        if ((i >> 8) != cur) {
+                            total += (int)(sum & 0xFFFFu);
+                            sum = 0;
+                            cur = i >> 8;
+                        }
+                        sum += d[p + i];
+                    }
+                    p += outend;
+                } else {
+                    return DF_READER;
+                }
+                total += (int)(sum & 0xFFFFu);
+                if (dl - p < 4 || total > bins * 1280) return DF_READER;
             } else {  // init_dsd_block_high (:343-389); its ptable is built by the decode kernel
                 if (dl - 2 < (mono ? 13 : 20) || d[3] != 20) return DF_READER;
                 s.dsd_rate_i = d[2];
@@ -568,10 +622,15 @@ WVF_HD void dframe_block(const DFile &fi, uint32_t k, const uint8_t *blob, const
     d.int32_ones = s.i32[2];
     d.int32_dups = s.i32[3];
     if (flags & DSD_FLAG) {  // DSD mode 0 (DsdUtils.cs:60-147: the raw bytes) or 3 (:391-493)
-        d.kind = s.dsd_mode == 3 ? KIND_DSD_HIGH : KIND_DSD_RAW;
+        d.kind = s.dsd_mode == 3 ? KIND_DSD_HIGH : (s.dsd_mode == 1 ? KIND_DSD_FAST : KIND_DSD_RAW);
         d.bits_off = fi.base + (uint64_t)s.dsd_off;
         d.dsd_data_len = (uint32_t)s.dsd_len;
         d.dsd_rate_i = s.dsd_rate_i;
+        if (s.dsd_mode == 1) {  // no table area: the decode kernel builds its tables (dsd_table_off unused)
+            d.dsd_history_bins = s.dsd_bins;
+            d.dsd_max_prob = s.dsd_maxp;
+            d.dsd_prob_off = fi.base + (uint64_t)s.dsd_prob;
+        }
         for (int c = 0; c < 2; c++)
             for (int k = 0; k < 6; k++) d.dsd_filters[c][k] = s.dsd_filt[c][k];
     } else {

@@ -63,6 +63,8 @@ struct DsdState {  // WavpackStream.dsds
     std::vector<int32_t> value_lookup;
     int32_t filt[2][7];
     int rate_i = 0;
+    int max_prob = 0;       // mode 1: max_probability
+    int32_t prob_ptr = 0;   // mode 1: data index of the probability data
 };
 
 struct Reader {  // System.IO.BinaryReader over the file bytes
@@ -637,6 +639,8 @@ class Framer {
         d.summed.assign((size_t)bins * 256, 0);
         d.prob.assign((size_t)bins * 256, 0);
         int max_probability = data[d.byteptr++];
+        d.max_prob = max_probability;
+        d.prob_ptr = d.byteptr;
         if (max_probability < 0xFF) {
             size_t outptr = 0, outend = d.prob.size();
             while (outptr < outend && d.byteptr < d.data_len) {
@@ -805,6 +809,8 @@ class Framer {
                 memcpy(t + bins * 768, dsd.lookup.data(), bins * 1280);
                 memcpy(t + bins * 2048, dsd.value_lookup.data(), bins * 4);
                 d.dsd_table_off = off;
+                d.dsd_max_prob = dsd.max_prob;
+                d.dsd_prob_off = blob_base + (uint64_t)dsd.data_off + (uint64_t)dsd.prob_ptr;
             } else if (dsd.mode == 3) {  // the kernel builds the ptable from dsd_rate_i (dsd_ptable_init)
                 memcpy(d.dsd_filters, dsd.filt, sizeof(d.dsd_filters));
             }
