@@ -40,14 +40,16 @@ def run(name, files, pcm=None, iters=5, fmt=False):
     ms = b.time(iters)
     # per launch group: end time of each group's kernels from the decode's start
     # (each group on its own stream), median of 3 single decodes
-    b.set_timing(True)
-    gts = []
-    for _ in range(3):
-        b.decode()
-        b.sync()
-        gts.append(b.group_times())
-    b.set_timing(False)
-    group_ms = {g: round(float(np.median([t[g] for t in gts])), 3) for g in gts[0]}
+    group_ms = None
+    if hasattr(b._L, "wvg_batch_group_times"):  # (absent from older A/B builds)
+        b.set_timing(True)
+        gts = []
+        for _ in range(3):
+            b.decode()
+            b.sync()
+            gts.append(b.group_times())
+        b.set_timing(False)
+        group_ms = {g: round(float(np.median([t[g] for t in gts])), 3) for g in gts[0]}
     out = b.download()
     crc = sum(b.result(i).crc_errors for i in range(len(files)) if b.infos[i].open_ok)
     ok = None

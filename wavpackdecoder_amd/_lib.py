@@ -124,7 +124,12 @@ def lib():
         "wvg_stream_close": (None, [vp]),
     }
     for name, (res, args) in sig.items():
-        fn = getattr(L, name)
+        try:
+            fn = getattr(L, name)
+        except AttributeError:
+            if os.environ.get("WVG_LIB"):  # an older experiment build (A/B runs): entry points it lacks stay unbound
+                continue
+            raise
         fn.restype = res
         fn.argtypes = args
     _lib = L
