@@ -52,6 +52,7 @@ using namespace wvg;
 // Every batch owns its streams, so batches of one context (or of several host
 // threads) run concurrently on the device; nothing synchronises the whole device.
 constexpr int kSide = kMaxTermSets + 3;  // term sets, generic PCM, DSD, DSD mode 1
+constexpr int kLanes = kSide;  // streams one decode launches on, at most (WVG_LANES: fewer)
 // The part of a device-framed descriptor the host reads (kind, flags, frames, the
 // call schedule, status, terms): everything up to and including term[].  The rest
 // (weights, histories, DSD, seek, sticky, .wvc, exact float) is zero or unused on
@@ -116,7 +117,7 @@ struct wvg_batch {
     wvg_ctx *ctx = nullptr;
     int chunk = 4096;
     hipStream_t stream = nullptr;          // the batch's own stream (default for decode/format/download)
-    hipStream_t side[kSide] = {nullptr};
+    hipStream_t side[kSide] = {nullptr};   // side streams: lanes 1 .. kLanes - 1 of a decode
     hipEvent_t fork = nullptr, join[kSide] = {nullptr};
     hipEvent_t done = nullptr;             // end of the last decode/format, on whatever stream it ran
     bool timing = false;                   // wvg_batch_set_timing: an event pair around every decode
@@ -134,6 +135,10 @@ struct wvg_batch {
            cap_pcml = 0, cap_dsd = 0, cap_pcm = 0, cap_segs = 0, cap_ts[kMaxTermSets] = {0};
     bool segs_uploaded = false;
     PinnedBuf blob;                                     // every file's bytes, 16-B aligned
+    // the blob goes to the device as it is filled (blob_push): bytes [0, blob_dev)
+    // are in d_blob already, and a DMA from the page-locked blob may be running
+    size_t blob_dev = 0;
+    bool blob_dma = false;
     PinnedBuf hout;                                     // wvg_batch_host_out: the output, downloaded
     PinnedBuf stage;                                    // page-locked copies of an upload's small host arrays
     PinnedBuf hst;                                      // page-locked landing area of the status download
@@ -145,9 +150,11 @@ struct wvg_batch {
     std::vector<uint32_t> pcm_list, dsd_list;           // wave-per-block kernels (generic PCM, DSD)
     uint32_t dsd_fast_lo = 0, dsd_fast_n = 0;          // the mode-1 range of dsd_list (sorted by kind)
     std::vector<uint32_t> ts_list[kMaxTermSets];        // two-wave kernels per term set
+    int64_t gframes[kSide] = {0};                       // frames per launch group (the lane assignment's load)
     uint32_t *d_ts[kMaxTermSets] = {nullptr};
     int force_lane = 0;                                 // WVG_FORCE_LANE=1: every PCM block on the generic kernel
     int prefer_pipe = 0;                                // WVG_PIPE=2: every PCM list on the pipelined kernel (A/B)
+    int lanes = kLanes;                                 // WVG_LANES: streams per decode (A/B of the queue mapping)
     std::vector<uint32_t> h_status, h_aux;
     int64_t bytes_in = 0, frames = 0;
     // format epilogue: per-file byte image of WavpackFormatSamples
@@ -268,6 +275,8 @@ wvg_batch *wvg_batch_new(wvg_ctx *c, int chunk_frames) {
     b->prefer_pipe = pp ? atoi(pp) : 0;
     // the decorr/entropy values of each block are parsed on the device (wv_meta_parse);
     // WVG_HOST_META=1 keeps them on the host framing (A/B comparisons)
+    const char *ln = getenv("WVG_LANES");
+    if (ln && atoi(ln) >= 1) b->lanes = atoi(ln) < kLanes ? atoi(ln) : kLanes;
     const char *rm = getenv("WVG_DFRAME_RANK_MIN");
     if (rm) b->rank_min = atoll(rm);
     const char *hm = getenv("WVG_HOST_META");
@@ -335,6 +344,45 @@ static hipError_t quiesce(wvg_batch *b) {
         if (e == hipSuccess) e = e2;
     }
     return e;
+}
+
+// Grow the page-locked blob: a larger one is a new allocation, so a DMA still
+// reading the old one must finish first.
+static bool blob_resize(wvg_batch *b, size_t n) {
+    if (n > b->blob.cap && b->blob_dma) {
+        hipStreamSynchronize(b->stream);
+        b->blob_dma = false;
+    }
+    return b->blob.resize(n);
+}
+
+// Send the blob bytes copied in since the last push (on the batch stream, ahead
+// of the framing kernels and decodes that read them): the DMA of files added
+// early overlaps the copying and framing of the rest.  A d_blob too small for
+// them is replaced (after anything in flight that reads it) and refilled whole.
+static hipError_t blob_push(wvg_batch *b, size_t upto = (size_t)-1) {
+    // a decode of the earlier files (on a caller's stream) may still read past their
+    // end, where new bytes now land
+    if (b->done) {
+        hipError_t e = hipEventSynchronize(b->done);
+        if (e != hipSuccess) return e;
+    }
+    const size_t need = b->blob.size() + 64;  // the whole blob and the reader's 0xFF tail
+    if (b->cap_blob < need) {
+        hipError_t e = quiesce(b);
+        if (e != hipSuccess) return e;
+        e = ensure(b->d_blob, b->cap_blob, b->cap_blob * 2 > need ? b->cap_blob * 2 : need);
+        if (e != hipSuccess) return e;
+        b->blob_dev = 0;
+    }
+    const size_t n = upto < b->blob.size() ? upto : b->blob.size();
+    if (n <= b->blob_dev) return hipSuccess;
+    hipError_t e = hipMemcpyAsync(b->d_blob + b->blob_dev, b->blob.data() + b->blob_dev, n - b->blob_dev,
+                                  hipMemcpyHostToDevice, b->stream);
+    if (e != hipSuccess) return e;
+    b->blob_dev = n;
+    b->blob_dma = true;
+    return hipSuccess;
 }
 
 void wvg_batch_free(wvg_batch *b) {
@@ -437,7 +485,7 @@ static int add_file(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open
     if (!b || (!file && len)) return WVG_ERR_ARG;
     b->uploaded = b->formatted = false;
     size_t base = (b->blob.size() + 15) & ~(size_t)15;
-    if (!b->blob.resize(base + len)) {
+    if (!blob_resize(b, base + len)) {
         b->ctx->err = "out of host memory";
         return WVG_ERR_ARG;
     }
@@ -452,6 +500,8 @@ int wvg_batch_reset(wvg_batch *b) {
     hipSetDevice(b->ctx->device);
     quiesce(b);  // nothing in flight reads the old contents (on the batch's or a caller's stream)
     b->blob.resize(0);
+    b->blob_dev = 0;
+    b->blob_dma = false;
     const bool defer = b->fo.defer_values;
     b->fo = FramingOutput();
     b->fo.defer_values = defer;
@@ -545,12 +595,14 @@ int wvg_batch_add_files(wvg_batch *b, int n, const uint8_t *const *files, const 
         base[(size_t)i] = (end + 15) & ~(size_t)15;
         end = base[(size_t)i] + lens[i];
     }
-    if (!b->blob.resize(end)) {
+    if (!blob_resize(b, end)) {
         b->ctx->err = "out of host memory";
         return WVG_ERR_ARG;
     }
     for (int i = 0; i < n; i++)
         if (lens[i]) memcpy(b->blob.data() + base[(size_t)i], files[i], lens[i]);
+    HIPCHK(b->ctx, hipSetDevice(b->ctx->device));
+    HIPCHK(b->ctx, blob_push(b));  // the DMA runs while the host threads frame the files
     std::vector<size_t> ln(lens, lens + n);
     std::vector<FramingOutput> fos;
     std::vector<FileInfo> fis;
@@ -571,7 +623,7 @@ int wvg_batch_add_file_wvc(wvg_batch *b, const uint8_t *file, size_t len, const 
     b->uploaded = b->formatted = false;
     const size_t base = (b->blob.size() + 15) & ~(size_t)15;
     const size_t cbase = (base + len + 15) & ~(size_t)15;
-    if (!b->blob.resize(cbase + wvc_len)) {
+    if (!blob_resize(b, cbase + wvc_len)) {
         b->ctx->err = "out of host memory";
         return WVG_ERR_ARG;
     }
@@ -603,12 +655,16 @@ int wvg_batch_add_files_device(wvg_batch *b, int n, const uint8_t *const *files,
         base[(size_t)i] = (end + 15) & ~(size_t)15;
         end = base[(size_t)i] + lens[i];
     }
-    if (!b->blob.resize(end)) {
+    if (!blob_resize(b, end)) {
         b->ctx->err = "out of host memory";
         return WVG_ERR_ARG;
     }
+    HIPCHK(b->ctx, hipSetDevice(b->ctx->device));
     for (int i = 0; i < n; i++) {
         if (lens[i]) memcpy(b->blob.data() + base[(size_t)i], files[i], lens[i]);
+        // send every few MiB: the DMA of the first files overlaps the copying of the rest
+        if (base[(size_t)i] + lens[i] >= b->blob_dev + ((size_t)8 << 20))
+            HIPCHK(b->ctx, blob_push(b, base[(size_t)i] + lens[i]));
         const int idx = (int)b->infos.size();
         FileInfo fi;
         fi.error = "not framed yet (wvg_batch_upload frames it)";
@@ -697,7 +753,7 @@ static int device_frame(wvg_batch *b, hipStream_t s) {
     }
     const size_t nb = bf.size();
     std::vector<DBlock> recs(nb);
-    std::vector<BlockDesc> dd(nb);
+    const uint8_t *heads = nullptr;  // each device descriptor's first kDescHead bytes (staging)
     if (nb && !b->dev_runs.empty()) {
         // an earlier device framing of this batch left descriptors in d_ddescs, which
         // this pass reuses: bring them to the host first (files added after an upload
@@ -737,12 +793,10 @@ static int device_frame(wvg_batch *b, hipStream_t s) {
         HIPCHK(c, hipMemcpyAsync(hd + kDescHead * nb, b->d_drecs, sizeof(DBlock) * nb, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
         tp[3] = now_ms();
-        for (size_t k = 0; k < nb; k++) {
-            memset(&dd[k], 0, sizeof(BlockDesc));
-            memcpy(&dd[k], hd + kDescHead * k, kDescHead);
-        }
+        heads = hd;
         memcpy(recs.data(), hd + kDescHead * nb, sizeof(DBlock) * nb);
     }
+    b->fo.descs.reserve(b->fo.descs.size() + nb);
     // commit: the accepted files at their reserved output ranges, in file order
     std::vector<size_t> host;
     for (size_t i = 0; i < nf; i++) {
@@ -752,8 +806,9 @@ static int device_frame(wvg_batch *b, hipStream_t s) {
         fi.first_desc = (int64_t)b->fo.descs.size();
         if (df[i].regular && dframe_file_info(df[i], recs.data() + blk0[i], fi)) {
             const size_t dst = b->fo.descs.size();
-            b->fo.descs.insert(b->fo.descs.end(), dd.begin() + (ptrdiff_t)blk0[i],
-                               dd.begin() + (ptrdiff_t)(blk0[i] + df[i].nblocks));
+            b->fo.descs.resize(dst + df[i].nblocks);  // zeroed; the host's view is each head
+            for (uint32_t k = 0; k < df[i].nblocks; k++)
+                memcpy(&b->fo.descs[dst + k], heads + kDescHead * (blk0[i] + k), kDescHead);
             if (!b->dev_runs.empty() && b->dev_runs.back().dst + b->dev_runs.back().n == dst &&
                 b->dev_runs.back().src + b->dev_runs.back().n == blk0[i])
                 b->dev_runs.back().n += df[i].nblocks;  // contiguous with the previous file's
@@ -813,10 +868,9 @@ int wvg_batch_upload(wvg_batch *b) {
     const double t_up0 = now_ms();
     b->formatted = false;
     // the blob is followed by 64 B of 0xFF (the reader's past-end fill)
-    const size_t blob_n = b->blob.size() + 64;
-    HIPCHK(c, ensure(b->d_blob, b->cap_blob, blob_n));
+    HIPCHK(c, blob_push(b));  // what the adds have not sent yet
+    if (!b->d_blob) HIPCHK(c, ensure(b->d_blob, b->cap_blob, 64));
     HIPCHK(c, hipMemsetAsync(b->d_blob + b->blob.size(), 0xFF, 64, s));
-    if (!b->blob.empty()) HIPCHK(c, hipMemcpyAsync(b->d_blob, b->blob.data(), b->blob.size(), hipMemcpyHostToDevice, s));
     if (!b->dfiles.empty()) {
         const int rc = device_frame(b, s);
         if (rc != WVG_OK) return rc;
@@ -900,6 +954,14 @@ int wvg_batch_upload(wvg_batch *b) {
         HIPCHK(c, put(b->d_ts[t], L.data(), sizeof(uint32_t) * L.size()));
     }
     if (soff > need) return WVG_ERR_SPACE;  // (cannot happen: the sizes above cover every put)
+    // frames per launch group: the load the decode's lane assignment balances
+    auto frames_of = [&](const std::vector<uint32_t> &L) {
+        int64_t f = 0;
+        for (uint32_t k : L) f += b->fo.descs[k].nframes;
+        return f;
+    };
+    for (int t = 0; t < kMaxTermSets; t++) b->gframes[t] = frames_of(b->ts_list[t]);
+    b->gframes[kMaxTermSets] = frames_of(b->pcm_list);
     HIPCHK(c, hipStreamSynchronize(s));  // the blob may change after this call
     if (trace) fprintf(stderr, "upload: %.3f ms (%zu blocks)\n", now_ms() - t_up0, nd);
     b->uploaded = true;
@@ -949,50 +1011,93 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
         b->tev.push_back(e1);
         HIPCHK(c, hipEventRecord(e0, s));
     }
-    // one stream slot per non-empty launch group: DSD, DSD mode 1, generic PCM,
-    // term sets 0..7.  DSD first (streams are created, and kernels submitted, in
-    // this order): its blocks are the longest serial chains, and streams beyond
-    // the hardware queues share a queue with the ones created before them.
+    // The non-empty launch groups (DSD, DSD mode 1, generic PCM, term sets 0..7)
+    // go onto at most kLanes streams: the batch stream and side streams.  A
+    // process has kLanes hardware queues (GPU_MAX_HW_QUEUES); streams beyond them
+    // share a queue, whose kernels then run one after another -- a PCM group
+    // queued behind the DSD group (its mode-3 blocks are the batch's longest
+    // serial chains) would wait for all of it.  So with more groups than lanes
+    // the DSD groups keep lanes of their own and the PCM groups share the rest,
+    // the largest first onto the least loaded (frames as the load).
+    const int kDsd = kMaxTermSets + 1, kDsd1 = kMaxTermSets + 2, kPcm = kMaxTermSets;
     int used[kSide], n = 0;
-    if (!b->dsd_list.empty()) used[n++] = kMaxTermSets + 1;
-    if (b->dsd_fast_n) used[n++] = kMaxTermSets + 2;
-    if (!b->pcm_list.empty()) used[n++] = kMaxTermSets;
+    if (!b->dsd_list.empty() && b->dsd_fast_n < b->dsd_list.size()) used[n++] = kDsd;
+    if (b->dsd_fast_n) used[n++] = kDsd1;
+    if (!b->pcm_list.empty()) used[n++] = kPcm;
     for (int t = 0; t < kMaxTermSets; t++)
         if (!b->ts_list[t].empty()) used[n++] = t;
-    auto slot = [&](int g) -> hipStream_t { return n > 1 ? b->side[g] : s; };
-    for (int i = 0; n > 1 && i < n; i++) {
-        const int g = used[i];
-        if (!b->side[g]) {
-            HIPCHK(c, hipStreamCreateWithFlags(&b->side[g], hipStreamNonBlocking));
-            HIPCHK(c, hipEventCreateWithFlags(&b->join[g], hipEventDisableTiming));
+    int lane_of[kSide];
+    const int nlanes = b->lanes;
+    const int nl = n < nlanes ? n : nlanes;
+    if (n <= nlanes) {
+        for (int i = 0; i < n; i++) lane_of[used[i]] = i;
+    } else {
+        int64_t load[kSide] = {0};
+        int first = 0;  // lanes before it are reserved for the DSD groups
+        for (int i = 0; i < n; i++)
+            if (used[i] == kDsd || used[i] == kDsd1) lane_of[used[i]] = first++;
+        if (first >= nl) first = 0;
+        int pcm[kSide], np = 0;
+        for (int i = 0; i < n; i++)
+            if (used[i] != kDsd && used[i] != kDsd1) pcm[np++] = used[i];
+        std::sort(pcm, pcm + np, [&](int x, int y) { return b->gframes[x] > b->gframes[y]; });
+        for (int i = 0; i < np; i++) {
+            int best = first;
+            for (int l = first; l < nl; l++)
+                if (load[l] < load[best]) best = l;
+            lane_of[pcm[i]] = best;
+            load[best] += b->gframes[pcm[i]];
         }
     }
-    if (n > 1) {
-        HIPCHK(c, hipEventRecord(b->fork, s));
-        for (int i = 0; i < n; i++) HIPCHK(c, hipStreamWaitEvent(b->side[used[i]], b->fork, 0));
+    for (int l = 1; l < nl; l++) {
+        if (!b->side[l - 1]) {
+            HIPCHK(c, hipStreamCreateWithFlags(&b->side[l - 1], hipStreamNonBlocking));
+            HIPCHK(c, hipEventCreateWithFlags(&b->join[l - 1], hipEventDisableTiming));
+        }
     }
-    HIPCHK(c, launch_decode(b->d_descs, b->d_pcml, (uint32_t)b->pcm_list.size(), b->d_dsd, (uint32_t)b->dsd_list.size(),
-                            b->dsd_fast_lo, b->dsd_fast_n, b->d_blob, b->d_tables, b->d_out, b->d_status, b->d_mute,
-                            slot(kMaxTermSets), slot(kMaxTermSets + 1), slot(kMaxTermSets + 2)));
-    for (int t = 0; t < kMaxTermSets; t++)
-        if (!b->ts_list[t].empty())
-            HIPCHK(c, launch_2wave(t, b->d_descs, b->d_ts[t], (uint32_t)b->ts_list[t].size(), b->d_blob, b->d_out,
-                                   b->d_status, b->d_mute, slot(t)));
-    if (b->timing) {  // per-group end times of this decode (one group: it ran on s)
+    auto lane = [&](int l) -> hipStream_t { return l == 0 ? s : b->side[l - 1]; };
+    auto slot = [&](int g) -> hipStream_t {
+        for (int i = 0; i < n; i++)
+            if (used[i] == g) return lane(lane_of[g]);
+        return s;  // (an empty group launches nothing)
+    };
+    if (nl > 1) {
+        HIPCHK(c, hipEventRecord(b->fork, s));
+        for (int l = 1; l < nl; l++) HIPCHK(c, hipStreamWaitEvent(lane(l), b->fork, 0));
+    }
+    if (b->timing) {
         b->gstart = b->tev[b->tev.size() - 2];
         b->gmask = 0;
-        for (int i = 0; i < n; i++) {
-            const int g = used[i];
-            if (!b->gev[g]) HIPCHK(c, hipEventCreate(&b->gev[g]));
-            HIPCHK(c, hipEventRecord(b->gev[g], slot(g)));
-            b->gmask |= 1u << g;
-        }
     }
-    if (n > 1) {
+    // per-group end times (timing on): an event on the group's lane right after its launch
+    auto mark = [&](int g) -> hipError_t {
+        if (!b->timing) return hipSuccess;
         for (int i = 0; i < n; i++) {
-            HIPCHK(c, hipEventRecord(b->join[used[i]], b->side[used[i]]));
-            HIPCHK(c, hipStreamWaitEvent(s, b->join[used[i]], 0));
+            if (used[i] != g) continue;
+            if (!b->gev[g]) {
+                hipError_t e = hipEventCreate(&b->gev[g]);
+                if (e != hipSuccess) return e;
+            }
+            b->gmask |= 1u << g;
+            return hipEventRecord(b->gev[g], slot(g));
         }
+        return hipSuccess;
+    };
+    HIPCHK(c, launch_decode(b->d_descs, b->d_pcml, (uint32_t)b->pcm_list.size(), b->d_dsd, (uint32_t)b->dsd_list.size(),
+                            b->dsd_fast_lo, b->dsd_fast_n, b->d_blob, b->d_tables, b->d_out, b->d_status, b->d_mute,
+                            slot(kPcm), slot(kDsd), slot(kDsd1)));
+    HIPCHK(c, mark(kDsd));
+    HIPCHK(c, mark(kDsd1));
+    HIPCHK(c, mark(kPcm));
+    for (int t = 0; t < kMaxTermSets; t++)
+        if (!b->ts_list[t].empty()) {
+            HIPCHK(c, launch_2wave(t, b->d_descs, b->d_ts[t], (uint32_t)b->ts_list[t].size(), b->d_blob, b->d_out,
+                                   b->d_status, b->d_mute, slot(t)));
+            HIPCHK(c, mark(t));
+        }
+    for (int l = 1; l < nl; l++) {
+        HIPCHK(c, hipEventRecord(b->join[l - 1], lane(l)));
+        HIPCHK(c, hipStreamWaitEvent(s, b->join[l - 1], 0));
     }
     HIPCHK(c, launch_dsd_fill(b->d_descs, b->d_dsd, (uint32_t)b->dsd_list.size(), b->d_status, b->d_mute, b->d_out, s));
     if (b->timing) HIPCHK(c, hipEventRecord(b->tev.back(), s));

@@ -40,6 +40,7 @@
 #include "wv_wave2.h"
 #include "wv_pipe.h"
 
+
 namespace wvg {
 
 // One 64-lane wave per block: every value derives from blockIdx.x, so the
@@ -335,23 +336,6 @@ __device__ __forceinline__ uint64_t dsd_decide(uint32_t value, uint32_t s, uint3
     return zm;
 }
 
-// dsd_decide without the lane mask: the outcome is only the next bit of b
-__device__ __forceinline__ void dsd_decide_b(uint32_t value, uint32_t s, uint32_t &high, uint32_t &low, uint32_t &b) {
-    uint32_t t, t1;
-    asm("s_sub_u32 %[t], %[hi], %[lo]\n\t"
-        "s_lshr_b32 %[t], %[t], 8\n\t"
-        "s_mul_i32 %[t], %[t], %[s]\n\t"
-        "s_add_u32 %[t], %[t], %[lo]\n\t"
-        "s_add_u32 %[t1], %[t], 1\n\t"
-        "s_cmp_le_u32 %[v], %[t]\n\t"
-        "s_cselect_b32 %[hi], %[t], %[hi]\n\t"
-        "s_cselect_b32 %[lo], %[lo], %[t1]\n\t"
-        "s_addc_u32 %[b], %[b], %[b]"
-        : [hi] "+s"(high), [lo] "+s"(low), [b] "+s"(b), [t] "=&s"(t), [t1] "=&s"(t1)
-        : [v] "s"(value), [s] "s"(s)
-        : "scc");
-}
-
 // Stereo mode 3: lane 0 holds channel 0's filter state and lane 1 channel
 // 1's, so one VALU instruction updates both channels (the chains are
 // independent; only the range coder and the ptable are shared).  A lone wave issues
@@ -410,77 +394,51 @@ __device__ __forceinline__ DsdResult dsd_high_v2(const BlockDesc &d, const uint8
                 for (int bit = 0; bit < 8; bit++) {
                     const uint32_t addr = ((uint32_t)q0 >> 6) & 0x3FCu;
                     int32_t pv = *(const int32_t *)(lds + addr);
-                    // the read is issued first (it cannot pass the memory clobber) and the filter
-                    // state "changes" after it, so none of the work below is scheduled ahead of it
-                    asm volatile("" : "+v"(q0), "+v"(q2), "+v"(q3), "+v"(q4), "+v"(q5), "+v"(q6), "+v"(q7), "+v"(q8)
-                                 : : "memory");
-                    // The whole filter update, before the decisions, under the LDS latency: it is
-                    // the bit-0 outcome plus a constant times the outcome (see above), so after
-                    // the decisions only q0's product and the ptable update remain on the chain.
+                    // decision-independent work, under the LDS latency
                     const int32_t v = add32(q0, shl32(q7, 3));
                     int32_t t;  // q0 - 8 * filter6, one 24-bit multiply-add
                     asm("v_mad_i32_i24 %0, %1, -8, %2" : "=v"(t) : "v"(q7), "v"(q0));
                     const int32_t sx = (v ^ t) >> 31;
-                    const int32_t dz0 = sx & ((v >> 31) | 1);  // factor step for filter0 = 0; -dz0 for -1
-                    const int32_t q8a = add32(q8, dz0), dq = sub32(0, shl32(dz0, 1));  // q8 + dz0 - 2 dz0 z
-                    const int32_t q2p = add32(q2, sub32(0, q2) >> 6);
-                    const int32_t q3p = add32(q3, sub32(0, q3) >> 4);
-                    const int32_t q4p = add32(q4, sub32(q3p, q4) >> 4);
-                    const int32_t q5p = add32(q5, sub32(q4p, q5) >> 4);
-                    const int32_t ddp = sub32(q5p, q6) >> 4;
-                    const int32_t q6p = add32(q6, ddp);
-                    const int32_t q7p = add32(q7, sub32(ddp, q7) >> 3);
-                    const int32_t d26 = sub32(q2p, q6p);
-                    // computed before the first use of pv, i.e. while the read is in flight
-                    asm volatile("" : "+v"(pv) : "v"(q8a), "v"(dq), "v"(q3p), "v"(q4p), "v"(q5p), "v"(q6p), "v"(q7p),
-                                 "v"(d26), "v"(q2p));
+                    const int32_t w = v >> 31;
+                    const int32_t dz0 = sx & (w | 1), dz1 = sx & (~w | 1);  // factor step for filter0 = 0 / -1
+                    const int32_t a20 = sub32(0, q2) >> 6, a21 = sub32(1 << 20, q2) >> 6;
+                    const int32_t a30 = sub32(0, q3) >> 4, a31 = sub32(1 << 20, q3) >> 4;
+                    // computed before the first use of pv, i.e. while the read is in flight (the
+                    // compiler would otherwise sink them past the decisions and wait at once)
+                    asm volatile("" : "+v"(pv) : "v"(dz0), "v"(dz1), "v"(a20), "v"(a21), "v"(a30), "v"(a31));
                     const uint32_t pa0 = (uint32_t)__builtin_amdgcn_readlane((int32_t)addr, 0);
                     const uint32_t pa1 = (uint32_t)__builtin_amdgcn_readlane((int32_t)addr, 1);
                     // channel 0's decision
                     const uint32_t ps = (uint32_t)pv >> 16;
                     const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane((int32_t)ps, 0);
                     uint32_t s1 = (uint32_t)__builtin_amdgcn_readlane((int32_t)ps, 1);
-                    dsd_decide_b(value, s0, high, low, b0);
+                    const uint64_t zm0 = dsd_decide(value, s0, high, low, b0, kEven);
+                    const bool z0 = zm0 != 0;
                     int32_t pvl = pv;
                     uint32_t wa = addr;
                     if (__builtin_expect(pa0 == pa1, 0)) {  // channel 1 reads channel 0's updated entry
                         const int32_t p0 = __builtin_amdgcn_readlane(pv, 0);
-                        const int32_t np0 = p0 + ((((b0 & 1u) ? kUp : kDown) - p0) >> 8);
+                        const int32_t np0 = p0 + (((z0 ? kUp : kDown) - p0) >> 8);
                         s1 = (uint32_t)np0 >> 16;
                         pvl = ch ? np0 : pv;
                         wa = ch ? addr : 1024u;
                     }
                     if (__builtin_expect((high ^ low) < 0x1000000u, 0)) dsd_renorm(src, bp, dlen, value, high, low);
                     // channel 1's decision
-                    dsd_decide_b(value, s1, high, low, b1);
+                    const uint64_t zm1 = dsd_decide(value, s1, high, low, b1, ~kEven);
                     if (__builtin_expect((high ^ low) < 0x1000000u, 0)) dsd_renorm(src, bp, dlen, value, high, low);
-                    // this lane's channel's outcome as 0 / 1: bit `ch` of (b1 bit 0) : (b0 bit 0)
-                    uint32_t cb, z;
-                    asm("s_and_b32 %[cb], %[b0], 1\n\t"
-                        "s_lshl1_add_u32 %[cb], %[b1], %[cb]"
-                        : [cb] "=&s"(cb) : [b0] "s"(b0), [b1] "s"(b1) : "scc");
-                    asm("v_bfe_u32 %0, %1, %2, 1" : "=v"(z) : "s"(cb), "v"(ch));
-                    int32_t q0n, tmp;
-                    // q2 - q6 = d26 + (2^14 - 2^4) z; the other filters move by z << k
-                    asm("v_lshl_add_u32 %[q7], %[z], 1, %[q7p]\n\t"
-                        "v_mad_i32_i24 %[q8], %[z], %[dq], %[q8a]\n\t"
-                        "v_mad_u32_u24 %[q0n], %[z], %[k26], %[d26]\n\t"
-                        "v_mul_i32_i24 %[tmp], %[q7], %[q8]\n\t"
-                        "v_ashrrev_i32 %[tmp], 2, %[tmp]\n\t"
-                        "v_add_u32 %[q0n], %[q0n], %[tmp]"
-                        : [q7] "=&v"(q7), [q8] "=&v"(q8), [q0n] "=&v"(q0n), [tmp] "=&v"(tmp)
-                        : [z] "v"(z), [q7p] "v"(q7p), [q8a] "v"(q8a), [dq] "v"(dq), [d26] "v"(d26),
-                          [k26] "s"(16368));
-                    q0 = q0n;
-                    // ptable update: kDown + z (kUp - kDown)
-                    int32_t kz;
-                    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(kz) : "v"(z), "s"(kUp - kDown), "v"(kDown));
-                    *(int32_t *)(lds + wa) = pvl + ((kz - pvl) >> 8);
-                    asm("v_lshl_add_u32 %0, %1, 14, %2" : "=v"(q2) : "v"(z), "v"(q2p));
-                    asm("v_lshl_add_u32 %0, %1, 16, %2" : "=v"(q3) : "v"(z), "v"(q3p));
-                    asm("v_lshl_add_u32 %0, %1, 12, %2" : "=v"(q4) : "v"(z), "v"(q4p));
-                    asm("v_lshl_add_u32 %0, %1, 8, %2" : "=v"(q5) : "v"(z), "v"(q5p));
-                    asm("v_lshl_add_u32 %0, %1, 4, %2" : "=v"(q6) : "v"(z), "v"(q6p));
+                    // this lane's channel's outcome
+                    const bool zl = __builtin_amdgcn_inverse_ballot_w64(zm0 | zm1);
+                    *(int32_t *)(lds + wa) = pvl + (((zl ? kUp : kDown) - pvl) >> 8);
+                    q8 = add32(q8, zl ? dz1 : dz0);
+                    q2 = add32(q2, zl ? a21 : a20);
+                    q3 = add32(q3, zl ? a31 : a30);
+                    q4 = add32(q4, sub32(q3, q4) >> 4);
+                    q5 = add32(q5, sub32(q4, q5) >> 4);
+                    const int32_t dd = sub32(q5, q6) >> 4;
+                    q6 = add32(q6, dd);
+                    q7 = add32(q7, sub32(dd, q7) >> 3);
+                    q0 = add32(sub32(q2, q6), __mul24(q7, q8) >> 2);
                 }
                 const int32_t v0 = (int32_t)(b0 & 0xFFu), v1 = (int32_t)(b1 & 0xFFu);
                 q8 = sub32(q8, add32(q8, 512) >> 10);
@@ -812,20 +770,7 @@ __device__ __forceinline__ DsdResult dsd_fast_v2(const BlockDesc &d, const uint8
                         if (mult == 0) { chunk_ok = false; break; }
                     }
                     const uint32_t x = value - low;
-                    // the products are full-rate 24-bit multiplies when mult < 2^24 (any bin with a
-                    // total >= 256; the counts are 16-bit), else quarter-rate 32-bit ones
-                    uint32_t q0, q1, q2, q3;
-                    if (__builtin_expect(mult < 0x1000000u, 1)) {
-                        q0 = __umul24(row.x, mult);
-                        q1 = __umul24(row.y, mult);
-                        q2 = __umul24(row.z, mult);
-                        q3 = __umul24(row.w, mult);
-                    } else {
-                        q0 = row.x * mult;
-                        q1 = row.y * mult;
-                        q2 = row.z * mult;
-                        q3 = row.w * mult;
-                    }
+                    const uint32_t q0 = row.x * mult, q1 = row.y * mult, q2 = row.z * mult, q3 = row.w * mult;
                     const bool c0 = q0 <= x, c1 = q1 <= x, c2 = q2 <= x, c3 = q3 <= x;
                     const uint32_t code = (uint32_t)(__popcll(__ballot(c0)) + __popcll(__ballot(c1)) +
                                                      __popcll(__ballot(c2)) + __popcll(__ballot(c3)));
@@ -902,18 +847,38 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
 // The framing ran the reference's checks on the same bytes (the data fills
 // exactly bins x 256 entries, the totals are in range), so the wave decodes 64
 // codes per step: a prefix sum of their run lengths gives each value its entry.
-// Codes read past the terminating one (at most 63 bytes) stay inside the blob.
-__device__ __forceinline__ void dsd_fast_tables(const BlockDesc &d, const uint8_t *blob, uint32_t bins, uint32_t *tab) {
+// Codes read past the terminating one (at most 63 bytes) stay inside the blob
+// (the value bytes and the payload follow).
+constexpr uint32_t kDsdProbStage = 8192u + 256u;  // bytes: up to 32 x 256 codes + the end codes + over-read
+__device__ __forceinline__ void dsd_fast_tables(const BlockDesc &d, const uint8_t *blob, uint32_t bins, uint32_t *tab,
+                                                uint32_t *stg) {
     const uint32_t lane = threadIdx.x;
     const uint32_t ne = bins * 256u;
-    const uint8_t *pd = blob + d.dsd_prob_off;
+    // the probability data (up to the 4 value bytes at bits_off) staged in LDS with
+    // dword loads, all in flight together, instead of a byte load per code step
+    const uint64_t a0 = d.dsd_prob_off & ~(uint64_t)3;
+    const uint32_t sh = (uint32_t)(d.dsd_prob_off & 3);
+    const uint64_t nb = d.bits_off > d.dsd_prob_off ? d.bits_off - d.dsd_prob_off : 0;
+    const bool staged = nb + sh + 64u + 4u <= kDsdProbStage;
+    if (staged) {
+        const uint32_t nd = (uint32_t)((sh + nb + 64u + 3u) / 4u);  // + the codes read past the end
+        const uint32_t *g = (const uint32_t *)(blob + a0);
+#pragma unroll 8
+        for (uint32_t i = lane; i < nd; i += 64) stg[i] = g[i];
+        __syncthreads();
+    }
+    auto byte_at = [&](uint32_t k) -> uint32_t {
+        if (!staged) return blob[d.dsd_prob_off + k];
+        const uint32_t q = sh + k;
+        return (stg[q >> 2] >> ((q & 3u) * 8u)) & 0xFFu;
+    };
     if (d.dsd_max_prob < 0xFF) {
         const uint32_t maxp = (uint32_t)d.dsd_max_prob;
         for (uint32_t i = lane; i < ne; i += 64) tab[i] = 0;
         __syncthreads();
         uint32_t outptr = 0, p = 0;
         while (outptr < ne) {
-            const uint32_t c = pd[p + lane];
+            const uint32_t c = byte_at(p + lane);
             const uint32_t len = c > maxp ? c - maxp : (c != 0 ? 1u : 0u);
             const uint32_t incl = wave_incl_scan(len);
             // the loop ends at the first 0 code, or once the entries are all filled
@@ -925,7 +890,7 @@ __device__ __forceinline__ void dsd_fast_tables(const BlockDesc &d, const uint8_
             if (ev) break;
         }
     } else {
-        for (uint32_t i = lane; i < ne; i += 64) tab[i] = pd[i];
+        for (uint32_t i = lane; i < ne; i += 64) tab[i] = byte_at(i);
     }
     __syncthreads();
     // running sums per bin: lane l holds entries 4l .. 4l + 3 of the row
@@ -957,13 +922,14 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_fast(const BlockD
                                                                     uint32_t *__restrict__ status,
                                                                     uint32_t *__restrict__ mute_chunk) {
     __shared__ uint32_t tab[kDsdFastLds / 4];
+    __shared__ uint32_t stg[kDsdProbStage / 4];
     const uint32_t bi = list[blockIdx.x];
     const BlockDesc &d = descs[bi];
     const bool lead = threadIdx.x == 0;
     const uint32_t bins = (uint32_t)d.dsd_history_bins;
     DevStoreWave st{out + d.out_off, (uint64_t)d.pre_end * d.out_nch, lead};
     DsdResult r;
-    if (bins <= 32u) dsd_fast_tables(d, blob, bins, tab);
+    if (bins <= 32u) dsd_fast_tables(d, blob, bins, tab, stg);
     // lane b: bin b's total and the reciprocal constants of dividing by it
     uint32_t vmag = 0, vsh1 = 0, vsh2 = 0;  // all zero for an empty bin (see dsd_fast_v2)
     if (threadIdx.x < bins && bins <= 32u) {
