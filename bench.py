@@ -46,6 +46,11 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+# one stream per launch group and several batches in flight: more hardware
+# queues than HIP's default 4 (set before anything initialises HIP; wvg_open does
+# the same when it is the first HIP call)
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec

@@ -27,10 +27,15 @@ For throughput use DecodeBatch: many files, one upload, one decode.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 
-from . import _lib as _L
+# more hardware queues than HIP's default 4 for the per-group streams (wv_api.cpp
+# wvg_open); only effective before the process's first HIP call
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+
+from . import _lib as _L  # noqa: E402
 
 SAMPLE_BUFFER_SIZE = 4096  # Defines.cs:18
 OPEN_2CH_MAX = 0x8         # Defines.cs:26

@@ -222,6 +222,13 @@ static hipError_t ensure(T *&p, size_t &cap, size_t bytes) {
 extern "C" {
 
 wvg_ctx *wvg_open(int device) {
+    // A decode launches one kernel group per stream (term sets, generic PCM, DSD,
+    // DSD mode 1) and keeps several batches in flight; HIP's default of 4 hardware
+    // queues per process makes streams share queues, and a queue runs its kernels
+    // one after another (a mixed batch then waits for its DSD mode-3 chains before
+    // the PCM groups queued behind them).  Ask for 16 unless the host chose a value;
+    // it takes effect only when this is the process's first HIP call.
+    setenv("GPU_MAX_HW_QUEUES", "16", 0);
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return nullptr;
     if (device < 0) hipGetDevice(&device);
@@ -1012,13 +1019,13 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
         HIPCHK(c, hipEventRecord(e0, s));
     }
     // The non-empty launch groups (DSD, DSD mode 1, generic PCM, term sets 0..7)
-    // go onto at most kLanes streams: the batch stream and side streams.  A
-    // process has kLanes hardware queues (GPU_MAX_HW_QUEUES); streams beyond them
-    // share a queue, whose kernels then run one after another -- a PCM group
-    // queued behind the DSD group (its mode-3 blocks are the batch's longest
-    // serial chains) would wait for all of it.  So with more groups than lanes
-    // the DSD groups keep lanes of their own and the PCM groups share the rest,
-    // the largest first onto the least loaded (frames as the load).
+    // each go onto a stream of their own (lanes: the batch stream and side
+    // streams).  Streams beyond the process's hardware queues (GPU_MAX_HW_QUEUES,
+    // raised to 16 by wvg_open) share a queue, whose kernels then run one after
+    // another -- a PCM group queued behind the DSD group (its mode-3 blocks are
+    // the batch's longest serial chains) waits for all of it.  With fewer lanes
+    // than groups (WVG_LANES, A/B) the DSD groups keep lanes of their own and the
+    // PCM groups share the rest, the largest first onto the least loaded.
     const int kDsd = kMaxTermSets + 1, kDsd1 = kMaxTermSets + 2, kPcm = kMaxTermSets;
     int used[kSide], n = 0;
     if (!b->dsd_list.empty() && b->dsd_fast_n < b->dsd_list.size()) used[n++] = kDsd;

@@ -849,6 +849,9 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
 // codes per step: a prefix sum of their run lengths gives each value its entry.
 // Codes read past the terminating one (at most 63 bytes) stay inside the blob
 // (the value bytes and the payload follow).
+#ifndef WV_M1_HOSTTAB
+#define WV_M1_HOSTTAB 0
+#endif
 constexpr uint32_t kDsdProbStage = 8192u + 256u;  // bytes: up to 32 x 256 codes + the end codes + over-read
 __device__ __forceinline__ void dsd_fast_tables(const BlockDesc &d, const uint8_t *blob, uint32_t bins, uint32_t *tab,
                                                 uint32_t *stg) {
@@ -929,7 +932,16 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_fast(const BlockD
     const uint32_t bins = (uint32_t)d.dsd_history_bins;
     DevStoreWave st{out + d.out_off, (uint64_t)d.pre_end * d.out_nch, lead};
     DsdResult r;
+#if WV_M1_HOSTTAB  // measurement build only: the host framing's tables (host-framed blocks)
+    {
+        const uint16_t *sum16 = (const uint16_t *)(tables + d.dsd_table_off + (size_t)bins * 256u);
+        const uint32_t ne = bins <= 32u ? bins * 256u : 0u;
+        for (uint32_t i = threadIdx.x; i < ne; i += 64) tab[i] = sum16[i];
+        __syncthreads();
+    }
+#else
     if (bins <= 32u) dsd_fast_tables(d, blob, bins, tab, stg);
+#endif
     // lane b: bin b's total and the reciprocal constants of dividing by it
     uint32_t vmag = 0, vsh1 = 0, vsh2 = 0;  // all zero for an empty bin (see dsd_fast_v2)
     if (threadIdx.x < bins && bins <= 32u) {

@@ -2067,6 +2067,9 @@ __device__ __forceinline__ void scalar_prefetch(uint32_t &pf, cdw_ptr base, uint
     pf = (o3 + 64u) & ~63u;
 }
 
+#ifndef WV_RECON_NOP
+#define WV_RECON_NOP 0
+#endif
 // LAYOUT 0: stereo; 1: mono (MONO_FLAG); 2: FALSE_STEREO (mono decode, 2 ints/frame)
 template <int LAYOUT, int... Ts>
 __device__ __forceinline__ void recon_impl(const BlockDesc &d, const uint8_t *blob, Shared &sh, int32_t *out_base, uint32_t *status_out,
@@ -2148,7 +2151,11 @@ __device__ __forceinline__ void recon_impl(const BlockDesc &d, const uint8_t *bl
                              (sm.chunk_end - 1 >= t0 && sm.chunk_end - 1 <= tlast);
         const bool quirk_in =
             MONO && (sm.crc_stop || (sm.bsp > 0 && sm.chunk_end - sm.bsp >= t0 && sm.chunk_end - sm.bsp <= tlast));
+#if WV_RECON_NOP  // measurement build only: the parser's throughput with a reconstruction that does nothing
+        if (false) {
+#else
         if (tvalid == t0 + BF && !seam_in && !quirk_in) {
+#endif
             if (joint) {
                 if (ident) recon_batch<LAYOUT, true, true, true>(ch, fx, sh.res, rbase, o0, o1, crc, ml, t0, tvalid, sm, mute_at, lane, cb);
                 else recon_batch<LAYOUT, true, true, false>(ch, fx, sh.res, rbase, o0, o1, crc, ml, t0, tvalid, sm, mute_at, lane, cb);
@@ -2157,8 +2164,10 @@ __device__ __forceinline__ void recon_impl(const BlockDesc &d, const uint8_t *bl
                 else recon_batch<LAYOUT, true, false, false>(ch, fx, sh.res, rbase, o0, o1, crc, ml, t0, tvalid, sm, mute_at, lane, cb);
             }
         } else {
+#if !WV_RECON_NOP
             if (joint) recon_batch<LAYOUT, false, true, false>(ch, fx, sh.res, rbase, o0, o1, crc, ml, t0, tvalid, sm, mute_at, lane, cb);
             else recon_batch<LAYOUT, false, false, false>(ch, fx, sh.res, rbase, o0, o1, crc, ml, t0, tvalid, sm, mute_at, lane, cb);
+#endif
         }
         // the batch's residuals have been read: release the ring space
         lds_publish(&sh.consumed, tend * WPF);
