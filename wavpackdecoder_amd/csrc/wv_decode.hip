@@ -852,11 +852,19 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
 #ifndef WV_M1_HOSTTAB
 #define WV_M1_HOSTTAB 0
 #endif
+//
+// Everything happens inside the 32-KiB row region (no LDS beyond it, so as many
+// waves per CU as the rows alone allow): the probabilities go to a byte array at
+// bytes [0, 8 KiB), the staged data sits at [8 KiB, 16.25 KiB), and the rows are
+// written last bin first -- row b covers the bytes of bins 4b .. 4b + 3, all
+// already summed by then (bin 0's own bytes are read before its row is written).
 constexpr uint32_t kDsdProbStage = 8192u + 256u;  // bytes: up to 32 x 256 codes + the end codes + over-read
-__device__ __forceinline__ void dsd_fast_tables(const BlockDesc &d, const uint8_t *blob, uint32_t bins, uint32_t *tab,
-                                                uint32_t *stg) {
+constexpr uint32_t kDsdStageAt = 2048u;            // dwords: the stage follows the 8-KiB byte array
+__device__ __forceinline__ void dsd_fast_tables(const BlockDesc &d, const uint8_t *blob, uint32_t bins, uint32_t *tab) {
     const uint32_t lane = threadIdx.x;
     const uint32_t ne = bins * 256u;
+    uint8_t *pb = (uint8_t *)tab;
+    uint32_t *stg = tab + kDsdStageAt;
     // the probability data (up to the 4 value bytes at bits_off) staged in LDS with
     // dword loads, all in flight together, instead of a byte load per code step
     const uint64_t a0 = d.dsd_prob_off & ~(uint64_t)3;
@@ -877,7 +885,7 @@ __device__ __forceinline__ void dsd_fast_tables(const BlockDesc &d, const uint8_
     };
     if (d.dsd_max_prob < 0xFF) {
         const uint32_t maxp = (uint32_t)d.dsd_max_prob;
-        for (uint32_t i = lane; i < ne; i += 64) tab[i] = 0;
+        for (uint32_t i = lane; i < ne / 16u; i += 64) ((uint4 *)pb)[i] = make_uint4(0, 0, 0, 0);
         __syncthreads();
         uint32_t outptr = 0, p = 0;
         while (outptr < ne) {
@@ -887,18 +895,22 @@ __device__ __forceinline__ void dsd_fast_tables(const BlockDesc &d, const uint8_
             // the loop ends at the first 0 code, or once the entries are all filled
             const uint64_t ev = __ballot(c == 0 || outptr + incl >= ne);
             const uint32_t last = ev ? (uint32_t)__builtin_ctzll(ev) : 63u;
-            if (lane <= last && c != 0 && c <= maxp) tab[outptr + incl - 1u] = c;
+            if (lane <= last && c != 0 && c <= maxp) pb[outptr + incl - 1u] = (uint8_t)c;
             outptr += (uint32_t)__builtin_amdgcn_readlane((int)incl, (int)last);
             p += last + 1u;
             if (ev) break;
         }
+    } else if (staged) {
+        for (uint32_t i = lane; i < ne / 4u; i += 64)
+            ((uint32_t *)pb)[i] = __builtin_amdgcn_alignbyte(stg[i + 1u], stg[i], sh);
     } else {
-        for (uint32_t i = lane; i < ne; i += 64) tab[i] = byte_at(i);
+        for (uint32_t i = lane; i < ne; i += 64) pb[i] = blob[d.dsd_prob_off + i];
     }
     __syncthreads();
-    // running sums per bin: lane l holds entries 4l .. 4l + 3 of the row
-    for (uint32_t b = 0; b < bins; b++) {
-        uint4 v = *(uint4 *)(tab + b * 256u + lane * 4u);
+    // running sums per bin, last bin first: lane l holds entries 4l .. 4l + 3 of the row
+    for (uint32_t b = bins; b-- > 0;) {
+        const uint32_t w = ((const uint32_t *)pb)[b * 64u + lane];
+        uint4 v = make_uint4(w & 0xFFu, (w >> 8) & 0xFFu, (w >> 16) & 0xFFu, w >> 24);
         v.y += v.x;
         v.z += v.y;
         v.w += v.z;
@@ -907,6 +919,7 @@ __device__ __forceinline__ void dsd_fast_tables(const BlockDesc &d, const uint8_
         v.y = (v.y + before) & 0xFFFFu;
         v.z = (v.z + before) & 0xFFFFu;
         v.w = (v.w + before) & 0xFFFFu;
+        __builtin_amdgcn_wave_barrier();
         *(uint4 *)(tab + b * 256u + lane * 4u) = v;
     }
     __syncthreads();
@@ -925,7 +938,7 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_fast(const BlockD
                                                                     uint32_t *__restrict__ status,
                                                                     uint32_t *__restrict__ mute_chunk) {
     __shared__ uint32_t tab[kDsdFastLds / 4];
-    __shared__ uint32_t stg[kDsdProbStage / 4];
+    static_assert(kDsdStageAt * 4u + kDsdProbStage <= kDsdFastLds, "the stage lives in the row region");
     const uint32_t bi = list[blockIdx.x];
     const BlockDesc &d = descs[bi];
     const bool lead = threadIdx.x == 0;
@@ -940,7 +953,7 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_fast(const BlockD
         __syncthreads();
     }
 #else
-    if (bins <= 32u) dsd_fast_tables(d, blob, bins, tab, stg);
+    if (bins <= 32u) dsd_fast_tables(d, blob, bins, tab);
 #endif
     // lane b: bin b's total and the reciprocal constants of dividing by it
     uint32_t vmag = 0, vsh1 = 0, vsh2 = 0;  // all zero for an empty bin (see dsd_fast_v2)
