@@ -144,6 +144,7 @@ def main():
     ap.add_argument("--c3-blocks", type=int, default=4096)
     ap.add_argument("--c3-copies", type=int, default=1)
     ap.add_argument("--c5-files", type=int, default=4000)
+    ap.add_argument("--dsd-files", type=int, default=64, help="files per DSD mode batch (one block each)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="also time the oracle on this many host threads")
     ap.add_argument("--inflight", type=int, default=1, help="also time this many copies of each batch in flight")
     a = ap.parse_args()
@@ -171,12 +172,14 @@ def main():
             run_wvc("C4 1024 x 22050 float32 hybrid+bitrate + .wvc (exact)", wv, wvc)
         elif c == "c5":
             run(f"C5 mixed corpus, files 0..{a.c5_files - 1}", corpora.c5(a.c5_files))
-        elif c.startswith("dsd"):  # dsd0 / dsd1 / dsd3: 64 stereo files of one 22,050-frame block in one mode
+        elif c.startswith("dsd"):  # dsd0 / dsd1 / dsd3: N stereo files of one 22,050-frame block in one mode
             from synth import wvsynth as S
             mode = int(c[3:])
-            files = [S.encode_dsd(S.dsd_random_like(22050, 2, seed=i, density=0.5),
-                                  S.DsdParams(nch=2, mode=mode, block_samples=22050)) for i in range(64)]
-            run(f"DSD mode {mode}: 64 files x 22050 frames stereo", files)
+            # 64 distinct files repeated: a DSD block's cost does not depend on its content's identity
+            base = [S.encode_dsd(S.dsd_random_like(22050, 2, seed=i, density=0.5),
+                                 S.DsdParams(nch=2, mode=mode, block_samples=22050)) for i in range(min(64, a.dsd_files))]
+            files = [base[i % len(base)] for i in range(a.dsd_files)]
+            run(f"DSD mode {mode}: {a.dsd_files} files x 22050 frames stereo", files)
 
 
 if __name__ == "__main__":
