@@ -24,7 +24,7 @@ hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint3
                          hipStream_t s_fast);
 int term_set_of(const BlockDesc &d, int prefer_pipe);
 hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, uint32_t n, const uint8_t *blob,
-                        int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s);
+                        int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s, int lane_mode);
 hipError_t launch_format(const FormatSeg *segs, uint32_t nseg, const int32_t *in, uint8_t *out, int dsd, hipStream_t s);
 hipError_t upload_dsd_ptables();
 hipError_t launch_dsd_fill(const BlockDesc *descs, const uint32_t *dsd_list, uint32_t n_dsd, const uint32_t *status,
@@ -155,6 +155,7 @@ struct wvg_batch {
     int force_lane = 0;                                 // WVG_FORCE_LANE=1: every PCM block on the generic kernel
     int prefer_pipe = 0;                                // WVG_PIPE=2: every PCM list on the pipelined kernel (A/B)
     int lanes = kLanes;                                 // WVG_LANES: streams per decode (A/B of the queue mapping)
+    int lane_mode = 0;                                  // term-set groups on the lane-per-block kernel (wvg_batch_set_kernel)
     std::vector<uint32_t> h_status, h_aux;
     int64_t bytes_in = 0, frames = 0;
     // format epilogue: per-file byte image of WavpackFormatSamples
@@ -284,6 +285,8 @@ wvg_batch *wvg_batch_new(wvg_ctx *c, int chunk_frames) {
     // WVG_HOST_META=1 keeps them on the host framing (A/B comparisons)
     const char *ln = getenv("WVG_LANES");
     if (ln && atoi(ln) >= 1) b->lanes = atoi(ln) < kLanes ? atoi(ln) : kLanes;
+    const char *lk = getenv("WVG_LANE_KERNEL");
+    b->lane_mode = lk ? atoi(lk) : 0;
     const char *rm = getenv("WVG_DFRAME_RANK_MIN");
     if (rm) b->rank_min = atoll(rm);
     const char *hm = getenv("WVG_HOST_META");
@@ -1099,7 +1102,7 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
     for (int t = 0; t < kMaxTermSets; t++)
         if (!b->ts_list[t].empty()) {
             HIPCHK(c, launch_2wave(t, b->d_descs, b->d_ts[t], (uint32_t)b->ts_list[t].size(), b->d_blob, b->d_out,
-                                   b->d_status, b->d_mute, slot(t)));
+                                   b->d_status, b->d_mute, slot(t), b->lane_mode));
             HIPCHK(c, mark(t));
         }
     for (int l = 1; l < nl; l++) {

@@ -39,6 +39,7 @@
 #include "wv_meta.h"
 #include "wv_wave2.h"
 #include "wv_pipe.h"
+#include "wv_lane.h"
 
 
 namespace wvg {
@@ -1059,6 +1060,23 @@ __global__ void __launch_bounds__(128) wv_pcm_2wave(const BlockDesc *__restrict_
     w2::block_2wave<Ts...>(descs, list, blob, out, status, aux);
 }
 
+// the lane-per-block kernel (wv_lane.h) and the two-wave kernel over the blocks
+// it handed back (ST_REDO; every other block's workgroup exits at once)
+template <int... Ts>
+__global__ void __launch_bounds__(64) wv_pcm_lane(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
+                                                  uint32_t n, const uint8_t *__restrict__ blob, int32_t *__restrict__ out,
+                                                  uint32_t *__restrict__ status) {
+    lane::lane_blocks<Ts...>(descs, list, n, blob, out, status);
+}
+template <int... Ts>
+__global__ void __launch_bounds__(128) wv_pcm_2wave_redo(const BlockDesc *__restrict__ descs,
+                                                         const uint32_t *__restrict__ list,
+                                                         const uint8_t *__restrict__ blob, int32_t *__restrict__ out,
+                                                         uint32_t *__restrict__ status, uint32_t *__restrict__ aux) {
+    if (!(status[list[blockIdx.x]] & lane::ST_REDO)) return;
+    w2::block_2wave<Ts...>(descs, list, blob, out, status, aux);
+}
+
 // pipelined reconstruction (wv_pipe.h): any term list, one kernel per "has -1/-2"
 template <bool NEG12>
 __global__ void __launch_bounds__(128) wv_pcm_pipe(const BlockDesc *__restrict__ descs,
@@ -1121,9 +1139,30 @@ int term_set_of(const BlockDesc &d, int prefer_pipe) {
 }
 
 hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, uint32_t n, const uint8_t *blob,
-                        int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s) {
+                        int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s, int lane_mode) {
     if (!n) return hipSuccess;
     dim3 g(n), b(128);
+    if (lane_mode && ts < kNumTermSets) {
+        dim3 gl((n + 63) / 64), bl(64);
+        switch (ts) {
+        case 0:
+            hipLaunchKernelGGL((wv_pcm_lane<WVG_TS_FAST>), gl, bl, 0, s, descs, list, n, blob, out, status);
+            if (lane_mode != 2)  // 2: the lane kernel alone (diagnostics: ST_REDO stays in the status)
+                hipLaunchKernelGGL((wv_pcm_2wave_redo<WVG_TS_FAST>), g, b, 0, s, descs, list, blob, out, status, aux);
+            break;
+        case 1:
+            hipLaunchKernelGGL((wv_pcm_lane<WVG_TS_DEFAULT>), gl, bl, 0, s, descs, list, n, blob, out, status);
+            if (lane_mode != 2)  // 2: the lane kernel alone (diagnostics: ST_REDO stays in the status)
+                hipLaunchKernelGGL((wv_pcm_2wave_redo<WVG_TS_DEFAULT>), g, b, 0, s, descs, list, blob, out, status, aux);
+            break;
+        case 2:
+            hipLaunchKernelGGL((wv_pcm_lane<WVG_TS_M5>), gl, bl, 0, s, descs, list, n, blob, out, status);
+            if (lane_mode != 2)  // 2: the lane kernel alone (diagnostics: ST_REDO stays in the status)
+                hipLaunchKernelGGL((wv_pcm_2wave_redo<WVG_TS_M5>), g, b, 0, s, descs, list, blob, out, status, aux);
+            break;
+        }
+        return hipGetLastError();
+    }
     switch (ts) {
     case 0: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_FAST>), g, b, 0, s, descs, list, blob, out, status, aux); break;
     case 1: hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_DEFAULT>), g, b, 0, s, descs, list, blob, out, status, aux); break;
