@@ -47,9 +47,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 # one stream per launch group and several batches in flight: more hardware
-# queues than HIP's default 4 (set before anything initialises HIP; wvg_open does
-# the same when it is the first HIP call)
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+# queues than HIP's default 4, which the GPU boxes export -- a stream beyond the
+# process's queues shares one, and kernels of one queue run one after another, so
+# the batches in flight would serialise to 4.  Set before anything initialises HIP
+# (wvg_open only fills it in when the host left it unset).  WVG_BENCH_HW_QUEUES
+# overrides; at most 32.
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("WVG_BENCH_HW_QUEUES", "24")
 
 import numpy as np  # noqa: E402
 

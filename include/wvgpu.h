@@ -169,6 +169,18 @@ int wvg_batch_upload(wvg_batch *b);
 int wvg_batch_decode(wvg_batch *b, void *stream);
 /* Wait for the batch's last decode / format (an event on the stream it ran on). */
 int wvg_batch_sync(wvg_batch *b);
+/* Which kernel decodes the batch's lossless PCM blocks whose decorr list has a
+ * compile-time specialisation (no reference counterpart: a scheduling choice).
+ * WVG_KERNEL_TWO_WAVE: one workgroup per block (a scalar parser wave and a
+ * reconstruction wave), the lowest latency for a batch alone.  WVG_KERNEL_LANE:
+ * one lane per block, 64 blocks per workgroup -- one SIMD issue slot moves 64
+ * blocks, so many batches in flight decode far more per second; blocks a lane
+ * cannot follow exactly are decoded again by the two-wave kernel within the same
+ * decode.  Results are identical either way.  Default: WVG_KERNEL_TWO_WAVE
+ * (WVG_LANE_KERNEL=1 in the environment selects the lane kernel for new batches). */
+#define WVG_KERNEL_TWO_WAVE 0
+#define WVG_KERNEL_LANE 1
+int wvg_batch_set_kernel(wvg_batch *b, int kernel);
 void *wvg_batch_stream(wvg_batch *b);  /* the batch's own hipStream_t */
 /* Device timing of every following decode (an event pair around each launch, on its
  * stream); wvg_batch_timed waits for them and returns the mean and the count. */

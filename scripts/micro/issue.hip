@@ -37,6 +37,20 @@ BENCH(k_mullo_dep, "v_mov_b32 v20, 3\n v_mov_b32 v21, 5\n", "v_mul_lo_u32 v20, v
 BENCH(k_mul24_dep, "v_mov_b32 v20, 3\n v_mov_b32 v21, 5\n", "v_mul_i32_i24 v20, v20, v21\n")
 BENCH(k_mad24_dep, "v_mov_b32 v20, 3\n v_mov_b32 v21, 5\n", "v_mad_i32_i24 v20, v20, v21, v21\n")
 
+// lane-kernel patterns: lane masks through SGPRs, 64-bit shifts, LDS round trips
+BENCH(k_cmp_cnd, "v_mov_b32 v20, 3\n v_mov_b32 v21, 5\n",
+      "v_cmp_gt_u32_e64 s[20:21], v20, v21\n v_cndmask_b32_e64 v20, v21, v20, s[20:21]\n")
+BENCH(k_cmp_sand_cnd, "v_mov_b32 v20, 3\n v_mov_b32 v21, 5\n s_mov_b64 s[24:25], -1\n",
+      "v_cmp_gt_u32_e64 s[20:21], v20, v21\n s_and_b64 s[22:23], s[20:21], s[24:25]\n v_cndmask_b32_e64 v20, v21, v20, s[22:23]\n")
+BENCH(k_cmp_scbr, "v_mov_b32 v20, 3\n v_mov_b32 v21, 5\n",
+      "v_cmp_gt_u32_e64 s[20:21], v20, v21\n s_cmp_eq_u64 s[20:21], 0\n s_cbranch_scc0 1\n s_nop 0\n v_add_u32 v20, v20, 1\n")
+BENCH(k_shr64v_dep, "v_mov_b32 v20, -1\n v_mov_b32 v21, -1\n", "v_lshrrev_b64 v[20:21], 1, v[20:21]\n")
+BENCH(k_ffbl_dep, "v_mov_b32 v20, 5\n", "v_ffbl_b32 v20, v20\n")
+BENCH(k_cnd_vcc_dep, "v_mov_b32 v20, 3\n v_mov_b32 v21, 5\n s_mov_b64 vcc, -1\n", "v_cndmask_b32 v20, v21, v20, vcc\n")
+BENCH(k_ds_dep, "v_mov_b32 v20, 0\n", "ds_read_b32 v20, v20\n s_waitcnt lgkmcnt(0)\n")
+BENCH(k_valu_ind4, "v_mov_b32 v20, 0\n v_mov_b32 v21, 0\n v_mov_b32 v22, 0\n v_mov_b32 v23, 0\n",
+      "v_add_u32 v20, v20, 1\n v_add_u32 v21, v21, 1\n v_add_u32 v22, v22, 1\n v_add_u32 v23, v23, 1\n")
+
 int main() {
     long long *d;
     hipMalloc(&d, 1024 * sizeof(long long));
@@ -47,7 +61,10 @@ int main() {
         {"s_branch", k_branch_taken}, {"cbranch_not_taken", k_cbranch_nt}, {"cbranch_taken", k_cbranch_t},
         {"valu_dep", k_valu_dep}, {"valu+rfl+salu", k_rfl}, {"writelane+sadd", k_wl}, {"salu+valu", k_mix},
         {"v_mad_i64_dep", k_mad64_dep}, {"v_mad_i64_ind(x2)", k_mad64_ind}, {"v_mul_lo_u32_dep", k_mullo_dep},
-        {"v_mul_i32_i24_dep", k_mul24_dep}, {"v_mad_i32_i24_dep", k_mad24_dep}};
+        {"v_mul_i32_i24_dep", k_mul24_dep}, {"v_mad_i32_i24_dep", k_mad24_dep},
+        {"v_cmp->v_cndmask", k_cmp_cnd}, {"v_cmp->s_and->v_cnd", k_cmp_sand_cnd}, {"v_cmp->s_cbranch(x5)", k_cmp_scbr},
+        {"v_lshrrev_b64_dep", k_shr64v_dep}, {"v_ffbl_dep", k_ffbl_dep}, {"v_cndmask_vcc_dep", k_cnd_vcc_dep},
+        {"ds_read_dep", k_ds_dep}, {"valu_ind(x4)", k_valu_ind4}};
     for (auto &k : ks) {
         for (int nb : {1, 1024, 2048}) {
             for (int rep = 0; rep < 2; rep++) hipLaunchKernelGGL(k.k, dim3(nb), dim3(64), 0, 0, d);

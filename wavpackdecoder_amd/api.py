@@ -166,6 +166,13 @@ class DecodeBatch:
     def sync(self):
         self._check(self._L.wvg_batch_sync(self._b))
 
+    def set_kernel(self, kernel: str):
+        """'two_wave' (one workgroup per block: lowest latency alone) or 'lane' (one lane
+        per block: the most blocks per second with many batches in flight)
+        -- wvg_batch_set_kernel; results are identical either way."""
+        k = {"two_wave": _L.WVG_KERNEL_TWO_WAVE, "lane": _L.WVG_KERNEL_LANE}[kernel]
+        self._check(self._L.wvg_batch_set_kernel(self._b, k))
+
     def set_timing(self, on: bool = True):
         """Record a device event pair around every following decode (wvg_batch_set_timing)."""
         self._check(self._L.wvg_batch_set_timing(self._b, int(bool(on))))

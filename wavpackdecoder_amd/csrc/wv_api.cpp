@@ -1126,6 +1126,12 @@ int wvg_batch_sync(wvg_batch *b) {
 
 void *wvg_batch_stream(wvg_batch *b) { return b ? (void *)b->stream : nullptr; }
 
+int wvg_batch_set_kernel(wvg_batch *b, int kernel) {
+    if (!b || (kernel != WVG_KERNEL_TWO_WAVE && kernel != WVG_KERNEL_LANE)) return WVG_ERR_ARG;
+    b->lane_mode = kernel == WVG_KERNEL_LANE ? 1 : 0;
+    return WVG_OK;
+}
+
 int wvg_batch_set_timing(wvg_batch *b, int on) {
     if (!b) return WVG_ERR_ARG;
     // pending pairs are dropped; their events are reused (re-recording an event is allowed)

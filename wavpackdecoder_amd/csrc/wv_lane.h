@@ -178,43 +178,31 @@ struct LState {
     int32_t nb;    // valid bits in win (>= 33 at every word start)
     uint32_t rp;   // ring dword merged next
     uint32_t nxt;  // ring dword rp, read ahead
-    uint64_t h0m, h1m;  // holding_zero / holding_one, one bit per lane (SGPR pairs)
+    uint32_t h0, h1;    // holding_zero / holding_one as 0/1 per lane (VGPRs: the fast word never
+                        // turns a lane value into an SGPR mask and back, ~20 cycles each way)
     uint32_t zacc;
     int32_t m[2][3];
-    uint32_t pmax;   // largest unary bit count of a non-held word (17: escape / bits error)
+    uint32_t pmax;   // 17: a bits error or a count too long for the lane (else smaller)
+    uint32_t rare;   // fast words: nonzero when a word needed the checked path (escape, run length)
     int32_t slack;   // least window bits left after a word (< 0: a word past the window)
     uint32_t bad;
 };
 
-// c ? a : b as one v_cndmask (the compiler otherwise turns nested selects
-// into divergent branches with register copies at every join)
-__device__ __forceinline__ uint32_t vsel(bool c, uint32_t a, uint32_t b) {
-    uint32_t r;
-    const uint64_t m = __builtin_amdgcn_ballot_w64(c);
-    asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
-    return r;
-}
-__device__ __forceinline__ int32_t vseli(bool c, int32_t a, int32_t b) {
-    return (int32_t)vsel(c, (uint32_t)a, (uint32_t)b);
-}
-// the same on a lane mask already in SGPRs (no compare re-derived per use)
+// Selects on lane masks (uint64_t in SGPRs, from ballots).  WV_LANE_ASM=1 forces
+// each one into a hand-written v_cndmask; the default lets the compiler emit the
+// same instructions and schedule them (the hazard recognizer puts an s_nop after
+// nearly every inline asm statement that feeds a VALU).
+#ifndef WV_LANE_ASM
+#define WV_LANE_ASM 0
+#endif
+__device__ __forceinline__ uint64_t lmask(bool c) { return __builtin_amdgcn_ballot_w64(c); }
+__device__ __forceinline__ bool lbit(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
+#if WV_LANE_ASM
 __device__ __forceinline__ uint32_t vselm(uint64_t m, uint32_t a, uint32_t b) {
     uint32_t r;
     asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
     return r;
 }
-__device__ __forceinline__ int32_t vselmi(uint64_t m, int32_t a, int32_t b) {
-    return (int32_t)vselm(m, (uint32_t)a, (uint32_t)b);
-}
-__device__ __forceinline__ uint64_t lmask(bool c) { return __builtin_amdgcn_ballot_w64(c); }
-// m + 5 k (one v_lshl_add: k * 4 + k, then the add; the compiler picks a 64-bit multiply-add)
-__device__ __forceinline__ int32_t add5(int32_t m, int32_t k) {
-    int32_t r;
-    asm("v_lshl_add_u32 %0, %1, 2, %1" : "=v"(r) : "v"(k));
-    return wvf::add32(m, r);
-}
-
-// small VALU helpers the compiler does not pick on its own
 __device__ __forceinline__ uint32_t addc(uint32_t a, uint64_t carry) {  // a + (this lane's bit of carry)
     uint32_t r;
     uint64_t co;
@@ -232,11 +220,18 @@ __device__ __forceinline__ int32_t mad24(int32_t a, int32_t b, int32_t c) {  // 
     asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
-__device__ __forceinline__ uint32_t add3(uint32_t a, uint32_t b, uint32_t c) {
-    uint32_t r;
-    asm("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(c));
-    return r;
+#else
+__device__ __forceinline__ uint32_t vselm(uint64_t m, uint32_t a, uint32_t b) { return lbit(m) ? a : b; }
+__device__ __forceinline__ uint32_t addc(uint32_t a, uint64_t carry) { return a + (lbit(carry) ? 1u : 0u); }
+template <int A, int B>
+__device__ __forceinline__ int32_t csel(uint64_t m) { return lbit(m) ? A : B; }
+__device__ __forceinline__ int32_t mad24(int32_t a, int32_t b, int32_t c) { return __mul24(a, b) + c; }
+#endif
+__device__ __forceinline__ int32_t vselmi(uint64_t m, int32_t a, int32_t b) {
+    return (int32_t)vselm(m, (uint32_t)a, (uint32_t)b);
 }
+__device__ __forceinline__ uint32_t vsel(bool c, uint32_t a, uint32_t b) { return vselm(lmask(c), a, b); }
+__device__ __forceinline__ uint32_t add3(uint32_t a, uint32_t b, uint32_t c) { return a + b + c; }
 
 // window refill: keep >= 32 bits by merging the dword read ahead (then read the next)
 __device__ __forceinline__ void lrefill(LState &s, const uint8_t *ring, uint32_t rbase) {
@@ -281,7 +276,8 @@ template <int C>
 __device__ __forceinline__ int32_t lword(LState &s, const uint8_t *ring, uint32_t rbase) {
     using namespace wvf;
     // zero-run mode (:304-352): both channels' median[0] < 2, nothing held
-    const uint64_t zrm = lmask((((uint32_t)(s.m[0][0] | s.m[1][0])) & ~1u) == 0u) & ~(s.h0m | s.h1m);
+    const uint64_t h0m0 = lmask(s.h0 != 0u), h1m0 = lmask(s.h1 != 0u);
+    const uint64_t zrm = lmask((((uint32_t)(s.m[0][0] | s.m[1][0])) & ~1u) == 0u) & ~(h0m0 | h1m0);
     bool zskip = false;
     if (__builtin_expect(zrm != 0ull, 0)) {
         if (__builtin_amdgcn_inverse_ballot_w64(zrm)) {
@@ -299,7 +295,7 @@ __device__ __forceinline__ int32_t lword(LState &s, const uint8_t *ring, uint32_
         }
     }
     const uint64_t zm = lmask(zskip);
-    const uint64_t hzm = s.h0m | zm;
+    const uint64_t hzm = h0m0 | zm;
     // unary count (:354-428): raw ones (capped at 16) and the bits they take
     const uint32_t lo = (uint32_t)s.win;
     uint32_t raw = (uint32_t)__builtin_ctz(~lo | 0x10000u);
@@ -318,13 +314,10 @@ __device__ __forceinline__ int32_t lword(LState &s, const uint8_t *ring, uint32_
     }
     p = vselm(hzm, 0u, p);
     lskip(s, p);
-    const uint32_t ones = vselm(hzm, 0u, addc(raw >> 1, s.h1m));
+    const uint32_t ones = vselm(hzm, 0u, addc(raw >> 1, h1m0));
     const uint64_t b0m = lmask((raw & 1u) != 0u);
-    // (lanes outside this path -- the other side of a tail group's FULL/partial
-    // split -- keep their bits)
-    const uint64_t exm = __builtin_amdgcn_read_exec();
-    s.h1m = (s.h1m & ~exm) | (~hzm & b0m);
-    s.h0m = (s.h0m & ~exm) | (~hzm & ~b0m & exm);
+    s.h1 = lbit(~hzm & b0m) ? 1u : 0u;
+    s.h0 = lbit(~hzm & ~b0m) ? 1u : 0u;
     const int32_t m0 = s.m[C][0], m1 = s.m[C][1], m2 = s.m[C][2];
     const uint32_t a0 = (uint32_t)(m0 >> 4), a1 = (uint32_t)(m1 >> 4), a2 = (uint32_t)(m2 >> 4);
     const uint64_t o0 = lmask(ones == 0u), o1 = lmask(ones == 1u), o2 = lmask(ones == 2u), ob = o0 | o1;
@@ -357,41 +350,155 @@ __device__ __forceinline__ int32_t lword(LState &s, const uint8_t *ring, uint32_
     return out;
 }
 
-template <int... Ts>
-struct LaneTerms {
-    static constexpr int n = sizeof...(Ts);
-    static constexpr int8_t t[sizeof...(Ts) + 1] = {(int8_t)Ts..., 0};
+// The fast word: lword without its two rare branches, VALU only.  A lane inside
+// a zero run counts it down (zskip); a word that would read a run length or an
+// escaped unary count only sets s.rare, and the group it is in is decoded again
+// from its starting state by lword (lane_parser).
+template <int C>
+__device__ __forceinline__ int32_t lword_fast(LState &s, const uint8_t *ring, uint32_t rbase) {
+    using namespace wvf;
+    // zero-run mode (:304-352): a pending run counts down; its entry is rare.  All
+    // as 0/1 lane values (a compound condition would go through SALU mask logic)
+    const uint32_t zx = (((uint32_t)(s.m[0][0] | s.m[1][0])) & ~1u) | s.h0 | s.h1;
+    const uint32_t zrv = zx == 0u ? 1u : 0u;       // the zero-run test holds
+    const uint32_t zdec = min(s.zacc, zrv);        // a pending run counts down
+    s.zacc -= zdec;
+    const uint32_t zsk = min(s.zacc, zdec);        // ... and this word is one of its zeros
+    const uint32_t lo = (uint32_t)s.win;
+    const uint32_t raw = (uint32_t)__builtin_ctz(~lo | 0x10000u);  // unary ones, capped at 16
+    const uint32_t keep = (s.h0 | zsk) - 1u;      // ~0 for a word that reads its unary count, 0 for a held zero
+    const uint32_t p = (raw + 1u) & keep;
+    // rare: 16 ones (LIMIT_ONES escape or a bits error: p == 17), or a run length to read
+    s.rare |= ((p + 15u) >> 5) | (zrv & (zdec ^ 1u));
+    const uint32_t ones = ((raw >> 1) + s.h1) & keep;
+    const uint32_t nh1 = raw & 1u & keep;
+    s.h1 = nh1;
+    s.h0 = (nh1 ^ 1u) & keep;
+    s.win >>= p;
+    s.nb -= (int32_t)p;
+    const int32_t m0 = s.m[C][0], m1 = s.m[C][1], m2 = s.m[C][2];
+    const uint32_t a0 = (uint32_t)(m0 >> 4), a1 = (uint32_t)(m1 >> 4), a2 = (uint32_t)(m2 >> 4);
+    const bool o0 = ones == 0u, o1 = ones == 1u, o2 = ones == 2u, ob = ones < 2u;
+    const uint32_t mc = o0 ? a0 : (o1 ? a1 : a2);
+    const uint32_t low1 = a0 + 1u;
+    const uint32_t low2 = __umul24(ones > 2u ? ones - 2u : 0u, a2 + 1u) + low1 + a1 + 1u;
+    const uint32_t low = o0 ? 0u : (o1 ? low1 : low2);
+    // median updates (:433-475), as in lword
+    s.m[C][0] = mad24((add32(m0, o0 ? 126 : 128)) >> 7, o0 ? -2 : 5, m0);
+    s.m[C][1] = mad24((add32(m1, o1 ? 62 : 64)) >> 6, o0 ? 0 : (o1 ? -2 : 5), m1);
+    s.m[C][2] = mad24((add32(m2, o2 ? 30 : 32)) >> 5, ob ? 0 : (o2 ? -2 : 5), m2);
+    // read_code(high - low = mc), then the sign bit
+    const uint32_t x = (uint32_t)s.win;
+    const uint32_t z = (uint32_t)__builtin_clz(mc | 1u);
+    const uint32_t ones_z = 0xFFFFFFFFu >> z;
+    const uint32_t ex = ones_z - mc;
+    const uint32_t nbt = z ^ 31u;
+    const uint32_t v = x & (ones_z >> 1);
+    const bool big = v >= ex;
+    const uint32_t code = big ? 2u * v + __builtin_amdgcn_ubfe(x, nbt, 1) - ex : v;
+    const uint32_t used = nbt + (big ? 1u : 0u);
+    const uint32_t mid = low + code;
+    const int32_t sg = __builtin_amdgcn_sbfe((int32_t)x, used, 1);  // 0 or -1
+    const uint32_t len = (used + 1u) & (zsk - 1u);
+    s.win >>= len;
+    s.nb -= (int32_t)len;
+    s.slack = min(s.slack, s.nb);
+    const int32_t out = (int32_t)((mid ^ (uint32_t)sg) & (zsk - 1u));
+    lrefill(s, ring, rbase);
+    return out;
+}
+
+// ---------------------------------------------------------------------------
+// Two waves per 64 blocks: the PARSER wave runs the words (lword) and hands each
+// frame's two residuals to the RECON wave through an LDS ring (RF frames per
+// lane); the recon wave runs the passes, joint stereo, the mute bound, the CRC,
+// the fixup shift and the stores.  They sit on different SIMDs, so a block's
+// critical path is its words alone.  The waves agree through two LDS counters
+// (frames produced / consumed, published per group of GF frames) with bounded
+// waits: a wait that runs out hands every block of the pair to the two-wave
+// kernel (ST_REDO).
+// ---------------------------------------------------------------------------
+constexpr int RF = 32;                     // residual frames in flight per lane
+constexpr uint32_t LSPIN = 1u << 24;       // bounded waits (polls)
+
+struct LShared {
+    uint32_t ringw[64 * RSTRIDE / 4];      // parser: payload units per lane
+    int2 res[RF * 64];                     // parser -> recon: residuals of frame t at [(t % RF) * 64 + lane]
+    uint32_t pflag[64];                    // parser -> recon: the block's parse verdict (bit 31: final)
+    uint32_t produced, consumed, abort;    // frames; abort: a wait ran out
 };
 
-// Per-block outcome when its last frame is done (the lane keeps decoding
-// garbage after it, with its stores off, so the wave's control flow stays
-// uniform and the holding-flag masks stay in SGPRs)
+// the parser's verdict for its lane now (after the block's last frame)
+__device__ __forceinline__ uint32_t pverdict(const LState &s, uint32_t u0) {
+    return 0x80000000u | s.bad | (s.pmax >= 17u ? 16u : 0u) | (s.slack < 0 ? 32u : 0u) |
+           (s.rp >= u0 * 4u ? 64u : 0u);
+}
+
+template <int U, bool FULL, bool FAST>
+__device__ __forceinline__ void pframe(LState &s, const uint8_t *ring, uint32_t rb, int2 *res, uint32_t lane,
+                                       uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin) {
+    const uint32_t t = g0 + U;
+    int2 r;
+    r.x = FAST ? lword_fast<0>(s, ring, rb) : lword<0>(s, ring, rb);
+    r.y = FAST ? lword_fast<1>(s, ring, rb) : lword<1>(s, ring, rb);
+    res[((t & (RF - 1)) << 6) + lane] = r;
+    if (!FULL && t + 1u == nfr) pfin = pverdict(s, u0);
+}
+template <bool FULL, bool FAST>
+__device__ __forceinline__ void pgroup(LState &s, const uint8_t *ring, uint32_t rb, int2 *res, uint32_t lane,
+                                       uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin) {
+    pframe<0, FULL, FAST>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    pframe<1, FULL, FAST>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    pframe<2, FULL, FAST>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    pframe<3, FULL, FAST>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    pframe<4, FULL, FAST>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    pframe<5, FULL, FAST>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    pframe<6, FULL, FAST>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    pframe<7, FULL, FAST>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+}
+// a group: the fast words first; if a live lane met a rare word, the group again
+// from its starting state with the checked words (the residual slots, the ring
+// and the group's loads are untouched by the first attempt's reads)
+template <bool FULL>
+__device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint32_t rb, int2 *res, uint32_t lane,
+                                           uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin) {
+    const LState s0 = s;
+    const uint32_t pfin0 = pfin;
+    s.rare = 0u;
+    pgroup<FULL, true>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    if (__builtin_expect(lmask(s.rare != 0u && g0 < nfr) != 0ull, 0)) {
+        s = s0;
+        pfin = pfin0;
+        pgroup<FULL, false>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    }
+}
+
 struct LEnd {
-    const BlockDesc *d;
     uint32_t *st;
     int32_t ml;
-    uint32_t u0;  // units written to the ring before this group
+    bool check;      // nframes == block_samples: check_crc_error applies
+    int32_t crc;     // the header's crc
+    const uint32_t *pflag;
+    uint32_t lane;
 };
-__device__ __forceinline__ void lane_finish(const LState &s, const LEnd &e, int32_t mx, int32_t mn, uint32_t crc) {
-    uint32_t bad = s.bad | (mx > e.ml || mn < -e.ml ? 8u : 0u) | (s.pmax >= 17u ? 16u : 0u) |
-                   (s.slack < 0 ? 32u : 0u) | (s.rp >= e.u0 * 4u ? 64u : 0u);
+__device__ __forceinline__ void lane_finish(uint32_t rbad, const LEnd &e, int32_t mx, int32_t mn, uint32_t crc) {
+    const uint32_t bad = (rbad | (e.pflag[e.lane] & 0x7FFFFFFFu) | (mx > e.ml || mn < -e.ml ? 8u : 0u));
     uint32_t st = 0;
-    if (e.d->nframes == e.d->block_samples) {
+    if (e.check) {
         st |= ST_CRC_CHECKED;
-        if ((int32_t)crc != e.d->crc) st |= ST_CRC_ERROR;
+        if ((int32_t)crc != e.crc) st |= ST_CRC_ERROR;
     }
     *e.st = bad ? (ST_REDO | (bad << 16)) : st;
 }
 
-// one frame t = g0 + U: two words, the passes, joint stereo, the mute bound,
-// the CRC, fixup and the store.  FULL: every lane of the wave is inside its block
+// one frame t = g0 + U of the recon wave.  FULL: every lane of the wave is inside its block
 template <int U, bool FULL, int... Ts>
-__device__ __forceinline__ void lframe(LState &s, LChain<Ts...> &ch, const uint8_t *ring, uint32_t rb, uint32_t g0,
-                                       uint32_t nfr, bool joint, int32_t &mx, int32_t &mn, uint32_t &crc, uint32_t sh,
-                                       int32_t *o, const LEnd &e) {
+__device__ __forceinline__ void rframe(LChain<Ts...> &ch, const int2 *res, uint32_t lane, uint32_t g0, uint32_t nfr,
+                                       bool joint, int32_t &mx, int32_t &mn, uint32_t &crc, uint32_t sh, int32_t *o,
+                                       uint32_t rbad, const LEnd &e) {
     const uint32_t t = g0 + U;
-    int32_t L = lword<0>(s, ring, rb);
-    int32_t R = lword<1>(s, ring, rb);
+    const int2 r = res[((t & (RF - 1)) << 6) + lane];
+    int32_t L = r.x, R = r.y;
     ch.template frame<U>(L, R);
     if (joint) {
         R = wvf::sub32(R, L >> 1);
@@ -405,25 +512,11 @@ __device__ __forceinline__ void lframe(LState &s, LChain<Ts...> &ch, const uint8
     v.x = (int32_t)((uint32_t)L << sh);
     v.y = (int32_t)((uint32_t)R << sh);
     if (FULL) {
-        *(int2 *)(o + 2u * t) = v;
+        if (nfr) *(int2 *)(o + 2u * t) = v;  // (a lane without a block of its own stores nothing)
     } else {
         if (t < nfr) *(int2 *)(o + 2u * t) = v;
-        if (t + 1u == nfr) lane_finish(s, e, mx, mn, crc);
+        if (t + 1u == nfr) lane_finish(rbad, e, mx, mn, crc);
     }
-}
-
-template <bool FULL, int... Ts>
-__device__ __forceinline__ void lgroup(LState &s, LChain<Ts...> &ch, const uint8_t *ring, uint32_t rb, uint32_t g0,
-                                       uint32_t nfr, bool joint, int32_t &mx, int32_t &mn, uint32_t &crc, uint32_t sh,
-                                       int32_t *o, const LEnd &e) {
-    lframe<0, FULL>(s, ch, ring, rb, g0, nfr, joint, mx, mn, crc, sh, o, e);
-    lframe<1, FULL>(s, ch, ring, rb, g0, nfr, joint, mx, mn, crc, sh, o, e);
-    lframe<2, FULL>(s, ch, ring, rb, g0, nfr, joint, mx, mn, crc, sh, o, e);
-    lframe<3, FULL>(s, ch, ring, rb, g0, nfr, joint, mx, mn, crc, sh, o, e);
-    lframe<4, FULL>(s, ch, ring, rb, g0, nfr, joint, mx, mn, crc, sh, o, e);
-    lframe<5, FULL>(s, ch, ring, rb, g0, nfr, joint, mx, mn, crc, sh, o, e);
-    lframe<6, FULL>(s, ch, ring, rb, g0, nfr, joint, mx, mn, crc, sh, o, e);
-    lframe<7, FULL>(s, ch, ring, rb, g0, nfr, joint, mx, mn, crc, sh, o, e);
 }
 
 // can this lane decode block d exactly (else ST_REDO)?
@@ -441,46 +534,62 @@ __device__ __forceinline__ bool lane_ok(const BlockDesc &d) {
     return true;
 }
 
+// the per-lane setup both waves share
+struct LBlock {
+    uint32_t bi, nfr, nmax, nmin;
+    bool ok, inl;
+};
 template <int... Ts>
-__device__ __forceinline__ void lane_blocks(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
-                                            uint32_t n, const uint8_t *__restrict__ blob, int32_t *__restrict__ out,
-                                            uint32_t *__restrict__ status) {
-    using namespace wvf;
-    __shared__ __attribute__((aligned(16))) uint32_t ringw[64 * RSTRIDE / 4];
-    const uint8_t *ring = (const uint8_t *)ringw;
-    const uint32_t lane = threadIdx.x;
-    const uint32_t rb = lane * RSTRIDE;  // this lane's ring
+__device__ __forceinline__ LBlock lane_block(const BlockDesc *descs, const uint32_t *list, uint32_t n, uint32_t lane) {
+    LBlock b;
     const uint32_t li = blockIdx.x * 64u + lane;
     // every lane stays in the wave (uniform loops keep the lane masks in SGPRs):
     // a lane past the list or with a block it does not take decodes 0 frames
-    const bool inl = li < n;
-    const uint32_t bi = inl ? list[li] : 0u;
-    const BlockDesc &d = descs[bi];
-    const bool ok = inl && lane_ok<Ts...>(d);
-    if (inl && !ok) status[bi] = ST_REDO | (1u << 16);
-    const uint32_t nfr = ok ? d.nframes : 0u;
+    b.inl = li < n;
+    b.bi = b.inl ? list[li] : 0u;
+    b.ok = b.inl && lane_ok<Ts...>(descs[b.bi]);
+    b.nfr = b.ok ? descs[b.bi].nframes : 0u;
     // the wave runs to its longest block; groups inside every block skip the per-frame end tests
-    uint32_t nmax = nfr, nmin = nfr ? nfr : 0xFFFFFFFFu;
+    uint32_t nmax = b.nfr, nmin = b.nfr ? b.nfr : 0xFFFFFFFFu;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
         nmax = max(nmax, (uint32_t)__shfl_xor((int)nmax, off));
         nmin = min(nmin, (uint32_t)__shfl_xor((int)nmin, off));
     }
-    nmax = __builtin_amdgcn_readfirstlane(nmax);
-    nmin = __builtin_amdgcn_readfirstlane(nmin);
-    const bool joint = (d.flags & JOINT_STEREO) != 0;
-    const uint32_t sh = (uint32_t)d.shift & 31u;
-    const int32_t ml = d.mute_limit;
-    int32_t *o = out + d.out_off;
+    b.nmax = __builtin_amdgcn_readfirstlane(nmax);
+    b.nmin = __builtin_amdgcn_readfirstlane(nmin);
+    return b;
+}
+
+// bounded wait until *ctr >= v (or the pair aborted); false when it ran out
+__device__ __forceinline__ bool lwait(uint32_t *ctr, uint32_t v, uint32_t *abort_flag) {
+    for (uint32_t spins = 0; spins < LSPIN; spins++) {
+        if (w2::uni(w2::lds_load_acq(ctr)) >= v) return true;
+        if (w2::uni(w2::lds_load_acq(abort_flag))) return false;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    w2::lds_store_rel(abort_flag, 1u);
+    return false;
+}
+
+template <int... Ts>
+__device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
+                                            uint32_t n, const uint8_t *__restrict__ blob, LShared &sh, uint32_t lane) {
+    using namespace wvf;
+    const LBlock lb = lane_block<Ts...>(descs, list, n, lane);
+    const BlockDesc &d = descs[lb.bi];
+    const uint32_t nfr = lb.nfr;
+    const uint8_t *ring = (const uint8_t *)sh.ringw;
+    uint8_t *ringm = (uint8_t *)sh.ringw;
+    const uint32_t rb = lane * RSTRIDE;  // this lane's ring
 
     // payload: 16-B units from the aligned base; bytes at or past e read 0xFF
     const uint64_t boff = d.bits_off;
     const uint4 *src = (const uint4 *)(blob + (boff & ~(uint64_t)15));
     const uint32_t skip = (uint32_t)(boff & 15u);
-    const uint32_t e = ok ? skip + d.bits_len : 0u;
+    const uint32_t e = lb.ok ? skip + d.bits_len : 0u;
     const uint32_t eu = (e + 15u) >> 4;
     const uint4 ffu = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-    uint8_t *ringm = (uint8_t *)ringw;
 #pragma unroll 4
     for (uint32_t u = 0; u < (uint32_t)RU; u++) {
         uint4 v = u < eu ? src[u] : ffu;
@@ -497,7 +606,8 @@ __device__ __forceinline__ void lane_blocks(const BlockDesc *__restrict__ descs,
     s.nb = 64 - (int32_t)((skip & 3u) * 8u);
     s.rp += 2u;
     s.nxt = *(const uint32_t *)(ring + rb + ((s.rp & (RU * 4u - 1u)) << 2));
-    s.h0m = s.h1m = 0ull;
+    s.h0 = s.h1 = 0u;
+    s.rare = 0u;
     s.zacc = 0u;
     s.pmax = 0u;
     s.slack = 0;
@@ -506,31 +616,29 @@ __device__ __forceinline__ void lane_blocks(const BlockDesc *__restrict__ descs,
     for (int c = 0; c < 2; c++)
 #pragma unroll
         for (int k = 0; k < 3; k++) s.m[c][k] = d.median[c][k];
-    LChain<Ts...> ch;
-    ch.init(d, 0);
-    uint32_t crc = 0xFFFFFFFFu;
-    int32_t mx = 0, mn = 0;
-
-    for (uint32_t g0 = 0; g0 < nmax; g0 += GF) {
-        // bounds that keep the group exact (else the two-wave kernel redoes the block;
+    uint32_t pfin = 0u;
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), lgkm/exp untouched: the loop's waits count only its own loads
+    for (uint32_t g0 = 0; g0 < lb.nmax; g0 += GF) {
+        // the recon wave has taken the frames this group overwrites
+        if (!lwait(&sh.consumed, g0 + GF > (uint32_t)RF ? g0 + GF - RF : 0u, &sh.abort)) return;
+        // a bound that keeps the group exact (else the two-wave kernel redoes the block;
         // the reason lands in status bits 16-23 beside ST_REDO, for diagnostics)
         const int32_t mm = max(max(max(s.m[0][0], s.m[0][1]), max(s.m[0][2], s.m[1][0])), max(s.m[1][1], s.m[1][2]));
-        s.bad |= (mm >= (1 << 26) ? 2u : 0u) | (ch.wbad() ? 4u : 0u);
-        // this group's loads: the units after fu that fit in the ring
+        s.bad |= (mm >= (1 << 26) ? 2u : 0u);
+        // this group's loads: the units after fu that fit in the ring (four every
+        // group, unconditionally: the waitcnt pass then knows exactly which memory
+        // operations are in flight; units past the stream re-read its last one)
         const uint32_t u0 = fu;
         const uint32_t room = (s.rp >> 2) + (uint32_t)RU - u0;
         const uint32_t nld = room < (uint32_t)NLD ? room : (uint32_t)NLD;
-        uint4 st0 = ffu, st1 = ffu, st2 = ffu, st3 = ffu;
-        if (nld > 0u && u0 < eu) st0 = src[u0];
-        if (nld > 1u && u0 + 1u < eu) st1 = src[u0 + 1u];
-        if (nld > 2u && u0 + 2u < eu) st2 = src[u0 + 2u];
-        if (nld > 3u && u0 + 3u < eu) st3 = src[u0 + 3u];
+        const uint32_t ulast = eu > 0u ? eu - 1u : 0u;
+        uint4 st0 = src[min(u0, ulast)], st1 = src[min(u0 + 1u, ulast)];
+        uint4 st2 = src[min(u0 + 2u, ulast)], st3 = src[min(u0 + 3u, ulast)];
         fu = u0 + nld;
-        const LEnd le = {&d, status + bi, ml, u0};
-        if (g0 + GF < nmin)  // (strict: the group holding a block's last frame runs lane_finish)
-            lgroup<true>(s, ch, ring, rb, g0, nfr, joint, mx, mn, crc, sh, o, le);
+        if (g0 + GF < lb.nmin)  // (strict: the group holding a block's last frame records its verdict)
+            pgroup_try<true>(s, ring, rb, sh.res, lane, g0, nfr, u0, pfin);
         else
-            lgroup<false>(s, ch, ring, rb, g0, nfr, joint, mx, mn, crc, sh, o, le);
+            pgroup_try<false>(s, ring, rb, sh.res, lane, g0, nfr, u0, pfin);
         // the reader stayed inside the units written before this group
         if (s.rp >= u0 * 4u) s.bad |= 64u;
         // the loads land in the ring (the unit holding the stream end gets its 0xFF tail)
@@ -550,9 +658,82 @@ __device__ __forceinline__ void lane_blocks(const BlockDesc *__restrict__ descs,
             if (u0 + 4u >= eu) st3 = ff_unit(st3, u0 + 3u, e);
             *(uint4 *)(ringm + rb + (((u0 + 3u) & (RU - 1)) << 4)) = st3;
         }
+        // publish the group: residuals and verdicts first, then the count
+        sh.pflag[lane] = pfin;
+        w2::lds_publish(&sh.produced, g0 + GF);
+    }
+}
+
+template <int... Ts>
+__device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
+                                           uint32_t n, int32_t *__restrict__ out, uint32_t *__restrict__ status,
+                                           LShared &sh, uint32_t lane) {
+    using namespace wvf;
+    const LBlock lb = lane_block<Ts...>(descs, list, n, lane);
+    const BlockDesc &d = descs[lb.bi];
+    const uint32_t nfr = lb.nfr;
+    if (lb.inl && !lb.ok) status[lb.bi] = ST_REDO | (1u << 16);
+    const bool joint = (d.flags & JOINT_STEREO) != 0;
+    const uint32_t sh_ = (uint32_t)d.shift & 31u;
+    const int32_t ml = d.mute_limit;
+    int32_t *o = out + d.out_off;
+    LChain<Ts...> ch;
+    ch.init(d, 0);
+    uint32_t crc = 0xFFFFFFFFu;
+    int32_t mx = 0, mn = 0;
+    uint32_t rbad = 0u;
+    const LEnd le = {status + lb.bi, ml, d.nframes == d.block_samples, d.crc, sh.pflag, lane};
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    for (uint32_t g0 = 0; g0 < lb.nmax; g0 += GF) {
+        if (!lwait(&sh.produced, g0 + GF, &sh.abort)) {
+            // the parser stopped: every unfinished block of the pair to the two-wave kernel
+            if (lb.ok && nfr > g0) status[lb.bi] = ST_REDO | (128u << 16);
+            return;
+        }
+        rbad |= ch.wbad() ? 4u : 0u;
+        if (g0 + GF < lb.nmin) {
+            rframe<0, true>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
+            rframe<1, true>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
+            rframe<2, true>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
+            rframe<3, true>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
+            rframe<4, true>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
+            rframe<5, true>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
+            rframe<6, true>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
+            rframe<7, true>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
+        } else {
+            rframe<0, false>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
+            rframe<1, false>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
+            rframe<2, false>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
+            rframe<3, false>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
+            rframe<4, false>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
+            rframe<5, false>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
+            rframe<6, false>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
+            rframe<7, false>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
+        }
+        // the group's residuals are read (DS ops of one wave complete in order)
+        w2::lds_publish(&sh.consumed, g0 + GF);
     }
     // (every block with frames was finished by lane_finish in its last group)
-    if (ok && nfr == 0u) status[bi] = (d.block_samples == 0u) ? ST_CRC_CHECKED | ((int32_t)0xFFFFFFFFu != d.crc ? ST_CRC_ERROR : 0u) : 0u;
+    if (lb.ok && nfr == 0u)
+        status[lb.bi] = (d.block_samples == 0u) ? ST_CRC_CHECKED | ((int32_t)0xFFFFFFFFu != d.crc ? ST_CRC_ERROR : 0u) : 0u;
+}
+
+template <int... Ts>
+__device__ __forceinline__ void lane_blocks(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
+                                            uint32_t n, const uint8_t *__restrict__ blob, int32_t *__restrict__ out,
+                                            uint32_t *__restrict__ status) {
+    __shared__ LShared sh;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    if (threadIdx.x == 0) {
+        sh.produced = 0u;
+        sh.consumed = 0u;
+        sh.abort = 0u;
+    }
+    __syncthreads();
+    if (wave == 0)
+        lane_parser<Ts...>(descs, list, n, blob, sh, lane);
+    else
+        lane_recon<Ts...>(descs, list, n, out, status, sh, lane);
 }
 
 }  // namespace lane
