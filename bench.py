@@ -14,15 +14,18 @@ N GPUs : one process per GPU.  Under torch.distributed.run the ranks come from
          file-partitioned across the ranks (LPT on estimated device cost).
          No data-path collective: only a CPU (gloo) barrier and max/sum reduces.
 value  : frames decoded by all ranks / max-over-ranks wall time of the K steps.
-         Steps are issued round-robin over --inflight (default 3) copies of the
-         batch, each with its own device buffers and HIP stream, so consecutive
-         steps overlap on the device as in a decode server with several batches
-         in flight: every step is still one complete decode of the whole batch
-         into its own output.  C2 has exactly one block per SIMD (1,024), and one
-         block is one serial entropy chain, so a single batch leaves each SIMD's
-         issue slots half idle; the line also reports the same K steps run one
-         batch at a time ("value_one_batch_at_a_time") and the per-launch device
-         times (launch_ms).
+         Steps are issued round-robin over --inflight copies of the batch, each
+         with its own device buffers and HIP stream, so consecutive steps overlap
+         on the device as in a decode server with several batches in flight:
+         every step is still one complete decode of the whole batch into its own
+         output.  The default kernel is the lane-per-block one (--kernel lane,
+         wv_lane.h): a block is one serial entropy chain, one lane decodes it, a
+         batch of 1,024 blocks is 16 workgroups, so the chip holds many batches at
+         once -- the default keeps min(K, 20) in flight.  --kernel two_wave is the
+         one-workgroup-per-block kernel (lowest latency for a batch alone; best at
+         3 in flight), measured beside it in "two_wave".  The line also reports
+         the same K steps run one batch at a time ("value_one_batch_at_a_time")
+         and the per-launch device times (launch_ms).
 
 Also printed in the same JSON line:
   roofline     : algorithmic bytes per launch (compressed bytes in + int32
@@ -301,9 +304,12 @@ def run_rank(args) -> None:
     # step k decodes copy k % inflight, so consecutive steps overlap on the device
     # the way a decode server keeps several batches in flight (every step is still
     # one complete decode of the whole batch into its own output)
+    inflight = args.inflight if args.inflight else (20 if args.kernel == "lane" else 3)
+    inflight = max(1, min(inflight, args.steps))
     batches = []
-    for _ in range(max(1, args.inflight)):
+    for _ in range(inflight):
         bb = DecodeBatch(4096)
+        bb.set_kernel(args.kernel)
         bb.add_files(files)  # host framing on worker threads
         bb.upload()
         batches.append(bb)
@@ -355,6 +361,23 @@ def run_rank(args) -> None:
             b.decode()
         b.sync()
         serial_dt = _reduce(pg, time.perf_counter() - t2, "max")
+    # the other kernel on the same batches, at its own best depth (reported beside `value`)
+    other = None
+    if not args.timed_only and args.kernel == "lane":
+        nb = min(3, len(batches))
+        for bb in batches[:nb]:
+            bb.set_kernel("two_wave")
+            bb.sync()
+        _barrier(pg)
+        t3 = time.perf_counter()
+        for k in range(args.steps):
+            batches[k % nb].decode()
+        for bb in batches[:nb]:
+            bb.sync()
+        dt_o = _reduce(pg, time.perf_counter() - t3, "max")
+        other = {"kernel": "two_wave", "batches_in_flight": nb, "value": None, "dt": dt_o}
+        for bb in batches[:nb]:
+            bb.set_kernel(args.kernel)
     dt = _reduce(pg, t1 - t0, "max")
     frames_total = _reduce(pg, float(frames_rank), "sum")
     kms_all = _gather(pg, kernel_ms, ws)
@@ -417,23 +440,28 @@ def run_rank(args) -> None:
                 else:
                     bb.download(pinned=True)
 
+        # (at most 4 request threads: the host side -- framing, page-locked copies -- is
+        # what this measures, and each batch's landing buffers are page-locked)
+        pbatches = batches[:4]
+
         def pipelined(pcm):
-            for bb in batches:  # first use allocates each batch's page-locked landing buffers: untimed
+            for bb in pbatches:  # first use allocates each batch's page-locked landing buffers: untimed
                 serve(bb, pcm, 1)
-            th = [threading.Thread(target=serve, args=(bb, pcm)) for bb in batches]
+            th = [threading.Thread(target=serve, args=(bb, pcm)) for bb in pbatches]
             t_p = time.perf_counter()
             for t in th:
                 t.start()
             for t in th:
                 t.join()
-            return frames_rank * rounds * len(batches) / (time.perf_counter() - t_p) / 1e6
+            return frames_rank * rounds * len(pbatches) / (time.perf_counter() - t_p) / 1e6
 
         e2e_pipe = pipelined(False)
         e2e_pcm = pipelined(True)
 
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     node_gbs = alg_bytes * args.steps * ws / dt / 1e9
-    traffic, traffic_src = pmc_traffic() if args.workload == "c2" else (None, None)
+    kname = "wv_pcm_lane<17, 17>" if args.kernel == "lane" else "wv_pcm_2wave<17, 17>"
+    traffic, traffic_src = pmc_traffic(kname) if args.workload == "c2" else (None, None)
     if rank == 0:
         cpu = None
         if not args.no_cpu and args.workload == "c2":
@@ -469,6 +497,12 @@ def run_rank(args) -> None:
                        "parallelism": f"file-shard x{ws}, no collectives"},
             "per_rank_kernel_ms": [round(x, 4) for x in kms_all],
             "value_one_batch_at_a_time": round(frames_total * args.steps / serial_dt / 1e6, 2) if serial_dt else None,
+            "kernel": args.kernel,
+            "two_wave": None if other is None else {
+                "value": round(frames_total * args.steps / other["dt"] / 1e6, 2),
+                "batches_in_flight": other["batches_in_flight"],
+                "what": "the same K steps on the one-workgroup-per-block kernel (wvg_batch_set_kernel "
+                        "WVG_KERNEL_TWO_WAVE) at its best depth, 3 batches in flight"},
             "hbm_gbs": round(node_gbs, 2),
             "launch_ms": {"in_flight_mean": round(kernel_ms, 4), "alone": round(solo_ms, 4),
                           "what": "device time of one decode launch (hipEvents on its stream): mean over the timed "
@@ -483,7 +517,7 @@ def run_rank(args) -> None:
                                                           "on the GPU (wvg_batch_add_files_device)"},
                                "pipelined": None if e2e_pipe is None else round(e2e_pipe, 2),
                                "pipelined_pcm": None if e2e_pcm is None else round(e2e_pcm, 2),
-                               "pipelined_what": "the same request served by one host thread per batch copy "
+                               "pipelined_what": "the same request served by one host thread per batch copy (at most 4) "
                                                  "(4 requests each), framing/copies/decode of different batches "
                                                  "overlapping; _pcm: formatted on the device (WavpackFormatSamples) "
                                                  "and downloaded as PCM bytes"},
@@ -493,7 +527,11 @@ def run_rank(args) -> None:
                          "traffic_unit": "bytes/launch (PMC FETCH_SIZE + WRITE_SIZE, scale calibrated in the profile)",
                          "traffic_source": traffic_src,
                          "kernel_ms": round(kernel_ms, 4), "alg_bytes_per_launch": alg_bytes,
-                         "binding_limit": "serial entropy decode per block (scalar issue of one wave), not HBM"},
+                         "kernel": kname,
+                         "node_achieved": round(node_gbs, 2),
+                         "node_frac": round(node_gbs / HBM_PEAK_GBS, 6),
+                         "binding_limit": "serial entropy decode per block: one lane's dependent word chain "
+                                          "(lane kernel) / one wave's scalar issue (two-wave kernel), not HBM"},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
@@ -512,8 +550,11 @@ def main():
     ap.add_argument("--blocks", type=int, default=1024)
     ap.add_argument("--block-frames", type=int, default=22050)
     ap.add_argument("--c5-files", type=int, default=4000)
-    ap.add_argument("--inflight", type=int, default=3,
-                    help="batch copies decoding concurrently (own buffers and streams); 1 = one batch at a time")
+    ap.add_argument("--inflight", type=int, default=None,
+                    help="batch copies decoding concurrently (own buffers and streams); 1 = one batch at a time "
+                         "(default: 20 for the lane kernel, 3 for the two-wave kernel, at most --steps)")
+    ap.add_argument("--kernel", choices=("lane", "two_wave"), default="lane",
+                    help="PCM kernel (wvg_batch_set_kernel): lane-per-block or one workgroup per block")
     ap.add_argument("--cpu-threads", type=int, default=None, help="override the socket/lease-derived thread count")
     ap.add_argument("--cpu-reps", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")

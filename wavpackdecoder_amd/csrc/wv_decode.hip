@@ -1063,7 +1063,7 @@ __global__ void __launch_bounds__(128) wv_pcm_2wave(const BlockDesc *__restrict_
 // the lane-per-block kernel (wv_lane.h) and the two-wave kernel over the blocks
 // it handed back (ST_REDO; every other block's workgroup exits at once)
 template <int... Ts>
-__global__ void __launch_bounds__(128) wv_pcm_lane(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
+__global__ void __launch_bounds__(256) wv_pcm_lane(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
                                                   uint32_t n, const uint8_t *__restrict__ blob, int32_t *__restrict__ out,
                                                   uint32_t *__restrict__ status) {
     lane::lane_blocks<Ts...>(descs, list, n, blob, out, status);
@@ -1143,7 +1143,7 @@ hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, ui
     if (!n) return hipSuccess;
     dim3 g(n), b(128);
     if (lane_mode && ts < kNumTermSets) {
-        dim3 gl((n + 63) / 64), bl(128);
+        dim3 gl((n + 64 * lane::LPAIRS - 1) / (64 * lane::LPAIRS)), bl(64 * lane::LPAIRS * 2);
         switch (ts) {
         case 0:
             hipLaunchKernelGGL((wv_pcm_lane<WVG_TS_FAST>), gl, bl, 0, s, descs, list, n, blob, out, status);

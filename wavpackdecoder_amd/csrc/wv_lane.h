@@ -540,9 +540,10 @@ struct LBlock {
     bool ok, inl;
 };
 template <int... Ts>
-__device__ __forceinline__ LBlock lane_block(const BlockDesc *descs, const uint32_t *list, uint32_t n, uint32_t lane) {
+__device__ __forceinline__ LBlock lane_block(const BlockDesc *descs, const uint32_t *list, uint32_t n, uint32_t grp,
+                                             uint32_t lane) {
     LBlock b;
-    const uint32_t li = blockIdx.x * 64u + lane;
+    const uint32_t li = grp * 64u + lane;
     // every lane stays in the wave (uniform loops keep the lane masks in SGPRs):
     // a lane past the list or with a block it does not take decodes 0 frames
     b.inl = li < n;
@@ -574,9 +575,10 @@ __device__ __forceinline__ bool lwait(uint32_t *ctr, uint32_t v, uint32_t *abort
 
 template <int... Ts>
 __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
-                                            uint32_t n, const uint8_t *__restrict__ blob, LShared &sh, uint32_t lane) {
+                                            uint32_t n, const uint8_t *__restrict__ blob, LShared &sh, uint32_t grp,
+                                            uint32_t lane) {
     using namespace wvf;
-    const LBlock lb = lane_block<Ts...>(descs, list, n, lane);
+    const LBlock lb = lane_block<Ts...>(descs, list, n, grp, lane);
     const BlockDesc &d = descs[lb.bi];
     const uint32_t nfr = lb.nfr;
     const uint8_t *ring = (const uint8_t *)sh.ringw;
@@ -667,9 +669,9 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
 template <int... Ts>
 __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
                                            uint32_t n, int32_t *__restrict__ out, uint32_t *__restrict__ status,
-                                           LShared &sh, uint32_t lane) {
+                                           LShared &sh, uint32_t grp, uint32_t lane) {
     using namespace wvf;
-    const LBlock lb = lane_block<Ts...>(descs, list, n, lane);
+    const LBlock lb = lane_block<Ts...>(descs, list, n, grp, lane);
     const BlockDesc &d = descs[lb.bi];
     const uint32_t nfr = lb.nfr;
     if (lb.inl && !lb.ok) status[lb.bi] = ST_REDO | (1u << 16);
@@ -718,22 +720,30 @@ __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, 
         status[lb.bi] = (d.block_samples == 0u) ? ST_CRC_CHECKED | ((int32_t)0xFFFFFFFFu != d.crc ? ST_CRC_ERROR : 0u) : 0u;
 }
 
+// LPAIRS (parser, recon) wave pairs per workgroup, each pair 64 blocks: waves
+// 2p and 2p + 1 of a workgroup go to different SIMDs of one CU, and a 4-wave
+// workgroup keeps another batch's pair off those SIMDs (two 2-wave workgroups on
+// one CU could put both parsers on one SIMD)
+constexpr int LPAIRS = 2;
 template <int... Ts>
 __device__ __forceinline__ void lane_blocks(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
                                             uint32_t n, const uint8_t *__restrict__ blob, int32_t *__restrict__ out,
                                             uint32_t *__restrict__ status) {
-    __shared__ LShared sh;
+    __shared__ LShared shp[LPAIRS];
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-    if (threadIdx.x == 0) {
+    const uint32_t pair = wave >> 1, grp = blockIdx.x * LPAIRS + pair;
+    LShared &sh = shp[pair];
+    if (lane == 0 && (wave & 1u) == 0u) {
         sh.produced = 0u;
         sh.consumed = 0u;
         sh.abort = 0u;
     }
     __syncthreads();
-    if (wave == 0)
-        lane_parser<Ts...>(descs, list, n, blob, sh, lane);
+    if (grp * 64u >= n) return;  // (both waves of the pair: uniform)
+    if ((wave & 1u) == 0u)
+        lane_parser<Ts...>(descs, list, n, blob, sh, grp, lane);
     else
-        lane_recon<Ts...>(descs, list, n, out, status, sh, lane);
+        lane_recon<Ts...>(descs, list, n, out, status, sh, grp, lane);
 }
 
 }  // namespace lane
