@@ -54,9 +54,9 @@ out = {
     "fetch_bytes_per_launch": fetch_kib * 1024 * scale,
     "write_bytes_per_launch": write_kib * 1024,
     "traffic_bytes_per_launch": fetch_kib * 1024 * scale + write_kib * 1024,
-    "note": "FETCH_SIZE/WRITE_SIZE in KiB. Payload read by scalar s_load_dwordx2: raw FETCH_SIZE calibrated against the "
-            "known read bytes (compressed payload + 1,392-B block descriptors) -> scale 1; WRITE from dword-per-lane "
-            "stores equals the int32 output byte count",
+    "note": os.environ.get("PMC_NOTE", "FETCH_SIZE/WRITE_SIZE in KiB. Payload read by scalar s_load_dwordx2: raw "
+            "FETCH_SIZE calibrated against the known read bytes (compressed payload + 1,392-B block descriptors) -> "
+            "scale 1; WRITE from dword-per-lane stores equals the int32 output byte count"),
 }
 with open(os.path.join(dst, f"{tag}_pmc.json"), "w") as f:
     json.dump(out, f, indent=1)
