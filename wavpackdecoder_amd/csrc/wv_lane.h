@@ -36,7 +36,7 @@ namespace wvg {
 namespace lane {
 
 constexpr uint32_t ST_REDO = 1u << 15;  // internal: decode this block again on the two-wave kernel
-constexpr int RU = 16;                  // ring units (16 B) per lane: 16 KiB of LDS per 64-block wave
+constexpr int RU = 32;                  // ring units (16 B) per lane: 33 KiB of LDS per 64 blocks (lane_blocks: why)
 constexpr int GF = 8;                   // frames per group (refill / bound-check cadence)
 constexpr int NLD = 4;                  // units a lane loads per group, at most (32 bits per word sustained)
 
@@ -720,10 +720,13 @@ __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, 
         status[lb.bi] = (d.block_samples == 0u) ? ST_CRC_CHECKED | ((int32_t)0xFFFFFFFFu != d.crc ? ST_CRC_ERROR : 0u) : 0u;
 }
 
-// LPAIRS (parser, recon) wave pairs per workgroup, each pair 64 blocks: waves
-// 2p and 2p + 1 of a workgroup go to different SIMDs of one CU, and a 4-wave
-// workgroup keeps another batch's pair off those SIMDs (two 2-wave workgroups on
-// one CU could put both parsers on one SIMD)
+// LPAIRS (parser, recon) wave pairs per workgroup, each pair 64 blocks: the 4 waves
+// of a workgroup take the 4 SIMDs of one CU.  Its LDS (2 x ~50 KiB: the 32-unit
+// payload rings) is more than half a CU's 160 KiB, so no second workgroup -- of
+// this batch or of another in flight -- can land on that CU and put two parser
+// waves on one SIMD: measured with 20 batches in flight, 16-unit rings (68 KiB per
+// workgroup, two per CU possible) ran at ~30,000 Msamples/s on most runs and
+// ~47,000 on some; a workgroup per CU keeps every launch at its one-batch time.
 constexpr int LPAIRS = 2;
 template <int... Ts>
 __device__ __forceinline__ void lane_blocks(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
