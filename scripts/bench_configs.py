@@ -23,6 +23,8 @@ import time
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# as bench.py: more hardware queues than the boxes' exported 4 (set before HIP starts)
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("WVG_BENCH_HW_QUEUES", "24")
 sys.path.insert(0, ROOT)
 
 from synth import corpora  # noqa: E402
@@ -32,6 +34,8 @@ from wavpackdecoder_amd.api import DecodeBatch  # noqa: E402
 def run(name, files, pcm=None, iters=5, fmt=False):
     t0 = time.perf_counter()
     b = DecodeBatch(4096)
+    if KERNEL != "two_wave":
+        b.set_kernel(KERNEL)
     b.add_files(files)  # host framing on worker threads
     t_frame = time.perf_counter() - t0
     b.upload()
@@ -72,6 +76,8 @@ def run(name, files, pcm=None, iters=5, fmt=False):
         copies = [b]
         for _ in range(INFLIGHT - 1):
             c = DecodeBatch(4096)
+            if KERNEL != "two_wave":
+                c.set_kernel(KERNEL)
             c.add_files(files)
             c.upload()
             copies.append(c)
@@ -117,6 +123,7 @@ def run_wvc(name, wv, wvc, iters=5):
 
 CPU_THREADS = 0
 INFLIGHT = 1
+KERNEL = "two_wave"
 
 
 def cpu_rate(files):
@@ -147,10 +154,13 @@ def main():
     ap.add_argument("--dsd-files", type=int, default=64, help="files per DSD mode batch (one block each)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="also time the oracle on this many host threads")
     ap.add_argument("--inflight", type=int, default=1, help="also time this many copies of each batch in flight")
+    ap.add_argument("--kernel", choices=("two_wave", "lane"), default="two_wave",
+                    help="PCM kernel for the term-set groups (wvg_batch_set_kernel)")
     a = ap.parse_args()
-    global CPU_THREADS, INFLIGHT
+    global CPU_THREADS, INFLIGHT, KERNEL
     CPU_THREADS = a.cpu_threads
     INFLIGHT = a.inflight
+    KERNEL = a.kernel
     from wavpackdecoder_amd import _lib
     import wavpackdecoder_amd.api as api
     api._ctx = _lib.lib().wvg_open(0)
