@@ -143,8 +143,8 @@ struct ByteSrcWave {
 
 // Payload bytes for the DSD range coders: a 64-bit big-endian window of the
 // next bytes (byte bp in bits 63..56), refilled a dword at a time from a
-// dword loaded one refill ahead (scalar loads, so the load latency is off the
-// decode chain).  Reads run at most 12 bytes past the consumed position:
+// dword loaded one refill ahead (a vector load, read into a scalar register
+// at its refill, so the load latency is off the decode chain).  Reads run at most 12 bytes past the consumed position:
 // inside the blob's 64-byte 0xFF tail at worst; bytes past the payload are
 // never shifted in (callers cap n by the bytes left).
 struct DsdWin {
@@ -159,16 +159,18 @@ struct DsdWin {
     __device__ __forceinline__ void init(const uint8_t *p) {
         const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
         w = (const uint32_t *)(p - sh);
-        win = (uint64_t)bswap_u(__builtin_amdgcn_readfirstlane(w[0])) << (32u + 8u * sh);
+        win = (uint64_t)bswap_u(w[0]) << (32u + 8u * sh);
         avail = 4u - sh;
-        nxt = __builtin_amdgcn_readfirstlane(w[1]);
+        nxt = w[1];
         ni = 2;
         refill();
     }
+    // nxt stays a vector register until the next refill moves it to a scalar
+    // one: the load's wait lands there, ~4 payload bytes (tens of decisions) later
     __device__ __forceinline__ void refill() {  // avail <= 4
         win |= (uint64_t)bswap_u(nxt) << (32u - 8u * avail);
         avail += 4u;
-        nxt = __builtin_amdgcn_readfirstlane(w[ni]);
+        nxt = w[ni];
         ni++;
     }
     // v shifted left by n bytes (s = 8n, n <= 4) with the next n bytes below it
@@ -197,6 +199,38 @@ __device__ __forceinline__ void dsd_renorm(DsdWin &src, uint32_t &bp, uint32_t d
     low = (uint32_t)((((uint64_t)low << 32) << s) >> 32);
     bp += n;
 }
+
+// Output of a wave-uniform DSD decoder staged in one vector register: value k
+// of a run of up to 64 goes to lane k (a select), and the run is written by
+// one 64-lane store.  A store per value from one lane would leave stores in
+// flight at every payload refill, whose load wait (vmcnt) waits for them too.
+struct StageOutWave {
+    int32_t *out;
+    uint64_t skip;  // values before this index are discarded (a seek's pre_end)
+    uint64_t base;  // output index of lane 0
+    uint32_t cnt;
+    int32_t stg;
+    __device__ __forceinline__ void flush() {
+        const uint32_t lane = threadIdx.x;
+        const uint64_t i = base + lane;
+        if (lane < cnt && i >= skip) out[i] = stg;
+        base += cnt;
+        cnt = 0;
+    }
+    __device__ __forceinline__ void put1(int32_t v0) {
+        const uint32_t lane = threadIdx.x;
+        stg = lane == cnt ? v0 : stg;
+        cnt += 1;
+        if (cnt == 64) flush();
+    }
+    __device__ __forceinline__ void put2(int32_t v0, int32_t v1) {  // cnt stays even
+        const uint32_t lane = threadIdx.x;
+        stg = lane == cnt ? v0 : stg;
+        stg = lane == cnt + 1 ? v1 : stg;
+        cnt += 2;
+        if (cnt == 64) flush();
+    }
+};
 
 // DsdUtils.init_dsd_block_high + decode_high (DsdUtils.cs:343-493) for one
 // block, wave-uniform, with the channel count a compile-time constant so the
@@ -313,14 +347,12 @@ __device__ __forceinline__ DsdResult dsd_high_wave(const BlockDesc &d, const uin
 }
 
 // One range-coder decision of decode_high (DsdUtils.cs:409-422) on the scalar
-// unit: split, compare, narrow; the outcome comes back as `lanes` (this
-// channel's lane mask) or 0, and as the next bit of the output byte.  In asm
-// so the compare's SCC feeds all four selects (the compiler re-derives it
-// from a saved mask after the split + 1 add).
-__device__ __forceinline__ uint64_t dsd_decide(uint32_t value, uint32_t s, uint32_t &high, uint32_t &low, uint32_t &b,
-                                               uint64_t lanes) {
-    uint64_t zm;
-    uint32_t t, t1;
+// unit: split, compare, narrow; the outcome comes back as the lane mask M of
+// the channel's lanes when the value is at or below the split (filter0 = -1),
+// else 0.  In asm so the compare's SCC feeds all three selects.
+template <uint32_t M>
+__device__ __forceinline__ uint32_t dsd_decide(uint32_t value, uint32_t s, uint32_t &high, uint32_t &low) {
+    uint32_t z, t, t1;
     asm("s_sub_u32 %[t], %[hi], %[lo]\n\t"
         "s_lshr_b32 %[t], %[t], 8\n\t"
         "s_mul_i32 %[t], %[t], %[s]\n\t"
@@ -329,25 +361,25 @@ __device__ __forceinline__ uint64_t dsd_decide(uint32_t value, uint32_t s, uint3
         "s_cmp_le_u32 %[v], %[t]\n\t"
         "s_cselect_b32 %[hi], %[t], %[hi]\n\t"
         "s_cselect_b32 %[lo], %[lo], %[t1]\n\t"
-        "s_cselect_b64 %[zm], %[ln], 0\n\t"
-        "s_addc_u32 %[b], %[b], %[b]"
-        : [hi] "+s"(high), [lo] "+s"(low), [b] "+s"(b), [zm] "=&s"(zm), [t] "=&s"(t), [t1] "=&s"(t1)
-        : [v] "s"(value), [s] "s"(s), [ln] "s"(lanes)
+        "s_cselect_b32 %[z], %[m], 0"
+        : [hi] "+s"(high), [lo] "+s"(low), [z] "=s"(z), [t] "=&s"(t), [t1] "=&s"(t1)
+        : [v] "s"(value), [s] "s"(s), [m] "i"(M)
         : "scc");
-    return zm;
+    return z;
 }
 
 // Stereo mode 3: lane 0 holds channel 0's filter state and lane 1 channel
-// 1's, so one VALU instruction updates both channels (the chains are
-// independent; only the range coder and the ptable are shared).  A lone wave issues
-// about one instruction per four cycles, so a decision costs what it issues
-// plus whatever latency is left exposed.  Per bit:
+// 1's (every even / odd lane a copy), so one VALU instruction updates both
+// channels (the chains are independent; only the range coder and the ptable
+// are shared).  A lone wave issues about one instruction per four cycles, so a
+// decision costs what it issues plus whatever latency is left exposed.  Per bit
+// (about 74 instructions for the two decisions):
 //  * the LDS read of both channels' ptable entries is issued first, and the
-//    parts of the filter update that do not depend on the decision (both
-//    outcomes of the factor step and of filter1/filter2's steps) are computed
-//    while it is in flight;
-//  * the two decisions stay scalar; their outcomes become one lane mask
-//    (inverse ballot), so each decision-dependent filter step is one select;
+//    factor step's decision-independent half (the sign test of value against
+//    value - 16 filter6) is computed while it is in flight;
+//  * the two decisions stay scalar and each returns its outcome as a lane mask
+//    (even lanes channel 0's, odd lanes channel 1's), so filter0 is one select
+//    and VALUE_ONE & filter0 one and;
 //  * both channels' ptable updates are one per-lane LDS write (when both
 //    channels hit one entry, channel 1's update starts from channel 0's and
 //    channel 0's write goes to a spare slot, ptable[256]);
@@ -356,13 +388,13 @@ __device__ __forceinline__ uint64_t dsd_decide(uint32_t value, uint32_t s, uint3
 //    0 / 2^20 and the factor decays by 1/1024 per byte), so their products
 //    are full-rate 24-bit multiplies with the same low 32 bits as C#'s
 //    wrapping int multiply;
-//  * the output bytes accumulate in scalar registers.
+//  * each lane accumulates minus its channel's output byte as B = 2 B + filter0
+//    (one shift-add), read out once per byte.
 // Same results and status bits as dsd_high_wave<2> (DsdUtils.cs:391-493).
 __device__ __forceinline__ DsdResult dsd_high_v2(const BlockDesc &d, const uint8_t *blob, const uint8_t *tables,
                                                  int32_t *ptable, DevStoreWave &out) {
     using namespace wvf;
     constexpr int32_t kUp = 0x010000FE, kDown = 0x00010000;
-    constexpr uint64_t kEven = 0x5555555555555555ull;
     const uint32_t dlen = d.dsd_data_len;
     const int ch = threadIdx.x & 1;
     DsdWin src;
@@ -380,6 +412,7 @@ __device__ __forceinline__ DsdResult dsd_high_v2(const BlockDesc &d, const uint8
         __syncthreads();
     }
     uint8_t *lds = (uint8_t *)ptable;
+    StageOutWave so{out.out, out.skip, 0, 0, 0};
     int32_t q2 = d.dsd_filters[ch][0], q3 = d.dsd_filters[ch][1], q4 = d.dsd_filters[ch][2];
     int32_t q5 = d.dsd_filters[ch][3], q6 = d.dsd_filters[ch][4], q8 = d.dsd_filters[ch][5];
     int32_t q7 = 0;
@@ -390,7 +423,7 @@ __device__ __forceinline__ DsdResult dsd_high_v2(const BlockDesc &d, const uint8
         if (!mute) {
             for (uint32_t j = 0; j < n; j++) {
                 int32_t q0 = add32(sub32(q2, q6), __mul24(q7, q8) >> 2);
-                uint32_t b0 = 0, b1 = 0;
+                int32_t nb = 0;  // minus this lane's channel's output byte so far
 #pragma unroll
                 for (int bit = 0; bit < 8; bit++) {
                     const uint32_t addr = ((uint32_t)q0 >> 6) & 0x3FCu;
@@ -400,24 +433,19 @@ __device__ __forceinline__ DsdResult dsd_high_v2(const BlockDesc &d, const uint8
                     int32_t t;  // q0 - 8 * filter6, one 24-bit multiply-add
                     asm("v_mad_i32_i24 %0, %1, -8, %2" : "=v"(t) : "v"(q7), "v"(q0));
                     const int32_t sx = (v ^ t) >> 31;
-                    const int32_t w = v >> 31;
-                    const int32_t dz0 = sx & (w | 1), dz1 = sx & (~w | 1);  // factor step for filter0 = 0 / -1
-                    const int32_t a20 = sub32(0, q2) >> 6, a21 = sub32(1 << 20, q2) >> 6;
-                    const int32_t a30 = sub32(0, q3) >> 4, a31 = sub32(1 << 20, q3) >> 4;
-                    // computed before the first use of pv, i.e. while the read is in flight (the
-                    // compiler would otherwise sink them past the decisions and wait at once)
-                    asm volatile("" : "+v"(pv) : "v"(dz0), "v"(dz1), "v"(a20), "v"(a21), "v"(a30), "v"(a31));
                     const uint32_t pa0 = (uint32_t)__builtin_amdgcn_readlane((int32_t)addr, 0);
                     const uint32_t pa1 = (uint32_t)__builtin_amdgcn_readlane((int32_t)addr, 1);
+                    const bool alias = pa0 == pa1;
+                    // computed before the first use of pv, i.e. while the read is in flight
+                    asm volatile("" : "+v"(pv) : "v"(sx), "s"(pa0), "s"(pa1));
                     // channel 0's decision
                     const uint32_t ps = (uint32_t)pv >> 16;
                     const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane((int32_t)ps, 0);
                     uint32_t s1 = (uint32_t)__builtin_amdgcn_readlane((int32_t)ps, 1);
-                    const uint64_t zm0 = dsd_decide(value, s0, high, low, b0, kEven);
-                    const bool z0 = zm0 != 0;
+                    const uint32_t z0 = dsd_decide<0x55555555u>(value, s0, high, low);
                     int32_t pvl = pv;
                     uint32_t wa = addr;
-                    if (__builtin_expect(pa0 == pa1, 0)) {  // channel 1 reads channel 0's updated entry
+                    if (__builtin_expect(alias, 0)) {  // channel 1 reads channel 0's updated entry
                         const int32_t p0 = __builtin_amdgcn_readlane(pv, 0);
                         const int32_t np0 = p0 + (((z0 ? kUp : kDown) - p0) >> 8);
                         s1 = (uint32_t)np0 >> 16;
@@ -426,14 +454,18 @@ __device__ __forceinline__ DsdResult dsd_high_v2(const BlockDesc &d, const uint8
                     }
                     if (__builtin_expect((high ^ low) < 0x1000000u, 0)) dsd_renorm(src, bp, dlen, value, high, low);
                     // channel 1's decision
-                    const uint64_t zm1 = dsd_decide(value, s1, high, low, b1, ~kEven);
+                    const uint32_t z1 = dsd_decide<0xAAAAAAAAu>(value, s1, high, low);
                     if (__builtin_expect((high ^ low) < 0x1000000u, 0)) dsd_renorm(src, bp, dlen, value, high, low);
-                    // this lane's channel's outcome
-                    const bool zl = __builtin_amdgcn_inverse_ballot_w64(zm0 | zm1);
+                    // this lane's channel's filter0: even lanes take z0, odd lanes z1
+                    const uint32_t zlo = z0 | z1;
+                    const bool zl = __builtin_amdgcn_inverse_ballot_w64(((uint64_t)zlo << 32) | zlo);
+                    const int32_t f0 = zl ? -1 : 0;
+                    nb = add32(shl32(nb, 1), f0);
                     *(int32_t *)(lds + wa) = pvl + (((zl ? kUp : kDown) - pvl) >> 8);
-                    q8 = add32(q8, zl ? dz1 : dz0);
-                    q2 = add32(q2, zl ? a21 : a20);
-                    q3 = add32(q3, zl ? a31 : a30);
+                    q8 = add32(q8, sx & (((v ^ f0) >> 31) | 1));
+                    const int32_t x = f0 & (1 << 20);
+                    q2 = add32(q2, sub32(x, q2) >> 6);
+                    q3 = add32(q3, sub32(x, q3) >> 4);
                     q4 = add32(q4, sub32(q3, q4) >> 4);
                     q5 = add32(q5, sub32(q4, q5) >> 4);
                     const int32_t dd = sub32(q5, q6) >> 4;
@@ -441,14 +473,13 @@ __device__ __forceinline__ DsdResult dsd_high_v2(const BlockDesc &d, const uint8
                     q7 = add32(q7, sub32(dd, q7) >> 3);
                     q0 = add32(sub32(q2, q6), __mul24(q7, q8) >> 2);
                 }
-                const int32_t v0 = (int32_t)(b0 & 0xFFu), v1 = (int32_t)(b1 & 0xFFu);
+                const int32_t v0 = -__builtin_amdgcn_readlane(nb, 0), v1 = -__builtin_amdgcn_readlane(nb, 1);
                 q8 = sub32(q8, add32(q8, 512) >> 10);
                 crc = add32(crc, add32(shl32(crc, 1), v0));
                 crc = add32(crc, add32(shl32(crc, 1), v1));
-                const uint64_t o = (uint64_t)(f + j) * 2u;
-                out.put(o, v0);
-                out.put(o + 1, v1);
+                so.put2(v0, v1);
             }
+            so.flush();
             if (f + n == d.block_samples && crc != d.crc) mute = true;
         }
         if (mute && !(res.status & ST_DSD_MUTE)) {
@@ -456,6 +487,7 @@ __device__ __forceinline__ DsdResult dsd_high_v2(const BlockDesc &d, const uint8
             res.mute_chunk = ci;
         }
         f += n;
+        so.base = (uint64_t)f * 2u;
         chunk_len = next_call_len(d, f);
         ci++;
     }
@@ -736,6 +768,7 @@ __device__ __forceinline__ DsdResult dsd_fast_v2(const BlockDesc &d, const uint8
     value = src.shift_in(0, 32, 4);  // init_dsd_block_fast checked >= 4 payload bytes
     bp = 4;
     uint4 row = *(const uint4 *)(rows + lane * 4u);  // bin 0
+    StageOutWave so{out.out, out.skip, 0, 0, 0};
     uint32_t f = 0, chunk_len = d.first_chunk, ci = 0;
     while (f < d.nframes) {
         uint32_t n = chunk_len;
@@ -797,17 +830,14 @@ __device__ __forceinline__ DsdResult dsd_fast_v2(const BlockDesc &d, const uint8
                 if (!chunk_ok) break;
 #pragma unroll
                 for (int c = 0; c < WCH; c++) crc = add32(crc, add32(shl32(crc, 1), v[c]));
-                const uint64_t o = (uint64_t)(f + j) * och;
-                if (WCH == 1 && !fstereo) {
-                    out.put(o, v[0]);
-                } else if (fstereo) {
-                    out.put(o, v[0]);
-                    out.put(o + 1, v[0]);
-                } else {
-                    out.put(o, v[0]);
-                    out.put(o + 1, v[1]);
-                }
+                if (WCH == 1 && !fstereo)
+                    so.put1(v[0]);
+                else if (fstereo)
+                    so.put2(v[0], v[0]);
+                else
+                    so.put2(v[0], v[1]);
             }
+            so.flush();
             if (!chunk_ok) {
                 mute = true;
                 res.status |= ST_NONDET;  // the rest of this chunk's region keeps stale caller data
@@ -819,6 +849,7 @@ __device__ __forceinline__ DsdResult dsd_fast_v2(const BlockDesc &d, const uint8
             res.mute_chunk = ci;
         }
         f += n;
+        so.base = (uint64_t)f * och;
         chunk_len = next_call_len(d, f);
         ci++;
     }
