@@ -102,3 +102,24 @@ def test_lane_c2_round_trip():
     out_l, res_l, _ = _decode([data], kernel="lane")
     assert res_l[0].crc_errors == 0
     assert np.array_equal(out_l, pcm.reshape(-1))
+
+
+def test_lane_high16_list():
+    # WavPack's 16-term 'high' list (C3's), a lane-only specialisation: 24- and
+    # 16-bit, noise (large medians: some blocks go back to the pipelined kernel),
+    # digital silence, ragged blocks and corrupted streams
+    files = [_stereo(20000, "music", S.TERMS_HIGH, seed=41, bits=24),
+             _stereo(20000, "noise", S.TERMS_HIGH, seed=42, bits=24),
+             _stereo(12345, "music", S.TERMS_HIGH, seed=43, block=997),
+             _stereo(20000, "zeros", S.TERMS_HIGH, seed=44, bits=24)]
+    _check(files, ["high24_music", "high24_noise", "high16_ragged", "high24_zeros"])
+    base = _stereo(20000, "music", S.TERMS_HIGH, seed=45, bits=24)
+    _check([V.corrupt(base, k) for k in range(8)], [f"high_corrupt#{k}" for k in range(8)])
+
+
+def test_lane_c3_round_trip():
+    from synth import corpora
+    pcm, data = corpora.c3(nblocks=24, return_pcm=True)
+    out_l, res_l, _ = _decode([data], kernel="lane")
+    assert res_l[0].crc_errors == 0
+    assert np.array_equal(out_l, pcm.reshape(-1))

@@ -1116,6 +1116,15 @@ __global__ void __launch_bounds__(128) wv_pcm_pipe(const BlockDesc *__restrict__
                                                    uint32_t *__restrict__ status, uint32_t *__restrict__ aux) {
     w2::block_pipe<NEG12>(descs, list, blob, out, status, aux);
 }
+// ... over the blocks a lane kernel handed back, for the lane-only term lists
+template <bool NEG12>
+__global__ void __launch_bounds__(128) wv_pcm_pipe_redo(const BlockDesc *__restrict__ descs,
+                                                        const uint32_t *__restrict__ list,
+                                                        const uint8_t *__restrict__ blob, int32_t *__restrict__ out,
+                                                        uint32_t *__restrict__ status, uint32_t *__restrict__ aux) {
+    if (!(status[list[blockIdx.x]] & lane::ST_REDO)) return;
+    w2::block_pipe<NEG12>(descs, list, blob, out, status, aux);
+}
 
 // the shallow lists WavPack writes most (decoder order, the reverse of the
 // encoder's): each is a compile-time VALU chain (wv_wave2.h); deeper or other
@@ -1136,6 +1145,18 @@ constexpr int kNumTermSets = 3;
 // list; kPipe / kPipe + 1: the pipelined kernel without / with stereo -1/-2 terms
 constexpr int kPipe = 3;
 static_assert(kNumTermSets <= kPipe, "term-set slots");
+
+// lists with a lane-kernel specialisation only (launch group kLaneBase + i): the
+// lane kernel when the batch asks for it, else the pipelined kernel.  WavPack's
+// 16-term 'high' list (C3's).
+#define WVG_TS_HIGH16 2, 18, -1, 8, 6, 3, 5, 7, 4, 2, 18, -2, 3, 2, 18, 18
+static const int8_t kLaneSets[][17] = {
+    {16, WVG_TS_HIGH16},
+};
+constexpr int kNumLaneSets = 1;
+constexpr int kLaneBase = kPipe + 2;
+static_assert(kLaneBase + kNumLaneSets <= 8, "launch groups (wv_api.cpp kMaxTermSets)");
+static const bool kLaneSetNeg12[kNumLaneSets] = {true};
 
 // which two-wave kernel decodes this block (-1: the generic wave kernel, for
 // int32 + wvx, .wvc, exact-float and chained blocks).  prefer_pipe 2: every list goes to the pipelined kernel
@@ -1166,6 +1187,14 @@ int term_set_of(const BlockDesc &d, int prefer_pipe) {
         }
         if (ok) return s;
     }
+    if (!mono) {
+        for (int s = 0; s < kNumLaneSets; s++) {
+            if (kLaneSets[s][0] != d.num_terms) continue;
+            bool ok = true;
+            for (int i = 0; i < d.num_terms && ok; i++) ok = kLaneSets[s][1 + i] == d.term[i];
+            if (ok) return kLaneBase + s;
+        }
+    }
     return pipe;
 }
 
@@ -1173,6 +1202,23 @@ hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, ui
                         int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s, int lane_mode) {
     if (!n) return hipSuccess;
     dim3 g(n), b(128);
+    if (ts >= kLaneBase && ts < kLaneBase + kNumLaneSets) {
+        const bool neg12 = kLaneSetNeg12[ts - kLaneBase];
+        if (!lane_mode) {
+            if (neg12) hipLaunchKernelGGL((wv_pcm_pipe<true>), g, b, 0, s, descs, list, blob, out, status, aux);
+            else hipLaunchKernelGGL((wv_pcm_pipe<false>), g, b, 0, s, descs, list, blob, out, status, aux);
+            return hipGetLastError();
+        }
+        dim3 gl((n + 64 * lane::LPAIRS - 1) / (64 * lane::LPAIRS)), bl(64 * lane::LPAIRS * 2);
+        switch (ts - kLaneBase) {
+        case 0: hipLaunchKernelGGL((wv_pcm_lane<WVG_TS_HIGH16>), gl, bl, 0, s, descs, list, n, blob, out, status); break;
+        }
+        if (lane_mode != 2) {
+            if (neg12) hipLaunchKernelGGL((wv_pcm_pipe_redo<true>), g, b, 0, s, descs, list, blob, out, status, aux);
+            else hipLaunchKernelGGL((wv_pcm_pipe_redo<false>), g, b, 0, s, descs, list, blob, out, status, aux);
+        }
+        return hipGetLastError();
+    }
     if (lane_mode && ts < kNumTermSets) {
         dim3 gl((n + 64 * lane::LPAIRS - 1) / (64 * lane::LPAIRS)), bl(64 * lane::LPAIRS * 2);
         switch (ts) {
