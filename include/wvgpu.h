@@ -175,8 +175,9 @@ int wvg_batch_sync(wvg_batch *b);
  * reconstruction wave), the lowest latency for a batch alone.  WVG_KERNEL_LANE:
  * one lane per block, 64 blocks per workgroup -- one SIMD issue slot moves 64
  * blocks, so many batches in flight decode far more per second; blocks a lane
- * cannot follow exactly are decoded again by the two-wave kernel within the same
- * decode.  Results are identical either way.  Default: WVG_KERNEL_TWO_WAVE
+ * cannot follow exactly are decoded again by the two-wave kernel (the pipelined
+ * kernel for WavPack's 16-term 'high' list, which has a lane specialisation only)
+ * within the same decode.  Results are identical either way.  Default: WVG_KERNEL_TWO_WAVE
  * (WVG_LANE_KERNEL=1 in the environment selects the lane kernel for new batches). */
 #define WVG_KERNEL_TWO_WAVE 0
 #define WVG_KERNEL_LANE 1

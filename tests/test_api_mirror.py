@@ -110,3 +110,19 @@ def test_stream_windows_match_oracle(window):
             continue  # 882,000 one-frame DMAs: covered by the shorter files
         for samples in (4096, 777):
             _same(_oracle_calls(data, samples), _mirror_calls(data, samples, window=window), f"{name}/{window}/{samples}")
+
+
+def test_dsd_calls_and_seeks_match_oracle():
+    """DSD modes 0/1/3 (stereo, mono, false stereo, RLE tables) and corrupted mode-1/3
+    streams (the final chunk's CRC mute) through the call sequence: caller chunks that
+    cut the decoders' 64-value output runs (37, 1000), and seeks whose discarded
+    values start mid-run (DsdUtils.cs:56-136, WavPackUtils.cs:200-282)."""
+    files = [(n, d) for n, d, c in V.dsd_cases()]
+    for n, d in list(files):
+        if n in ("dsd_m1_ch2_fs0", "dsd_m3_ch2_fs0"):
+            files += [(f"{n}_corrupt#{k}", V.corrupt(d, k, start=200)) for k in range(3)]
+    for name, data in files:
+        for samples in (37, 1000):
+            _same(_oracle_calls(data, samples), _mirror_calls(data, samples), f"{name}/{samples}")
+        for target in (3, 5001, 9999):
+            _same(_oracle_calls(data, 4096, seek=target), _mirror_calls(data, 4096, seek=target), f"{name}@{target}")
