@@ -113,13 +113,15 @@ def test_stream_windows_match_oracle(window):
 
 
 def test_dsd_calls_and_seeks_match_oracle():
-    """DSD modes 0/1/3 (stereo, mono, false stereo, RLE tables) and corrupted mode-1/3
+    """DSD modes 0/1/3 (stereo, mono, false stereo, RLE tables) and corrupted mode-3
     streams (the final chunk's CRC mute) through the call sequence: caller chunks that
     cut the decoders' 64-value output runs (37, 1000), and seeks whose discarded
-    values start mid-run (DsdUtils.cs:56-136, WavPackUtils.cs:200-282)."""
+    values start mid-run (DsdUtils.cs:56-136, WavPackUtils.cs:200-282).  (A corrupted
+    mode-1 stream can stop decoding mid-chunk, leaving the rest of the caller's
+    buffer as it was -- ST_NONDET, not comparable call by call.)"""
     files = [(n, d) for n, d, c in V.dsd_cases()]
     for n, d in list(files):
-        if n in ("dsd_m1_ch2_fs0", "dsd_m3_ch2_fs0"):
+        if n == "dsd_m3_ch2_fs0":
             files += [(f"{n}_corrupt#{k}", V.corrupt(d, k, start=200)) for k in range(3)]
     for name, data in files:
         for samples in (37, 1000):

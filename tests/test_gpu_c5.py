@@ -39,12 +39,16 @@ def c5_corpus():
     return files, refs
 
 
-@pytest.mark.parametrize("framing", ["host", "device"])
-def test_c5_batch_matches_oracle(gpu_batch_cls, c5_corpus, framing):
+@pytest.mark.parametrize("framing,kernel", [("host", "two_wave"), ("device", "two_wave"), ("host", "lane")])
+def test_c5_batch_matches_oracle(gpu_batch_cls, c5_corpus, framing, kernel):
+    """kernel 'lane': every PCM kind of the corpus has a lane instantiation (stereo16 {17,17} and
+    default lists, mono16 / false stereo on the mono default list, 24-bit stereo and mono on the
+    16-term lists)."""
     files, refs = c5_corpus
     kinds = _kinds(files)
     assert set(kinds) == {"stereo16", "mono16", "false_stereo", "stereo24", "mono24", "dsd0", "dsd1", "dsd3"}
     b = gpu_batch_cls(4096)
+    b.set_kernel(kernel)
     if framing == "host":
         idx = b.add_files(files, threads=8)
     else:

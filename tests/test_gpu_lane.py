@@ -123,3 +123,27 @@ def test_lane_c3_round_trip():
     out_l, res_l, _ = _decode([data], kernel="lane")
     assert res_l[0].crc_errors == 0
     assert np.array_equal(out_l, pcm.reshape(-1))
+
+
+def _mono(frames, kind="music", terms=S.TERMS_MONO_HIGH[:5], block=4000, seed=0, bits=16, fs=False):
+    m = S.audio_like(frames, 1, bits, seed=seed, kind=kind)
+    if fs:
+        return S.encode_pcm(np.repeat(m, 2, axis=1), S.EncParams(nch=2, false_stereo=True, terms=terms,
+                                                                 block_samples=block, bytes_per_sample=bits // 8))
+    return S.encode_pcm(m, S.EncParams(nch=1, terms=terms, block_samples=block, bytes_per_sample=bits // 8))
+
+
+def test_lane_mono_and_false_stereo():
+    # the mono lane kernel: WavPack's mono default list (5 terms) and 16-term mono list,
+    # 16/24-bit, false stereo (stored twice), silence, noise, ragged and corrupted streams
+    files = [_mono(20000, seed=51), _mono(20000, seed=52, fs=True), _mono(20000, "noise", seed=53),
+             _mono(20000, "zeros", seed=54), _mono(12345, seed=55, block=997),
+             _mono(20000, terms=S.TERMS_MONO_HIGH, seed=56, bits=24),
+             _mono(20000, "noise", terms=S.TERMS_MONO_HIGH, seed=57, bits=24),
+             _mono(9001, terms=S.TERMS_MONO_HIGH, seed=58, bits=24, fs=True)]
+    _check(files, ["m5", "m5_fs", "m5_noise", "m5_zeros", "m5_ragged", "mhigh24", "mhigh24_noise", "mhigh24_fs"])
+    base = _mono(20000, seed=59)
+    _check([V.corrupt(base, k) for k in range(6)], [f"mono_corrupt#{k}" for k in range(6)])
+    for chunk in (1000, 37):
+        _check([_mono(9000, seed=60, block=3000), _mono(9000, seed=61, fs=True, block=3000)], ["m_chunk", "fs_chunk"],
+               chunk)

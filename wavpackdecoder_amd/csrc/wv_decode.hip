@@ -1091,13 +1091,14 @@ __global__ void __launch_bounds__(128) wv_pcm_2wave(const BlockDesc *__restrict_
     w2::block_2wave<Ts...>(descs, list, blob, out, status, aux);
 }
 
-// the lane-per-block kernel (wv_lane.h) and the two-wave kernel over the blocks
-// it handed back (ST_REDO; every other block's workgroup exits at once)
-template <int... Ts>
+// the lane-per-block kernel (wv_lane.h; MONO: mono and false-stereo blocks) and
+// the two-wave kernel over the blocks it handed back (ST_REDO; every other
+// block's workgroup exits at once)
+template <bool MONO, int... Ts>
 __global__ void __launch_bounds__(256) wv_pcm_lane(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
                                                   uint32_t n, const uint8_t *__restrict__ blob, int32_t *__restrict__ out,
                                                   uint32_t *__restrict__ status) {
-    lane::lane_blocks<Ts...>(descs, list, n, blob, out, status);
+    lane::lane_blocks<MONO, Ts...>(descs, list, n, blob, out, status);
 }
 template <int... Ts>
 __global__ void __launch_bounds__(128) wv_pcm_2wave_redo(const BlockDesc *__restrict__ descs,
@@ -1148,15 +1149,20 @@ static_assert(kNumTermSets <= kPipe, "term-set slots");
 
 // lists with a lane-kernel specialisation only (launch group kLaneBase + i): the
 // lane kernel when the batch asks for it, else the pipelined kernel.  WavPack's
-// 16-term 'high' list (C3's).
+// 16-term 'high' lists: stereo (C3's, C5's 24-bit stereo) and mono (C5's 24-bit
+// mono).  The mono lane kernel also takes the M5 set's blocks (WavPack's mono
+// default list: C5's 16-bit mono and false-stereo files).
 #define WVG_TS_HIGH16 2, 18, -1, 8, 6, 3, 5, 7, 4, 2, 18, -2, 3, 2, 18, 18
+#define WVG_TS_MONO_HIGH16 1, 17, 2, 18, 8, 6, 3, 5, 7, 4, 2, 18, 3, 2, 18, 18
 static const int8_t kLaneSets[][17] = {
     {16, WVG_TS_HIGH16},
+    {16, WVG_TS_MONO_HIGH16},
 };
-constexpr int kNumLaneSets = 1;
+constexpr int kNumLaneSets = 2;
 constexpr int kLaneBase = kPipe + 2;
 static_assert(kLaneBase + kNumLaneSets <= 8, "launch groups (wv_api.cpp kMaxTermSets)");
-static const bool kLaneSetNeg12[kNumLaneSets] = {true};
+static const bool kLaneSetMono[kNumLaneSets] = {false, true};
+static const bool kLaneSetNeg12[kNumLaneSets] = {true, false};
 
 // which two-wave kernel decodes this block (-1: the generic wave kernel, for
 // int32 + wvx, .wvc, exact-float and chained blocks).  prefer_pipe 2: every list goes to the pipelined kernel
@@ -1187,9 +1193,9 @@ int term_set_of(const BlockDesc &d, int prefer_pipe) {
         }
         if (ok) return s;
     }
-    if (!mono) {
+    {
         for (int s = 0; s < kNumLaneSets; s++) {
-            if (kLaneSets[s][0] != d.num_terms) continue;
+            if (kLaneSetMono[s] != mono || kLaneSets[s][0] != d.num_terms) continue;
             bool ok = true;
             for (int i = 0; i < d.num_terms && ok; i++) ok = kLaneSets[s][1 + i] == d.term[i];
             if (ok) return kLaneBase + s;
@@ -1211,7 +1217,8 @@ hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, ui
         }
         dim3 gl((n + 64 * lane::LPAIRS - 1) / (64 * lane::LPAIRS)), bl(64 * lane::LPAIRS * 2);
         switch (ts - kLaneBase) {
-        case 0: hipLaunchKernelGGL((wv_pcm_lane<WVG_TS_HIGH16>), gl, bl, 0, s, descs, list, n, blob, out, status); break;
+        case 0: hipLaunchKernelGGL((wv_pcm_lane<false, WVG_TS_HIGH16>), gl, bl, 0, s, descs, list, n, blob, out, status); break;
+        case 1: hipLaunchKernelGGL((wv_pcm_lane<true, WVG_TS_MONO_HIGH16>), gl, bl, 0, s, descs, list, n, blob, out, status); break;
         }
         if (lane_mode != 2) {
             if (neg12) hipLaunchKernelGGL((wv_pcm_pipe_redo<true>), g, b, 0, s, descs, list, blob, out, status, aux);
@@ -1223,17 +1230,18 @@ hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, ui
         dim3 gl((n + 64 * lane::LPAIRS - 1) / (64 * lane::LPAIRS)), bl(64 * lane::LPAIRS * 2);
         switch (ts) {
         case 0:
-            hipLaunchKernelGGL((wv_pcm_lane<WVG_TS_FAST>), gl, bl, 0, s, descs, list, n, blob, out, status);
+            hipLaunchKernelGGL((wv_pcm_lane<false, WVG_TS_FAST>), gl, bl, 0, s, descs, list, n, blob, out, status);
             if (lane_mode != 2)  // 2: the lane kernel alone (diagnostics: ST_REDO stays in the status)
                 hipLaunchKernelGGL((wv_pcm_2wave_redo<WVG_TS_FAST>), g, b, 0, s, descs, list, blob, out, status, aux);
             break;
         case 1:
-            hipLaunchKernelGGL((wv_pcm_lane<WVG_TS_DEFAULT>), gl, bl, 0, s, descs, list, n, blob, out, status);
+            hipLaunchKernelGGL((wv_pcm_lane<false, WVG_TS_DEFAULT>), gl, bl, 0, s, descs, list, n, blob, out, status);
             if (lane_mode != 2)  // 2: the lane kernel alone (diagnostics: ST_REDO stays in the status)
                 hipLaunchKernelGGL((wv_pcm_2wave_redo<WVG_TS_DEFAULT>), g, b, 0, s, descs, list, blob, out, status, aux);
             break;
         case 2:
-            hipLaunchKernelGGL((wv_pcm_lane<WVG_TS_M5>), gl, bl, 0, s, descs, list, n, blob, out, status);
+            // (the mono default list: its blocks are mono or false stereo; a stereo block goes to the redo)
+            hipLaunchKernelGGL((wv_pcm_lane<true, WVG_TS_M5>), gl, bl, 0, s, descs, list, n, blob, out, status);
             if (lane_mode != 2)  // 2: the lane kernel alone (diagnostics: ST_REDO stays in the status)
                 hipLaunchKernelGGL((wv_pcm_2wave_redo<WVG_TS_M5>), g, b, 0, s, descs, list, blob, out, status, aux);
             break;

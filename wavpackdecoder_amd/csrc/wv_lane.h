@@ -17,8 +17,8 @@
 // the word loop only ever reads LDS (one dword per 32 bits consumed, fetched a
 // refill ahead of its use).
 //
-// Scope: lossless PCM stereo blocks whose decorr term list is one of the
-// two-wave kernel's compile-time lists, with no sticky state, wvx/wvc/exact
+// Scope: lossless PCM blocks (stereo; or mono and false stereo, MONO) whose
+// decorr term list has a compile-time instantiation, with no sticky state, wvx/wvc/exact
 // float, seek discard or framing verdict.  Everything the lane does not follow
 // exactly -- a zero-run length or unary escape past the window, the LIMIT_ONES
 // escape, a word longer than the window, a mute, a weight that could leave
@@ -62,10 +62,12 @@ struct LPass {
         }
     }
     // frame t (t % 8 == U): the sample-major form of decorr_stereo_pass
-    // (pass_stereo, wv_decode_core.h; the ring of terms 1..8 read at t & 7, written at (t + T) & 7)
-    template <int U>
+    // (pass_stereo, wv_decode_core.h; the ring of terms 1..8 read at t & 7, written at (t + T) & 7);
+    // MONO: decorr_mono_pass (UnpackUtils.cs:1085-1154), channel A alone
+    template <int U, bool MONO>
     __device__ __forceinline__ void frame(int32_t &L, int32_t &R) {
         using namespace wvf;
+        static_assert(!MONO || T > 0, "mono lists have positive terms only");
         if constexpr (T == 17 || T == 18) {
             const int32_t sa = T == 17 ? sub32(mul32(2, hA[0]), hA[1]) : (sub32(mul32(3, hA[0]), hA[1]) >> 1);
             const int32_t oa = add32(aw(wA, sa), L);
@@ -73,6 +75,7 @@ struct LPass {
             hA[1] = hA[0];
             hA[0] = oa;
             L = oa;
+            if constexpr (MONO) return;
             const int32_t sb = T == 17 ? sub32(mul32(2, hB[0]), hB[1]) : (sub32(mul32(3, hB[0]), hB[1]) >> 1);
             const int32_t ob = add32(aw(wB, sb), R);
             wB = w2::vupd(wB, sb, R, dl);
@@ -85,6 +88,7 @@ struct LPass {
             wA = w2::vupd(wA, sa, L, dl);
             hA[(U + T) & 7] = oa;
             L = oa;
+            if constexpr (MONO) return;
             const int32_t sb = hB[U & 7];
             const int32_t ob = add32(aw(wB, sb), R);
             wB = w2::vupd(wB, sb, R, dl);
@@ -132,7 +136,7 @@ struct LChain;
 template <>
 struct LChain<> {
     __device__ __forceinline__ void init(const BlockDesc &, int) {}
-    template <int U>
+    template <int U, bool MONO>
     __device__ __forceinline__ void frame(int32_t &, int32_t &) {}
     __device__ __forceinline__ bool wbad() const { return false; }
 };
@@ -144,10 +148,10 @@ struct LChain<T, Ts...> {
         p.init(d, i);
         rest.init(d, i + 1);
     }
-    template <int U>
+    template <int U, bool MONO>
     __device__ __forceinline__ void frame(int32_t &L, int32_t &R) {
-        p.template frame<U>(L, R);
-        rest.template frame<U>(L, R);
+        p.template frame<U, MONO>(L, R);
+        rest.template frame<U, MONO>(L, R);
     }
     __device__ __forceinline__ bool wbad() const { return p.wbad() || rest.wbad(); }
 };
@@ -434,42 +438,43 @@ __device__ __forceinline__ uint32_t pverdict(const LState &s, uint32_t u0) {
            (s.rp >= u0 * 4u ? 64u : 0u);
 }
 
-template <int U, bool FULL, bool FAST>
+template <int U, bool FULL, bool FAST, bool MONO>
 __device__ __forceinline__ void pframe(LState &s, const uint8_t *ring, uint32_t rb, int2 *res, uint32_t lane,
                                        uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin) {
     const uint32_t t = g0 + U;
     int2 r;
     r.x = FAST ? lword_fast<0>(s, ring, rb) : lword<0>(s, ring, rb);
-    r.y = FAST ? lword_fast<1>(s, ring, rb) : lword<1>(s, ring, rb);
+    if constexpr (MONO) r.y = 0;
+    else r.y = FAST ? lword_fast<1>(s, ring, rb) : lword<1>(s, ring, rb);
     res[((t & (RF - 1)) << 6) + lane] = r;
     if (!FULL && t + 1u == nfr) pfin = pverdict(s, u0);
 }
-template <bool FULL, bool FAST>
+template <bool FULL, bool FAST, bool MONO>
 __device__ __forceinline__ void pgroup(LState &s, const uint8_t *ring, uint32_t rb, int2 *res, uint32_t lane,
                                        uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin) {
-    pframe<0, FULL, FAST>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
-    pframe<1, FULL, FAST>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
-    pframe<2, FULL, FAST>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
-    pframe<3, FULL, FAST>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
-    pframe<4, FULL, FAST>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
-    pframe<5, FULL, FAST>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
-    pframe<6, FULL, FAST>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
-    pframe<7, FULL, FAST>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    pframe<0, FULL, FAST, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    pframe<1, FULL, FAST, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    pframe<2, FULL, FAST, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    pframe<3, FULL, FAST, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    pframe<4, FULL, FAST, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    pframe<5, FULL, FAST, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    pframe<6, FULL, FAST, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    pframe<7, FULL, FAST, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
 }
 // a group: the fast words first; if a live lane met a rare word, the group again
 // from its starting state with the checked words (the residual slots, the ring
 // and the group's loads are untouched by the first attempt's reads)
-template <bool FULL>
+template <bool FULL, bool MONO>
 __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint32_t rb, int2 *res, uint32_t lane,
                                            uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin) {
     const LState s0 = s;
     const uint32_t pfin0 = pfin;
     s.rare = 0u;
-    pgroup<FULL, true>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    pgroup<FULL, true, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
     if (__builtin_expect(lmask(s.rare != 0u && g0 < nfr) != 0ull, 0)) {
         s = s0;
         pfin = pfin0;
-        pgroup<FULL, false>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+        pgroup<FULL, false, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
     }
 }
 
@@ -491,15 +496,30 @@ __device__ __forceinline__ void lane_finish(uint32_t rbad, const LEnd &e, int32_
     *e.st = bad ? (ST_REDO | (bad << 16)) : st;
 }
 
-// one frame t = g0 + U of the recon wave.  FULL: every lane of the wave is inside its block
-template <int U, bool FULL, int... Ts>
+// one frame t = g0 + U of the recon wave.  FULL: every lane of the wave is inside its block.
+// MONO: one sample per frame (UnpackUtils.cs:571-588: crc = 3 crc + v), stored once, or
+// twice for FALSE_STEREO (fst; :655-664, after the fixup)
+template <int U, bool FULL, bool MONO, int... Ts>
 __device__ __forceinline__ void rframe(LChain<Ts...> &ch, const int2 *res, uint32_t lane, uint32_t g0, uint32_t nfr,
                                        bool joint, int32_t &mx, int32_t &mn, uint32_t &crc, uint32_t sh, int32_t *o,
-                                       uint32_t rbad, const LEnd &e) {
+                                       uint32_t rbad, const LEnd &e, bool fst) {
     const uint32_t t = g0 + U;
     const int2 r = res[((t & (RF - 1)) << 6) + lane];
     int32_t L = r.x, R = r.y;
-    ch.template frame<U>(L, R);
+    ch.template frame<U, MONO>(L, R);
+    if constexpr (MONO) {
+        mx = max(mx, L);
+        mn = min(mn, L);
+        crc = crc * 3u + (uint32_t)L;
+        const int32_t v = (int32_t)((uint32_t)L << sh);
+        const bool st = FULL ? nfr != 0u : t < nfr;
+        if (st) {
+            if (fst) *(int2 *)(o + 2u * t) = make_int2(v, v);
+            else o[t] = v;
+        }
+        if (!FULL && t + 1u == nfr) lane_finish(rbad, e, mx, mn, crc);
+        return;
+    }
     if (joint) {
         R = wvf::sub32(R, L >> 1);
         L = wvf::add32(L, R);
@@ -520,13 +540,14 @@ __device__ __forceinline__ void rframe(LChain<Ts...> &ch, const int2 *res, uint3
 }
 
 // can this lane decode block d exactly (else ST_REDO)?
-template <int... Ts>
+template <bool MONO, int... Ts>
 __device__ __forceinline__ bool lane_ok(const BlockDesc &d) {
     using namespace wvf;
     if (d.kind != KIND_PCM) return false;
-    if (d.flags & (HYBRID_FLAG | MONO_DATA | FLOAT_DATA | INT32_DATA)) return false;
+    if (d.flags & (HYBRID_FLAG | FLOAT_DATA | INT32_DATA)) return false;
+    if (((d.flags & MONO_DATA) != 0) != MONO) return false;
     if (d.inherit || d.chain_len >= 2 || d.wvx_state || d.wvc_len || d.xfloat || d.pre_end || d.fstatus) return false;
-    if (d.out_off & 1u) return false;  // 8-B stores
+    if ((!MONO || (d.flags & FALSE_STEREO)) && (d.out_off & 1u)) return false;  // 8-B stores
     if (d.num_terms != (int32_t)sizeof...(Ts)) return false;
     constexpr int8_t terms[sizeof...(Ts) + 1] = {(int8_t)Ts..., 0};
     for (int i = 0; i < (int)sizeof...(Ts); i++)
@@ -539,7 +560,7 @@ struct LBlock {
     uint32_t bi, nfr, nmax, nmin;
     bool ok, inl;
 };
-template <int... Ts>
+template <bool MONO, int... Ts>
 __device__ __forceinline__ LBlock lane_block(const BlockDesc *descs, const uint32_t *list, uint32_t n, uint32_t grp,
                                              uint32_t lane) {
     LBlock b;
@@ -548,7 +569,7 @@ __device__ __forceinline__ LBlock lane_block(const BlockDesc *descs, const uint3
     // a lane past the list or with a block it does not take decodes 0 frames
     b.inl = li < n;
     b.bi = b.inl ? list[li] : 0u;
-    b.ok = b.inl && lane_ok<Ts...>(descs[b.bi]);
+    b.ok = b.inl && lane_ok<MONO, Ts...>(descs[b.bi]);
     b.nfr = b.ok ? descs[b.bi].nframes : 0u;
     // the wave runs to its longest block; groups inside every block skip the per-frame end tests
     uint32_t nmax = b.nfr, nmin = b.nfr ? b.nfr : 0xFFFFFFFFu;
@@ -573,12 +594,12 @@ __device__ __forceinline__ bool lwait(uint32_t *ctr, uint32_t v, uint32_t *abort
     return false;
 }
 
-template <int... Ts>
+template <bool MONO, int... Ts>
 __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
                                             uint32_t n, const uint8_t *__restrict__ blob, LShared &sh, uint32_t grp,
                                             uint32_t lane) {
     using namespace wvf;
-    const LBlock lb = lane_block<Ts...>(descs, list, n, grp, lane);
+    const LBlock lb = lane_block<MONO, Ts...>(descs, list, n, grp, lane);
     const BlockDesc &d = descs[lb.bi];
     const uint32_t nfr = lb.nfr;
     const uint8_t *ring = (const uint8_t *)sh.ringw;
@@ -625,7 +646,8 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
         if (!lwait(&sh.consumed, g0 + GF > (uint32_t)RF ? g0 + GF - RF : 0u, &sh.abort)) return;
         // a bound that keeps the group exact (else the two-wave kernel redoes the block;
         // the reason lands in status bits 16-23 beside ST_REDO, for diagnostics)
-        const int32_t mm = max(max(max(s.m[0][0], s.m[0][1]), max(s.m[0][2], s.m[1][0])), max(s.m[1][1], s.m[1][2]));
+        const int32_t mm = MONO ? max(max(s.m[0][0], s.m[0][1]), s.m[0][2])
+                                : max(max(max(s.m[0][0], s.m[0][1]), max(s.m[0][2], s.m[1][0])), max(s.m[1][1], s.m[1][2]));
         s.bad |= (mm >= (1 << 26) ? 2u : 0u);
         // this group's loads: the units after fu that fit in the ring (four every
         // group, unconditionally: the waitcnt pass then knows exactly which memory
@@ -638,9 +660,9 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
         uint4 st2 = src[min(u0 + 2u, ulast)], st3 = src[min(u0 + 3u, ulast)];
         fu = u0 + nld;
         if (g0 + GF < lb.nmin)  // (strict: the group holding a block's last frame records its verdict)
-            pgroup_try<true>(s, ring, rb, sh.res, lane, g0, nfr, u0, pfin);
+            pgroup_try<true, MONO>(s, ring, rb, sh.res, lane, g0, nfr, u0, pfin);
         else
-            pgroup_try<false>(s, ring, rb, sh.res, lane, g0, nfr, u0, pfin);
+            pgroup_try<false, MONO>(s, ring, rb, sh.res, lane, g0, nfr, u0, pfin);
         // the reader stayed inside the units written before this group
         if (s.rp >= u0 * 4u) s.bad |= 64u;
         // the loads land in the ring (the unit holding the stream end gets its 0xFF tail)
@@ -666,14 +688,15 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
     }
 }
 
-template <int... Ts>
+template <bool MONO, int... Ts>
 __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
                                            uint32_t n, int32_t *__restrict__ out, uint32_t *__restrict__ status,
                                            LShared &sh, uint32_t grp, uint32_t lane) {
     using namespace wvf;
-    const LBlock lb = lane_block<Ts...>(descs, list, n, grp, lane);
+    const LBlock lb = lane_block<MONO, Ts...>(descs, list, n, grp, lane);
     const BlockDesc &d = descs[lb.bi];
     const uint32_t nfr = lb.nfr;
+    const bool fst = (d.flags & FALSE_STEREO) != 0;
     if (lb.inl && !lb.ok) status[lb.bi] = ST_REDO | (1u << 16);
     const bool joint = (d.flags & JOINT_STEREO) != 0;
     const uint32_t sh_ = (uint32_t)d.shift & 31u;
@@ -694,23 +717,23 @@ __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, 
         }
         rbad |= ch.wbad() ? 4u : 0u;
         if (g0 + GF < lb.nmin) {
-            rframe<0, true>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
-            rframe<1, true>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
-            rframe<2, true>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
-            rframe<3, true>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
-            rframe<4, true>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
-            rframe<5, true>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
-            rframe<6, true>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
-            rframe<7, true>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
+            rframe<0, true, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
+            rframe<1, true, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
+            rframe<2, true, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
+            rframe<3, true, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
+            rframe<4, true, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
+            rframe<5, true, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
+            rframe<6, true, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
+            rframe<7, true, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
         } else {
-            rframe<0, false>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
-            rframe<1, false>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
-            rframe<2, false>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
-            rframe<3, false>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
-            rframe<4, false>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
-            rframe<5, false>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
-            rframe<6, false>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
-            rframe<7, false>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le);
+            rframe<0, false, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
+            rframe<1, false, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
+            rframe<2, false, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
+            rframe<3, false, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
+            rframe<4, false, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
+            rframe<5, false, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
+            rframe<6, false, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
+            rframe<7, false, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
         }
         // the group's residuals are read (DS ops of one wave complete in order)
         w2::lds_publish(&sh.consumed, g0 + GF);
@@ -728,7 +751,7 @@ __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, 
 // workgroup, two per CU possible) ran at ~30,000 Msamples/s on most runs and
 // ~47,000 on some; a workgroup per CU keeps every launch at its one-batch time.
 constexpr int LPAIRS = 2;
-template <int... Ts>
+template <bool MONO, int... Ts>
 __device__ __forceinline__ void lane_blocks(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
                                             uint32_t n, const uint8_t *__restrict__ blob, int32_t *__restrict__ out,
                                             uint32_t *__restrict__ status) {
@@ -744,9 +767,9 @@ __device__ __forceinline__ void lane_blocks(const BlockDesc *__restrict__ descs,
     __syncthreads();
     if (grp * 64u >= n) return;  // (both waves of the pair: uniform)
     if ((wave & 1u) == 0u)
-        lane_parser<Ts...>(descs, list, n, blob, sh, grp, lane);
+        lane_parser<MONO, Ts...>(descs, list, n, blob, sh, grp, lane);
     else
-        lane_recon<Ts...>(descs, list, n, out, status, sh, grp, lane);
+        lane_recon<MONO, Ts...>(descs, list, n, out, status, sh, grp, lane);
 }
 
 }  // namespace lane
