@@ -10,5 +10,5 @@ timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench.log 2
 echo "bench rc=$rc"; tail -1 gpurun_out/bench.log | cut -c1-400; [ $rc -ne 0 ] && exit $rc
 TAG=$TAG bash scripts/profile.sh || exit 1
 WVG_LANE_KERNEL=2 bash scripts/pmc_sq.sh > /dev/null || exit 1
-python3 scripts/pmc_sq_sum.py "wv_pcm_lane<17, 17>" > gpurun_out/pmc_sq_lane.txt; cat gpurun_out/pmc_sq_lane.txt
+python3 scripts/pmc_sq_sum.py "wv_pcm_lane<false, 17, 17>" > gpurun_out/pmc_sq_lane.txt; cat gpurun_out/pmc_sq_lane.txt
 exit 0
