@@ -20,12 +20,18 @@ value  : frames decoded by all ranks / max-over-ranks wall time of the K steps.
          every step is still one complete decode of the whole batch into its own
          output.  The default kernel is the lane-per-block one (--kernel lane,
          wv_lane.h): a block is one serial entropy chain, one lane decodes it, a
-         batch of 1,024 blocks is 16 workgroups, so the chip holds many batches at
-         once -- the default keeps min(K, 20) in flight.  --kernel two_wave is the
+         batch of 1,024 blocks is 8 workgroups of 4 waves (two parser/reconstruction
+         pairs of 64 blocks each, one workgroup per CU), so the chip holds many
+         batches at once -- the default keeps min(K, 20) in flight.  --kernel two_wave is the
          one-workgroup-per-block kernel (lowest latency for a batch alone; best at
          3 in flight), measured beside it in "two_wave".  The line also reports
          the same K steps run one batch at a time ("value_one_batch_at_a_time")
          and the per-launch device times (launch_ms).
+
+After the timed region every in-flight copy is downloaded and checked (C2): its
+int32 output must equal the generator's PCM bit for bit, every block's CRC must
+match (crc_errors == 0), and no block may have been handed back by the lane
+kernel to its fallback (WVG_ST_REDONE; reported as "redo_blocks").
 
 Also printed in the same JSON line:
   roofline     : algorithmic bytes per launch (compressed bytes in + int32
@@ -179,6 +185,30 @@ def pmc_traffic(kernel_substr: str = "wv_pcm_2wave<17, 17>"):
     return float(best[1]["traffic_bytes_per_launch"]), os.path.relpath(best[0], ROOT)
 
 
+# the bench kernel's name as rocprofv3 reports it (profiles/<tag>_pmc.json "kernel")
+KERNEL_NAMES = {"lane": "wv_pcm_lane<false, 17, 17>", "two_wave": "wv_pcm_2wave<17, 17>"}
+
+
+def verify(batches, files, pcm) -> dict:
+    """Download every batch copy and check what its last decode produced: C2's
+    int32 output equals the generator's PCM, no CRC error in any file
+    (WavPackUtils.cs:273-275), and no block went through the lane kernel's
+    fallback (WVG_ST_REDONE).  Raises on any failure."""
+    from wavpackdecoder_amd import _lib
+    crc = redo = blocks = 0
+    for bb in batches:
+        out = bb.download()
+        if pcm is not None:
+            assert np.array_equal(out, pcm.reshape(-1)), "decoded PCM differs from the generator's"
+        crc += sum(bb.result(i).crc_errors for i in range(len(files)) if bb.infos[i].open_ok)
+        st = bb.block_status()
+        redo += int(np.count_nonzero(st & _lib.WVG_ST_REDONE))
+        blocks += int(st.size)
+    assert crc == 0, f"{crc} CRC errors in a synthetic corpus"
+    return {"copies": len(batches), "blocks": blocks, "crc_errors": crc, "redo_blocks": redo,
+            "pcm_equal": pcm is not None}
+
+
 # ---------------------------------------------------------------------------
 # CPU baseline (BASELINE.md:35-38)
 # ---------------------------------------------------------------------------
@@ -328,13 +358,8 @@ def run_rank(args) -> None:
         batches[k % len(batches)].decode()
     for bb in batches:
         bb.sync()
-    crc = 0
-    if args.check or args.workload == "c5":
-        out = b.download()
-        if pcm is not None and args.check:
-            assert np.array_equal(out, pcm.reshape(-1)), "decoded PCM differs from the generator's"
-        crc = sum(b.result(i).crc_errors for i in range(len(files)) if b.infos[i].open_ok)
-        assert crc == 0, "CRC errors in a synthetic corpus"
+    if args.check:
+        verify(batches, files, pcm)
 
     # device time of every launch in the timed region (an event pair around each
     # decode on the stream it runs on)
@@ -386,6 +411,8 @@ def run_rank(args) -> None:
         other = {"kernel": "two_wave", "batches_in_flight": nb, "value": None, "dt": dt_o}
         for bb in batches[:nb]:
             bb.set_kernel(args.kernel)
+    # the timed decodes were real: every copy's output, CRCs and kernel routing
+    ver = verify(batches, files, pcm)
     dt = _reduce(pg, t1 - t0, "max")
     frames_total = _reduce(pg, float(frames_rank), "sum")
     kms_all = _gather(pg, kernel_ms, ws)
@@ -396,7 +423,7 @@ def run_rank(args) -> None:
     if args.timed_only:  # profiling runs: only the timed region's launches reach the profiler
         if rank == 0:
             print(json.dumps({"metric": METRIC, "value": round(value, 2), "kernel_ms": round(kernel_ms, 4),
-                              "batches_in_flight": len(batches)}), flush=True)
+                              "batches_in_flight": len(batches), "verified": ver}), flush=True)
         for bb in batches:
             bb.close()
         if pg is not None:
@@ -470,7 +497,7 @@ def run_rank(args) -> None:
         kernel_ms = solo_ms if solo_ms > 0 else b.time(3)
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     node_gbs = alg_bytes * args.steps * ws / dt / 1e9
-    kname = "wv_pcm_lane<17, 17>" if args.kernel == "lane" else "wv_pcm_2wave<17, 17>"
+    kname = KERNEL_NAMES[args.kernel]
     traffic, traffic_src = pmc_traffic(kname) if args.workload == "c2" else (None, None)
     if rank == 0:
         cpu = None
@@ -545,6 +572,7 @@ def run_rank(args) -> None:
                          "binding_limit": "serial entropy decode per block: one lane's dependent word chain "
                                           "(lane kernel) / one wave's scalar issue (two-wave kernel), not HBM"},
             "cpu_baseline": cpu,
+            "verified": ver,
         }
         print(json.dumps(line), flush=True)
     for bb in batches:

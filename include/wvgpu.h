@@ -51,6 +51,9 @@ extern "C" {
 #define WVG_ST_DSD_MUTE 0x40u
 #define WVG_ST_NONDET 0x80u      /* reference output depends on stale caller-buffer contents */
 #define WVG_ST_TIMEOUT 0x100u    /* the parser/reconstruction handshake timed out: output invalid (not a reference outcome) */
+#define WVG_ST_REDONE 0x200u     /* wvg_batch_block_status only: the lane kernel handed this block back and the
+                                    one-workgroup-per-block kernel decoded it (a cost, never a result: masked out
+                                    of wvg_file_result.status_or) */
 
 typedef struct wvg_ctx wvg_ctx;
 typedef struct wvg_batch wvg_batch;
@@ -207,6 +210,12 @@ int32_t *wvg_batch_host_out(wvg_batch *b);
 int wvg_batch_file_result(wvg_batch *b, int file, wvg_file_result *res);
 /* per-block status words (after download), one per decoded block in file order */
 int wvg_batch_block_status(wvg_batch *b, uint32_t *out, int64_t cap);
+/* Diagnostics (batches created with WVG_LANE_COUNTERS=1 in the environment): per
+ * parser wave of term set `ts`'s last lane-kernel decode, 8 words -- cycles, groups,
+ * then groups taken as a zero-run bulk step / no-run words / split no-run words /
+ * run-aware words / checked words at once / checked replay.  Returns the wave
+ * count (out needs 8 per wave), WVG_ERR_ARG without counters. */
+int wvg_batch_lane_counters(wvg_batch *b, int ts, uint32_t *out, int64_t cap);
 /* The blocks of one file (after download): for block k, end_frame[k] = the number of
  * frames the caller has received when the block's last frame is unpacked (that is
  * when WavpackUnpackSamples runs check_crc_error, WavPackUtils.cs:273-275), and its

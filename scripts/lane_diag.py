@@ -1,34 +1,114 @@
 #!/usr/bin/env python3
-"""Why the lane kernel hands C2 blocks back: decode C2 with WVG_LANE_KERNEL=2 (the
-lane kernel alone, ST_REDO left in the status) and count the reason bits."""
+"""Why the lane kernel hands blocks back: decode a config with WVG_LANE_KERNEL=2
+(the lane kernel alone, ST_REDO left in the status) and count the reason bits
+(status bits 16-23, wv_lane.h; bits 24-31: the parser's reasons in the first group that
+set any), then the lane kernel's time alone and, with the
+fallback on (WVG_LANE_KERNEL=1), the same batch's time.
+
+usage: lane_diag.py [c2|c3|c1|c5|c4] ...  (default c2) -> one JSON line per config
+
+Reason bits: 1 outside the lane's scope (lane_ok), 2 medians >= 2^26, 4 a weight
+that could leave int16, 8 a mute, 16 a bits error / count too long, 32 a word past
+the window, 64 a ring underrun, 128 the partner wave stopped."""
 import collections
-import ctypes
+import json
 import os
+import subprocess
 import sys
 
 import numpy as np
 
-os.environ.setdefault("WVG_LANE_KERNEL", "2")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-from synth import corpora  # noqa: E402
-from wavpackdecoder_amd.api import DecodeBatch  # noqa: E402
+REASONS = {1: "scope", 2: "median_bound", 4: "weight_int16", 8: "mute", 16: "bits_error", 32: "past_window",
+           64: "ring_underrun", 128: "partner_stopped"}
 
-data = corpora.c2()
-b = DecodeBatch(4096)
-b.add_file(data)
-b.upload()
-b.decode()
-b.sync()
-b.download()
-n = b.num_blocks
-st = np.zeros(n, dtype=np.uint32)
-b._L.wvg_batch_block_status(b._b, st.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), n)
-redo = (st & (1 << 15)) != 0
-why = collections.Counter()
-for s in st[redo]:
-    why[int(s) >> 16] += 1
-print("blocks", n, "redo", int(redo.sum()), "reasons", dict(why))
-print("redo block indices", np.nonzero(redo)[0][:40].tolist())
-ms = b.time(5)
-print("lane kernel alone ms", ms)
+
+def files_of(cfg):
+    from synth import corpora
+    if cfg == "c2":
+        return [corpora.c2()]
+    if cfg == "c3":
+        return [corpora.c3()]
+    if cfg == "c1":
+        return [corpora.c1()]
+    if cfg == "c4":
+        return [corpora.c4()]
+    if cfg == "c5":
+        return corpora.c5(4000)
+    raise SystemExit(f"unknown config {cfg}")
+
+
+def one(cfg):
+    from wavpackdecoder_amd.api import DecodeBatch
+    files = files_of(cfg)
+    b = DecodeBatch(4096)  # (WVG_LANE_KERNEL=2 from the environment: no set_kernel, which would set 1)
+    b.add_files(files)
+    b.upload()
+    b.decode()
+    b.sync()
+    b.download()
+    st = b.block_status()
+    redo = (st & (1 << 15)) != 0
+    why, first = collections.Counter(), collections.Counter()
+    for s in st[redo]:
+        r, r0 = (int(s) >> 16) & 0xFF, int(s) >> 24
+        for bit, name in REASONS.items():
+            if r & bit:
+                why[name] += 1
+            if r0 & bit:
+                first[name] += 1
+    ms = b.time(3)
+    waves = {}
+    for ts in range(8):  # per term set: the slowest parser waves and their group paths
+        try:
+            c = b.lane_counters(ts)
+        except RuntimeError:
+            continue
+        if c.size == 0 or c[:, 1].sum() == 0:
+            continue
+        order = np.argsort(-c[:, 0].astype(np.int64))
+        waves[f"ts{ts}"] = {"waves": int(c.shape[0]), "cycles_max": int(c[order[0], 0]),
+                            "cycles_median": int(np.median(c[:, 0])),
+                            "slowest": [dict(zip(("wave", "cycles", "groups", "bulk", "norun", "split", "fast",
+                                                  "checked", "replay"), [int(i)] + [int(v) for v in c[i]]))
+                                        for i in order[:4]],
+                            "totals": dict(zip(("groups", "bulk", "norun", "split", "fast", "checked", "replay"),
+                                               [int(v) for v in c[:, 1:].sum(axis=0)]))}
+    b.close()
+    return {"config": cfg, "lane_waves": waves, "blocks": int(st.size), "redo_blocks": int(redo.sum()),
+            "redo_fraction": round(float(redo.mean()) if st.size else 0.0, 5), "reasons": dict(why), "first_reasons": dict(first),
+            "redo_first": np.nonzero(redo)[0][:16].tolist(), "lane_kernel_alone_ms": round(ms, 3)}
+
+
+def with_fallback(cfg):
+    from wavpackdecoder_amd.api import DecodeBatch
+    b = DecodeBatch(4096)
+    b.set_kernel("lane")
+    b.add_files(files_of(cfg))
+    b.upload()
+    b.decode()
+    b.sync()
+    ms = b.time(3)
+    b.download()
+    st = b.block_status()
+    b.close()
+    return {"with_fallback_ms": round(ms, 3), "redone": int(np.count_nonzero(st & 0x200))}
+
+
+if __name__ == "__main__":
+    cfgs = sys.argv[1:] or ["c2"]
+    if os.environ.get("WVG_LANE_KERNEL") == "1":  # (child: the fallback run)
+        print(json.dumps(with_fallback(cfgs[0])), flush=True)
+        sys.exit(0)
+    os.environ["WVG_LANE_KERNEL"] = "2"
+    os.environ["WVG_LANE_COUNTERS"] = "1"
+    for cfg in cfgs:
+        d = one(cfg)
+        # the fallback run in a child (the kernel mode is read when a batch is created)
+        env = dict(os.environ, WVG_LANE_KERNEL="1")
+        out = subprocess.run([sys.executable, os.path.abspath(__file__), cfg], env=env, capture_output=True,
+                             text=True, timeout=600)
+        if out.returncode == 0:
+            d.update(json.loads(out.stdout.strip().splitlines()[-1]))
+        print(json.dumps(d), flush=True)

@@ -4,6 +4,7 @@
 // runs) for the host, so `pytest -m "not gpu"` can check the decode logic
 // against the oracle on a machine without a GPU.  It is never loaded by the
 // product package (wavpackdecoder_amd), which only runs the HIP kernels.
+#include <stddef.h>
 #include <string.h>
 
 #include <vector>
@@ -23,6 +24,17 @@ struct HostStore {
 };
 
 extern "C" {
+// the descriptor layout the Python side indexes raw descriptor bytes with
+int emu_desc_layout(int64_t *out, int n) {
+    const int64_t v[7] = {(int64_t)sizeof(BlockDesc), (int64_t)offsetof(BlockDesc, kind),
+                          (int64_t)offsetof(BlockDesc, dsd_table_off), (int64_t)offsetof(BlockDesc, inherit),
+                          (int64_t)offsetof(BlockDesc, median), (int64_t)offsetof(BlockDesc, bits_off),
+                          (int64_t)offsetof(BlockDesc, bits_len)};
+    static_assert(offsetof(BlockDesc, chain_len) == offsetof(BlockDesc, inherit) + 8, "inherit, inherit_passes, chain_len");
+    for (int i = 0; i < n && i < 7; i++) out[i] = v[i];
+    return 7;
+}
+
 // Frames n files back to back into one batch the way wvg_batch_add_file does
 // and counts descriptor writes outside their file's reserved output range:
 // *bad_reserved with file_out_extent (the product rule), *bad_values when only

@@ -75,9 +75,19 @@ def file_info(data: bytes) -> dict:
 INFO_FIELDS_FULL = INFO_FIELDS + ("lossy_blocks", "is_five", "file_format", "header_off", "header_len", "trailer_off",
                                   "trailer_len", "first_call_frames", "config_flags", "sample_index0", "exception",
                                   "nondet")
-DESC_BYTES = 1440  # sizeof(BlockDesc)
-DESC_KIND = 32           # offsetof(BlockDesc, kind)
-DESC_DSD_TABLE_OFF = 1312  # offsetof(BlockDesc, dsd_table_off)
+
+
+def _desc_layout():
+    v = np.zeros(7, dtype=np.int64)
+    f = lib().emu_desc_layout
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    f(v.ctypes.data, 7)
+    return (int(x) for x in v)
+
+
+# sizeof(BlockDesc) and offsetof kind / dsd_table_off / inherit / median / bits_off / bits_len (wv_desc.h)
+DESC_BYTES, DESC_KIND, DESC_DSD_TABLE_OFF, DESC_INHERIT, DESC_MEDIAN, DESC_BITS_OFF, DESC_BITS_LEN = _desc_layout()
 KIND_DSD_FAST = 2
 
 

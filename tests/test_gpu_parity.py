@@ -15,13 +15,17 @@ pytestmark = pytest.mark.gpu
 # kernel routes: "2wave" (the product routing: compile-time shallow term lists,
 # the pipelined kernel for every other list, the generic kernel for int32+wvx),
 # "generic" (the wave-per-block kernel for every PCM block), "pipe" (the
-# pipelined kernel for every PCM block without wvx)
-ROUTES = {"2wave": ("0", "0"), "generic": ("1", "0"), "pipe": ("0", "2"), False: ("0", "0"), True: ("1", "0")}
+# pipelined kernel for every PCM block without wvx), "lane" (the throughput
+# kernel, wvg_batch_set_kernel(WVG_KERNEL_LANE): one lane per block for every
+# instantiated lossless list, its hand-backs and every other block as "2wave")
+ROUTES = {"2wave": {}, "generic": {"WVG_FORCE_LANE": "1"}, "pipe": {"WVG_PIPE": "2"},
+          "lane": {"WVG_LANE_KERNEL": "1"}, False: {}, True: {"WVG_FORCE_LANE": "1"}}
+ROUTE_VARS = ("WVG_FORCE_LANE", "WVG_PIPE", "WVG_LANE_KERNEL")
 
 
 def _gpu_decode(files, chunk, batch_cls, force_lane=False):
     import os
-    env = dict(zip(("WVG_FORCE_LANE", "WVG_PIPE"), ROUTES[force_lane]))
+    env = {k: ROUTES[force_lane].get(k, "0") for k in ROUTE_VARS}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -61,7 +65,7 @@ def _check_one(data, chunk, batch_cls, name, force_lane=False):
     np.testing.assert_array_equal(got, ref.samples, err_msg=name)
 
 
-@pytest.mark.parametrize("lane", ["2wave", "generic", "pipe"])
+@pytest.mark.parametrize("lane", ["2wave", "generic", "pipe", "lane"])
 @pytest.mark.parametrize("case", V.pcm_cases(), ids=lambda c: c[0])
 def test_pcm_modes(case, lane, gpu_batch_cls):
     name, data, chunk = case
@@ -100,7 +104,7 @@ def test_corrupted_streams(gpu_batch_cls):
     base = S.encode_pcm(x, S.EncParams(terms=S.TERMS_DEFAULT, block_samples=4000))
     basem = S.encode_pcm(m, S.EncParams(nch=1, terms=S.TERMS_MONO_HIGH, block_samples=3001))
     basex = V.int32_file(x, sent_bits=6, ones=2, wvx=2, max_width=21)
-    for lane in ("2wave", "generic", "pipe"):
+    for lane in ("2wave", "generic", "pipe", "lane"):
         for k in range(10):
             _check_one(V.corrupt(base, k), 4096, gpu_batch_cls, f"stereo#{k}", lane)
             _check_one(V.corrupt(basem, 100 + k), 1000, gpu_batch_cls, f"mono#{k}", lane)

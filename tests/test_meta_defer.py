@@ -21,7 +21,7 @@ from synth import wvsynth as S
 from tests import vectors as V
 from tests.emu import emu as E
 
-DESC_BYTES = 1440
+from tests.emu.emu import DESC_BYTES  # noqa: E402  (sizeof(BlockDesc), from the emu build)
 
 
 def frame(data: bytes, defer: bool, seek: int = -1, chunk: int = 4096):

@@ -46,8 +46,9 @@ def test_sticky_passes_lossless(case):
 def _descs(data, chunk=4096):
     from tests.test_meta_defer import DESC_BYTES, frame
     raw, n, _ = frame(data, True, -1, chunk)
-    # BlockDesc: inherit, inherit_passes, chain_len at byte 1388 (wv_desc.h; 8 B of tail padding follow)
-    return [np.frombuffer(raw[k * DESC_BYTES + 1388:k * DESC_BYTES + 1400], np.uint32) for k in range(n)]
+    # BlockDesc: inherit, inherit_passes, chain_len (wv_desc.h)
+    o = E.DESC_INHERIT
+    return [np.frombuffer(raw[k * DESC_BYTES + o:k * DESC_BYTES + o + 12], np.uint32) for k in range(n)]
 
 
 def test_chain_layout():

@@ -22,6 +22,7 @@ WVG_ST_UNSUPPORTED = 0x20
 WVG_ST_DSD_MUTE = 0x40
 WVG_ST_NONDET = 0x80
 WVG_ST_TIMEOUT = 0x100
+WVG_ST_REDONE = 0x200  # block status only: decoded by the lane kernel's fallback
 WVG_ERR_ARG = -2
 WVG_ERR_OPEN = -3
 WVG_ERR_TIMEOUT = -5
@@ -106,6 +107,7 @@ def lib():
         "wvg_batch_host_out": (vp, [vp]),
         "wvg_batch_file_result": (i32, [vp, i32, ctypes.POINTER(WvgFileResult)]),
         "wvg_batch_block_status": (i32, [vp, vp, i64]),
+        "wvg_batch_lane_counters": (i32, [vp, i32, vp, i64]),
         "wvg_batch_file_blocks": (i32, [vp, i32, vp, vp, i64]),
         "wvg_batch_time": (i32, [vp, i32, ctypes.POINTER(ctypes.c_float)]),
         "wvg_decode_file": (i32, [vp, ctypes.c_char_p, ctypes.c_size_t, i32, vp, i64, ctypes.POINTER(WvgFileInfo),
@@ -145,7 +147,7 @@ EXPORTED = ("wvg_open", "wvg_close", "wvg_last_error", "wvg_batch_new", "wvg_bat
             "wvg_batch_upload", "wvg_batch_reset", "wvg_batch_decode", "wvg_batch_sync", "wvg_batch_stream", "wvg_batch_set_timing", "wvg_batch_set_kernel",
             "wvg_batch_timed", "wvg_batch_group_times", "wvg_batch_out_ints", "wvg_batch_device_out",
             "wvg_batch_num_blocks", "wvg_batch_bytes_in", "wvg_batch_frames", "wvg_batch_download", "wvg_batch_host_out",
-            "wvg_batch_file_result", "wvg_batch_block_status", "wvg_batch_file_blocks", "wvg_batch_time", "wvg_decode_file",
+            "wvg_batch_file_result", "wvg_batch_block_status", "wvg_batch_lane_counters", "wvg_batch_file_blocks", "wvg_batch_time", "wvg_decode_file",
             "wvg_probe_file", "wvg_format_samples", "wvg_batch_format", "wvg_batch_pcm_bytes", "wvg_batch_pcm_offset",
             "wvg_batch_device_pcm", "wvg_batch_download_pcm", "wvg_batch_host_pcm", "wvg_batch_wav",
             "wvg_stream_open", "wvg_stream_unpack", "wvg_stream_set_sample", "wvg_stream_state", "wvg_stream_close")

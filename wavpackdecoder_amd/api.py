@@ -31,11 +31,20 @@ import os
 
 import numpy as np
 
-# more hardware queues than HIP's default 4 for the per-group streams (wv_api.cpp
-# wvg_open); only effective before the process's first HIP call
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
-
 from . import _lib as _L  # noqa: E402
+
+
+def configure_hw_queues(n: int = 16) -> None:
+    """Opt-in: ask HIP for `n` hardware queues per process (GPU_MAX_HW_QUEUES; HIP's
+    default is 4).  A decode runs its launch groups on streams of their own and a
+    server keeps several batches in flight; streams beyond the process's queues
+    share one and their kernels serialise.  It only takes effect before the
+    process's first HIP call, and it applies to every HIP user of the process, so
+    the library never sets it by itself: call this (or export the variable in the
+    launcher) first."""
+    if not 1 <= int(n) <= 32:
+        raise ValueError("GPU_MAX_HW_QUEUES must be in 1..32")
+    os.environ["GPU_MAX_HW_QUEUES"] = str(int(n))
 
 SAMPLE_BUFFER_SIZE = 4096  # Defines.cs:18
 OPEN_2CH_MAX = 0x8         # Defines.cs:26
@@ -239,6 +248,16 @@ class DecodeBatch:
             raise RuntimeError("block status unavailable (download first)")
         return st[:k]
 
+    def lane_counters(self, ts: int) -> np.ndarray:
+        """Diagnostics (a batch made with WVG_LANE_COUNTERS=1): per parser wave of term set
+        `ts`'s last lane decode [cycles, groups, bulk, norun, split, fast, checked, replay]
+        (wvg_batch_lane_counters)."""
+        buf = np.zeros(8 * 4096, dtype=np.uint32)
+        k = self._L.wvg_batch_lane_counters(self._b, int(ts), buf.ctypes.data, buf.size)
+        if k < 0:
+            raise RuntimeError("lane counters unavailable (WVG_LANE_COUNTERS=1 before the batch is made)")
+        return buf[: 8 * k].reshape(k, 8)
+
     def file_blocks(self, i: int):
         """(end_frame, status) per block of file i (wvg_batch_file_blocks)."""
         n = self.num_blocks + 1
@@ -386,6 +405,8 @@ def SetSample(wpc: WavpackContext, sample: int) -> bool:
     rc = _L.lib().wvg_stream_set_sample(wpc._stream(), int(sample))
     if rc == _L.WVG_ERR_EXCEPTION:
         raise WavpackException("the reference's SetSample raises an exception on this file")
+    if rc == _L.WVG_ERR_TIMEOUT:
+        raise DecoderTimeout(_L.lib().wvg_last_error(_context()).decode())
     if rc < 0:
         raise RuntimeError(f"libwvgpu error {rc}: {_L.lib().wvg_last_error(_context()).decode()}")
     return rc == 1

@@ -24,7 +24,8 @@ hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint3
                          hipStream_t s_fast);
 int term_set_of(const BlockDesc &d, int prefer_pipe);
 hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, uint32_t n, const uint8_t *blob,
-                        int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s, int lane_mode);
+                        int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s, int lane_mode,
+                        const uint32_t *lane_list, uint32_t lane_n, uint32_t *lane_dbg);
 hipError_t launch_format(const FormatSeg *segs, uint32_t nseg, const int32_t *in, uint8_t *out, int dsd, hipStream_t s);
 hipError_t upload_dsd_ptables();
 hipError_t launch_dsd_fill(const BlockDesc *descs, const uint32_t *dsd_list, uint32_t n_dsd, const uint32_t *status,
@@ -41,6 +42,7 @@ hipError_t launch_dframe_block(const DFile *files, const uint32_t *blk_file, con
 hipError_t launch_meta(BlockDesc *descs, const MetaJob *jobs, uint32_t njobs, const MetaItem *items, const uint8_t *blob,
                        hipStream_t s);
 constexpr int kMaxTermSets = 8;
+constexpr size_t kLaneDbgWaves = 4096;  // lane-kernel counters (WVG_LANE_COUNTERS): parser waves per term set
 constexpr uint32_t kFormatSeg = 65536;  // values per format work item
 }
 
@@ -151,7 +153,9 @@ struct wvg_batch {
     uint32_t dsd_fast_lo = 0, dsd_fast_n = 0;          // the mode-1 range of dsd_list (sorted by kind)
     std::vector<uint32_t> ts_list[kMaxTermSets];        // two-wave kernels per term set
     int64_t gframes[kSide] = {0};                       // frames per launch group (the lane assignment's load)
-    uint32_t *d_ts[kMaxTermSets] = {nullptr};
+    uint32_t *d_ts[kMaxTermSets] = {nullptr};      // per term set: the list, then the lane kernels' order of it
+    std::vector<uint32_t> ts_lane[kMaxTermSets];  // the lane order (kLaneGap entries included)
+    uint32_t *d_lane_dbg = nullptr;               // WVG_LANE_COUNTERS=1: per parser wave cycles + groups by path
     int force_lane = 0;                                 // WVG_FORCE_LANE=1: every PCM block on the generic kernel
     int prefer_pipe = 0;                                // WVG_PIPE=2: every PCM list on the pipelined kernel (A/B)
     int lanes = kLanes;                                 // WVG_LANES: streams per decode (A/B of the queue mapping)
@@ -227,9 +231,9 @@ wvg_ctx *wvg_open(int device) {
     // DSD mode 1) and keeps several batches in flight; HIP's default of 4 hardware
     // queues per process makes streams share queues, and a queue runs its kernels
     // one after another (a mixed batch then waits for its DSD mode-3 chains before
-    // the PCM groups queued behind them).  Ask for 16 unless the host chose a value;
-    // it takes effect only when this is the process's first HIP call.
-    setenv("GPU_MAX_HW_QUEUES", "16", 0);
+    // the PCM groups queued behind them).  The queue count is the host's choice
+    // (GPU_MAX_HW_QUEUES before the process's first HIP call): the
+    // library never changes the process environment.
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return nullptr;
     if (device < 0) hipGetDevice(&device);
@@ -291,11 +295,19 @@ wvg_batch *wvg_batch_new(wvg_ctx *c, int chunk_frames) {
     if (rm) b->rank_min = atoll(rm);
     const char *hm = getenv("WVG_HOST_META");
     b->fo.defer_values = !(hm && hm[0] == '1');
+    const char *lc = getenv("WVG_LANE_COUNTERS");
+    if (lc && lc[0] == '1') {
+        const size_t bytes = sizeof(uint32_t) * 8u * kLaneDbgWaves * kMaxTermSets;
+        if (hipMalloc(&b->d_lane_dbg, bytes) != hipSuccess || hipMemset(b->d_lane_dbg, 0, bytes) != hipSuccess)
+            b->d_lane_dbg = nullptr;
+    }
     return b;
 }
 
 static void free_dev(wvg_batch *b) {
     hipFree(b->d_blob);
+    hipFree(b->d_lane_dbg);
+    b->d_lane_dbg = nullptr;
     hipFree(b->d_tables);
     hipFree(b->d_pcm);
     hipFree(b->d_descs);
@@ -868,6 +880,42 @@ int wvg_batch_framing_stats(const wvg_batch *b, int64_t *device_files, int64_t *
     return WVG_OK;
 }
 
+// Sort each term-set list (longest blocks first) and build the lane kernels' order of
+// it (wvg_batch::ts_lane): called by the upload before it sizes its staging.
+static void build_lane_orders(wvg_batch *b) {
+    // Each list by length (longest first), then payload bytes per frame.  The lane
+    // order (d_ts[t] + n; a lane kernel decodes 64 consecutive entries per wave):
+    //  * blocks of under half a payload bit per frame -- digital silence, one zero run
+    //    -- in waves of their own (padded with kLaneGap to the next 64), where every
+    //    group is one bulk step of the runs (wv_lane.h): a silent block in a wave of
+    //    music would hold that wave to the run-aware words for the whole block;
+    //  * the others in list order, so that blocks of one kind share waves: full-scale
+    //    noise (large medians: the split words) with noise, music with music -- a wave's
+    //    time is its slowest lane's.
+    auto by_len_density = [&](uint32_t x, uint32_t y) {
+        const BlockDesc &p = b->fo.descs[x], &q = b->fo.descs[y];
+        if (p.nframes != q.nframes) return p.nframes > q.nframes;
+        const uint64_t dp = (uint64_t)p.bits_len * q.nframes, dq = (uint64_t)q.bits_len * p.nframes;
+        return dp != dq ? dp < dq : x < y;
+    };
+    auto silent = [&](uint32_t k) { return (uint64_t)b->fo.descs[k].bits_len * 16u < b->fo.descs[k].nframes; };
+    auto pad = [](std::vector<uint32_t> &v) {
+        while (v.size() & 63u) v.push_back(kLaneGap);
+    };
+    std::vector<uint32_t> rest;
+    for (int t = 0; t < kMaxTermSets; t++) {
+        std::vector<uint32_t> &L = b->ts_list[t], &LL = b->ts_lane[t];
+        LL.clear();
+        if (L.empty()) continue;
+        std::sort(L.begin(), L.end(), by_len_density);
+        rest.clear();
+        for (uint32_t k : L) (silent(k) ? LL : rest).push_back(k);
+        if (!LL.empty() && !rest.empty()) pad(LL);
+        LL.insert(LL.end(), rest.begin(), rest.end());
+        while (!LL.empty() && LL.back() == kLaneGap) LL.pop_back();
+    }
+}
+
 int wvg_batch_upload(wvg_batch *b) {
     if (!b) return WVG_ERR_ARG;
     wvg_ctx *c = b->ctx;
@@ -895,7 +943,9 @@ int wvg_batch_upload(wvg_batch *b) {
     size_t need = al(sizeof(BlockDesc) * nd) + al(sizeof(MetaItem) * b->fo.items.size()) +
                   al(sizeof(MetaJob) * b->fo.jobs.size()) + al(b->fo.tables.size()) + al(sizeof(uint32_t) * (nd + 1)) +
                   al(sizeof(uint32_t) * b->pcm_list.size()) + al(sizeof(uint32_t) * b->dsd_list.size());
-    for (int t = 0; t < kMaxTermSets; t++) need += al(sizeof(uint32_t) * b->ts_list[t].size());
+    build_lane_orders(b);
+    for (int t = 0; t < kMaxTermSets; t++)
+        need += al(sizeof(uint32_t) * b->ts_list[t].size()) + al(sizeof(uint32_t) * b->ts_lane[t].size());
     if (!b->stage.resize(need)) return WVG_ERR_SPACE;
     size_t soff = 0;
     auto put = [&](void *dst, const void *src, size_t bytes) -> hipError_t {
@@ -957,11 +1007,11 @@ int wvg_batch_upload(wvg_batch *b) {
     HIPCHK(c, put(b->d_pcml, b->pcm_list.data(), sizeof(uint32_t) * np));
     HIPCHK(c, put(b->d_dsd, b->dsd_list.data(), sizeof(uint32_t) * ns));
     for (int t = 0; t < kMaxTermSets; t++) {
-        std::vector<uint32_t> &L = b->ts_list[t];
+        const std::vector<uint32_t> &L = b->ts_list[t], &LL = b->ts_lane[t];
         if (L.empty()) continue;
-        std::sort(L.begin(), L.end(), by_kind_len);
-        HIPCHK(c, ensure(b->d_ts[t], b->cap_ts[t], sizeof(uint32_t) * L.size()));
+        HIPCHK(c, ensure(b->d_ts[t], b->cap_ts[t], sizeof(uint32_t) * (L.size() + LL.size())));
         HIPCHK(c, put(b->d_ts[t], L.data(), sizeof(uint32_t) * L.size()));
+        HIPCHK(c, put(b->d_ts[t] + L.size(), LL.data(), sizeof(uint32_t) * LL.size()));
     }
     if (soff > need) return WVG_ERR_SPACE;  // (cannot happen: the sizes above cover every put)
     // frames per launch group: the load the decode's lane assignment balances
@@ -1102,7 +1152,11 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
     for (int t = 0; t < kMaxTermSets; t++)
         if (!b->ts_list[t].empty()) {
             HIPCHK(c, launch_2wave(t, b->d_descs, b->d_ts[t], (uint32_t)b->ts_list[t].size(), b->d_blob, b->d_out,
-                                   b->d_status, b->d_mute, slot(t), b->lane_mode));
+                                   b->d_status, b->d_mute, slot(t), b->lane_mode, b->d_ts[t] + b->ts_list[t].size(),
+                                   (uint32_t)b->ts_lane[t].size(),
+                                   b->d_lane_dbg && b->ts_lane[t].size() <= 64u * kLaneDbgWaves
+                                       ? b->d_lane_dbg + (size_t)t * kLaneDbgWaves * 8u
+                                       : nullptr));
             HIPCHK(c, mark(t));
         }
     for (int l = 1; l < nl; l++) {
@@ -1208,6 +1262,17 @@ int wvg_batch_download(wvg_batch *b, int32_t *host_out, int64_t cap_ints) {
 
 int32_t *wvg_batch_host_out(wvg_batch *b) { return b && !b->hout.empty() ? (int32_t *)b->hout.data() : nullptr; }
 
+int wvg_batch_lane_counters(wvg_batch *b, int ts, uint32_t *out, int64_t cap) {
+    if (!b || ts < 0 || ts >= kMaxTermSets || !b->d_lane_dbg) return WVG_ERR_ARG;
+    const size_t nw = (b->ts_lane[ts].size() + 63) / 64;
+    if (nw > kLaneDbgWaves) return WVG_ERR_ARG;
+    if (cap < (int64_t)(8 * nw)) return WVG_ERR_SPACE;
+    HIPCHK(b->ctx, hipStreamSynchronize(b->stream));
+    HIPCHK(b->ctx, hipMemcpy(out, b->d_lane_dbg + (size_t)ts * kLaneDbgWaves * 8u, sizeof(uint32_t) * 8 * nw,
+                             hipMemcpyDeviceToHost));
+    return (int)nw;
+}
+
 int wvg_batch_block_status(wvg_batch *b, uint32_t *out, int64_t cap) {
     if (!b || !b->downloaded) return WVG_ERR_ARG;
     int64_t n = (int64_t)b->h_status.size();
@@ -1239,7 +1304,7 @@ static int64_t exception_call_frame(const wvg_batch *b, const FileInfo &fi, cons
 // the status word a block contributes to the file result
 static uint32_t block_verdict(const wvg_batch *b, int64_t k) {
     const BlockDesc &d = b->fo.descs[(size_t)k];
-    uint32_t st = b->h_status[(size_t)k];
+    uint32_t st = b->h_status[(size_t)k] & ~(uint32_t)ST_REDONE;  // (which kernel decoded it is not a result)
     // a block decoded from state the device cannot see (only in malformed
     // files): the reference decodes garbage and its CRC check fails
     if ((st & ST_UNSUPPORTED) && d.nframes == d.block_samples) st |= ST_CRC_CHECKED | ST_CRC_ERROR;
@@ -1562,6 +1627,7 @@ struct wvg_stream {
     int64_t lo[2] = {0, 0}, hi[2] = {0, 0};  // frames staged in stage[k] (hi == lo: none)
     hipEvent_t ev[2] = {nullptr, nullptr};
     int cur = 0;
+    int broken = 0;               // a SetSample whose decode failed: every later call returns this code
 };
 
 static int stream_fetch(wvg_stream *s, int k, int64_t from) {
@@ -1659,6 +1725,7 @@ void wvg_stream_close(wvg_stream *s) {
 
 int64_t wvg_stream_unpack(wvg_stream *s, int32_t *buffer, int64_t samples) {
     if (!s || samples < 0 || (!buffer && samples)) return WVG_ERR_ARG;
+    if (s->broken) return s->broken;
     if (samples > INT32_MAX) return WVG_ERR_ARG;
     if (!s->chunk || ((int)samples != s->chunk && s->pos == 0 && samples > 0)) {
         // the first call (or a new request size before any frame went out): the decode is
@@ -1699,6 +1766,7 @@ int64_t wvg_stream_unpack(wvg_stream *s, int32_t *buffer, int64_t samples) {
 
 int wvg_stream_set_sample(wvg_stream *s, int64_t sample) {
     if (!s || sample < 0) return WVG_ERR_ARG;
+    if (s->broken) return s->broken;
     // the block search runs on the host framing (WavPackUtils.cs:521-594)
     FramingOutput fo;
     FileInfo fi;
@@ -1707,11 +1775,22 @@ int wvg_stream_set_sample(wvg_stream *s, int64_t sample) {
     if (!fi.open_ok) return 0;
     if (fi.seek_result < 0) return WVG_ERR_EXCEPTION;
     if (fi.seek_result == 0) return 0;
-    s->errors_before += s->errors;
+    // the new seek and error count are committed only once its decode succeeded
+    const int64_t before = s->errors_before + s->errors, prev_seek = s->seek;
     s->seek = sample;
     // decode now: the discard calls' block ends count towards the errors at once
     const int rc = stream_decode(s, s->chunk ? s->chunk : SAMPLE_BUFFER_SIZE);
-    if (rc != WVG_OK) return rc;  // (the index is where the decode's first call starts: info.sample_index0)
+    if (rc != WVG_OK) {
+        // s->info and s->b may already belong to the new decode: nothing may be served
+        // from mixed state, so the stream is invalid from here on
+        s->seek = prev_seek;
+        s->chunk = 0;
+        s->pos = s->limit = 0;
+        s->lo[0] = s->hi[0] = s->lo[1] = s->hi[1] = 0;
+        s->broken = rc;
+        return rc;
+    }
+    s->errors_before = before;  // (the index is where the decode's first call starts: info.sample_index0)
     stream_count_blocks(s);
     return 1;
 }

@@ -1091,15 +1091,8 @@ __global__ void __launch_bounds__(128) wv_pcm_2wave(const BlockDesc *__restrict_
     w2::block_2wave<Ts...>(descs, list, blob, out, status, aux);
 }
 
-// the lane-per-block kernel (wv_lane.h; MONO: mono and false-stereo blocks) and
-// the two-wave kernel over the blocks it handed back (ST_REDO; every other
-// block's workgroup exits at once)
-template <bool MONO, int... Ts>
-__global__ void __launch_bounds__(256) wv_pcm_lane(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
-                                                  uint32_t n, const uint8_t *__restrict__ blob, int32_t *__restrict__ out,
-                                                  uint32_t *__restrict__ status) {
-    lane::lane_blocks<MONO, Ts...>(descs, list, n, blob, out, status);
-}
+// the two-wave kernel over the blocks the lane-per-block kernel (wv_lane.hip)
+// handed back (ST_REDO; every other block's workgroup exits at once)
 template <int... Ts>
 __global__ void __launch_bounds__(128) wv_pcm_2wave_redo(const BlockDesc *__restrict__ descs,
                                                          const uint32_t *__restrict__ list,
@@ -1107,6 +1100,7 @@ __global__ void __launch_bounds__(128) wv_pcm_2wave_redo(const BlockDesc *__rest
                                                          uint32_t *__restrict__ status, uint32_t *__restrict__ aux) {
     if (!(status[list[blockIdx.x]] & lane::ST_REDO)) return;
     w2::block_2wave<Ts...>(descs, list, blob, out, status, aux);
+    if (threadIdx.x == 64) status[list[blockIdx.x]] |= ST_REDONE;  // (the lane that stored the status: wave 1's lane 0)
 }
 
 // pipelined reconstruction (wv_pipe.h): any term list, one kernel per "has -1/-2"
@@ -1125,14 +1119,12 @@ __global__ void __launch_bounds__(128) wv_pcm_pipe_redo(const BlockDesc *__restr
                                                         uint32_t *__restrict__ status, uint32_t *__restrict__ aux) {
     if (!(status[list[blockIdx.x]] & lane::ST_REDO)) return;
     w2::block_pipe<NEG12>(descs, list, blob, out, status, aux);
+    if (threadIdx.x == 64) status[list[blockIdx.x]] |= ST_REDONE;  // (the lane that stored the status: wave 1's lane 0)
 }
 
 // the shallow lists WavPack writes most (decoder order, the reverse of the
 // encoder's): each is a compile-time VALU chain (wv_wave2.h); deeper or other
-// lists run the pipelined kernel
-#define WVG_TS_FAST 17, 17
-#define WVG_TS_DEFAULT -2, 3, 2, 18, 18
-#define WVG_TS_M5 18, 3, 2, 18, 18
+// lists run the pipelined kernel (WVG_TS_*: wv_lane.h)
 
 static const int8_t kTermSets[][17] = {
     // {count, terms...}
@@ -1152,8 +1144,6 @@ static_assert(kNumTermSets <= kPipe, "term-set slots");
 // 16-term 'high' lists: stereo (C3's, C5's 24-bit stereo) and mono (C5's 24-bit
 // mono).  The mono lane kernel also takes the M5 set's blocks (WavPack's mono
 // default list: C5's 16-bit mono and false-stereo files).
-#define WVG_TS_HIGH16 2, 18, -1, 8, 6, 3, 5, 7, 4, 2, 18, -2, 3, 2, 18, 18
-#define WVG_TS_MONO_HIGH16 1, 17, 2, 18, 8, 6, 3, 5, 7, 4, 2, 18, 3, 2, 18, 18
 static const int8_t kLaneSets[][17] = {
     {16, WVG_TS_HIGH16},
     {16, WVG_TS_MONO_HIGH16},
@@ -1205,7 +1195,8 @@ int term_set_of(const BlockDesc &d, int prefer_pipe) {
 }
 
 hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, uint32_t n, const uint8_t *blob,
-                        int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s, int lane_mode) {
+                        int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s, int lane_mode,
+                        const uint32_t *lane_list, uint32_t lane_n, uint32_t *lane_dbg) {
     if (!n) return hipSuccess;
     dim3 g(n), b(128);
     if (ts >= kLaneBase && ts < kLaneBase + kNumLaneSets) {
@@ -1215,11 +1206,8 @@ hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, ui
             else hipLaunchKernelGGL((wv_pcm_pipe<false>), g, b, 0, s, descs, list, blob, out, status, aux);
             return hipGetLastError();
         }
-        dim3 gl((n + 64 * lane::LPAIRS - 1) / (64 * lane::LPAIRS)), bl(64 * lane::LPAIRS * 2);
-        switch (ts - kLaneBase) {
-        case 0: hipLaunchKernelGGL((wv_pcm_lane<false, WVG_TS_HIGH16>), gl, bl, 0, s, descs, list, n, blob, out, status); break;
-        case 1: hipLaunchKernelGGL((wv_pcm_lane<true, WVG_TS_MONO_HIGH16>), gl, bl, 0, s, descs, list, n, blob, out, status); break;
-        }
+        dim3 gl((lane_n + 64 * lane::LPAIRS - 1) / (64 * lane::LPAIRS)), bl(64 * lane::LPAIRS * 2);
+        if (hipError_t e = launch_lane(ts - kLaneBase == 0 ? LANE_HIGH16 : LANE_MONO_HIGH16, gl, bl, s, descs, lane_list, lane_n, blob, out, status, lane_dbg); e != hipSuccess) return e;
         if (lane_mode != 2) {
             if (neg12) hipLaunchKernelGGL((wv_pcm_pipe_redo<true>), g, b, 0, s, descs, list, blob, out, status, aux);
             else hipLaunchKernelGGL((wv_pcm_pipe_redo<false>), g, b, 0, s, descs, list, blob, out, status, aux);
@@ -1227,21 +1215,21 @@ hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, ui
         return hipGetLastError();
     }
     if (lane_mode && ts < kNumTermSets) {
-        dim3 gl((n + 64 * lane::LPAIRS - 1) / (64 * lane::LPAIRS)), bl(64 * lane::LPAIRS * 2);
+        dim3 gl((lane_n + 64 * lane::LPAIRS - 1) / (64 * lane::LPAIRS)), bl(64 * lane::LPAIRS * 2);
         switch (ts) {
         case 0:
-            hipLaunchKernelGGL((wv_pcm_lane<false, WVG_TS_FAST>), gl, bl, 0, s, descs, list, n, blob, out, status);
+            if (hipError_t e = launch_lane(LANE_FAST, gl, bl, s, descs, lane_list, lane_n, blob, out, status, lane_dbg); e != hipSuccess) return e;
             if (lane_mode != 2)  // 2: the lane kernel alone (diagnostics: ST_REDO stays in the status)
                 hipLaunchKernelGGL((wv_pcm_2wave_redo<WVG_TS_FAST>), g, b, 0, s, descs, list, blob, out, status, aux);
             break;
         case 1:
-            hipLaunchKernelGGL((wv_pcm_lane<false, WVG_TS_DEFAULT>), gl, bl, 0, s, descs, list, n, blob, out, status);
+            if (hipError_t e = launch_lane(LANE_DEFAULT, gl, bl, s, descs, lane_list, lane_n, blob, out, status, lane_dbg); e != hipSuccess) return e;
             if (lane_mode != 2)  // 2: the lane kernel alone (diagnostics: ST_REDO stays in the status)
                 hipLaunchKernelGGL((wv_pcm_2wave_redo<WVG_TS_DEFAULT>), g, b, 0, s, descs, list, blob, out, status, aux);
             break;
         case 2:
             // (the mono default list: its blocks are mono or false stereo; a stereo block goes to the redo)
-            hipLaunchKernelGGL((wv_pcm_lane<true, WVG_TS_M5>), gl, bl, 0, s, descs, list, n, blob, out, status);
+            if (hipError_t e = launch_lane(LANE_M5, gl, bl, s, descs, lane_list, lane_n, blob, out, status, lane_dbg); e != hipSuccess) return e;
             if (lane_mode != 2)  // 2: the lane kernel alone (diagnostics: ST_REDO stays in the status)
                 hipLaunchKernelGGL((wv_pcm_2wave_redo<WVG_TS_M5>), g, b, 0, s, descs, list, blob, out, status, aux);
             break;

@@ -30,9 +30,11 @@ enum StatusBits : uint32_t {
     ST_DSD_MUTE = 1u << 6,     // DSD chunk(s) muted with 0x55 (post-pass fill, DsdUtils.cs:104-117)
     ST_NONDET = 1u << 7,       // reference output depends on stale caller-buffer contents
     ST_TIMEOUT = 1u << 8,      // a kernel's bounded LDS wait ran out (decoder fault, not a reference outcome)
+    ST_REDONE = 1u << 9,       // handed back by the lane kernel and decoded by its fallback (block status only)
 };
 
 constexpr int MAXP = 16;  // MAX_NTERMS
+constexpr uint32_t kLaneGap = 0xFFFFFFFFu;  // an empty lane in a lane kernel's block list
 
 struct alignas(16) BlockDesc {
     // --- bitstreams (byte offsets into the batch blob)
@@ -66,6 +68,25 @@ struct alignas(16) BlockDesc {
     // --- decorrelation passes in decoder order (UnpackUtils.cs:156-360)
     int32_t num_terms;
     uint32_t fstatus;       // StatusBits the framing already knows (UNSUPPORTED, NONDET, ...)
+    // --- seek (WavPackUtils.cs:521-594): after SetSample the block is decoded from
+    // its start by discard calls of pre_chunk frames up to frame pre_end, whose
+    // output is dropped; frame pre_end lands at out_off (which then lies
+    // pre_end * out_nch ints before the file's output, as a wrapped offset)
+    uint32_t pre_end;       // 0: no discard phase
+    uint32_t pre_chunk;     // SAMPLE_BUFFER_SIZE / reduced channels (WavPackUtils.cs:576)
+    // --- sticky state (UnpackUtils.cs:24-68, Appendix B-8): what this block takes
+    // from the decode of the block before it instead of from its own metadata
+    uint32_t inherit;         // InheritBits (0: everything comes from the descriptor)
+    uint32_t inherit_passes;  // bit i: pass i's weights, bit 16 + i: its samples continue
+    uint32_t chain_len;       // first block of a chain: blocks decoded in sequence from it (>= 2)
+    uint32_t wvc_len;         // .wvc correction stream bytes (below; 0: the reference's decode)
+    // --- exact float output (OPEN_EXACT_FLOAT, beyond the reference): 0 = the
+    // reference's float_values; else XF_ON | float_flags | float_max_exp << 8 |
+    // ID_FLOAT_INFO's float_shift << 16 (the wvx stream, if any, in wvx_off/len)
+    uint32_t xfloat;
+    // (everything up to here and term[] is the descriptor's head: the fields the host
+    // reads to route a block -- term_set_of, commit_file -- all lie inside the part of
+    // a device-framed descriptor the host sees, wv_api.cpp kDescHead)
     int8_t term[MAXP];
     int8_t delta[MAXP];
     int16_t weight_A[MAXP];
@@ -78,27 +99,11 @@ struct alignas(16) BlockDesc {
     uint64_t dsd_table_off; // offset into the batch's DSD table area (fast mode)
     int32_t dsd_rate_i;
     int32_t dsd_filters[2][7];  // filter1..5, factor (high mode), per channel
-    // --- seek (WavPackUtils.cs:521-594): after SetSample the block is decoded from
-    // its start by discard calls of pre_chunk frames up to frame pre_end, whose
-    // output is dropped; frame pre_end lands at out_off (which then lies
-    // pre_end * out_nch ints before the file's output, as a wrapped offset)
-    uint32_t pre_end;       // 0: no discard phase
-    uint32_t pre_chunk;     // SAMPLE_BUFFER_SIZE / reduced channels (WavPackUtils.cs:576)
-    // --- sticky state (UnpackUtils.cs:24-68, Appendix B-8): what this block takes
-    // from the decode of the block before it instead of from its own metadata
-    uint32_t inherit;         // InheritBits (0: everything comes from the descriptor)
-    uint32_t inherit_passes;  // bit i: pass i's weights, bit 16 + i: its samples continue
-    uint32_t chain_len;       // first block of a chain: blocks decoded in sequence from it (>= 2)
     // --- .wvc correction (beyond the reference): the hybrid block's
-    // ID_WVC_BITSTREAM in the correction file; crc then holds the .wvc header's
-    // crc (of the exact output) and crc_lossy the .wv header's
+    // ID_WVC_BITSTREAM in the correction file (wvc_len bytes); crc then holds the .wvc
+    // header's crc (of the exact output) and crc_lossy the .wv header's
     uint64_t wvc_off;
-    uint32_t wvc_len;         // 0: no correction stream (the reference's decode)
     int32_t crc_lossy;
-    // --- exact float output (OPEN_EXACT_FLOAT, beyond the reference): 0 = the
-    // reference's float_values; else XF_ON | float_flags | float_max_exp << 8 |
-    // ID_FLOAT_INFO's float_shift << 16 (the wvx stream, if any, in wvx_off/len)
-    uint32_t xfloat;
     // --- DSD mode 1 (DsdUtils.cs:149-242): the probability data after the
     // history-bits and max_probability bytes (run-length coded unless
     // max_probability is 0xFF), from which the decode kernel builds its

@@ -156,10 +156,31 @@ struct LChain<T, Ts...> {
     __device__ __forceinline__ bool wbad() const { return p.wbad() || rest.wbad(); }
 };
 
-// Each lane's ring is RU units at rbase = lane * RSTRIDE bytes of LDS (the
-// 16-B pad spreads the lanes' unit writes over the banks); dword rp (a count
-// of dwords from the lane's 16-B aligned stream base) is at rbase + (rp % (4 RU)) * 4
-constexpr uint32_t RSTRIDE = RU * 16u + 16u;
+// The 64 lanes' rings are interleaved by dword: dword k of a lane's stream (a count
+// of dwords from its 16-B aligned base) sits in ring slot (~k) % (4 RU), and slot p of
+// lane l at byte (p * 64 + l) * 4 of its pair's ring (RING_BYTES each, one array for
+// the workgroup) -- every lane's read of its next dword, whatever its position, hits
+// bank l (no conflicts).  The read position is the byte offset itself (LState.ra:
+// pair ring, slot, lane); the advance to the next dword is one v_lshl_add and one
+// v_bfi that keeps the slot bits (RSLOT) inside the ring.  (The slots run downwards
+// so that a unit's four dwords sit in four consecutive slots.)
+constexpr uint32_t RING_BYTES = RU * 16u * 64u;
+constexpr uint32_t RSLOT = (RU * 4u - 1u) << 8;
+static_assert((RING_BYTES & (RING_BYTES - 1u)) == 0u && RSLOT == RING_BYTES - 256u, "ring layout");
+__device__ __forceinline__ uint32_t rslot(uint32_t k) { return ((~k) << 8) & RSLOT; }
+// ra after moving `adv` (0 or 1) dwords on, given as 0 / ~0 (a lane mask value)
+__device__ __forceinline__ uint32_t ring_step(uint32_t ra, uint32_t adv_mask) {
+    const uint32_t n = ra + (adv_mask << 8);
+    return (n & RSLOT) | (ra & ~RSLOT);
+}
+// unit u (dwords 4u..4u+3) of the lane whose column is `col` (pair ring + lane * 4)
+__device__ __forceinline__ void put_unit(uint8_t *ring, uint32_t col, uint32_t u, uint4 v) {
+    const uint32_t a = rslot(4u * u + 3u) | col;  // dword 4u + 3: the lowest of the four slots
+    *(uint32_t *)(ring + a + 768u) = v.x;
+    *(uint32_t *)(ring + a + 512u) = v.y;
+    *(uint32_t *)(ring + a + 256u) = v.z;
+    *(uint32_t *)(ring + a) = v.w;
+}
 
 // bytes at or past the stream end read as 0xFF (BitsUtils.cs:125-139): unit u
 // relative to a stream ending at byte e
@@ -180,16 +201,21 @@ __device__ __forceinline__ uint4 ff_unit(uint4 v, uint32_t u, uint32_t e) {
 struct LState {
     uint64_t win;  // bit window, LSB = next bit; bits at or above nb are zero
     int32_t nb;    // valid bits in win (>= 33 at every word start)
-    uint32_t rp;   // ring dword merged next
-    uint32_t nxt;  // ring dword rp, read ahead
-    uint32_t h0, h1;    // holding_zero / holding_one as 0/1 per lane (VGPRs: the fast word never
-                        // turns a lane value into an SGPR mask and back, ~20 cycles each way)
+    uint32_t ra;   // ring byte offset of the stream dword merged next (ring_step)
+    uint32_t nxt;  // that dword, read ahead
+    uint32_t rp;   // that dword's index k, as of the group's start (rpos: now)
+    uint32_t ra0;  // ra at the group's start
+    uint32_t keep;      // holding_zero as a lane mask: 0 when the next word holds a zero, else ~0
+    uint32_t h1;        // holding_one as 0/1 (VGPRs: the fast words never turn a lane value into an
+                        // SGPR mask and back, ~20 cycles each way)
     uint32_t zacc;
     int32_t m[2][3];
     uint32_t pmax;   // 17: a bits error or a count too long for the lane (else smaller)
     uint32_t rare;   // fast words: nonzero when a word needed the checked path (escape, run length)
+    uint32_t rmax;   // no-run words: the largest raw unary count (16: an escape -> the checked path)
     int32_t slack;   // least window bits left after a word (< 0: a word past the window)
     uint32_t bad;
+    uint32_t bad0;   // (diagnostics) the reasons of the first group that set any: status bits 24-31
 };
 
 // Selects on lane masks (uint64_t in SGPRs, from ballots).  WV_LANE_ASM=1 forces
@@ -235,6 +261,10 @@ __device__ __forceinline__ int32_t vselmi(uint64_t m, int32_t a, int32_t b) {
     return (int32_t)vselm(m, (uint32_t)a, (uint32_t)b);
 }
 __device__ __forceinline__ uint32_t vsel(bool c, uint32_t a, uint32_t b) { return vselm(lmask(c), a, b); }
+// v_mul_u32_u24 whatever the compiler knows of the operands' range (__umul24 masks them
+// first and may become v_mul_lo_u32, a quarter-rate instruction)
+extern "C" __device__ uint32_t wv_lane_mul_u24(uint32_t a, uint32_t b) __asm("llvm.amdgcn.mul.u24");
+__device__ __forceinline__ uint32_t mul_u24(uint32_t a, uint32_t b) { return wv_lane_mul_u24(a, b); }
 __device__ __forceinline__ uint32_t add3(uint32_t a, uint32_t b, uint32_t c) { return a + b + c; }
 
 // window refill: keep >= 32 bits by merging the dword read ahead (then read the next)
@@ -242,8 +272,8 @@ __device__ __forceinline__ void lrefill(LState &s, const uint8_t *ring, uint32_t
     const bool need = s.nb <= 32;
     s.win |= (uint64_t)vsel(need, s.nxt, 0u) << ((uint32_t)s.nb & 63u);
     s.nb += need ? 32 : 0;
-    s.rp += need ? 1u : 0u;
-    s.nxt = *(const uint32_t *)(ring + rbase + ((s.rp & (RU * 4u - 1u)) << 2));
+    s.ra = ring_step(s.ra, need ? ~0u : 0u);
+    s.nxt = *(const uint32_t *)(ring + s.ra);
 }
 __device__ __forceinline__ void lskip(LState &s, uint32_t n) {  // consume n <= 63 bits
     s.win >>= n;
@@ -280,7 +310,7 @@ template <int C>
 __device__ __forceinline__ int32_t lword(LState &s, const uint8_t *ring, uint32_t rbase) {
     using namespace wvf;
     // zero-run mode (:304-352): both channels' median[0] < 2, nothing held
-    const uint64_t h0m0 = lmask(s.h0 != 0u), h1m0 = lmask(s.h1 != 0u);
+    const uint64_t h0m0 = lmask(s.keep == 0u), h1m0 = lmask(s.h1 != 0u);
     const uint64_t zrm = lmask((((uint32_t)(s.m[0][0] | s.m[1][0])) & ~1u) == 0u) & ~(h0m0 | h1m0);
     bool zskip = false;
     if (__builtin_expect(zrm != 0ull, 0)) {
@@ -318,24 +348,27 @@ __device__ __forceinline__ int32_t lword(LState &s, const uint8_t *ring, uint32_
     }
     p = vselm(hzm, 0u, p);
     lskip(s, p);
+    lrefill(s, ring, rbase);  // (the code after up to 17 unary bits: up to 26 more bits)
     const uint32_t ones = vselm(hzm, 0u, addc(raw >> 1, h1m0));
     const uint64_t b0m = lmask((raw & 1u) != 0u);
     s.h1 = lbit(~hzm & b0m) ? 1u : 0u;
-    s.h0 = lbit(~hzm & ~b0m) ? 1u : 0u;
+    s.keep = lbit(~hzm & ~b0m) ? 0u : ~0u;
     const int32_t m0 = s.m[C][0], m1 = s.m[C][1], m2 = s.m[C][2];
     const uint32_t a0 = (uint32_t)(m0 >> 4), a1 = (uint32_t)(m1 >> 4), a2 = (uint32_t)(m2 >> 4);
     const uint64_t o0 = lmask(ones == 0u), o1 = lmask(ones == 1u), o2 = lmask(ones == 2u), ob = o0 | o1;
     const uint32_t mc = vselm(o0, a0, vselm(o1, a1, a2));
     const uint32_t low1 = a0 + 1u;
-    const uint32_t low2 = (uint32_t)mad24((int32_t)(ones > 2u ? ones - 2u : 0u), (int32_t)(a2 + 1u), (int32_t)(low1 + a1 + 1u));
+    // (32-bit products, C#'s int wrap: this word also serves groups whose medians
+    // are past the fast words' 24-bit operands)
+    const uint32_t low2 = (ones > 2u ? ones - 2u : 0u) * (a2 + 1u) + low1 + a1 + 1u;
     const uint32_t low = vselm(o0, 0u, vselm(o1, low1, low2));
     // median updates (:433-475; DIV0/1/2 as shifts): m + ((m + off) >> s) * mult with
     // (off, mult) = (D - 2, -2) for the bucket's own median, (D, 5) below it, (-, 0) above
-    s.m[C][0] = mad24((int32_t)(add3((uint32_t)m0, 128u, (uint32_t)csel<-2, 0>(o0))) >> 7, csel<-2, 5>(o0), m0);
-    s.m[C][1] = mad24((int32_t)(add3((uint32_t)m1, 64u, (uint32_t)csel<-2, 0>(o1))) >> 6,
-                      vselmi(o0, 0, csel<-2, 5>(o1)), m1);
-    s.m[C][2] = mad24((int32_t)(add3((uint32_t)m2, 32u, (uint32_t)csel<-2, 0>(o2))) >> 5,
-                      vselmi(ob, 0, csel<-2, 5>(o2)), m2);
+    s.m[C][0] = add32(m0, mul32((int32_t)(add3((uint32_t)m0, 128u, (uint32_t)csel<-2, 0>(o0))) >> 7, csel<-2, 5>(o0)));
+    s.m[C][1] = add32(m1, mul32((int32_t)(add3((uint32_t)m1, 64u, (uint32_t)csel<-2, 0>(o1))) >> 6,
+                                vselmi(o0, 0, csel<-2, 5>(o1))));
+    s.m[C][2] = add32(m2, mul32((int32_t)(add3((uint32_t)m2, 32u, (uint32_t)csel<-2, 0>(o2))) >> 5,
+                                vselmi(ob, 0, csel<-2, 5>(o2))));
     // read_code(high - low = mc) (WordsUtils.cs:546-570), then the sign bit
     const uint32_t x = (uint32_t)s.win;
     const uint32_t z = (uint32_t)__builtin_clz(mc | 1u);
@@ -363,21 +396,21 @@ __device__ __forceinline__ int32_t lword_fast(LState &s, const uint8_t *ring, ui
     using namespace wvf;
     // zero-run mode (:304-352): a pending run counts down; its entry is rare.  All
     // as 0/1 lane values (a compound condition would go through SALU mask logic)
-    const uint32_t zx = (((uint32_t)(s.m[0][0] | s.m[1][0])) & ~1u) | s.h0 | s.h1;
+    const uint32_t zx = (((uint32_t)(s.m[0][0] | s.m[1][0])) & ~1u) | (s.keep + 1u) | s.h1;
     const uint32_t zrv = zx == 0u ? 1u : 0u;       // the zero-run test holds
     const uint32_t zdec = min(s.zacc, zrv);        // a pending run counts down
     s.zacc -= zdec;
     const uint32_t zsk = min(s.zacc, zdec);        // ... and this word is one of its zeros
     const uint32_t lo = (uint32_t)s.win;
     const uint32_t raw = (uint32_t)__builtin_ctz(~lo | 0x10000u);  // unary ones, capped at 16
-    const uint32_t keep = (s.h0 | zsk) - 1u;      // ~0 for a word that reads its unary count, 0 for a held zero
+    const uint32_t keep = s.keep & (zsk - 1u);    // ~0 for a word that reads its unary count, 0 for a held zero
     const uint32_t p = (raw + 1u) & keep;
     // rare: 16 ones (LIMIT_ONES escape or a bits error: p == 17), or a run length to read
     s.rare |= ((p + 15u) >> 5) | (zrv & (zdec ^ 1u));
     const uint32_t ones = ((raw >> 1) + s.h1) & keep;
     const uint32_t nh1 = raw & 1u & keep;
     s.h1 = nh1;
-    s.h0 = (nh1 ^ 1u) & keep;
+    s.keep = (uint32_t)__builtin_amdgcn_sbfe((int32_t)(nh1 | ~keep), 0, 1);  // a zero is held after an even count
     s.win >>= p;
     s.nb -= (int32_t)p;
     const int32_t m0 = s.m[C][0], m1 = s.m[C][1], m2 = s.m[C][2];
@@ -412,6 +445,88 @@ __device__ __forceinline__ int32_t lword_fast(LState &s, const uint8_t *ring, ui
     return out;
 }
 
+// The no-run word: lword_fast for a group in which no lane can enter the zero-run
+// mode (lane_parser checks, per group, that max(median[0] of both channels) >= 18:
+// a median[0] falls by at most 2 per word while it is below 130, so the test
+// (:304-306, both channels' median[0] < 2) cannot hold in the group's 8 words per
+// channel, and no run is pending).  Per word, in issue order of need:
+//   unary count raw <= 16 (16: the LIMIT_ONES escape, left to the checked word via
+//   s.rmax); a held zero reads no unary bits (raw & keep); q = the unary bits taken;
+//   the bucket's medians and bounds (:433-475) as selects; read_code (:546-570) on
+//   the 32 bits after the unary part (x, one v_alignbit from the 64-bit window); the
+//   word's total length taken from the window once; the refill merges the dword
+//   read ahead when 32 bits or fewer are left.
+// merge the dword read ahead when 32 bits or fewer are left (and read the next)
+__device__ __forceinline__ void lmerge(LState &s, const uint8_t *ring) {
+    const uint32_t mg = (uint32_t)((s.nb - 33) >> 31);  // ~0: merge
+    const uint32_t sh = (uint32_t)s.nb;
+    __builtin_assume(sh < 64u);
+    s.win |= (uint64_t)(s.nxt & mg) << sh;
+    s.nb = mad24((int32_t)mg, -32, s.nb);
+    s.ra = ring_step(s.ra, mg);
+    s.nxt = *(const uint32_t *)(ring + s.ra);
+}
+// SPLIT: the window is refilled between the unary part and the code as well, for
+// groups whose medians allow codes longer than the 33 bits a word may count on
+// otherwise (pgroup_try)
+template <int C, bool SPLIT>
+__device__ __forceinline__ int32_t lword_nz(LState &s, const uint8_t *ring, uint32_t rbase) {
+    using namespace wvf;
+    const uint32_t lo = (uint32_t)s.win, hi = (uint32_t)(s.win >> 32);
+    const uint32_t raw0 = (uint32_t)__builtin_ctz(~lo | 0x10000u);  // unary ones, capped at 16
+    s.rmax = max(s.rmax, raw0);
+    const uint32_t raw = raw0 & s.keep;          // a held zero: no unary count (ones 0, holding_one clear)
+    const uint32_t ones = (raw >> 1) + s.h1;
+    const uint32_t q = raw - s.keep;             // unary bits taken: raw + 1, or 0 for a held zero
+    s.h1 = raw & 1u;
+    s.keep = (uint32_t)__builtin_amdgcn_sbfe((int32_t)(raw | ~s.keep), 0, 1);  // an even count holds a zero
+    const int32_t m0 = s.m[C][0], m1 = s.m[C][1], m2 = s.m[C][2];
+    const uint32_t a0 = (uint32_t)(m0 >> 4), a1 = (uint32_t)(m1 >> 4), a2 = (uint32_t)(m2 >> 4);
+    const bool o0 = ones == 0u, o1 = ones == 1u;
+    const uint32_t mc = o0 ? a0 : (o1 ? a1 : a2);
+    // (low as selects of values computed unconditionally: a conditional multiply
+    // becomes a divergent branch)
+    const uint32_t l3 = mul_u24(ones > 2u ? ones - 2u : 0u, a2 + 1u) + a1 + 1u;
+    const uint32_t low = vselm(lmask(o0), 0u, add3(a0, 1u, vselm(lmask(o1), 0u, l3)));
+    // median k moves by ((m + DIVk + adj) >> sk) * mult: mult 5 above the bucket, -2 in it
+    // (adj -2), 0 below; both read from nibble tables at the bucket index min(ones, 3)
+    const uint32_t k4 = min(ones, 3u) << 2;
+    s.m[C][0] = mad24(add3((uint32_t)m0, 128u, (uint32_t)__builtin_amdgcn_sbfe(0x000E, k4, 4)) >> 7,
+                      __builtin_amdgcn_sbfe(0x555E, k4, 4), m0);
+    s.m[C][1] = mad24(add3((uint32_t)m1, 64u, (uint32_t)__builtin_amdgcn_sbfe(0x00E0, k4, 4)) >> 6,
+                      __builtin_amdgcn_sbfe(0x55E0, k4, 4), m1);
+    s.m[C][2] = mad24(add3((uint32_t)m2, 32u, (uint32_t)__builtin_amdgcn_sbfe(0x0E00, k4, 4)) >> 5,
+                      __builtin_amdgcn_sbfe(0x5E00, k4, 4), m2);
+    // read_code(mc): nbt = bitcount - 1 bits, one more when v >= extras
+    uint32_t x;
+    if constexpr (SPLIT) {
+        __builtin_assume(q < 64u);
+        s.win >>= q;
+        s.nb -= (int32_t)q;
+        s.slack = min(s.slack, s.nb);
+        lmerge(s, ring);
+        x = (uint32_t)s.win;
+    } else {
+        x = __builtin_amdgcn_alignbit(hi, lo, q);
+    }
+    const uint32_t z = (uint32_t)__builtin_clz(mc | 1u);
+    const uint32_t ex = (0xFFFFFFFFu >> z) - mc;
+    const uint32_t nbt = z ^ 31u;
+    const uint32_t v = __builtin_amdgcn_ubfe(x, 0, nbt);
+    const bool big = v >= ex;
+    const uint32_t t = v + __builtin_amdgcn_ubfe(x, nbt, 1) - ex;  // code = v + t when big
+    const uint32_t mid = add3(low, v, big ? t : 0u);
+    const uint32_t used = nbt + (big ? 1u : 0u);
+    const int32_t sg = __builtin_amdgcn_sbfe((int32_t)x, used, 1);  // 0 or -1
+    const uint32_t tot = SPLIT ? used + 1u : add3(q, used, 1u);
+    __builtin_assume(tot < 64u);
+    s.win >>= tot;
+    s.nb -= (int32_t)tot;
+    s.slack = min(s.slack, s.nb);
+    lmerge(s, ring);
+    return (int32_t)(mid ^ (uint32_t)sg);
+}
+
 // ---------------------------------------------------------------------------
 // Two waves per 64 blocks: the PARSER wave runs the words (lword) and hands each
 // frame's two residuals to the RECON wave through an LDS ring (RF frames per
@@ -426,30 +541,41 @@ constexpr int RF = 32;                     // residual frames in flight per lane
 constexpr uint32_t LSPIN = 1u << 24;       // bounded waits (polls)
 
 struct LShared {
-    uint32_t ringw[64 * RSTRIDE / 4];      // parser: payload units per lane
     int2 res[RF * 64];                     // parser -> recon: residuals of frame t at [(t % RF) * 64 + lane]
     uint32_t pflag[64];                    // parser -> recon: the block's parse verdict (bit 31: final)
     uint32_t produced, consumed, abort;    // frames; abort: a wait ran out
 };
 
+// the index of the stream dword merged next (< 128 advances since the group's start)
+__device__ __forceinline__ uint32_t rpos(const LState &s) { return s.rp + (((s.ra0 - s.ra) & RSLOT) >> 8); }
+
 // the parser's verdict for its lane now (after the block's last frame)
 __device__ __forceinline__ uint32_t pverdict(const LState &s, uint32_t u0) {
-    return 0x80000000u | s.bad | (s.pmax >= 17u ? 16u : 0u) | (s.slack < 0 ? 32u : 0u) |
-           (s.rp >= u0 * 4u ? 64u : 0u);
+    const uint32_t r = s.bad | (s.pmax >= 17u ? 16u : 0u) | (s.slack < 0 ? 32u : 0u) | (rpos(s) >= u0 * 4u ? 64u : 0u);
+    return 0x80000000u | r | ((s.bad0 ? s.bad0 : r) << 8);
 }
 
-template <int U, bool FULL, bool FAST, bool MONO>
+// word kinds: WK_CHECKED lword, WK_FAST lword_fast, WK_NORUN / WK_NORUN_SPLIT lword_nz
+enum { WK_CHECKED = 0, WK_FAST = 1, WK_NORUN = 2, WK_NORUN_SPLIT = 3 };
+template <int K, int C>
+__device__ __forceinline__ int32_t lword_k(LState &s, const uint8_t *ring, uint32_t rb) {
+    if constexpr (K == WK_NORUN) return lword_nz<C, false>(s, ring, rb);
+    else if constexpr (K == WK_NORUN_SPLIT) return lword_nz<C, true>(s, ring, rb);
+    else if constexpr (K == WK_FAST) return lword_fast<C>(s, ring, rb);
+    else return lword<C>(s, ring, rb);
+}
+template <int U, bool FULL, int FAST, bool MONO>
 __device__ __forceinline__ void pframe(LState &s, const uint8_t *ring, uint32_t rb, int2 *res, uint32_t lane,
                                        uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin) {
     const uint32_t t = g0 + U;
     int2 r;
-    r.x = FAST ? lword_fast<0>(s, ring, rb) : lword<0>(s, ring, rb);
+    r.x = lword_k<FAST, 0>(s, ring, rb);
     if constexpr (MONO) r.y = 0;
-    else r.y = FAST ? lword_fast<1>(s, ring, rb) : lword<1>(s, ring, rb);
+    else r.y = lword_k<FAST, 1>(s, ring, rb);
     res[((t & (RF - 1)) << 6) + lane] = r;
     if (!FULL && t + 1u == nfr) pfin = pverdict(s, u0);
 }
-template <bool FULL, bool FAST, bool MONO>
+template <bool FULL, int FAST, bool MONO>
 __device__ __forceinline__ void pgroup(LState &s, const uint8_t *ring, uint32_t rb, int2 *res, uint32_t lane,
                                        uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin) {
     pframe<0, FULL, FAST, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
@@ -461,20 +587,75 @@ __device__ __forceinline__ void pgroup(LState &s, const uint8_t *ring, uint32_t 
     pframe<6, FULL, FAST, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
     pframe<7, FULL, FAST, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
 }
-// a group: the fast words first; if a live lane met a rare word, the group again
-// from its starting state with the checked words (the residual slots, the ring
-// and the group's loads are untouched by the first attempt's reads)
+// a group: the fast words first -- the no-run words when no live lane can meet a
+// zero run in it (lword_nz), else lword_fast; if a live lane met a rare word, the
+// group again from its starting state with the checked words (the residual slots,
+// the ring and the group's loads are untouched by the first attempt's reads)
+// The fast words assume every median below 2^26 at the group's start (their
+// 24-bit products: a median grows at most 3.2x in a group's 8 words per channel) and
+// a window that holds each word (s.slack); a group with a larger median goes to the
+// checked words at once (32-bit arithmetic), a fast group that met a longer word is
+// decoded again by them (they refill between a word's parts).  mm: the lanes' largest
+// median at the group's start.
+// (diagnostics) groups per path of one parser wave: wvg_batch_lane_counters
+struct LCount {
+    uint32_t groups, bulk, norun, split, fast, checked, replay;
+};
 template <bool FULL, bool MONO>
 __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint32_t rb, int2 *res, uint32_t lane,
-                                           uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin) {
+                                           uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin, int32_t mm,
+                                           LCount &cnt) {
+    cnt.groups++;
+    const bool live = g0 < nfr;
+    s.slack = 0;
+    // every live lane inside a zero run for the group's words (:304-316: while the
+    // run's count is past 1 a word is a zero that reads nothing and changes no state
+    // but the count): one bulk step -- the silence waves (the host's lane order)
+    constexpr uint32_t WPG = MONO ? GF : 2 * GF;
+    const bool zrun = ((((uint32_t)(s.m[0][0] | s.m[1][0])) & ~1u) | ~s.keep | s.h1) == 0u && s.zacc > WPG;
+    if (lmask(live && !zrun) == 0ull) {
+#pragma unroll
+        for (int u = 0; u < GF; u++) res[(((g0 + u) & (RF - 1)) << 6) + lane] = make_int2(0, 0);
+        s.zacc -= WPG;
+        if (!FULL && live && nfr <= g0 + GF) pfin = pverdict(s, u0);
+        cnt.bulk++;
+        return;
+    }
+    if (__builtin_expect(lmask(live && mm >= (1 << 26)) != 0ull, 0)) {
+        pgroup<FULL, WK_CHECKED, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+        s.bad |= s.slack < 0 ? 32u : 0u;
+        cnt.checked++;
+        return;
+    }
     const LState s0 = s;
     const uint32_t pfin0 = pfin;
-    s.rare = 0u;
-    pgroup<FULL, true, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
-    if (__builtin_expect(lmask(s.rare != 0u && g0 < nfr) != 0ull, 0)) {
+    const bool norun = max(s.m[0][0], s.m[1][0]) >= 2 + 2 * GF && s.zacc == 0u;
+    if (lmask(live && !norun) == 0ull) {
+        // a word may count on 33 bits: 17 of unary count (16 ones are an escape) and a
+        // code of 15 + 1 while every median stays below 2^19 -- at most 3.2x its value
+        // at the group's start, hence 2^17; with larger medians the window is refilled
+        // between a word's parts (a group with a longer word goes to the checked words)
+        s.rmax = 0u;
+        if (lmask(live && mm >= (1 << 17)) == 0ull) {
+            pgroup<FULL, WK_NORUN, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+            cnt.norun++;
+        } else {
+            pgroup<FULL, WK_NORUN_SPLIT, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+            cnt.split++;
+        }
+        s.rare = s.rmax >> 4;  // (an escape: the checked words)
+    } else {
+        s.rare = 0u;
+        pgroup<FULL, WK_FAST, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+        cnt.fast++;
+    }
+    if (__builtin_expect(lmask((s.rare != 0u || s.slack < 0) && live) != 0ull, 0)) {
         s = s0;
         pfin = pfin0;
-        pgroup<FULL, false, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+        s.slack = 0;
+        pgroup<FULL, WK_CHECKED, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+        s.bad |= s.slack < 0 ? 32u : 0u;
+        cnt.replay++;
     }
 }
 
@@ -487,13 +668,14 @@ struct LEnd {
     uint32_t lane;
 };
 __device__ __forceinline__ void lane_finish(uint32_t rbad, const LEnd &e, int32_t mx, int32_t mn, uint32_t crc) {
-    const uint32_t bad = (rbad | (e.pflag[e.lane] & 0x7FFFFFFFu) | (mx > e.ml || mn < -e.ml ? 8u : 0u));
+    const uint32_t pf = e.pflag[e.lane];
+    const uint32_t bad = (rbad | (pf & 0xFFu) | (mx > e.ml || mn < -e.ml ? 8u : 0u));
     uint32_t st = 0;
     if (e.check) {
         st |= ST_CRC_CHECKED;
         if ((int32_t)crc != e.crc) st |= ST_CRC_ERROR;
     }
-    *e.st = bad ? (ST_REDO | (bad << 16)) : st;
+    *e.st = bad ? (ST_REDO | (bad << 16) | (((pf >> 8) & 0xFFu) << 24)) : st;
 }
 
 // one frame t = g0 + U of the recon wave.  FULL: every lane of the wave is inside its block.
@@ -567,7 +749,7 @@ __device__ __forceinline__ LBlock lane_block(const BlockDesc *descs, const uint3
     const uint32_t li = grp * 64u + lane;
     // every lane stays in the wave (uniform loops keep the lane masks in SGPRs):
     // a lane past the list or with a block it does not take decodes 0 frames
-    b.inl = li < n;
+    b.inl = li < n && list[li] != kLaneGap;
     b.bi = b.inl ? list[li] : 0u;
     b.ok = b.inl && lane_ok<MONO, Ts...>(descs[b.bi]);
     b.nfr = b.ok ? descs[b.bi].nframes : 0u;
@@ -596,15 +778,17 @@ __device__ __forceinline__ bool lwait(uint32_t *ctr, uint32_t v, uint32_t *abort
 
 template <bool MONO, int... Ts>
 __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
-                                            uint32_t n, const uint8_t *__restrict__ blob, LShared &sh, uint32_t grp,
-                                            uint32_t lane) {
+                                            uint32_t n, const uint8_t *__restrict__ blob, LShared &sh,
+                                            uint8_t *ringm, uint32_t pair, uint32_t grp, uint32_t lane,
+                                            uint32_t *__restrict__ dbg) {
     using namespace wvf;
+    const uint64_t t_start = __builtin_readcyclecounter();
+    LCount cnt = {0, 0, 0, 0, 0, 0, 0};
     const LBlock lb = lane_block<MONO, Ts...>(descs, list, n, grp, lane);
     const BlockDesc &d = descs[lb.bi];
     const uint32_t nfr = lb.nfr;
-    const uint8_t *ring = (const uint8_t *)sh.ringw;
-    uint8_t *ringm = (uint8_t *)sh.ringw;
-    const uint32_t rb = lane * RSTRIDE;  // this lane's ring
+    const uint8_t *ring = ringm;
+    const uint32_t rb = pair * RING_BYTES + lane * 4u;  // this lane's column of its pair's ring
 
     // payload: 16-B units from the aligned base; bytes at or past e read 0xFF
     const uint64_t boff = d.bits_off;
@@ -617,24 +801,30 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
     for (uint32_t u = 0; u < (uint32_t)RU; u++) {
         uint4 v = u < eu ? src[u] : ffu;
         if (u + 1u >= eu) v = ff_unit(v, u, e);
-        *(uint4 *)(ringm + rb + (u << 4)) = v;
+        put_unit(ringm, rb, u, v);
     }
     uint32_t fu = RU;  // next unit to load
 
     LState s;
     s.rp = skip >> 2;
-    s.win = (uint64_t)(*(const uint32_t *)(ring + rb + ((s.rp & (RU * 4u - 1u)) << 2))) |
-            ((uint64_t)(*(const uint32_t *)(ring + rb + (((s.rp + 1u) & (RU * 4u - 1u)) << 2))) << 32);
+    s.ra = rslot(s.rp) | rb;
+    s.win = (uint64_t)(*(const uint32_t *)(ring + s.ra)) |
+            ((uint64_t)(*(const uint32_t *)(ring + (rslot(s.rp + 1u) | rb))) << 32);
     s.win >>= (skip & 3u) * 8u;
     s.nb = 64 - (int32_t)((skip & 3u) * 8u);
     s.rp += 2u;
-    s.nxt = *(const uint32_t *)(ring + rb + ((s.rp & (RU * 4u - 1u)) << 2));
-    s.h0 = s.h1 = 0u;
+    s.ra = rslot(s.rp) | rb;
+    s.ra0 = s.ra;
+    s.nxt = *(const uint32_t *)(ring + s.ra);
+    s.keep = ~0u;
+    s.h1 = 0u;
     s.rare = 0u;
+    s.rmax = 0u;
     s.zacc = 0u;
     s.pmax = 0u;
     s.slack = 0;
     s.bad = 0u;
+    s.bad0 = 0u;
 #pragma unroll
     for (int c = 0; c < 2; c++)
 #pragma unroll
@@ -648,7 +838,7 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
         // the reason lands in status bits 16-23 beside ST_REDO, for diagnostics)
         const int32_t mm = MONO ? max(max(s.m[0][0], s.m[0][1]), s.m[0][2])
                                 : max(max(max(s.m[0][0], s.m[0][1]), max(s.m[0][2], s.m[1][0])), max(s.m[1][1], s.m[1][2]));
-        s.bad |= (mm >= (1 << 26) ? 2u : 0u);
+        s.bad |= (mm >= (1 << 29) ? 2u : 0u);  // (the checked words' int32 products hold to 2^31)
         // this group's loads: the units after fu that fit in the ring (four every
         // group, unconditionally: the waitcnt pass then knows exactly which memory
         // operations are in flight; units past the stream re-read its last one)
@@ -660,31 +850,45 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
         uint4 st2 = src[min(u0 + 2u, ulast)], st3 = src[min(u0 + 3u, ulast)];
         fu = u0 + nld;
         if (g0 + GF < lb.nmin)  // (strict: the group holding a block's last frame records its verdict)
-            pgroup_try<true, MONO>(s, ring, rb, sh.res, lane, g0, nfr, u0, pfin);
+            pgroup_try<true, MONO>(s, ring, rb, sh.res, lane, g0, nfr, u0, pfin, mm, cnt);
         else
-            pgroup_try<false, MONO>(s, ring, rb, sh.res, lane, g0, nfr, u0, pfin);
+            pgroup_try<false, MONO>(s, ring, rb, sh.res, lane, g0, nfr, u0, pfin, mm, cnt);
         // the reader stayed inside the units written before this group
+        s.rp = rpos(s);
+        s.ra0 = s.ra;
         if (s.rp >= u0 * 4u) s.bad |= 64u;
+        if (!s.bad0) s.bad0 = s.bad | (s.pmax >= 17u ? 16u : 0u);
         // the loads land in the ring (the unit holding the stream end gets its 0xFF tail)
         if (nld > 0u) {
             if (u0 + 1u >= eu) st0 = ff_unit(st0, u0, e);
-            *(uint4 *)(ringm + rb + (((u0) & (RU - 1)) << 4)) = st0;
+            put_unit(ringm, rb, u0, st0);
         }
         if (nld > 1u) {
             if (u0 + 2u >= eu) st1 = ff_unit(st1, u0 + 1u, e);
-            *(uint4 *)(ringm + rb + (((u0 + 1u) & (RU - 1)) << 4)) = st1;
+            put_unit(ringm, rb, u0 + 1u, st1);
         }
         if (nld > 2u) {
             if (u0 + 3u >= eu) st2 = ff_unit(st2, u0 + 2u, e);
-            *(uint4 *)(ringm + rb + (((u0 + 2u) & (RU - 1)) << 4)) = st2;
+            put_unit(ringm, rb, u0 + 2u, st2);
         }
         if (nld > 3u) {
             if (u0 + 4u >= eu) st3 = ff_unit(st3, u0 + 3u, e);
-            *(uint4 *)(ringm + rb + (((u0 + 3u) & (RU - 1)) << 4)) = st3;
+            put_unit(ringm, rb, u0 + 3u, st3);
         }
         // publish the group: residuals and verdicts first, then the count
         sh.pflag[lane] = pfin;
         w2::lds_publish(&sh.produced, g0 + GF);
+    }
+    if (dbg && lane == 0u) {  // (diagnostics: cycles and groups per path of this wave)
+        uint32_t *o = dbg + grp * 8u;
+        o[0] = (uint32_t)(__builtin_readcyclecounter() - t_start);
+        o[1] = cnt.groups;
+        o[2] = cnt.bulk;
+        o[3] = cnt.norun;
+        o[4] = cnt.split;
+        o[5] = cnt.fast;
+        o[6] = cnt.checked;
+        o[7] = cnt.replay;
     }
 }
 
@@ -754,8 +958,9 @@ constexpr int LPAIRS = 2;
 template <bool MONO, int... Ts>
 __device__ __forceinline__ void lane_blocks(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
                                             uint32_t n, const uint8_t *__restrict__ blob, int32_t *__restrict__ out,
-                                            uint32_t *__restrict__ status) {
+                                            uint32_t *__restrict__ status, uint32_t *__restrict__ dbg) {
     __shared__ LShared shp[LPAIRS];
+    __shared__ uint32_t rings[LPAIRS * RING_BYTES / 4];  // the parsers' payload rings (put_unit, ring_step)
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     const uint32_t pair = wave >> 1, grp = blockIdx.x * LPAIRS + pair;
     LShared &sh = shp[pair];
@@ -767,10 +972,24 @@ __device__ __forceinline__ void lane_blocks(const BlockDesc *__restrict__ descs,
     __syncthreads();
     if (grp * 64u >= n) return;  // (both waves of the pair: uniform)
     if ((wave & 1u) == 0u)
-        lane_parser<MONO, Ts...>(descs, list, n, blob, sh, grp, lane);
+        lane_parser<MONO, Ts...>(descs, list, n, blob, sh, (uint8_t *)rings, pair, grp, lane, dbg);
     else
         lane_recon<MONO, Ts...>(descs, list, n, out, status, sh, grp, lane);
 }
 
 }  // namespace lane
+
+// the term lists with a lane instantiation (decoder order, the reverse of the
+// encoder's; wv_lane.hip): WavPack's fast, default and mono-default lists, and
+// its 16-term 'high' lists (stereo: C3's and C5's 24-bit stereo; mono)
+#define WVG_TS_FAST 17, 17
+#define WVG_TS_DEFAULT -2, 3, 2, 18, 18
+#define WVG_TS_M5 18, 3, 2, 18, 18
+#define WVG_TS_HIGH16 2, 18, -1, 8, 6, 3, 5, 7, 4, 2, 18, -2, 3, 2, 18, 18
+#define WVG_TS_MONO_HIGH16 1, 17, 2, 18, 8, 6, 3, 5, 7, 4, 2, 18, 3, 2, 18, 18
+enum LaneList { LANE_FAST = 0, LANE_DEFAULT, LANE_M5, LANE_HIGH16, LANE_MONO_HIGH16 };
+// the lane kernel of one list over n blocks (wv_lane.hip)
+// dbg (nullptr: off): per parser wave 8 words (cycles, groups by path: LCount)
+hipError_t launch_lane(int which, dim3 grid, dim3 block, hipStream_t s, const BlockDesc *descs, const uint32_t *list,
+                       uint32_t n, const uint8_t *blob, int32_t *out, uint32_t *status, uint32_t *dbg);
 }  // namespace wvg
