@@ -211,10 +211,11 @@ int wvg_batch_file_result(wvg_batch *b, int file, wvg_file_result *res);
 /* per-block status words (after download), one per decoded block in file order */
 int wvg_batch_block_status(wvg_batch *b, uint32_t *out, int64_t cap);
 /* Diagnostics (batches created with WVG_LANE_COUNTERS=1 in the environment): per
- * parser wave of term set `ts`'s last lane-kernel decode, 8 words -- cycles, groups,
+ * parser wave of term set `ts`'s last lane-kernel decode, 16 words -- cycles, groups,
  * then groups taken as a zero-run bulk step / no-run words / split no-run words /
- * run-aware words / checked words at once / checked replay.  Returns the wave
- * count (out needs 8 per wave), WVG_ERR_ARG without counters. */
+ * run-aware words / checked words at once / checked replay, then the cycles spent
+ * waiting for the reconstruction wave and for the payload loads.  Returns the wave
+ * count (out needs 16 per wave), WVG_ERR_ARG without counters. */
 int wvg_batch_lane_counters(wvg_batch *b, int ts, uint32_t *out, int64_t cap);
 /* The blocks of one file (after download): for block k, end_frame[k] = the number of
  * frames the caller has received when the block's last frame is unpacked (that is

@@ -71,10 +71,11 @@ def one(cfg):
         waves[f"ts{ts}"] = {"waves": int(c.shape[0]), "cycles_max": int(c[order[0], 0]),
                             "cycles_median": int(np.median(c[:, 0])),
                             "slowest": [dict(zip(("wave", "cycles", "groups", "bulk", "norun", "split", "fast",
-                                                  "checked", "replay"), [int(i)] + [int(v) for v in c[i]]))
+                                                  "checked", "replay", "wait_consumed", "wait_loads"),
+                                                 [int(i)] + [int(v) for v in c[i][:10]]))
                                         for i in order[:4]],
                             "totals": dict(zip(("groups", "bulk", "norun", "split", "fast", "checked", "replay"),
-                                               [int(v) for v in c[:, 1:].sum(axis=0)]))}
+                                               [int(v) for v in c[:, 1:8].sum(axis=0)]))}
     b.close()
     return {"config": cfg, "lane_waves": waves, "blocks": int(st.size), "redo_blocks": int(redo.sum()),
             "redo_fraction": round(float(redo.mean()) if st.size else 0.0, 5), "reasons": dict(why), "first_reasons": dict(first),

@@ -250,13 +250,13 @@ class DecodeBatch:
 
     def lane_counters(self, ts: int) -> np.ndarray:
         """Diagnostics (a batch made with WVG_LANE_COUNTERS=1): per parser wave of term set
-        `ts`'s last lane decode [cycles, groups, bulk, norun, split, fast, checked, replay]
-        (wvg_batch_lane_counters)."""
-        buf = np.zeros(8 * 4096, dtype=np.uint32)
+        `ts`'s last lane decode [cycles, groups, bulk, norun, split, fast, checked, replay,
+        wait_consumed, wait_loads, 0...] (wvg_batch_lane_counters)."""
+        buf = np.zeros(16 * 4096, dtype=np.uint32)
         k = self._L.wvg_batch_lane_counters(self._b, int(ts), buf.ctypes.data, buf.size)
         if k < 0:
             raise RuntimeError("lane counters unavailable (WVG_LANE_COUNTERS=1 before the batch is made)")
-        return buf[: 8 * k].reshape(k, 8)
+        return buf[: 16 * k].reshape(k, 16)
 
     def file_blocks(self, i: int):
         """(end_frame, status) per block of file i (wvg_batch_file_blocks)."""

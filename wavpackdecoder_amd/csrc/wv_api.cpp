@@ -21,7 +21,7 @@ namespace wvg {
 hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint32_t n_pcm, const uint32_t *dsd_list,
                          uint32_t n_dsd, uint32_t fast_lo, uint32_t n_fast, const uint8_t *blob, const uint8_t *tables,
                          int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s_pcm, hipStream_t s_dsd,
-                         hipStream_t s_fast);
+                         hipStream_t s_fast, int lane_mode, uint32_t high_lo, uint32_t n_high_mono);
 int term_set_of(const BlockDesc &d, int prefer_pipe);
 hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, uint32_t n, const uint8_t *blob,
                         int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s, int lane_mode,
@@ -151,6 +151,7 @@ struct wvg_batch {
     int64_t out_ints = 0;
     std::vector<uint32_t> pcm_list, dsd_list;           // wave-per-block kernels (generic PCM, DSD)
     uint32_t dsd_fast_lo = 0, dsd_fast_n = 0;          // the mode-1 range of dsd_list (sorted by kind)
+    uint32_t dsd_high_lo = 0, dsd_high_mono = 0;       // the mode-3 range [high_lo, end): stereo, then mono blocks
     std::vector<uint32_t> ts_list[kMaxTermSets];        // two-wave kernels per term set
     int64_t gframes[kSide] = {0};                       // frames per launch group (the lane assignment's load)
     uint32_t *d_ts[kMaxTermSets] = {nullptr};      // per term set: the list, then the lane kernels' order of it
@@ -297,7 +298,7 @@ wvg_batch *wvg_batch_new(wvg_ctx *c, int chunk_frames) {
     b->fo.defer_values = !(hm && hm[0] == '1');
     const char *lc = getenv("WVG_LANE_COUNTERS");
     if (lc && lc[0] == '1') {
-        const size_t bytes = sizeof(uint32_t) * 8u * kLaneDbgWaves * kMaxTermSets;
+        const size_t bytes = sizeof(uint32_t) * 16u * kLaneDbgWaves * kMaxTermSets;
         if (hipMalloc(&b->d_lane_dbg, bytes) != hipSuccess || hipMemset(b->d_lane_dbg, 0, bytes) != hipSuccess)
             b->d_lane_dbg = nullptr;
     }
@@ -990,14 +991,26 @@ int wvg_batch_upload(wvg_batch *b) {
     // free: every block writes its own output range; DSD fills follow on the same stream)
     auto by_kind_len = [&](uint32_t x, uint32_t y) {
         const BlockDesc &p = b->fo.descs[x], &q = b->fo.descs[y];
-        return p.kind != q.kind ? p.kind < q.kind : (p.nframes != q.nframes ? p.nframes > q.nframes : x < y);
+        if (p.kind != q.kind) return p.kind < q.kind;
+        if (p.kind == KIND_DSD_HIGH) {  // stereo blocks before mono ones (one lane kernel each)
+            const bool pm = (p.flags & wvf::MONO_DATA) != 0, qm = (q.flags & wvf::MONO_DATA) != 0;
+            if (pm != qm) return qm;
+        }
+        return p.nframes != q.nframes ? p.nframes > q.nframes : x < y;
     };
     std::sort(b->pcm_list.begin(), b->pcm_list.end(), by_kind_len);
     std::sort(b->dsd_list.begin(), b->dsd_list.end(), by_kind_len);
     // the mode-1 blocks are one range of the kind-sorted list (their own kernel)
     b->dsd_fast_lo = b->dsd_fast_n = 0;
+    b->dsd_high_lo = (uint32_t)b->dsd_list.size();
+    b->dsd_high_mono = 0;
     for (size_t k = 0; k < b->dsd_list.size(); k++) {
-        if (b->fo.descs[b->dsd_list[k]].kind != KIND_DSD_FAST) continue;
+        const BlockDesc &d = b->fo.descs[b->dsd_list[k]];
+        if (d.kind == KIND_DSD_HIGH) {
+            if (b->dsd_high_lo == b->dsd_list.size()) b->dsd_high_lo = (uint32_t)k;
+            if (d.flags & wvf::MONO_DATA) b->dsd_high_mono++;
+        }
+        if (d.kind != KIND_DSD_FAST) continue;
         if (!b->dsd_fast_n) b->dsd_fast_lo = (uint32_t)k;
         b->dsd_fast_n++;
     }
@@ -1145,7 +1158,7 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
     };
     HIPCHK(c, launch_decode(b->d_descs, b->d_pcml, (uint32_t)b->pcm_list.size(), b->d_dsd, (uint32_t)b->dsd_list.size(),
                             b->dsd_fast_lo, b->dsd_fast_n, b->d_blob, b->d_tables, b->d_out, b->d_status, b->d_mute,
-                            slot(kPcm), slot(kDsd), slot(kDsd1)));
+                            slot(kPcm), slot(kDsd), slot(kDsd1), b->lane_mode, b->dsd_high_lo, b->dsd_high_mono));
     HIPCHK(c, mark(kDsd));
     HIPCHK(c, mark(kDsd1));
     HIPCHK(c, mark(kPcm));
@@ -1155,7 +1168,7 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
                                    b->d_status, b->d_mute, slot(t), b->lane_mode, b->d_ts[t] + b->ts_list[t].size(),
                                    (uint32_t)b->ts_lane[t].size(),
                                    b->d_lane_dbg && b->ts_lane[t].size() <= 64u * kLaneDbgWaves
-                                       ? b->d_lane_dbg + (size_t)t * kLaneDbgWaves * 8u
+                                       ? b->d_lane_dbg + (size_t)t * kLaneDbgWaves * 16u
                                        : nullptr));
             HIPCHK(c, mark(t));
         }
@@ -1266,9 +1279,9 @@ int wvg_batch_lane_counters(wvg_batch *b, int ts, uint32_t *out, int64_t cap) {
     if (!b || ts < 0 || ts >= kMaxTermSets || !b->d_lane_dbg) return WVG_ERR_ARG;
     const size_t nw = (b->ts_lane[ts].size() + 63) / 64;
     if (nw > kLaneDbgWaves) return WVG_ERR_ARG;
-    if (cap < (int64_t)(8 * nw)) return WVG_ERR_SPACE;
+    if (cap < (int64_t)(16 * nw)) return WVG_ERR_SPACE;
     HIPCHK(b->ctx, hipStreamSynchronize(b->stream));
-    HIPCHK(b->ctx, hipMemcpy(out, b->d_lane_dbg + (size_t)ts * kLaneDbgWaves * 8u, sizeof(uint32_t) * 8 * nw,
+    HIPCHK(b->ctx, hipMemcpy(out, b->d_lane_dbg + (size_t)ts * kLaneDbgWaves * 16u, sizeof(uint32_t) * 16 * nw,
                              hipMemcpyDeviceToHost));
     return (int)nw;
 }

@@ -110,6 +110,19 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_pcm_wave(const BlockD
 // more per 22,050-frame block when each block built its own)
 __device__ int32_t g_dsd_ptables[256 * 256];
 
+// the table rows' device address (a kernel argument of the DSD lane kernel)
+const int32_t *dsd_ptables_device() {
+    static const int32_t *p = nullptr;
+    if (!p) {
+        void *a = nullptr;
+        if (hipGetSymbolAddress(&a, HIP_SYMBOL(g_dsd_ptables)) == hipSuccess) p = (const int32_t *)a;
+    }
+    return p;
+}
+hipError_t launch_dsd3_lane(const BlockDesc *descs, const uint32_t *list, uint32_t n, const uint8_t *blob,
+                            const int32_t *ptables, int32_t *out, uint32_t *status, uint32_t *mute_chunk,
+                            uint32_t n_mono, hipStream_t s);
+
 hipError_t upload_dsd_ptables() {
     std::vector<int32_t> t(256 * 256);
     for (int r = 0; r < 256; r++) dsd_ptable_init(r, t.data() + (size_t)r * 256, 0, 1);
@@ -701,11 +714,16 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_wave(const BlockD
                                                                     int32_t *__restrict__ out,
                                                                     uint32_t *__restrict__ status,
                                                                     uint32_t *__restrict__ mute_chunk,
-                                                                    uint32_t skip_fast) {
+                                                                    uint32_t mode) {
     __shared__ int32_t pt_lds[260];  // mode 3's adaptive ptable, one per block (+ dsd_high_v2's spare slot)
     const uint32_t bi = list[blockIdx.x];
     const BlockDesc &d = descs[bi];
-    if (skip_fast && d.kind == KIND_DSD_FAST) return;  // wv_decode_dsd_fast's
+    // mode bit 0: skip mode-1 blocks (wv_decode_dsd_fast's); bit 1: skip mode-3 blocks
+    // (the lane kernel's, wv_dsd_lane.hip); bit 2: only the blocks the lane kernel
+    // handed back (ST_REDO)
+    if ((mode & 1u) && d.kind == KIND_DSD_FAST) return;
+    if ((mode & 2u) && d.kind == KIND_DSD_HIGH) return;
+    if ((mode & 4u) && !(status[bi] & lane::ST_REDO)) return;
     const bool lead = threadIdx.x == 0;
     DevStoreWave st{out + d.out_off, (uint64_t)d.pre_end * d.out_nch, lead};
     DsdResult r;
@@ -724,7 +742,7 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_wave(const BlockD
     else
         r = decode_dsd_block(d, blob, tables, pt_lds, st, g_dsd_ptables);
     if (lead) {
-        status[bi] = d.fstatus | r.status;
+        status[bi] = d.fstatus | r.status | ((mode & 4u) ? (uint32_t)ST_REDONE : 0u);
         mute_chunk[bi] = r.mute_chunk;
     }
 }
@@ -1150,7 +1168,11 @@ static const int8_t kLaneSets[][17] = {
 };
 constexpr int kNumLaneSets = 2;
 constexpr int kLaneBase = kPipe + 2;
-static_assert(kLaneBase + kNumLaneSets <= 8, "launch groups (wv_api.cpp kMaxTermSets)");
+// hybrid stereo blocks of the default list (HYBRID_BITRATE, no HYBRID_BALANCE, not
+// int32: C4's float hybrid): the hybrid lane kernel when the batch asks for it,
+// else the default list's two-wave kernel
+constexpr int kHyDefault = kLaneBase + kNumLaneSets;
+static_assert(kHyDefault < 8, "launch groups (wv_api.cpp kMaxTermSets)");
 static const bool kLaneSetMono[kNumLaneSets] = {false, true};
 static const bool kLaneSetNeg12[kNumLaneSets] = {true, false};
 
@@ -1181,7 +1203,11 @@ int term_set_of(const BlockDesc &d, int prefer_pipe) {
             if (t != d.term[i]) ok = false;
             if (mono && t < 0) ok = false;
         }
-        if (ok) return s;
+        if (ok) {
+            const uint32_t hy = d.flags & (HYBRID_FLAG | HYBRID_BITRATE | HYBRID_BALANCE | INT32_DATA);
+            if (s == 1 && !mono && hy == (HYBRID_FLAG | HYBRID_BITRATE)) return kHyDefault;
+            return s;
+        }
     }
     {
         for (int s = 0; s < kNumLaneSets; s++) {
@@ -1211,6 +1237,16 @@ hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, ui
         if (lane_mode != 2) {
             if (neg12) hipLaunchKernelGGL((wv_pcm_pipe_redo<true>), g, b, 0, s, descs, list, blob, out, status, aux);
             else hipLaunchKernelGGL((wv_pcm_pipe_redo<false>), g, b, 0, s, descs, list, blob, out, status, aux);
+        }
+        return hipGetLastError();
+    }
+    if (ts == kHyDefault) {
+        if (lane_mode) {
+            dim3 gl((lane_n + 64 * lane::LPAIRS - 1) / (64 * lane::LPAIRS)), bl(64 * lane::LPAIRS * 2);
+            if (hipError_t e = launch_lane(LANE_HY_DEFAULT, gl, bl, s, descs, lane_list, lane_n, blob, out, status, lane_dbg); e != hipSuccess) return e;
+            if (lane_mode != 2) hipLaunchKernelGGL((wv_pcm_2wave_redo<WVG_TS_DEFAULT>), g, b, 0, s, descs, list, blob, out, status, aux);
+        } else {
+            hipLaunchKernelGGL((wv_pcm_2wave<WVG_TS_DEFAULT>), g, b, 0, s, descs, list, blob, out, status, aux);
         }
         return hipGetLastError();
     }
@@ -1258,15 +1294,28 @@ namespace wvg {
 // DSD blocks: the mode-1 range [fast_lo, fast_lo + n_fast) of the kind-sorted
 // list by wv_decode_dsd_fast on s_fast, every other DSD block by one
 // wv_decode_dsd_wave launch on s_dsd (mute fills: launch_dsd_fill, after the join)
+// With lane_mode, the mode-3 range [high_lo, n_dsd) (stereo first, then n_high_mono
+// mono blocks) goes to the lane-per-block kernel (wv_dsd_lane.hip) after the wave
+// kernel's other blocks, and the wave kernel then decodes what it handed back.
 hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint32_t n_pcm, const uint32_t *dsd_list,
                          uint32_t n_dsd, uint32_t fast_lo, uint32_t n_fast, const uint8_t *blob, const uint8_t *tables,
                          int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s_pcm, hipStream_t s_dsd,
-                         hipStream_t s_fast) {
+                         hipStream_t s_fast, int lane_mode, uint32_t high_lo, uint32_t n_high_mono) {
     // the DSD kernels first: their blocks are the batch's longest serial chains
     const uint32_t skip = n_fast ? 1u : 0u;
-    if (n_dsd > n_fast) {
-        hipLaunchKernelGGL(wv_decode_dsd_wave, dim3(n_dsd), dim3(64), 0, s_dsd, descs, dsd_list, blob, tables, out,
-                           status, aux, skip);
+    const uint32_t n_high = lane_mode ? n_dsd - high_lo : 0u;
+    if (n_dsd > n_fast + n_high) {
+        hipLaunchKernelGGL(wv_decode_dsd_wave, dim3(n_dsd - n_high), dim3(64), 0, s_dsd, descs, dsd_list, blob, tables,
+                           out, status, aux, skip | (n_high ? 2u : 0u));
+    }
+    if (n_high) {
+        if (hipError_t e = launch_dsd3_lane(descs, dsd_list + high_lo, n_high, blob, dsd_ptables_device(), out, status,
+                                            aux, n_high_mono, s_dsd);
+            e != hipSuccess)
+            return e;
+        if (lane_mode != 2)  // 2: the lane kernel alone (diagnostics: ST_REDO stays in the status)
+            hipLaunchKernelGGL(wv_decode_dsd_wave, dim3(n_high), dim3(64), 0, s_dsd, descs, dsd_list + high_lo, blob,
+                               tables, out, status, aux, 4u);
     }
     if (n_fast) {
         const uint32_t *fl = dsd_list + fast_lo;

@@ -1,0 +1,270 @@
+// wv_dsd_lane.hip -- DSD mode 3 (DsdUtils.init_dsd_block_high + decode_high,
+// DsdUtils.cs:321-493) with one lane per block: the throughput kernel for
+// batches with many mode-3 blocks (wvg_batch_set_kernel(WVG_KERNEL_LANE)).
+//
+// A mode-3 block is one serial range-coder chain (8 binary decisions per
+// channel byte, each reading and updating an adaptive 256-entry probability
+// table), so the wave-per-block kernel (wv_decode.hip, dsd_high_v2) spends a
+// whole wave on one chain.  Here each lane of a wave owns one block: its range
+// coder (low, high, value), both channels' filter states and its probability
+// table, which sits in LDS interleaved by lane (entry e of lane l at
+// (e * 64 + l) * 4: every lane's read hits bank l, and the address of the entry a
+// filter value selects is one v_and_or).  One VALU instruction moves 64 chains.
+//
+// Payload bytes come from a per-lane 64-bit big-endian window refilled a dword at
+// a time from a dword loaded one refill ahead (global loads, one per 4 bytes),
+// twice per frame: a half frame (8 decisions) can then take up to 5 bytes -- 40
+// bits of information in 8 binary decisions, which no real stream approaches.  A
+// lane whose window runs dry, or a block outside the kernel's scope (a seek's
+// discard calls, state from an earlier block, a framing verdict), is marked
+// ST_REDO and decoded again right after by the wave-per-block kernel, so results
+// are exactly the wave kernel's, which the GPU tests hold against the oracle.
+#include <hip/hip_runtime.h>
+
+#include "wv_desc.h"
+#include "wv_format.h"
+
+namespace wvg {
+namespace dlane {
+
+constexpr uint32_t ST_REDO = 1u << 15;  // as wv_lane.h: decode this block again (wave kernel)
+constexpr int32_t kUp = 0x010000FE, kDown = 0x00010000;  // DsdUtils.cs UP / DOWN
+
+__device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
+
+// per-lane payload window: byte bp of the payload in bits 63..56 of win, `avail`
+// bytes valid, nxt = the dword after them (loaded one refill ahead)
+struct Win {
+    const uint32_t *w;
+    uint64_t win;
+    int32_t avail;
+    uint32_t ni, nxt;
+    __device__ __forceinline__ void init(const uint8_t *p) {
+        const uint32_t sh = (uint32_t)((uintptr_t)p & 3u);
+        w = (const uint32_t *)(p - sh);
+        win = (uint64_t)bswap(w[0]) << (32u + 8u * sh);
+        avail = 4 - (int32_t)sh;
+        nxt = w[1];
+        ni = 2;
+        refill();
+    }
+    // avail <= 4: four more bytes below the valid ones (branch-free: a lane with
+    // more keeps its window and its read-ahead dword)
+    __device__ __forceinline__ void refill() {
+        const bool m = avail <= 4;
+        const uint32_t sh = (uint32_t)(32 - 8 * (m ? avail : 0)) & 63u;
+        win |= m ? (uint64_t)bswap(nxt) << sh : 0ull;
+        avail += m ? 4 : 0;
+        const uint32_t nn = w[ni];  // (read every time: the address is always inside the blob's tail)
+        nxt = m ? nn : nxt;
+        ni += m ? 1u : 0u;
+    }
+};
+
+// one range-coder decision of decode_high (DsdUtils.cs:409-429) and the
+// renormalisation after it (the byte loop as one shift of n = leading zero bytes of
+// high ^ low, capped by the bytes left): returns filter0 (-1 when value <= split)
+__device__ __forceinline__ int32_t decide(uint32_t &low, uint32_t &high, uint32_t &value, uint32_t pv, Win &src,
+                                          uint32_t &left) {
+    const uint32_t split = low + __umul24((high - low) >> 8, pv >> 16);  // (24-bit by 9-bit: exact)
+    const bool zero = value <= split;
+    high = zero ? split : high;
+    low = zero ? low : split + 1u;
+    uint32_t n = (uint32_t)__builtin_clz((high ^ low) | 1u) >> 3;  // 0..3, 4 below: a zero xor
+    n = ((high ^ low) == 0u) ? 4u : n;
+    n = min(n, left);
+    const uint32_t s = n << 3;  // 0..32
+    value = (uint32_t)(((((uint64_t)value << 32) | (src.win >> 32)) << s) >> 32);
+    high = (uint32_t)(((((uint64_t)high << 32) | 0xFFFFFFFFull) << s) >> 32);
+    low = (uint32_t)(((uint64_t)low << s) & 0xFFFFFFFFull);
+    src.win <<= s;
+    src.avail -= (int32_t)n;
+    left -= n;
+    return zero ? -1 : 0;
+}
+
+// a channel's filter state (DSDfilters: value q0, filter1..6 q2..q7, factor q8)
+struct Filt {
+    int32_t q0, q2, q3, q4, q5, q6, q7, q8, byte;
+};
+__device__ __forceinline__ int32_t fval(const Filt &f) {  // filter1 - filter5 + (filter6 * factor >> 2)
+    return (f.q2 - f.q6) + (__mul24(f.q7, f.q8) >> 2);
+}
+// the filter update after a decision (DsdUtils.cs:430-441); filter6 and factor stay
+// far inside 24 bits for any stream (convex updates of 0 / 2^20; the factor decays
+// 1/1024 per byte), so the products are 24-bit multiplies with C#'s low 32 bits
+__device__ __forceinline__ void fupd(Filt &f, int32_t f0) {
+    const int32_t v = f.q0 + (f.q7 << 3);
+    const int32_t t = f.q0 - (f.q7 << 3);          // value - filter6 * 16, after the += filter6 * 8
+    f.byte = (f.byte << 1) | (f0 & 1);
+    f.q8 += (((v ^ f0) >> 31) | 1) & ((v ^ t) >> 31);
+    const int32_t x = f0 & (1 << 20);
+    f.q2 += (x - f.q2) >> 6;
+    f.q3 += (x - f.q3) >> 4;
+    f.q4 += (f.q3 - f.q4) >> 4;
+    f.q5 += (f.q4 - f.q5) >> 4;
+    const int32_t dd = (f.q5 - f.q6) >> 4;
+    f.q6 += dd;
+    f.q7 += (dd - f.q7) >> 3;
+    f.q0 = fval(f);
+}
+
+// can this lane decode block d exactly (else ST_REDO)?  CH: channels decoded
+template <int CH>
+__device__ __forceinline__ bool dsd3_ok(const BlockDesc &d) {
+    using namespace wvf;
+    if (d.kind != KIND_DSD_HIGH) return false;
+    if (((d.flags & MONO_DATA) ? 1 : 2) != CH) return false;
+    if (CH == 2 && (d.flags & FALSE_STEREO)) return false;
+    if (d.inherit || d.chain_len >= 2 || d.pre_end || d.fstatus) return false;
+    if (d.dsd_data_len < 4u) return false;
+    const bool two = CH == 2 || (d.flags & FALSE_STEREO);
+    if (two && (d.out_off & 1u)) return false;  // 8-B stores
+    return true;
+}
+
+// One workgroup = one wave = 64 blocks; the probability tables take 64 KiB of
+// LDS, so two waves share a CU (on two of its SIMDs).
+template <int CH>
+__device__ __forceinline__ void dsd3_lanes(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
+                                           uint32_t n, const uint8_t *__restrict__ blob,
+                                           const int32_t *__restrict__ ptables, int32_t *__restrict__ out,
+                                           uint32_t *__restrict__ status, uint32_t *__restrict__ mute_chunk) {
+    using namespace wvf;
+    __shared__ int32_t pt[256 * 64];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t li = blockIdx.x * 64u + lane;
+    const bool inl = li < n;
+    const uint32_t bi = inl ? list[li] : 0u;
+    const BlockDesc &d = descs[bi];
+    const bool ok = inl && dsd3_ok<CH>(d);
+    if (inl && !ok) status[bi] = ST_REDO | (1u << 16);
+    const uint32_t nfr = ok ? d.nframes : 0u;
+    // the wave runs to its longest block (uniform loop; finished lanes idle along)
+    uint32_t nmax = nfr;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) nmax = max(nmax, (uint32_t)__shfl_xor((int)nmax, off));
+    nmax = __builtin_amdgcn_readfirstlane(nmax);
+    if (nmax == 0u) return;
+    // this lane's probability table: the block's starting row (init_ptable for its rate_i)
+    uint8_t *ptb = (uint8_t *)pt;
+    const uint32_t col = lane * 4u;
+    {
+        const int32_t *row = ptables + (uint32_t)(ok ? (d.dsd_rate_i & 255) : 0) * 256u;
+        for (uint32_t e = 0; e < 256u; e++) *(int32_t *)(ptb + (e << 8) + col) = row[e];
+    }
+    Win src;
+    src.init(blob + (ok ? d.bits_off : 0));
+    uint32_t left = ok ? d.dsd_data_len : 4u;
+    uint32_t low = 0u, high = 0xFFFFFFFFu, value = 0u;
+    value = (uint32_t)(src.win >> 32);  // init_dsd_block_high's 4 value bytes
+    src.win <<= 32;
+    src.avail -= 4;
+    left -= 4u;
+    src.refill();
+    Filt f[CH];
+#pragma unroll
+    for (int c = 0; c < CH; c++) {
+        f[c].q2 = d.dsd_filters[c][0];
+        f[c].q3 = d.dsd_filters[c][1];
+        f[c].q4 = d.dsd_filters[c][2];
+        f[c].q5 = d.dsd_filters[c][3];
+        f[c].q6 = d.dsd_filters[c][4];
+        f[c].q7 = 0;
+        f[c].q8 = d.dsd_filters[c][5];
+        f[c].q0 = fval(f[c]);
+        f[c].byte = 0;
+    }
+    const bool fst = (d.flags & FALSE_STEREO) != 0;
+    const uint32_t och = (CH == 2 || fst) ? 2u : 1u;
+    int32_t *o = out + d.out_off;
+    int32_t crc = -1;
+    int32_t dry = 0;  // least window bytes seen (< 0: the window ran dry, ST_REDO)
+    __syncthreads();
+    for (uint32_t t = 0; t < nmax; t++) {
+#pragma unroll
+        for (int bit = 0; bit < 8; bit++) {
+            if (bit == 4) src.refill();
+            // both channels' entries first (each depends on its own filter only)
+            uint32_t a[CH];
+            int32_t pv[CH];
+#pragma unroll
+            for (int c = 0; c < CH; c++) {
+                a[c] = ((uint32_t)f[c].q0 & 0xFF00u) | col;
+                pv[c] = *(const int32_t *)(ptb + a[c]);
+            }
+            int32_t f0[CH], nv[CH];
+#pragma unroll
+            for (int c = 0; c < CH; c++) {
+                // channel 1 takes the entry channel 0 just updated when both chose it
+                // (forwarded; its store then lands after channel 0's)
+                if (CH == 2 && c == 1) pv[CH - 1] = a[CH - 1] == a[0] ? nv[0] : pv[CH - 1];
+                f0[c] = decide(low, high, value, (uint32_t)pv[c], src, left);
+                nv[c] = pv[c] + (((f0[c] ? kUp : kDown) - pv[c]) >> 8);
+                *(int32_t *)(ptb + a[c]) = nv[c];
+            }
+#pragma unroll
+            for (int c = 0; c < CH; c++) fupd(f[c], f0[c]);
+        }
+        dry = min(dry, src.avail);
+        src.refill();
+        // the frame's bytes, CRC (crc += 2 crc + v per value), factor decay (:484-492)
+        int32_t v[CH];
+#pragma unroll
+        for (int c = 0; c < CH; c++) {
+            v[c] = f[c].byte & 0xFF;
+            crc = crc * 3 + v[c];
+            f[c].q8 -= (f[c].q8 + 512) >> 10;
+            f[c].q0 = fval(f[c]);  // (the next frame's value, :395-396, with the decayed factor)
+        }
+        if (t < nfr) {
+            if (och == 2u) *(int2 *)(o + 2u * t) = make_int2(v[0], v[CH - 1]);
+            else o[t] = v[0];
+        }
+    }
+    if (!ok) return;
+    uint32_t st = 0;
+    if (dry < 0) {
+        status[bi] = ST_REDO | (64u << 16);
+        return;
+    }
+    if (d.nframes == d.block_samples) {
+        st |= ST_CRC_CHECKED;
+        if (crc != d.crc) {
+            // DsdUtils.cs:99-101: the final call mutes (its values become 0x55: wv_dsd_fill)
+            st |= ST_CRC_ERROR | ST_DSD_MUTE;
+            const uint32_t fc = d.first_chunk, ck = d.chunk ? d.chunk : 1u;
+            mute_chunk[bi] = d.nframes <= fc ? 0u : 1u + (d.nframes - fc - 1u) / ck;
+        }
+    }
+    status[bi] = st;
+}
+
+}  // namespace dlane
+
+template <int CH>
+__global__ void __launch_bounds__(64) wv_dsd3_lane(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
+                                                   uint32_t n, const uint8_t *__restrict__ blob,
+                                                   const int32_t *__restrict__ ptables, int32_t *__restrict__ out,
+                                                   uint32_t *__restrict__ status, uint32_t *__restrict__ mute_chunk) {
+    dlane::dsd3_lanes<CH>(descs, list, n, blob, ptables, out, status, mute_chunk);
+}
+
+// mode-3 blocks [0, n) of list (mono and stereo alike: one launch per channel
+// count, each lane taking only its own kind; the others are handed back)
+hipError_t launch_dsd3_lane(const BlockDesc *descs, const uint32_t *list, uint32_t n, const uint8_t *blob,
+                            const int32_t *ptables, int32_t *out, uint32_t *status, uint32_t *mute_chunk,
+                            uint32_t n_mono, hipStream_t s) {
+    if (!n) return hipSuccess;
+    // list order: the stereo blocks first, then n_mono mono blocks (the host sorts them)
+    const uint32_t ns = n - n_mono;
+    if (ns)
+        hipLaunchKernelGGL((wv_dsd3_lane<2>), dim3((ns + 63) / 64), dim3(64), 0, s, descs, list, ns, blob, ptables, out,
+                           status, mute_chunk);
+    if (n_mono)
+        hipLaunchKernelGGL((wv_dsd3_lane<1>), dim3((n_mono + 63) / 64), dim3(64), 0, s, descs, list + ns, n_mono, blob,
+                           ptables, out, status, mute_chunk);
+    return hipGetLastError();
+}
+
+}  // namespace wvg

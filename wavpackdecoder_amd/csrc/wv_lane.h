@@ -39,6 +39,7 @@ constexpr uint32_t ST_REDO = 1u << 15;  // internal: decode this block again on 
 constexpr int RU = 32;                  // ring units (16 B) per lane: 33 KiB of LDS per 64 blocks (lane_blocks: why)
 constexpr int GF = 8;                   // frames per group (refill / bound-check cadence)
 constexpr int NLD = 4;                  // units a lane loads per group, at most (32 bits per word sustained)
+constexpr int LPAIRS = 2;               // (parser, reconstruction) wave pairs per workgroup (lane_blocks)
 
 __device__ __forceinline__ int32_t aw(int32_t w, int32_t s) {  // apply_weight (UnpackUtils.cs:703)
     return (int32_t)(((int64_t)w * (int64_t)s + 512) >> 10);
@@ -216,6 +217,10 @@ struct LState {
     int32_t slack;   // least window bits left after a word (< 0: a word past the window)
     uint32_t bad;
     uint32_t bad0;   // (diagnostics) the reasons of the first group that set any: status bits 24-31
+    // hybrid words (HYBRID_FLAG | HYBRID_BITRATE): slow_level, bitrate_acc/delta, error limit per channel
+    int32_t slow[2];
+    int64_t acc[2], dlt[2];
+    int32_t el[2];
 };
 
 // Selects on lane masks (uint64_t in SGPRs, from ballots).  WV_LANE_ASM=1 forces
@@ -296,6 +301,77 @@ __device__ __forceinline__ uint32_t lgamma(LState &s, const uint8_t *ring, uint3
     return v;
 }
 
+// ---- hybrid words (HYBRID_FLAG with HYBRID_BITRATE, stereo) ----
+// The exp2 / log2 byte tables (WordsUtils.cs) in LDS after the payload rings.
+constexpr uint32_t TAB_EXP2 = LPAIRS * RING_BYTES, TAB_LOG2 = TAB_EXP2 + 256u;
+// exp2s(L) for L > 0 (WordsUtils.cs:633-646): value (9 bits) scaled by 2^(e - 9) as
+// one shift pair, exact for e <= 22 (else the lane hands its block back); 0 for L <= 0
+__device__ __forceinline__ int32_t lexp2s_pos(int32_t L, const uint8_t *ring, uint32_t &bad) {
+    const uint32_t e = (uint32_t)L >> 8;
+    const uint32_t v = (uint32_t)ring[TAB_EXP2 + ((uint32_t)L & 0xFFu)] | 0x100u;
+    bad |= (L > 0 && e > 22u) ? 2u : 0u;
+    return L > 0 ? (int32_t)((v << (e & 31u)) >> 9) : 0;
+}
+// update_error_limit (WordsUtils.cs:195-261; stereo, HYBRID_BITRATE, no HYBRID_BALANCE):
+// before the first word of a frame, in lanes where that word is not a zero-run zero
+__device__ __forceinline__ void lhy_errlim(LState &s, const uint8_t *ring, bool apply) {
+    using namespace wvf;
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+        const int64_t acc = s.acc[c] + s.dlt[c];
+        const int32_t br = (int32_t)(acc >> 16);
+        const int32_t sl = add32(s.slow[c], SLO) >> SLS;
+        const int32_t el = lexp2s_pos(add32(sub32(sl, br), 0x100), ring, s.bad);
+        s.acc[c] = apply ? acc : s.acc[c];
+        s.el[c] = apply ? el : s.el[c];
+    }
+}
+// a hybrid word's magnitude from the 32 bits x after its unary part: read_code(high -
+// low) + low when the error limit is 0, else the bisection (:486-492) -- one bit per
+// step while high - low > error_limit, as a uniform loop over the lanes still in it
+// (the reference's 64-bit bounds: the lane hands back a word whose high passes
+// 2^30, and a bisection longer than the 31 bits of x)
+__device__ __forceinline__ void lhy_code(uint32_t x, uint32_t low, uint32_t mc, int32_t el, uint32_t &mid,
+                                         uint32_t &used, uint32_t &bad) {
+    const uint32_t z = (uint32_t)__builtin_clz(mc | 1u);
+    const uint32_t ex = (0xFFFFFFFFu >> z) - mc;
+    const uint32_t nbt = z ^ 31u;
+    const uint32_t v = __builtin_amdgcn_ubfe(x, 0, nbt);
+    const bool big = v >= ex;
+    const uint32_t t = v + __builtin_amdgcn_ubfe(x, nbt, 1) - ex;
+    const uint32_t mid_rc = add3(low, v, big ? t : 0u);
+    const uint32_t used_rc = nbt + (big ? 1u : 0u);
+    uint32_t lo = low, hi = low + mc, md = (lo + hi + 1u) >> 1, ub = 0u;
+    uint32_t am = (el != 0 && (int32_t)mc > el) ? ~0u : 0u;
+    while (lmask(am != 0u) != 0ull) {
+        const uint32_t bm = (uint32_t)__builtin_amdgcn_sbfe((int32_t)x, ub, 1);
+        const uint32_t slo = am & bm, shi = am & ~bm;
+        lo = (md & slo) | (lo & ~slo);
+        hi = ((md - 1u) & shi) | (hi & ~shi);
+        ub -= am;
+        md = (hi + lo + 1u) >> 1;
+        am &= (uint32_t)((int32_t)((uint32_t)el + lo - hi) >> 31) & (ub < 31u ? ~0u : 0u);
+    }
+    const bool cut = ub >= 31u && (int32_t)((uint32_t)el + lo - hi) < 0;
+    bad |= ((low | (low + mc)) >= (1u << 30) || cut) ? 2u : 0u;
+    mid = el == 0 ? mid_rc : md;
+    used = el == 0 ? used_rc : ub;
+}
+// slow_level after a word (HYBRID_BITRATE, :501-502): slow - (slow + SLO) >> SLS + mylog2(mid)
+// (mylog2, WordsUtils.cs:588-608: the 8 bits below the leading one index the table)
+__device__ __forceinline__ int32_t lhy_slow(int32_t slow, uint32_t mid, const uint8_t *ring) {
+    using namespace wvf;
+    const uint32_t a = mid + (mid >> 9);
+    const uint32_t cz = (uint32_t)__clz((int32_t)a);  // 32 for 0
+    const uint32_t idx = ((a << (cz & 31u)) >> 23) & 0xFFu;
+    const int32_t lg = (int32_t)(((32u - cz) << 8) + (uint32_t)ring[TAB_LOG2 + idx]);
+    return add32(sub32(slow, add32(slow, SLO) >> SLS), lg);
+}
+__device__ __forceinline__ int32_t lhy_decay(int32_t slow) {  // a zero-run zero's slow_level (:316-317)
+    using namespace wvf;
+    return sub32(slow, add32(slow, SLO) >> SLS);
+}
+
 // get_words for one residual of channel C (WordsUtils.cs:290-503, lossless:
 // error_limit 0): the word as branch-free selects on lane masks.  Two rare
 // parts branch, taken when some lane needs them: the zero-run mode's entry (a
@@ -306,7 +382,7 @@ __device__ __forceinline__ uint32_t lgamma(LState &s, const uint8_t *ring, uint3
 // run (zskip) runs the word as a held zero over all-zero medians that consumes
 // nothing, which leaves its state as it was -- and the checks it feeds are those
 // of the word that ends the run, which reads the same window with the same state.
-template <int C>
+template <int C, bool HY = false>
 __device__ __forceinline__ int32_t lword(LState &s, const uint8_t *ring, uint32_t rbase) {
     using namespace wvf;
     // zero-run mode (:304-352): both channels' median[0] < 2, nothing held
@@ -330,6 +406,10 @@ __device__ __forceinline__ int32_t lword(LState &s, const uint8_t *ring, uint32_
     }
     const uint64_t zm = lmask(zskip);
     const uint64_t hzm = h0m0 | zm;
+    if constexpr (HY) {
+        s.slow[C] = zskip ? lhy_decay(s.slow[C]) : s.slow[C];
+        if constexpr (C == 0) lhy_errlim(s, ring, !zskip);
+    }
     // unary count (:354-428): raw ones (capped at 16) and the bits they take
     const uint32_t lo = (uint32_t)s.win;
     uint32_t raw = (uint32_t)__builtin_ctz(~lo | 0x10000u);
@@ -371,18 +451,25 @@ __device__ __forceinline__ int32_t lword(LState &s, const uint8_t *ring, uint32_
                                 vselmi(ob, 0, csel<-2, 5>(o2))));
     // read_code(high - low = mc) (WordsUtils.cs:546-570), then the sign bit
     const uint32_t x = (uint32_t)s.win;
-    const uint32_t z = (uint32_t)__builtin_clz(mc | 1u);
-    const uint32_t ones_z = 0xFFFFFFFFu >> z;
-    const uint32_t ex = ones_z - mc;
-    const uint32_t nbt = z ^ 31u;
-    const uint32_t v = x & (ones_z >> 1);
-    const uint64_t bigm = lmask(v >= ex);
-    const uint32_t code = vselm(bigm, 2u * v + __builtin_amdgcn_ubfe(x, nbt, 1) - ex, v);
-    const uint32_t used = addc(nbt, bigm);
-    const uint32_t mid = low + code;
+    uint32_t mid, used;
+    if constexpr (HY) {
+        lhy_code(x, low, mc, s.el[C], mid, used, s.bad);
+        s.slack = min(s.slack, 31 - (int32_t)used);  // (the sign must lie in x)
+    } else {
+        const uint32_t z = (uint32_t)__builtin_clz(mc | 1u);
+        const uint32_t ones_z = 0xFFFFFFFFu >> z;
+        const uint32_t ex = ones_z - mc;
+        const uint32_t nbt = z ^ 31u;
+        const uint32_t v = x & (ones_z >> 1);
+        const uint64_t bigm = lmask(v >= ex);
+        const uint32_t code = vselm(bigm, 2u * v + __builtin_amdgcn_ubfe(x, nbt, 1) - ex, v);
+        used = addc(nbt, bigm);
+        mid = low + code;
+    }
     const int32_t sg = __builtin_amdgcn_sbfe((int32_t)x, used, 1);  // 0 or -1
     lskip(s, vselm(zm, 0u, used + 1u));
     const int32_t out = (int32_t)vselm(zm, 0u, mid ^ (uint32_t)sg);
+    if constexpr (HY) s.slow[C] = zskip ? s.slow[C] : lhy_slow(s.slow[C], mid, ring);
     lrefill(s, ring, rbase);
     return out;
 }
@@ -469,8 +556,9 @@ __device__ __forceinline__ void lmerge(LState &s, const uint8_t *ring) {
 // SPLIT: the window is refilled between the unary part and the code as well, for
 // groups whose medians allow codes longer than the 33 bits a word may count on
 // otherwise (pgroup_try)
-template <int C, bool SPLIT>
+template <int C, bool SPLIT, bool HY = false>
 __device__ __forceinline__ int32_t lword_nz(LState &s, const uint8_t *ring, uint32_t rbase) {
+    static_assert(!HY || SPLIT, "a hybrid word's bisection bits follow a refill");
     using namespace wvf;
     const uint32_t lo = (uint32_t)s.win, hi = (uint32_t)(s.win >> 32);
     const uint32_t raw0 = (uint32_t)__builtin_ctz(~lo | 0x10000u);  // unary ones, capped at 16
@@ -480,6 +568,7 @@ __device__ __forceinline__ int32_t lword_nz(LState &s, const uint8_t *ring, uint
     const uint32_t q = raw - s.keep;             // unary bits taken: raw + 1, or 0 for a held zero
     s.h1 = raw & 1u;
     s.keep = (uint32_t)__builtin_amdgcn_sbfe((int32_t)(raw | ~s.keep), 0, 1);  // an even count holds a zero
+    if constexpr (HY && C == 0) lhy_errlim(s, ring, true);
     const int32_t m0 = s.m[C][0], m1 = s.m[C][1], m2 = s.m[C][2];
     const uint32_t a0 = (uint32_t)(m0 >> 4), a1 = (uint32_t)(m1 >> 4), a2 = (uint32_t)(m2 >> 4);
     const bool o0 = ones == 0u, o1 = ones == 1u;
@@ -509,14 +598,20 @@ __device__ __forceinline__ int32_t lword_nz(LState &s, const uint8_t *ring, uint
     } else {
         x = __builtin_amdgcn_alignbit(hi, lo, q);
     }
-    const uint32_t z = (uint32_t)__builtin_clz(mc | 1u);
-    const uint32_t ex = (0xFFFFFFFFu >> z) - mc;
-    const uint32_t nbt = z ^ 31u;
-    const uint32_t v = __builtin_amdgcn_ubfe(x, 0, nbt);
-    const bool big = v >= ex;
-    const uint32_t t = v + __builtin_amdgcn_ubfe(x, nbt, 1) - ex;  // code = v + t when big
-    const uint32_t mid = add3(low, v, big ? t : 0u);
-    const uint32_t used = nbt + (big ? 1u : 0u);
+    uint32_t mid, used;
+    if constexpr (HY) {
+        lhy_code(x, low, mc, s.el[C], mid, used, s.bad);
+        s.slack = min(s.slack, 31 - (int32_t)used);  // (the sign must lie in x)
+    } else {
+        const uint32_t z = (uint32_t)__builtin_clz(mc | 1u);
+        const uint32_t ex = (0xFFFFFFFFu >> z) - mc;
+        const uint32_t nbt = z ^ 31u;
+        const uint32_t v = __builtin_amdgcn_ubfe(x, 0, nbt);
+        const bool big = v >= ex;
+        const uint32_t t = v + __builtin_amdgcn_ubfe(x, nbt, 1) - ex;  // code = v + t when big
+        mid = add3(low, v, big ? t : 0u);
+        used = nbt + (big ? 1u : 0u);
+    }
     const int32_t sg = __builtin_amdgcn_sbfe((int32_t)x, used, 1);  // 0 or -1
     const uint32_t tot = SPLIT ? used + 1u : add3(q, used, 1u);
     __builtin_assume(tot < 64u);
@@ -524,6 +619,7 @@ __device__ __forceinline__ int32_t lword_nz(LState &s, const uint8_t *ring, uint
     s.nb -= (int32_t)tot;
     s.slack = min(s.slack, s.nb);
     lmerge(s, ring);
+    if constexpr (HY) s.slow[C] = lhy_slow(s.slow[C], mid, ring);
     return (int32_t)(mid ^ (uint32_t)sg);
 }
 
@@ -557,35 +653,35 @@ __device__ __forceinline__ uint32_t pverdict(const LState &s, uint32_t u0) {
 
 // word kinds: WK_CHECKED lword, WK_FAST lword_fast, WK_NORUN / WK_NORUN_SPLIT lword_nz
 enum { WK_CHECKED = 0, WK_FAST = 1, WK_NORUN = 2, WK_NORUN_SPLIT = 3 };
-template <int K, int C>
+template <int K, int C, bool HY>
 __device__ __forceinline__ int32_t lword_k(LState &s, const uint8_t *ring, uint32_t rb) {
-    if constexpr (K == WK_NORUN) return lword_nz<C, false>(s, ring, rb);
-    else if constexpr (K == WK_NORUN_SPLIT) return lword_nz<C, true>(s, ring, rb);
+    if constexpr (K == WK_NORUN) return lword_nz<C, HY, HY>(s, ring, rb);
+    else if constexpr (K == WK_NORUN_SPLIT) return lword_nz<C, true, HY>(s, ring, rb);
     else if constexpr (K == WK_FAST) return lword_fast<C>(s, ring, rb);
-    else return lword<C>(s, ring, rb);
+    else return lword<C, HY>(s, ring, rb);
 }
-template <int U, bool FULL, int FAST, bool MONO>
+template <int U, bool FULL, int FAST, bool MONO, bool HY>
 __device__ __forceinline__ void pframe(LState &s, const uint8_t *ring, uint32_t rb, int2 *res, uint32_t lane,
                                        uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin) {
     const uint32_t t = g0 + U;
     int2 r;
-    r.x = lword_k<FAST, 0>(s, ring, rb);
+    r.x = lword_k<FAST, 0, HY>(s, ring, rb);
     if constexpr (MONO) r.y = 0;
-    else r.y = lword_k<FAST, 1>(s, ring, rb);
+    else r.y = lword_k<FAST, 1, HY>(s, ring, rb);
     res[((t & (RF - 1)) << 6) + lane] = r;
     if (!FULL && t + 1u == nfr) pfin = pverdict(s, u0);
 }
-template <bool FULL, int FAST, bool MONO>
+template <bool FULL, int FAST, bool MONO, bool HY>
 __device__ __forceinline__ void pgroup(LState &s, const uint8_t *ring, uint32_t rb, int2 *res, uint32_t lane,
                                        uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin) {
-    pframe<0, FULL, FAST, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
-    pframe<1, FULL, FAST, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
-    pframe<2, FULL, FAST, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
-    pframe<3, FULL, FAST, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
-    pframe<4, FULL, FAST, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
-    pframe<5, FULL, FAST, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
-    pframe<6, FULL, FAST, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
-    pframe<7, FULL, FAST, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    pframe<0, FULL, FAST, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    pframe<1, FULL, FAST, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    pframe<2, FULL, FAST, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    pframe<3, FULL, FAST, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    pframe<4, FULL, FAST, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    pframe<5, FULL, FAST, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    pframe<6, FULL, FAST, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    pframe<7, FULL, FAST, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
 }
 // a group: the fast words first -- the no-run words when no live lane can meet a
 // zero run in it (lword_nz), else lword_fast; if a live lane met a rare word, the
@@ -600,8 +696,9 @@ __device__ __forceinline__ void pgroup(LState &s, const uint8_t *ring, uint32_t 
 // (diagnostics) groups per path of one parser wave: wvg_batch_lane_counters
 struct LCount {
     uint32_t groups, bulk, norun, split, fast, checked, replay;
+    uint64_t wait_consumed, wait_loads;  // cycles in the group-start wait and the group-end load wait
 };
-template <bool FULL, bool MONO>
+template <bool FULL, bool MONO, bool HY>
 __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint32_t rb, int2 *res, uint32_t lane,
                                            uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin, int32_t mm,
                                            LCount &cnt) {
@@ -615,14 +712,20 @@ __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint3
     const bool zrun = ((((uint32_t)(s.m[0][0] | s.m[1][0])) & ~1u) | ~s.keep | s.h1) == 0u && s.zacc > WPG;
     if (lmask(live && !zrun) == 0ull) {
 #pragma unroll
-        for (int u = 0; u < GF; u++) res[(((g0 + u) & (RF - 1)) << 6) + lane] = make_int2(0, 0);
+        for (int u = 0; u < GF; u++) {
+            res[(((g0 + u) & (RF - 1)) << 6) + lane] = make_int2(0, 0);
+            if constexpr (HY) {  // every zero of a run decays its channel's slow_level
+                s.slow[0] = lhy_decay(s.slow[0]);
+                if constexpr (!MONO) s.slow[1] = lhy_decay(s.slow[1]);
+            }
+        }
         s.zacc -= WPG;
         if (!FULL && live && nfr <= g0 + GF) pfin = pverdict(s, u0);
         cnt.bulk++;
         return;
     }
     if (__builtin_expect(lmask(live && mm >= (1 << 26)) != 0ull, 0)) {
-        pgroup<FULL, WK_CHECKED, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+        pgroup<FULL, WK_CHECKED, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
         s.bad |= s.slack < 0 ? 32u : 0u;
         cnt.checked++;
         return;
@@ -637,23 +740,29 @@ __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint3
         // between a word's parts (a group with a longer word goes to the checked words)
         s.rmax = 0u;
         if (lmask(live && mm >= (1 << 17)) == 0ull) {
-            pgroup<FULL, WK_NORUN, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+            pgroup<FULL, WK_NORUN, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
             cnt.norun++;
         } else {
-            pgroup<FULL, WK_NORUN_SPLIT, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+            pgroup<FULL, WK_NORUN_SPLIT, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
             cnt.split++;
         }
         s.rare = s.rmax >> 4;  // (an escape: the checked words)
+    } else if constexpr (HY) {  // (no run-aware fast words for hybrid blocks: the checked words)
+        s.slack = 0;
+        pgroup<FULL, WK_CHECKED, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+        s.bad |= s.slack < 0 ? 32u : 0u;
+        cnt.checked++;
+        return;
     } else {
         s.rare = 0u;
-        pgroup<FULL, WK_FAST, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+        pgroup<FULL, WK_FAST, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
         cnt.fast++;
     }
     if (__builtin_expect(lmask((s.rare != 0u || s.slack < 0) && live) != 0ull, 0)) {
         s = s0;
         pfin = pfin0;
         s.slack = 0;
-        pgroup<FULL, WK_CHECKED, MONO>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+        pgroup<FULL, WK_CHECKED, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
         s.bad |= s.slack < 0 ? 32u : 0u;
         cnt.replay++;
     }
@@ -681,10 +790,16 @@ __device__ __forceinline__ void lane_finish(uint32_t rbad, const LEnd &e, int32_
 // one frame t = g0 + U of the recon wave.  FULL: every lane of the wave is inside its block.
 // MONO: one sample per frame (UnpackUtils.cs:571-588: crc = 3 crc + v), stored once, or
 // twice for FALSE_STEREO (fst; :655-664, after the fixup)
-template <int U, bool FULL, bool MONO, int... Ts>
+// HY: the whole fixup (fixup_tail: float_values, or the lossy clip and shift), else the shift
+template <bool HY>
+__device__ __forceinline__ int32_t lfix(int32_t x, uint32_t sh, const Fixup &fx) {
+    if constexpr (HY) return fixup_tail(fx, x);
+    else return (int32_t)((uint32_t)x << sh);
+}
+template <int U, bool FULL, bool MONO, bool HY, int... Ts>
 __device__ __forceinline__ void rframe(LChain<Ts...> &ch, const int2 *res, uint32_t lane, uint32_t g0, uint32_t nfr,
                                        bool joint, int32_t &mx, int32_t &mn, uint32_t &crc, uint32_t sh, int32_t *o,
-                                       uint32_t rbad, const LEnd &e, bool fst) {
+                                       uint32_t rbad, const LEnd &e, bool fst, const Fixup &fx) {
     const uint32_t t = g0 + U;
     const int2 r = res[((t & (RF - 1)) << 6) + lane];
     int32_t L = r.x, R = r.y;
@@ -693,7 +808,7 @@ __device__ __forceinline__ void rframe(LChain<Ts...> &ch, const int2 *res, uint3
         mx = max(mx, L);
         mn = min(mn, L);
         crc = crc * 3u + (uint32_t)L;
-        const int32_t v = (int32_t)((uint32_t)L << sh);
+        const int32_t v = lfix<HY>(L, sh, fx);
         const bool st = FULL ? nfr != 0u : t < nfr;
         if (st) {
             if (fst) *(int2 *)(o + 2u * t) = make_int2(v, v);
@@ -711,8 +826,8 @@ __device__ __forceinline__ void rframe(LChain<Ts...> &ch, const int2 *res, uint3
     // crc = (crc * 3 + L) * 3 + R (UnpackUtils.cs:620-626)
     crc = crc * 9u + (uint32_t)L * 3u + (uint32_t)R;
     int2 v;
-    v.x = (int32_t)((uint32_t)L << sh);
-    v.y = (int32_t)((uint32_t)R << sh);
+    v.x = lfix<HY>(L, sh, fx);
+    v.y = lfix<HY>(R, sh, fx);
     if (FULL) {
         if (nfr) *(int2 *)(o + 2u * t) = v;  // (a lane without a block of its own stores nothing)
     } else {
@@ -722,11 +837,17 @@ __device__ __forceinline__ void rframe(LChain<Ts...> &ch, const int2 *res, uint3
 }
 
 // can this lane decode block d exactly (else ST_REDO)?
-template <bool MONO, int... Ts>
+template <bool MONO, bool HY, int... Ts>
 __device__ __forceinline__ bool lane_ok(const BlockDesc &d) {
     using namespace wvf;
     if (d.kind != KIND_PCM) return false;
-    if (d.flags & (HYBRID_FLAG | FLOAT_DATA | INT32_DATA)) return false;
+    if constexpr (HY) {  // hybrid with HYBRID_BITRATE, no HYBRID_BALANCE; integer or float (float_values)
+        static_assert(!MONO, "hybrid lanes: stereo");
+        if ((d.flags & (HYBRID_FLAG | HYBRID_BITRATE | HYBRID_BALANCE | INT32_DATA)) != (HYBRID_FLAG | HYBRID_BITRATE))
+            return false;
+    } else if (d.flags & (HYBRID_FLAG | FLOAT_DATA | INT32_DATA)) {
+        return false;
+    }
     if (((d.flags & MONO_DATA) != 0) != MONO) return false;
     if (d.inherit || d.chain_len >= 2 || d.wvx_state || d.wvc_len || d.xfloat || d.pre_end || d.fstatus) return false;
     if ((!MONO || (d.flags & FALSE_STEREO)) && (d.out_off & 1u)) return false;  // 8-B stores
@@ -742,7 +863,7 @@ struct LBlock {
     uint32_t bi, nfr, nmax, nmin;
     bool ok, inl;
 };
-template <bool MONO, int... Ts>
+template <bool MONO, bool HY, int... Ts>
 __device__ __forceinline__ LBlock lane_block(const BlockDesc *descs, const uint32_t *list, uint32_t n, uint32_t grp,
                                              uint32_t lane) {
     LBlock b;
@@ -751,7 +872,7 @@ __device__ __forceinline__ LBlock lane_block(const BlockDesc *descs, const uint3
     // a lane past the list or with a block it does not take decodes 0 frames
     b.inl = li < n && list[li] != kLaneGap;
     b.bi = b.inl ? list[li] : 0u;
-    b.ok = b.inl && lane_ok<MONO, Ts...>(descs[b.bi]);
+    b.ok = b.inl && lane_ok<MONO, HY, Ts...>(descs[b.bi]);
     b.nfr = b.ok ? descs[b.bi].nframes : 0u;
     // the wave runs to its longest block; groups inside every block skip the per-frame end tests
     uint32_t nmax = b.nfr, nmin = b.nfr ? b.nfr : 0xFFFFFFFFu;
@@ -776,15 +897,15 @@ __device__ __forceinline__ bool lwait(uint32_t *ctr, uint32_t v, uint32_t *abort
     return false;
 }
 
-template <bool MONO, int... Ts>
+template <bool MONO, bool HY, int... Ts>
 __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
                                             uint32_t n, const uint8_t *__restrict__ blob, LShared &sh,
                                             uint8_t *ringm, uint32_t pair, uint32_t grp, uint32_t lane,
                                             uint32_t *__restrict__ dbg) {
     using namespace wvf;
     const uint64_t t_start = __builtin_readcyclecounter();
-    LCount cnt = {0, 0, 0, 0, 0, 0, 0};
-    const LBlock lb = lane_block<MONO, Ts...>(descs, list, n, grp, lane);
+    LCount cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const LBlock lb = lane_block<MONO, HY, Ts...>(descs, list, n, grp, lane);
     const BlockDesc &d = descs[lb.bi];
     const uint32_t nfr = lb.nfr;
     const uint8_t *ring = ringm;
@@ -826,14 +947,23 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
     s.bad = 0u;
     s.bad0 = 0u;
 #pragma unroll
-    for (int c = 0; c < 2; c++)
+    for (int c = 0; c < 2; c++) {
 #pragma unroll
         for (int k = 0; k < 3; k++) s.m[c][k] = d.median[c][k];
+        if constexpr (HY) {
+            s.slow[c] = d.slow_level[c];
+            s.acc[c] = d.bitrate_acc[c];
+            s.dlt[c] = d.bitrate_delta[c];
+            s.el[c] = 0;
+        }
+    }
     uint32_t pfin = 0u;
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), lgkm/exp untouched: the loop's waits count only its own loads
     for (uint32_t g0 = 0; g0 < lb.nmax; g0 += GF) {
         // the recon wave has taken the frames this group overwrites
+        const uint64_t tw0 = dbg ? __builtin_readcyclecounter() : 0;
         if (!lwait(&sh.consumed, g0 + GF > (uint32_t)RF ? g0 + GF - RF : 0u, &sh.abort)) return;
+        if (dbg) cnt.wait_consumed += __builtin_readcyclecounter() - tw0;
         // a bound that keeps the group exact (else the two-wave kernel redoes the block;
         // the reason lands in status bits 16-23 beside ST_REDO, for diagnostics)
         const int32_t mm = MONO ? max(max(s.m[0][0], s.m[0][1]), s.m[0][2])
@@ -850,15 +980,20 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
         uint4 st2 = src[min(u0 + 2u, ulast)], st3 = src[min(u0 + 3u, ulast)];
         fu = u0 + nld;
         if (g0 + GF < lb.nmin)  // (strict: the group holding a block's last frame records its verdict)
-            pgroup_try<true, MONO>(s, ring, rb, sh.res, lane, g0, nfr, u0, pfin, mm, cnt);
+            pgroup_try<true, MONO, HY>(s, ring, rb, sh.res, lane, g0, nfr, u0, pfin, mm, cnt);
         else
-            pgroup_try<false, MONO>(s, ring, rb, sh.res, lane, g0, nfr, u0, pfin, mm, cnt);
+            pgroup_try<false, MONO, HY>(s, ring, rb, sh.res, lane, g0, nfr, u0, pfin, mm, cnt);
         // the reader stayed inside the units written before this group
         s.rp = rpos(s);
         s.ra0 = s.ra;
         if (s.rp >= u0 * 4u) s.bad |= 64u;
         if (!s.bad0) s.bad0 = s.bad | (s.pmax >= 17u ? 16u : 0u);
         // the loads land in the ring (the unit holding the stream end gets its 0xFF tail)
+        if (dbg) {
+            const uint64_t tl0 = __builtin_readcyclecounter();
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+            cnt.wait_loads += __builtin_readcyclecounter() - tl0;
+        }
         if (nld > 0u) {
             if (u0 + 1u >= eu) st0 = ff_unit(st0, u0, e);
             put_unit(ringm, rb, u0, st0);
@@ -880,7 +1015,7 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
         w2::lds_publish(&sh.produced, g0 + GF);
     }
     if (dbg && lane == 0u) {  // (diagnostics: cycles and groups per path of this wave)
-        uint32_t *o = dbg + grp * 8u;
+        uint32_t *o = dbg + grp * 16u;
         o[0] = (uint32_t)(__builtin_readcyclecounter() - t_start);
         o[1] = cnt.groups;
         o[2] = cnt.bulk;
@@ -889,15 +1024,17 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
         o[5] = cnt.fast;
         o[6] = cnt.checked;
         o[7] = cnt.replay;
+        o[8] = (uint32_t)cnt.wait_consumed;
+        o[9] = (uint32_t)cnt.wait_loads;
     }
 }
 
-template <bool MONO, int... Ts>
+template <bool MONO, bool HY, int... Ts>
 __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
                                            uint32_t n, int32_t *__restrict__ out, uint32_t *__restrict__ status,
                                            LShared &sh, uint32_t grp, uint32_t lane) {
     using namespace wvf;
-    const LBlock lb = lane_block<MONO, Ts...>(descs, list, n, grp, lane);
+    const LBlock lb = lane_block<MONO, HY, Ts...>(descs, list, n, grp, lane);
     const BlockDesc &d = descs[lb.bi];
     const uint32_t nfr = lb.nfr;
     const bool fst = (d.flags & FALSE_STEREO) != 0;
@@ -908,6 +1045,8 @@ __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, 
     int32_t *o = out + d.out_off;
     LChain<Ts...> ch;
     ch.init(d, 0);
+    Fixup fx;
+    if constexpr (HY) fixup_init(fx, d);
     uint32_t crc = 0xFFFFFFFFu;
     int32_t mx = 0, mn = 0;
     uint32_t rbad = 0u;
@@ -921,23 +1060,23 @@ __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, 
         }
         rbad |= ch.wbad() ? 4u : 0u;
         if (g0 + GF < lb.nmin) {
-            rframe<0, true, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
-            rframe<1, true, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
-            rframe<2, true, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
-            rframe<3, true, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
-            rframe<4, true, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
-            rframe<5, true, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
-            rframe<6, true, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
-            rframe<7, true, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
+            rframe<0, true, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<1, true, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<2, true, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<3, true, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<4, true, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<5, true, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<6, true, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<7, true, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
         } else {
-            rframe<0, false, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
-            rframe<1, false, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
-            rframe<2, false, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
-            rframe<3, false, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
-            rframe<4, false, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
-            rframe<5, false, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
-            rframe<6, false, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
-            rframe<7, false, MONO>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst);
+            rframe<0, false, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<1, false, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<2, false, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<3, false, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<4, false, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<5, false, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<6, false, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<7, false, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
         }
         // the group's residuals are read (DS ops of one wave complete in order)
         w2::lds_publish(&sh.consumed, g0 + GF);
@@ -954,13 +1093,13 @@ __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, 
 // waves on one SIMD: measured with 20 batches in flight, 16-unit rings (68 KiB per
 // workgroup, two per CU possible) ran at ~30,000 Msamples/s on most runs and
 // ~47,000 on some; a workgroup per CU keeps every launch at its one-batch time.
-constexpr int LPAIRS = 2;
-template <bool MONO, int... Ts>
+template <bool MONO, bool HY, int... Ts>
 __device__ __forceinline__ void lane_blocks(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
                                             uint32_t n, const uint8_t *__restrict__ blob, int32_t *__restrict__ out,
                                             uint32_t *__restrict__ status, uint32_t *__restrict__ dbg) {
     __shared__ LShared shp[LPAIRS];
-    __shared__ uint32_t rings[LPAIRS * RING_BYTES / 4];  // the parsers' payload rings (put_unit, ring_step)
+    // the parsers' payload rings (put_unit, ring_step), then (HY) the exp2 / log2 tables
+    __shared__ uint32_t rings[LPAIRS * RING_BYTES / 4 + (HY ? 128 : 0)];
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     const uint32_t pair = wave >> 1, grp = blockIdx.x * LPAIRS + pair;
     LShared &sh = shp[pair];
@@ -969,12 +1108,19 @@ __device__ __forceinline__ void lane_blocks(const BlockDesc *__restrict__ descs,
         sh.consumed = 0u;
         sh.abort = 0u;
     }
+    if constexpr (HY) {
+        if (threadIdx.x < 128u) {
+            const uint32_t i = threadIdx.x & 63u;
+            const auto *tab = (const __attribute__((address_space(4))) uint32_t *)(threadIdx.x < 64u ? c_exp2_table : c_log2_table);
+            rings[(threadIdx.x < 64u ? TAB_EXP2 : TAB_LOG2) / 4u + i] = tab[i];
+        }
+    }
     __syncthreads();
     if (grp * 64u >= n) return;  // (both waves of the pair: uniform)
     if ((wave & 1u) == 0u)
-        lane_parser<MONO, Ts...>(descs, list, n, blob, sh, (uint8_t *)rings, pair, grp, lane, dbg);
+        lane_parser<MONO, HY, Ts...>(descs, list, n, blob, sh, (uint8_t *)rings, pair, grp, lane, dbg);
     else
-        lane_recon<MONO, Ts...>(descs, list, n, out, status, sh, grp, lane);
+        lane_recon<MONO, HY, Ts...>(descs, list, n, out, status, sh, grp, lane);
 }
 
 }  // namespace lane
@@ -987,9 +1133,9 @@ __device__ __forceinline__ void lane_blocks(const BlockDesc *__restrict__ descs,
 #define WVG_TS_M5 18, 3, 2, 18, 18
 #define WVG_TS_HIGH16 2, 18, -1, 8, 6, 3, 5, 7, 4, 2, 18, -2, 3, 2, 18, 18
 #define WVG_TS_MONO_HIGH16 1, 17, 2, 18, 8, 6, 3, 5, 7, 4, 2, 18, 3, 2, 18, 18
-enum LaneList { LANE_FAST = 0, LANE_DEFAULT, LANE_M5, LANE_HIGH16, LANE_MONO_HIGH16 };
+enum LaneList { LANE_FAST = 0, LANE_DEFAULT, LANE_M5, LANE_HIGH16, LANE_MONO_HIGH16, LANE_HY_DEFAULT };
 // the lane kernel of one list over n blocks (wv_lane.hip)
-// dbg (nullptr: off): per parser wave 8 words (cycles, groups by path: LCount)
+// dbg (nullptr: off): per parser wave 16 words (cycles, groups by path, wait cycles: LCount)
 hipError_t launch_lane(int which, dim3 grid, dim3 block, hipStream_t s, const BlockDesc *descs, const uint32_t *list,
                        uint32_t n, const uint8_t *blob, int32_t *out, uint32_t *status, uint32_t *dbg);
 }  // namespace wvg
