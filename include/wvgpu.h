@@ -214,7 +214,8 @@ int wvg_batch_block_status(wvg_batch *b, uint32_t *out, int64_t cap);
  * parser wave of term set `ts`'s last lane-kernel decode, 16 words -- cycles, groups,
  * then groups taken as a zero-run bulk step / no-run words / split no-run words /
  * run-aware words / checked words at once / checked replay, then the cycles spent
- * waiting for the reconstruction wave and for the payload loads.  Returns the wave
+ * waiting for the reconstruction wave and for the payload loads, in the groups'
+ * words and in their ring stores (low 32 bits of each count).  Returns the wave
  * count (out needs 16 per wave), WVG_ERR_ARG without counters. */
 int wvg_batch_lane_counters(wvg_batch *b, int ts, uint32_t *out, int64_t cap);
 /* The blocks of one file (after download): for block k, end_frame[k] = the number of

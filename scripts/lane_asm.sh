@@ -3,7 +3,7 @@
 # usage: bash scripts/lane_asm.sh [out.s]
 set -e
 OUT=${1:-/tmp/wv_lane_fast.s}
-/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -mllvm -structurizecfg-skip-uniform-regions=true \
+/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -mllvm -structurizecfg-skip-uniform-regions=true -mllvm -amdgpu-sched-strategy=max-ilp \
   -DWV_LANE_ONLY_FAST --cuda-device-only -S -o "$OUT" "$(dirname "$0")/../wavpackdecoder_amd/csrc/wv_lane.hip"
 python3 - "$OUT" <<'PY'
 import re, sys

@@ -71,8 +71,8 @@ def one(cfg):
         waves[f"ts{ts}"] = {"waves": int(c.shape[0]), "cycles_max": int(c[order[0], 0]),
                             "cycles_median": int(np.median(c[:, 0])),
                             "slowest": [dict(zip(("wave", "cycles", "groups", "bulk", "norun", "split", "fast",
-                                                  "checked", "replay", "wait_consumed", "wait_loads"),
-                                                 [int(i)] + [int(v) for v in c[i][:10]]))
+                                                  "checked", "replay", "wait_consumed", "wait_loads", "words", "stage"),
+                                                 [int(i)] + [int(v) for v in c[i][:12]]))
                                         for i in order[:4]],
                             "totals": dict(zip(("groups", "bulk", "norun", "split", "fast", "checked", "replay"),
                                                [int(v) for v in c[:, 1:8].sum(axis=0)]))}

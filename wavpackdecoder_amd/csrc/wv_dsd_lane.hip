@@ -200,13 +200,13 @@ __device__ __forceinline__ void dsd3_lanes(const BlockDesc *__restrict__ descs, 
                 // (forwarded; its store then lands after channel 0's)
                 if (CH == 2 && c == 1) pv[CH - 1] = a[CH - 1] == a[0] ? nv[0] : pv[CH - 1];
                 f0[c] = decide(low, high, value, (uint32_t)pv[c], src, left);
+                dry = min(dry, src.avail);  // (a half frame past the window: its refill comes too late)
                 nv[c] = pv[c] + (((f0[c] ? kUp : kDown) - pv[c]) >> 8);
                 *(int32_t *)(ptb + a[c]) = nv[c];
             }
 #pragma unroll
             for (int c = 0; c < CH; c++) fupd(f[c], f0[c]);
         }
-        dry = min(dry, src.avail);
         src.refill();
         // the frame's bytes, CRC (crc += 2 crc + v per value), factor decay (:484-492)
         int32_t v[CH];

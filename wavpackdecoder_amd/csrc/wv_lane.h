@@ -553,9 +553,11 @@ __device__ __forceinline__ void lmerge(LState &s, const uint8_t *ring) {
     s.ra = ring_step(s.ra, mg);
     s.nxt = *(const uint32_t *)(ring + s.ra);
 }
-// SPLIT: the window is refilled between the unary part and the code as well, for
-// groups whose medians allow codes longer than the 33 bits a word may count on
-// otherwise (pgroup_try)
+// SPLIT: the window is refilled between the unary part and the code instead of
+// after the word, for groups whose medians allow codes longer than the 33 bits a
+// word may count on otherwise (pgroup_try): the code and sign then have >= 33 bits,
+// and the next word's unary part whatever is left (>= 1 bit; a unary count that runs
+// past it shows as slack < 0, and the group is replayed by the checked words)
 template <int C, bool SPLIT, bool HY = false>
 __device__ __forceinline__ int32_t lword_nz(LState &s, const uint8_t *ring, uint32_t rbase) {
     static_assert(!HY || SPLIT, "a hybrid word's bisection bits follow a refill");
@@ -618,7 +620,7 @@ __device__ __forceinline__ int32_t lword_nz(LState &s, const uint8_t *ring, uint
     s.win >>= tot;
     s.nb -= (int32_t)tot;
     s.slack = min(s.slack, s.nb);
-    lmerge(s, ring);
+    if constexpr (!SPLIT) lmerge(s, ring);
     if constexpr (HY) s.slow[C] = lhy_slow(s.slow[C], mid, ring);
     return (int32_t)(mid ^ (uint32_t)sg);
 }
@@ -655,7 +657,7 @@ __device__ __forceinline__ uint32_t pverdict(const LState &s, uint32_t u0) {
 enum { WK_CHECKED = 0, WK_FAST = 1, WK_NORUN = 2, WK_NORUN_SPLIT = 3 };
 template <int K, int C, bool HY>
 __device__ __forceinline__ int32_t lword_k(LState &s, const uint8_t *ring, uint32_t rb) {
-    if constexpr (K == WK_NORUN) return lword_nz<C, HY, HY>(s, ring, rb);
+    if constexpr (K == WK_NORUN) return lword_nz<C, false, false>(s, ring, rb);  // (not HY: pgroup_try)
     else if constexpr (K == WK_NORUN_SPLIT) return lword_nz<C, true, HY>(s, ring, rb);
     else if constexpr (K == WK_FAST) return lword_fast<C>(s, ring, rb);
     else return lword<C, HY>(s, ring, rb);
@@ -697,6 +699,7 @@ __device__ __forceinline__ void pgroup(LState &s, const uint8_t *ring, uint32_t 
 struct LCount {
     uint32_t groups, bulk, norun, split, fast, checked, replay;
     uint64_t wait_consumed, wait_loads;  // cycles in the group-start wait and the group-end load wait
+    uint64_t words, stage;               // cycles in the group's words (pgroup_try) and in its ring stores
 };
 template <bool FULL, bool MONO, bool HY>
 __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint32_t rb, int2 *res, uint32_t lane,
@@ -739,11 +742,12 @@ __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint3
         // at the group's start, hence 2^17; with larger medians the window is refilled
         // between a word's parts (a group with a longer word goes to the checked words)
         s.rmax = 0u;
-        if (lmask(live && mm >= (1 << 17)) == 0ull) {
+        if (!HY && lmask(live && mm >= (1 << 17)) == 0ull) {
             pgroup<FULL, WK_NORUN, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
             cnt.norun++;
         } else {
             pgroup<FULL, WK_NORUN_SPLIT, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+            lmerge(s, ring);  // (the next group's words start from >= 33 bits)
             cnt.split++;
         }
         s.rare = s.rmax >> 4;  // (an escape: the checked words)
@@ -904,7 +908,7 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
                                             uint32_t *__restrict__ dbg) {
     using namespace wvf;
     const uint64_t t_start = __builtin_readcyclecounter();
-    LCount cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    LCount cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const LBlock lb = lane_block<MONO, HY, Ts...>(descs, list, n, grp, lane);
     const BlockDesc &d = descs[lb.bi];
     const uint32_t nfr = lb.nfr;
@@ -979,10 +983,12 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
         uint4 st0 = src[min(u0, ulast)], st1 = src[min(u0 + 1u, ulast)];
         uint4 st2 = src[min(u0 + 2u, ulast)], st3 = src[min(u0 + 3u, ulast)];
         fu = u0 + nld;
+        const uint64_t tg0 = dbg ? __builtin_readcyclecounter() : 0;
         if (g0 + GF < lb.nmin)  // (strict: the group holding a block's last frame records its verdict)
             pgroup_try<true, MONO, HY>(s, ring, rb, sh.res, lane, g0, nfr, u0, pfin, mm, cnt);
         else
             pgroup_try<false, MONO, HY>(s, ring, rb, sh.res, lane, g0, nfr, u0, pfin, mm, cnt);
+        if (dbg) cnt.words += __builtin_readcyclecounter() - tg0;
         // the reader stayed inside the units written before this group
         s.rp = rpos(s);
         s.ra0 = s.ra;
@@ -994,6 +1000,7 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
             __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
             cnt.wait_loads += __builtin_readcyclecounter() - tl0;
         }
+        const uint64_t ts0 = dbg ? __builtin_readcyclecounter() : 0;
         if (nld > 0u) {
             if (u0 + 1u >= eu) st0 = ff_unit(st0, u0, e);
             put_unit(ringm, rb, u0, st0);
@@ -1010,6 +1017,7 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
             if (u0 + 4u >= eu) st3 = ff_unit(st3, u0 + 3u, e);
             put_unit(ringm, rb, u0 + 3u, st3);
         }
+        if (dbg) cnt.stage += __builtin_readcyclecounter() - ts0;
         // publish the group: residuals and verdicts first, then the count
         sh.pflag[lane] = pfin;
         w2::lds_publish(&sh.produced, g0 + GF);
@@ -1026,6 +1034,8 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
         o[7] = cnt.replay;
         o[8] = (uint32_t)cnt.wait_consumed;
         o[9] = (uint32_t)cnt.wait_loads;
+        o[10] = (uint32_t)cnt.words;
+        o[11] = (uint32_t)cnt.stage;
     }
 }
 
