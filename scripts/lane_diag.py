@@ -5,7 +5,7 @@
 set any), then the lane kernel's time alone and, with the
 fallback on (WVG_LANE_KERNEL=1), the same batch's time.
 
-usage: lane_diag.py [c2|c3|c1|c5|c4] ...  (default c2) -> one JSON line per config
+usage: lane_diag.py [c2|c3|c1|c5|c4|dsd3s|dsd3m|dsd3mix|hymix] ...  (default c2) -> one JSON line per config
 
 Reason bits: 1 outside the lane's scope (lane_ok), 2 medians >= 2^26, 4 a weight
 that could leave int16, 8 a mute, 16 a bits error / count too long, 32 a word past
@@ -36,6 +36,37 @@ def files_of(cfg):
         return [corpora.c4()]
     if cfg == "c5":
         return corpora.c5(4000)
+    if cfg == "hymix":  # the hybrid lane GPU test's mixed batch
+        sys.path.insert(0, ROOT)
+        from tests.test_gpu_hybrid_lane import _hy
+        rng = np.random.default_rng(7)
+        out = []
+        for k in range(140):
+            kind = ("music", "music", "noise", "zeros")[k % 4] if k % 7 else "music"
+            frames = int(rng.integers(1, 12000))
+            out.append(_hy(frames, 300 + k, bits=24 if k % 3 == 1 else 16, flt=k % 3 == 0,
+                           bitrate=int(rng.integers(512, 2048)), block=int(rng.choice([1000, 4410, 7000])), kind=kind,
+                           silence=(frames // 4, frames // 2) if k % 5 == 0 else None))
+        return out
+    if cfg == "dsd3mix":  # the DSD lane GPU test's mixed batch
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from synth import wvsynth as S
+        rng = np.random.default_rng(5)
+        out = []
+        for k in range(150):
+            nch, fs = ((2, False), (1, False), (2, True))[k % 3]
+            frames, block = int(rng.integers(1, 9000)), int(rng.choice([777, 2000, 5000]))
+            dd = S.dsd_random_like(frames, 1 if fs else nch, seed=100 + k, density=float(rng.uniform(0.05, 0.6)))
+            dd = np.repeat(dd, 2, axis=1) if fs else dd
+            out.append(S.encode_dsd(dd, S.DsdParams(nch=nch, false_stereo=fs, mode=3, block_samples=block,
+                                                    rate_i=int(rng.integers(0, 40)))))
+        return out
+    if cfg in ("dsd3s", "dsd3m"):  # DSD mode 3 stereo / mono files (the DSD lane kernel)
+        from synth import wvsynth as S
+        nch = 2 if cfg == "dsd3s" else 1
+        return [S.encode_dsd(S.dsd_random_like(fr, nch, seed=101 + k, density=0.3),
+                             S.DsdParams(nch=nch, mode=3, block_samples=2000, rate_i=7))
+                for k, fr in enumerate((4638, 700, 22050, 22050))]
     raise SystemExit(f"unknown config {cfg}")
 
 

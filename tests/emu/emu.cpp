@@ -96,11 +96,20 @@ int64_t emu_decode_from(const uint8_t *file, size_t len, int64_t seek_to, int ch
             DsdResult r = decode_dsd_block(d, file, fo.tables.data(), ptable.data(), hs);
             st |= r.status;
             if (r.status & ST_DSD_MUTE) {
-                // chunks from mute_chunk on: fill n*call_nch from the call start
+                // chunks from mute_chunk on: fill n*call_nch from the call start (a false-stereo
+                // block's final call that failed its CRC first goes back to one value per
+                // frame: wv_dsd_fill / dsd_fs_unexpand)
+                const bool fs = (d.flags & wvf::FALSE_STEREO) && !(d.flags & wvf::MONO_FLAG) &&
+                                d.nframes == d.block_samples;
                 uint32_t f = 0, cl = d.first_chunk;
                 for (uint32_t ci = 0; f < d.nframes; ci++) {
                     uint32_t n = cl < d.nframes - f ? cl : d.nframes - f;
                     if (ci >= r.mute_chunk && f >= d.pre_end) {
+                        if (fs && ci == r.mute_chunk && f + n == d.nframes) {
+                            const int64_t p = (int64_t)d.out_off + (int64_t)f * d.out_nch;
+                            for (int64_t k = 0; k < (int64_t)n; k++) out[p + k] = out[p + 2 * k];
+                            if (f == 0 && d.first_bsp > 0) st |= ST_NONDET;
+                        }
                         int64_t start = (int64_t)d.out_off + (int64_t)f * d.out_nch - (ci == 0 ? d.first_bsp : 0);
                         fills.push_back({start, (int64_t)n * d.call_nch});
                     }

@@ -15,7 +15,7 @@ import pytest
 from oracle import oracle as O
 from synth import wvsynth as S
 from tests import vectors as V
-from wavpackdecoder_amd._lib import WVG_ST_REDONE, WVG_ST_TIMEOUT
+from wavpackdecoder_amd._lib import WVG_ST_NONDET, WVG_ST_REDONE, WVG_ST_TIMEOUT
 
 pytestmark = pytest.mark.gpu
 
@@ -55,6 +55,9 @@ def _check(files, names, chunk=4096):
         assert r.exception == 0, name
         assert r.frames == ref.frames, name
         got = out[info.out_offset: info.out_offset + ref.frames * ref.nch]
+        if r.status_or & WVG_ST_NONDET:  # (the reference reads the caller's stale buffer there)
+            assert r.crc_errors == ref.crc_errors, name
+            continue
         bad = np.nonzero(got != ref.samples)[0]
         assert bad.size == 0 and r.crc_errors == ref.crc_errors, \
             f"{name}: crc_errors {r.crc_errors} vs {ref.crc_errors}, {bad.size} values differ from index " \

@@ -28,7 +28,7 @@ hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, ui
                         const uint32_t *lane_list, uint32_t lane_n, uint32_t *lane_dbg);
 hipError_t launch_format(const FormatSeg *segs, uint32_t nseg, const int32_t *in, uint8_t *out, int dsd, hipStream_t s);
 hipError_t upload_dsd_ptables();
-hipError_t launch_dsd_fill(const BlockDesc *descs, const uint32_t *dsd_list, uint32_t n_dsd, const uint32_t *status,
+hipError_t launch_dsd_fill(const BlockDesc *descs, const uint32_t *dsd_list, uint32_t n_dsd, uint32_t *status,
                            const uint32_t *aux, int32_t *out, hipStream_t s);
 hipError_t launch_dframe_rank(DFile *files, const uint32_t *tile_file, uint32_t ntiles, const uint32_t *rank_files,
                               uint32_t nrank, const uint8_t *blob, uint32_t *cand, uint32_t cand_cap, uint32_t *cnt,

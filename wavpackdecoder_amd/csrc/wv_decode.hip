@@ -1028,27 +1028,42 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_fast(const BlockD
     }
 }
 
-// one thread per DSD block; fills only for blocks that muted
+// one thread per DSD block; fills only for blocks that muted.  A false-stereo
+// block whose final call failed its CRC (the mute set after that call's decode,
+// DsdUtils.cs:99-119) returns before the stereo expansion: the call's values stay
+// one per frame from its buffer position (dsd_fs_unexpand), and the second half of
+// the expanded range keeps the caller's stale buffer where the fill does not reach
+// it -- a block that starts inside its call (ST_NONDET)
+__device__ __forceinline__ void dsd_fs_unexpand(const BlockDesc &d, uint32_t f, uint32_t len, int32_t *out,
+                                                uint32_t &st) {
+    const int64_t p = (int64_t)d.out_off + (int64_t)f * d.out_nch;
+    for (int64_t k = 0; k < (int64_t)len; k++) out[p + k] = out[p + 2 * k];  // (ascending: reads ahead of writes)
+    if (f == 0 && d.first_bsp > 0) st |= ST_NONDET;
+}
 extern "C" __global__ void __launch_bounds__(64) wv_dsd_fill(const BlockDesc *__restrict__ descs,
                                                              const uint32_t *__restrict__ list, uint32_t n,
-                                                             const uint32_t *__restrict__ status,
+                                                             uint32_t *__restrict__ status,
                                                              const uint32_t *__restrict__ mute_chunk,
                                                              int32_t *__restrict__ out) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint32_t bi = list[i];
     const BlockDesc &d = descs[bi];
-    if (!(status[bi] & ST_DSD_MUTE)) return;
+    uint32_t st = status[bi];
+    if (!(st & ST_DSD_MUTE)) return;
+    const bool fs = (d.flags & wvf::FALSE_STEREO) && !(d.flags & wvf::MONO_FLAG) && d.nframes == d.block_samples;
     uint32_t f = 0, cl = d.first_chunk, mc = mute_chunk[bi];
     for (uint32_t ci = 0; f < d.nframes; ci++) {
         uint32_t len = cl < d.nframes - f ? cl : d.nframes - f;
         if (ci >= mc && f >= d.pre_end) {  // a seek's discard calls fill a buffer that is dropped
+            if (fs && ci == mc && f + len == d.nframes) dsd_fs_unexpand(d, f, len, out, st);
             int64_t start = (int64_t)d.out_off + (int64_t)f * d.out_nch - (ci == 0 ? (int64_t)d.first_bsp : 0);
             for (int64_t k = 0; k < (int64_t)len * d.call_nch; k++) out[start + k] = 0x55;
         }
         f += len;
         cl = next_call_len(d, f);
     }
+    status[bi] = st;
 }
 
 // read_decorr_weights / read_decorr_samples / read_entropy_vars /
@@ -1331,7 +1346,7 @@ hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint3
 // every decode launch has joined it: a fill starts at its call's buffer start,
 // i.e. inside the output of earlier blocks of the same call, which may be PCM
 // or DSD blocks decoded on other streams
-hipError_t launch_dsd_fill(const BlockDesc *descs, const uint32_t *dsd_list, uint32_t n_dsd, const uint32_t *status,
+hipError_t launch_dsd_fill(const BlockDesc *descs, const uint32_t *dsd_list, uint32_t n_dsd, uint32_t *status,
                            const uint32_t *aux, int32_t *out, hipStream_t s) {
     if (!n_dsd) return hipSuccess;
     hipLaunchKernelGGL(wv_dsd_fill, dim3((n_dsd + 63) / 64), dim3(64), 0, s, descs, dsd_list, n_dsd, status, aux, out);

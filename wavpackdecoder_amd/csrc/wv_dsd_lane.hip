@@ -13,9 +13,9 @@
 //
 // Payload bytes come from a per-lane 64-bit big-endian window refilled a dword at
 // a time from a dword loaded one refill ahead (global loads, one per 4 bytes),
-// twice per frame: a half frame (8 decisions) can then take up to 5 bytes -- 40
-// bits of information in 8 binary decisions, which no real stream approaches.  A
-// lane whose window runs dry, or a block outside the kernel's scope (a seek's
+// every 4 decisions (>= 5 bytes then): a block's first frames, while its filters
+// adapt, take up to ~4 bytes per 4 decisions.  A lane whose window runs dry
+// (checked after every decision), or a block outside the kernel's scope (a seek's
 // discard calls, state from an earlier block, a framing verdict), is marked
 // ST_REDO and decoded again right after by the wave-per-block kernel, so results
 // are exactly the wave kernel's, which the GPU tests hold against the oracle.
@@ -118,8 +118,6 @@ __device__ __forceinline__ bool dsd3_ok(const BlockDesc &d) {
     if (CH == 2 && (d.flags & FALSE_STEREO)) return false;
     if (d.inherit || d.chain_len >= 2 || d.pre_end || d.fstatus) return false;
     if (d.dsd_data_len < 4u) return false;
-    const bool two = CH == 2 || (d.flags & FALSE_STEREO);
-    if (two && (d.out_off & 1u)) return false;  // 8-B stores
     return true;
 }
 
@@ -184,7 +182,9 @@ __device__ __forceinline__ void dsd3_lanes(const BlockDesc *__restrict__ descs, 
     for (uint32_t t = 0; t < nmax; t++) {
 #pragma unroll
         for (int bit = 0; bit < 8; bit++) {
-            if (bit == 4) src.refill();
+            // (a refill every 4 decisions: a block's first frames, before the filters
+            // adapt, can take 4 bytes per 4 decisions)
+            if (CH == 2 ? (bit & 1) == 0 && bit != 0 : bit == 4) src.refill();
             // both channels' entries first (each depends on its own filter only)
             uint32_t a[CH];
             int32_t pv[CH];
@@ -200,7 +200,7 @@ __device__ __forceinline__ void dsd3_lanes(const BlockDesc *__restrict__ descs, 
                 // (forwarded; its store then lands after channel 0's)
                 if (CH == 2 && c == 1) pv[CH - 1] = a[CH - 1] == a[0] ? nv[0] : pv[CH - 1];
                 f0[c] = decide(low, high, value, (uint32_t)pv[c], src, left);
-                dry = min(dry, src.avail);  // (a half frame past the window: its refill comes too late)
+                dry = min(dry, t < nfr ? src.avail : 0);  // (a half frame past the window: its refill comes too late)
                 nv[c] = pv[c] + (((f0[c] ? kUp : kDown) - pv[c]) >> 8);
                 *(int32_t *)(ptb + a[c]) = nv[c];
             }
@@ -213,12 +213,15 @@ __device__ __forceinline__ void dsd3_lanes(const BlockDesc *__restrict__ descs, 
 #pragma unroll
         for (int c = 0; c < CH; c++) {
             v[c] = f[c].byte & 0xFF;
-            crc = crc * 3 + v[c];
+            crc = t < nfr ? crc * 3 + v[c] : crc;  // (a lane past its block's end idles along)
             f[c].q8 -= (f[c].q8 + 512) >> 10;
             f[c].q0 = fval(f[c]);  // (the next frame's value, :395-396, with the decayed factor)
         }
         if (t < nfr) {
-            if (och == 2u) *(int2 *)(o + 2u * t) = make_int2(v[0], v[CH - 1]);
+            if (och == 2u) {  // (two dword stores: a file's output may start at an odd int)
+                o[2u * t] = v[0];
+                o[2u * t + 1u] = v[CH - 1];
+            }
             else o[t] = v[0];
         }
     }
@@ -231,10 +234,11 @@ __device__ __forceinline__ void dsd3_lanes(const BlockDesc *__restrict__ descs, 
     if (d.nframes == d.block_samples) {
         st |= ST_CRC_CHECKED;
         if (crc != d.crc) {
-            // DsdUtils.cs:99-101: the final call mutes (its values become 0x55: wv_dsd_fill)
-            st |= ST_CRC_ERROR | ST_DSD_MUTE;
-            const uint32_t fc = d.first_chunk, ck = d.chunk ? d.chunk : 1u;
-            mute_chunk[bi] = d.nframes <= fc ? 0u : 1u + (d.nframes - fc - 1u) / ck;
+            // DsdUtils.cs:99-117: the final call mutes -- 0x55 from the caller's buffer
+            // start, and a false-stereo block's values left unexpanded -- the wave kernel's
+            // call-by-call output; a corrupt block is rare: decoded again there
+            status[bi] = ST_REDO | (8u << 16);
+            return;
         }
     }
     status[bi] = st;

@@ -175,8 +175,17 @@ __device__ __forceinline__ uint32_t ring_step(uint32_t ra, uint32_t adv_mask) {
     return (n & RSLOT) | (ra & ~RSLOT);
 }
 // unit u (dwords 4u..4u+3) of the lane whose column is `col` (pair ring + lane * 4)
+__device__ __forceinline__ uint32_t unit_addr(uint32_t col, uint32_t u) {
+    return rslot(4u * u + 3u) | col;  // dword 4u + 3: the lowest of the four slots
+}
+__device__ __forceinline__ void put_unit_at(uint8_t *ring, uint32_t a, uint4 v) {
+    *(uint32_t *)(ring + a + 768u) = v.x;
+    *(uint32_t *)(ring + a + 512u) = v.y;
+    *(uint32_t *)(ring + a + 256u) = v.z;
+    *(uint32_t *)(ring + a) = v.w;
+}
 __device__ __forceinline__ void put_unit(uint8_t *ring, uint32_t col, uint32_t u, uint4 v) {
-    const uint32_t a = rslot(4u * u + 3u) | col;  // dword 4u + 3: the lowest of the four slots
+    const uint32_t a = unit_addr(col, u);
     *(uint32_t *)(ring + a + 768u) = v.x;
     *(uint32_t *)(ring + a + 512u) = v.y;
     *(uint32_t *)(ring + a + 256u) = v.z;
@@ -184,11 +193,11 @@ __device__ __forceinline__ void put_unit(uint8_t *ring, uint32_t col, uint32_t u
 }
 
 // bytes at or past the stream end read as 0xFF (BitsUtils.cs:125-139): unit u
-// relative to a stream ending at byte e
+// relative to a stream ending at byte e (branch-free: the real bytes of v, 0..4,
+// keep their value)
 __device__ __forceinline__ uint32_t ff_tail(uint32_t v, uint32_t pos, uint32_t e) {
-    if (pos >= e) return 0xFFFFFFFFu;
-    const uint32_t keep = e - pos;  // bytes of v that are real
-    return keep >= 4 ? v : (v | (0xFFFFFFFFu << (keep * 8)));
+    const uint32_t keep = min(e > pos ? e - pos : 0u, 4u);
+    return v | (uint32_t)(0xFFFFFFFFFFFFFFFFull << (keep * 8u));
 }
 __device__ __forceinline__ uint4 ff_unit(uint4 v, uint32_t u, uint32_t e) {
     const uint32_t b = u * 16u;
@@ -304,6 +313,9 @@ __device__ __forceinline__ uint32_t lgamma(LState &s, const uint8_t *ring, uint3
 // ---- hybrid words (HYBRID_FLAG with HYBRID_BITRATE, stereo) ----
 // The exp2 / log2 byte tables (WordsUtils.cs) in LDS after the payload rings.
 constexpr uint32_t TAB_EXP2 = LPAIRS * RING_BYTES, TAB_LOG2 = TAB_EXP2 + 256u;
+// a unit a lane does not take this group (no room in its ring) is written here instead
+// (4 slots of 64 lanes: every lane's put_unit_at stays branch-free)
+constexpr uint32_t RING_DUMMY = TAB_LOG2 + 256u, LDS_AFTER_RINGS = 512u + 1024u;
 // exp2s(L) for L > 0 (WordsUtils.cs:633-646): value (9 bits) scaled by 2^(e - 9) as
 // one shift pair, exact for e <= 22 (else the lane hands its block back); 0 for L <= 0
 __device__ __forceinline__ int32_t lexp2s_pos(int32_t L, const uint8_t *ring, uint32_t &bad) {
@@ -328,9 +340,12 @@ __device__ __forceinline__ void lhy_errlim(LState &s, const uint8_t *ring, bool 
 }
 // a hybrid word's magnitude from the 32 bits x after its unary part: read_code(high -
 // low) + low when the error limit is 0, else the bisection (:486-492) -- one bit per
-// step while high - low > error_limit, as a uniform loop over the lanes still in it
-// (the reference's 64-bit bounds: the lane hands back a word whose high passes
-// 2^30, and a bisection longer than the 31 bits of x)
+// step while high - low > error_limit.  The bisection runs on (lo, n = high - low + 1):
+// mid = lo + (n >> 1), a 1 bit keeps the upper n - (n >> 1) values, a 0 bit the lower
+// n >> 1.  Every lane still in it is at the same step (they all start at bit 0), so the
+// step's bit index is uniform; four steps per test of the wave's exit condition (a
+// lane that is done idles through them).  The reference's 64-bit bounds: the lane
+// hands back a word whose high reaches 2^31, and a bisection past the 31 bits of x.
 __device__ __forceinline__ void lhy_code(uint32_t x, uint32_t low, uint32_t mc, int32_t el, uint32_t &mid,
                                          uint32_t &used, uint32_t &bad) {
     const uint32_t z = (uint32_t)__builtin_clz(mc | 1u);
@@ -341,21 +356,24 @@ __device__ __forceinline__ void lhy_code(uint32_t x, uint32_t low, uint32_t mc, 
     const uint32_t t = v + __builtin_amdgcn_ubfe(x, nbt, 1) - ex;
     const uint32_t mid_rc = add3(low, v, big ? t : 0u);
     const uint32_t used_rc = nbt + (big ? 1u : 0u);
-    uint32_t lo = low, hi = low + mc, md = (lo + hi + 1u) >> 1, ub = 0u;
-    uint32_t am = (el != 0 && (int32_t)mc > el) ? ~0u : 0u;
-    while (lmask(am != 0u) != 0ull) {
-        const uint32_t bm = (uint32_t)__builtin_amdgcn_sbfe((int32_t)x, ub, 1);
-        const uint32_t slo = am & bm, shi = am & ~bm;
-        lo = (md & slo) | (lo & ~slo);
-        hi = ((md - 1u) & shi) | (hi & ~shi);
-        ub -= am;
-        md = (hi + lo + 1u) >> 1;
-        am &= (uint32_t)((int32_t)((uint32_t)el + lo - hi) >> 31) & (ub < 31u ? ~0u : 0u);
+    const uint32_t E = (uint32_t)el + 1u;
+    uint32_t lo = low, n = mc + 1u, ub = 0u;
+    uint32_t am = (el != 0 && n > E) ? ~0u : 0u;
+    for (uint32_t j = 0; lmask(am != 0u) != 0ull; j += 4u) {
+#pragma unroll
+        for (uint32_t u = 0; u < 4u; u++) {
+            const uint32_t h = n >> 1;
+            const uint32_t bm = (uint32_t)__builtin_amdgcn_sbfe((int32_t)x, j + u, 1);
+            lo += bm & am & h;
+            const uint32_t nn = h + (bm & n & 1u);
+            n = (am & nn) | (~am & n);
+            ub -= am;
+            am = n > E ? am : 0u;
+        }
     }
-    const bool cut = ub >= 31u && (int32_t)((uint32_t)el + lo - hi) < 0;
-    bad |= ((low | (low + mc)) >= (1u << 30) || cut) ? 2u : 0u;
-    mid = el == 0 ? mid_rc : md;
-    used = el == 0 ? used_rc : ub;
+    bad |= ((low | (low + mc)) >= 0x80000000u || ub > 31u) ? 2u : 0u;
+    mid = el == 0 ? mid_rc : lo + (n >> 1);
+    used = el == 0 ? used_rc : min(ub, 31u);
 }
 // slow_level after a word (HYBRID_BITRATE, :501-502): slow - (slow + SLO) >> SLS + mylog2(mid)
 // (mylog2, WordsUtils.cs:588-608: the 8 bits below the leading one index the table)
@@ -558,7 +576,9 @@ __device__ __forceinline__ void lmerge(LState &s, const uint8_t *ring) {
 // word may count on otherwise (pgroup_try): the code and sign then have >= 33 bits,
 // and the next word's unary part whatever is left (>= 1 bit; a unary count that runs
 // past it shows as slack < 0, and the group is replayed by the checked words)
-template <int C, bool SPLIT, bool HY = false>
+// W32: 32-bit products (C#'s int wrap) for groups whose medians pass the 24-bit
+// operands (pgroup_try: below 2^29 at the group's start, so none wraps in the group)
+template <int C, bool SPLIT, bool HY = false, bool W32 = false>
 __device__ __forceinline__ int32_t lword_nz(LState &s, const uint8_t *ring, uint32_t rbase) {
     static_assert(!HY || SPLIT, "a hybrid word's bisection bits follow a refill");
     using namespace wvf;
@@ -577,17 +597,26 @@ __device__ __forceinline__ int32_t lword_nz(LState &s, const uint8_t *ring, uint
     const uint32_t mc = o0 ? a0 : (o1 ? a1 : a2);
     // (low as selects of values computed unconditionally: a conditional multiply
     // becomes a divergent branch)
-    const uint32_t l3 = mul_u24(ones > 2u ? ones - 2u : 0u, a2 + 1u) + a1 + 1u;
+    const uint32_t l3 = (W32 ? (ones > 2u ? ones - 2u : 0u) * (a2 + 1u) : mul_u24(ones > 2u ? ones - 2u : 0u, a2 + 1u)) +
+                        a1 + 1u;
     const uint32_t low = vselm(lmask(o0), 0u, add3(a0, 1u, vselm(lmask(o1), 0u, l3)));
     // median k moves by ((m + DIVk + adj) >> sk) * mult: mult 5 above the bucket, -2 in it
     // (adj -2), 0 below; both read from nibble tables at the bucket index min(ones, 3)
     const uint32_t k4 = min(ones, 3u) << 2;
-    s.m[C][0] = mad24(add3((uint32_t)m0, 128u, (uint32_t)__builtin_amdgcn_sbfe(0x000E, k4, 4)) >> 7,
-                      __builtin_amdgcn_sbfe(0x555E, k4, 4), m0);
-    s.m[C][1] = mad24(add3((uint32_t)m1, 64u, (uint32_t)__builtin_amdgcn_sbfe(0x00E0, k4, 4)) >> 6,
-                      __builtin_amdgcn_sbfe(0x55E0, k4, 4), m1);
-    s.m[C][2] = mad24(add3((uint32_t)m2, 32u, (uint32_t)__builtin_amdgcn_sbfe(0x0E00, k4, 4)) >> 5,
-                      __builtin_amdgcn_sbfe(0x5E00, k4, 4), m2);
+    const int32_t d0 = (int32_t)add3((uint32_t)m0, 128u, (uint32_t)__builtin_amdgcn_sbfe(0x000E, k4, 4)) >> 7;
+    const int32_t d1 = (int32_t)add3((uint32_t)m1, 64u, (uint32_t)__builtin_amdgcn_sbfe(0x00E0, k4, 4)) >> 6;
+    const int32_t d2 = (int32_t)add3((uint32_t)m2, 32u, (uint32_t)__builtin_amdgcn_sbfe(0x0E00, k4, 4)) >> 5;
+    const int32_t x0 = __builtin_amdgcn_sbfe(0x555E, k4, 4), x1 = __builtin_amdgcn_sbfe(0x55E0, k4, 4);
+    const int32_t x2 = __builtin_amdgcn_sbfe(0x5E00, k4, 4);
+    if constexpr (W32) {
+        s.m[C][0] = wvf::add32(m0, wvf::mul32(d0, x0));
+        s.m[C][1] = wvf::add32(m1, wvf::mul32(d1, x1));
+        s.m[C][2] = wvf::add32(m2, wvf::mul32(d2, x2));
+    } else {
+        s.m[C][0] = mad24(d0, x0, m0);
+        s.m[C][1] = mad24(d1, x1, m1);
+        s.m[C][2] = mad24(d2, x2, m2);
+    }
     // read_code(mc): nbt = bitcount - 1 bits, one more when v >= extras
     uint32_t x;
     if constexpr (SPLIT) {
@@ -654,11 +683,12 @@ __device__ __forceinline__ uint32_t pverdict(const LState &s, uint32_t u0) {
 }
 
 // word kinds: WK_CHECKED lword, WK_FAST lword_fast, WK_NORUN / WK_NORUN_SPLIT lword_nz
-enum { WK_CHECKED = 0, WK_FAST = 1, WK_NORUN = 2, WK_NORUN_SPLIT = 3 };
+enum { WK_CHECKED = 0, WK_FAST = 1, WK_NORUN = 2, WK_NORUN_SPLIT = 3, WK_NORUN_SPLIT32 = 4 };
 template <int K, int C, bool HY>
 __device__ __forceinline__ int32_t lword_k(LState &s, const uint8_t *ring, uint32_t rb) {
     if constexpr (K == WK_NORUN) return lword_nz<C, false, false>(s, ring, rb);  // (not HY: pgroup_try)
     else if constexpr (K == WK_NORUN_SPLIT) return lword_nz<C, true, HY>(s, ring, rb);
+    else if constexpr (K == WK_NORUN_SPLIT32) return lword_nz<C, true, HY, true>(s, ring, rb);
     else if constexpr (K == WK_FAST) return lword_fast<C>(s, ring, rb);
     else return lword<C, HY>(s, ring, rb);
 }
@@ -703,7 +733,7 @@ struct LCount {
 };
 template <bool FULL, bool MONO, bool HY>
 __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint32_t rb, int2 *res, uint32_t lane,
-                                           uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin, int32_t mm,
+                                           uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin, uint32_t mm,
                                            LCount &cnt) {
     cnt.groups++;
     const bool live = g0 < nfr;
@@ -727,7 +757,14 @@ __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint3
         cnt.bulk++;
         return;
     }
-    if (__builtin_expect(lmask(live && mm >= (1 << 26)) != 0ull, 0)) {
+    const bool m26 = lmask(live && mm >= (1u << 26)) != 0ull;  // (past the 24-bit products)
+    const bool norun = max(s.m[0][0], s.m[1][0]) >= 2 + 2 * GF && s.zacc == 0u;
+#ifndef WV_LANE_HY_PATH  // (diagnostic builds: 1 hybrid groups with large medians, 2 every hybrid group, checked)
+#define WV_LANE_HY_PATH 0
+#endif
+    const bool allnr = lmask(live && !norun) == 0ull &&
+                       !(HY && ((WV_LANE_HY_PATH == 1 && m26) || WV_LANE_HY_PATH == 2));
+    if (__builtin_expect(m26 && !allnr, 0)) {
         pgroup<FULL, WK_CHECKED, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
         s.bad |= s.slack < 0 ? 32u : 0u;
         cnt.checked++;
@@ -735,14 +772,17 @@ __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint3
     }
     const LState s0 = s;
     const uint32_t pfin0 = pfin;
-    const bool norun = max(s.m[0][0], s.m[1][0]) >= 2 + 2 * GF && s.zacc == 0u;
-    if (lmask(live && !norun) == 0ull) {
+    if (allnr) {
         // a word may count on 33 bits: 17 of unary count (16 ones are an escape) and a
         // code of 15 + 1 while every median stays below 2^19 -- at most 3.2x its value
         // at the group's start, hence 2^17; with larger medians the window is refilled
         // between a word's parts (a group with a longer word goes to the checked words)
         s.rmax = 0u;
-        if (!HY && lmask(live && mm >= (1 << 17)) == 0ull) {
+        if (__builtin_expect(m26, 0)) {  // (medians below 2^29, none wraps in the group; or hybrid words)
+            pgroup<FULL, WK_NORUN_SPLIT32, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+            lmerge(s, ring);
+            cnt.split++;
+        } else if (!HY && lmask(live && mm >= (1u << 17)) == 0ull) {
             pgroup<FULL, WK_NORUN, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
             cnt.norun++;
         } else {
@@ -791,6 +831,12 @@ __device__ __forceinline__ void lane_finish(uint32_t rbad, const LEnd &e, int32_
     *e.st = bad ? (ST_REDO | (bad << 16) | (((pf >> 8) & 0xFFu) << 24)) : st;
 }
 
+// a frame's two values (two dword stores: a file's output may start at an odd int)
+__device__ __forceinline__ void st2(int32_t *p, int2 v) {
+    p[0] = v.x;
+    p[1] = v.y;
+}
+
 // one frame t = g0 + U of the recon wave.  FULL: every lane of the wave is inside its block.
 // MONO: one sample per frame (UnpackUtils.cs:571-588: crc = 3 crc + v), stored once, or
 // twice for FALSE_STEREO (fst; :655-664, after the fixup)
@@ -815,7 +861,7 @@ __device__ __forceinline__ void rframe(LChain<Ts...> &ch, const int2 *res, uint3
         const int32_t v = lfix<HY>(L, sh, fx);
         const bool st = FULL ? nfr != 0u : t < nfr;
         if (st) {
-            if (fst) *(int2 *)(o + 2u * t) = make_int2(v, v);
+            if (fst) st2(o + 2u * t, make_int2(v, v));
             else o[t] = v;
         }
         if (!FULL && t + 1u == nfr) lane_finish(rbad, e, mx, mn, crc);
@@ -833,9 +879,9 @@ __device__ __forceinline__ void rframe(LChain<Ts...> &ch, const int2 *res, uint3
     v.x = lfix<HY>(L, sh, fx);
     v.y = lfix<HY>(R, sh, fx);
     if (FULL) {
-        if (nfr) *(int2 *)(o + 2u * t) = v;  // (a lane without a block of its own stores nothing)
+        if (nfr) st2(o + 2u * t, v);  // (a lane without a block of its own stores nothing)
     } else {
-        if (t < nfr) *(int2 *)(o + 2u * t) = v;
+        if (t < nfr) st2(o + 2u * t, v);
         if (t + 1u == nfr) lane_finish(rbad, e, mx, mn, crc);
     }
 }
@@ -854,7 +900,6 @@ __device__ __forceinline__ bool lane_ok(const BlockDesc &d) {
     }
     if (((d.flags & MONO_DATA) != 0) != MONO) return false;
     if (d.inherit || d.chain_len >= 2 || d.wvx_state || d.wvc_len || d.xfloat || d.pre_end || d.fstatus) return false;
-    if ((!MONO || (d.flags & FALSE_STEREO)) && (d.out_off & 1u)) return false;  // 8-B stores
     if (d.num_terms != (int32_t)sizeof...(Ts)) return false;
     constexpr int8_t terms[sizeof...(Ts) + 1] = {(int8_t)Ts..., 0};
     for (int i = 0; i < (int)sizeof...(Ts); i++)
@@ -921,11 +966,13 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
     const uint32_t skip = (uint32_t)(boff & 15u);
     const uint32_t e = lb.ok ? skip + d.bits_len : 0u;
     const uint32_t eu = (e + 15u) >> 4;
-    const uint4 ffu = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+    const uint32_t ulast = eu > 0u ? eu - 1u : 0u;
+    // (units past the stream re-read its last one and read as 0xFF; the 0xFF fill
+    // only where some lane's stream ends: a wave-uniform branch)
 #pragma unroll 4
     for (uint32_t u = 0; u < (uint32_t)RU; u++) {
-        uint4 v = u < eu ? src[u] : ffu;
-        if (u + 1u >= eu) v = ff_unit(v, u, e);
+        uint4 v = src[min(u, ulast)];
+        if (lmask(lb.ok && u + 1u >= eu) != 0ull) v = ff_unit(v, u, e);
         put_unit(ringm, rb, u, v);
     }
     uint32_t fu = RU;  // next unit to load
@@ -970,16 +1017,19 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
         if (dbg) cnt.wait_consumed += __builtin_readcyclecounter() - tw0;
         // a bound that keeps the group exact (else the two-wave kernel redoes the block;
         // the reason lands in status bits 16-23 beside ST_REDO, for diagnostics)
-        const int32_t mm = MONO ? max(max(s.m[0][0], s.m[0][1]), s.m[0][2])
-                                : max(max(max(s.m[0][0], s.m[0][1]), max(s.m[0][2], s.m[1][0])), max(s.m[1][1], s.m[1][2]));
-        s.bad |= (mm >= (1 << 29) ? 2u : 0u);  // (the checked words' int32 products hold to 2^31)
+        // (unsigned: a median that wrapped negative counts as past every bound)
+        const uint32_t *um = (const uint32_t *)&s.m[0][0];
+        const uint32_t mm = MONO ? max(max(um[0], um[1]), um[2])
+                                 : max(max(max(um[0], um[1]), max(um[2], um[3])), max(um[4], um[5]));
+        // (the checked words' int32 products hold to 2^31; a hybrid word checks its own
+        // bounds -- lhy_code: any median, wrapped or not, is exact or handed back)
+        if constexpr (!HY) s.bad |= (mm >= (1u << 29) ? 2u : 0u);
         // this group's loads: the units after fu that fit in the ring (four every
         // group, unconditionally: the waitcnt pass then knows exactly which memory
         // operations are in flight; units past the stream re-read its last one)
         const uint32_t u0 = fu;
         const uint32_t room = (s.rp >> 2) + (uint32_t)RU - u0;
         const uint32_t nld = room < (uint32_t)NLD ? room : (uint32_t)NLD;
-        const uint32_t ulast = eu > 0u ? eu - 1u : 0u;
         uint4 st0 = src[min(u0, ulast)], st1 = src[min(u0 + 1u, ulast)];
         uint4 st2 = src[min(u0 + 2u, ulast)], st3 = src[min(u0 + 3u, ulast)];
         fu = u0 + nld;
@@ -1001,22 +1051,19 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
             cnt.wait_loads += __builtin_readcyclecounter() - tl0;
         }
         const uint64_t ts0 = dbg ? __builtin_readcyclecounter() : 0;
-        if (nld > 0u) {
-            if (u0 + 1u >= eu) st0 = ff_unit(st0, u0, e);
-            put_unit(ringm, rb, u0, st0);
+        // (branch-free: the 0xFF fill in the groups where some lane's stream ends, a
+        // wave-uniform test; a unit without room in the lane's ring to the dummy slots)
+        if (lmask(lb.ok && u0 + (uint32_t)NLD >= eu) != 0ull) {
+            st0 = ff_unit(st0, u0, e);
+            st1 = ff_unit(st1, u0 + 1u, e);
+            st2 = ff_unit(st2, u0 + 2u, e);
+            st3 = ff_unit(st3, u0 + 3u, e);
         }
-        if (nld > 1u) {
-            if (u0 + 2u >= eu) st1 = ff_unit(st1, u0 + 1u, e);
-            put_unit(ringm, rb, u0 + 1u, st1);
-        }
-        if (nld > 2u) {
-            if (u0 + 3u >= eu) st2 = ff_unit(st2, u0 + 2u, e);
-            put_unit(ringm, rb, u0 + 2u, st2);
-        }
-        if (nld > 3u) {
-            if (u0 + 4u >= eu) st3 = ff_unit(st3, u0 + 3u, e);
-            put_unit(ringm, rb, u0 + 3u, st3);
-        }
+        const uint32_t dcol = RING_DUMMY + lane * 4u;
+        put_unit_at(ringm, nld > 0u ? unit_addr(rb, u0) : dcol, st0);
+        put_unit_at(ringm, nld > 1u ? unit_addr(rb, u0 + 1u) : dcol, st1);
+        put_unit_at(ringm, nld > 2u ? unit_addr(rb, u0 + 2u) : dcol, st2);
+        put_unit_at(ringm, nld > 3u ? unit_addr(rb, u0 + 3u) : dcol, st3);
         if (dbg) cnt.stage += __builtin_readcyclecounter() - ts0;
         // publish the group: residuals and verdicts first, then the count
         sh.pflag[lane] = pfin;
@@ -1108,8 +1155,8 @@ __device__ __forceinline__ void lane_blocks(const BlockDesc *__restrict__ descs,
                                             uint32_t n, const uint8_t *__restrict__ blob, int32_t *__restrict__ out,
                                             uint32_t *__restrict__ status, uint32_t *__restrict__ dbg) {
     __shared__ LShared shp[LPAIRS];
-    // the parsers' payload rings (put_unit, ring_step), then (HY) the exp2 / log2 tables
-    __shared__ uint32_t rings[LPAIRS * RING_BYTES / 4 + (HY ? 128 : 0)];
+    // the parsers' payload rings (put_unit, ring_step), the exp2 / log2 tables (HY), the dummy unit slots
+    __shared__ uint32_t rings[(LPAIRS * RING_BYTES + LDS_AFTER_RINGS) / 4];
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     const uint32_t pair = wave >> 1, grp = blockIdx.x * LPAIRS + pair;
     LShared &sh = shp[pair];
