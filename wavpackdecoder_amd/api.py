@@ -176,9 +176,9 @@ class DecodeBatch:
         self._check(self._L.wvg_batch_sync(self._b))
 
     def set_kernel(self, kernel: str):
-        """'two_wave' (one workgroup per block: lowest latency alone) or 'lane' (one lane
-        per block: the most blocks per second with many batches in flight)
-        -- wvg_batch_set_kernel; results are identical either way."""
+        """'lane' (the default: one lane per block, the most blocks per second with
+        batches in flight) or 'two_wave' (one workgroup per block: lowest latency for one
+        small batch alone) -- wvg_batch_set_kernel; results are identical either way."""
         k = {"two_wave": _L.WVG_KERNEL_TWO_WAVE, "lane": _L.WVG_KERNEL_LANE}[kernel]
         self._check(self._L.wvg_batch_set_kernel(self._b, k))
 
@@ -251,7 +251,7 @@ class DecodeBatch:
     def lane_counters(self, ts: int) -> np.ndarray:
         """Diagnostics (a batch made with WVG_LANE_COUNTERS=1): per parser wave of term set
         `ts`'s last lane decode [cycles, groups, bulk, norun, split, fast, checked, replay,
-        wait_consumed, wait_loads, 0...] (wvg_batch_lane_counters)."""
+        wait_consumed, wait_loads, words, stage, 0...] (wvg_batch_lane_counters)."""
         buf = np.zeros(16 * 4096, dtype=np.uint32)
         k = self._L.wvg_batch_lane_counters(self._b, int(ts), buf.ctypes.data, buf.size)
         if k < 0:

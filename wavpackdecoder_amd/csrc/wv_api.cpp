@@ -160,7 +160,7 @@ struct wvg_batch {
     int force_lane = 0;                                 // WVG_FORCE_LANE=1: every PCM block on the generic kernel
     int prefer_pipe = 0;                                // WVG_PIPE=2: every PCM list on the pipelined kernel (A/B)
     int lanes = kLanes;                                 // WVG_LANES: streams per decode (A/B of the queue mapping)
-    int lane_mode = 0;                                  // term-set groups on the lane-per-block kernel (wvg_batch_set_kernel)
+    int lane_mode = 1;                                  // term-set groups on the lane-per-block kernel (wvg_batch_set_kernel)
     std::vector<uint32_t> h_status, h_aux;
     int64_t bytes_in = 0, frames = 0;
     // format epilogue: per-file byte image of WavpackFormatSamples
@@ -291,7 +291,7 @@ wvg_batch *wvg_batch_new(wvg_ctx *c, int chunk_frames) {
     const char *ln = getenv("WVG_LANES");
     if (ln && atoi(ln) >= 1) b->lanes = atoi(ln) < kLanes ? atoi(ln) : kLanes;
     const char *lk = getenv("WVG_LANE_KERNEL");
-    b->lane_mode = lk ? atoi(lk) : 0;
+    b->lane_mode = lk ? atoi(lk) : 1;  // (default: the lane kernels, wvg_batch_set_kernel)
     const char *rm = getenv("WVG_DFRAME_RANK_MIN");
     if (rm) b->rank_min = atoll(rm);
     const char *hm = getenv("WVG_HOST_META");
