@@ -211,7 +211,8 @@ int32_t *wvg_batch_host_out(wvg_batch *b);
 int wvg_batch_file_result(wvg_batch *b, int file, wvg_file_result *res);
 /* per-block status words (after download), one per decoded block in file order */
 int wvg_batch_block_status(wvg_batch *b, uint32_t *out, int64_t cap);
-/* Diagnostics (batches created with WVG_LANE_COUNTERS=1 in the environment): per
+/* Diagnostics (a library built with -DWV_LANE_COUNTERS=1 -- make counters -- and
+ * batches created with WVG_LANE_COUNTERS=1 in the environment; zeros otherwise): per
  * parser wave of term set `ts`'s last lane-kernel decode, 16 words -- cycles, groups,
  * then groups taken as a zero-run bulk step / no-run words / split no-run words /
  * run-aware words / checked words at once / checked replay, then the cycles spent

@@ -20,6 +20,10 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+# the per-wave counters need the diagnostics build (make -C wavpackdecoder_amd counters)
+_CNT = os.path.join(ROOT, "wavpackdecoder_amd", "build_cnt", "libwvgpu.so")
+if os.path.exists(_CNT) and "WVG_LIB" not in os.environ:
+    os.environ["WVG_LIB"] = _CNT
 REASONS = {1: "scope", 2: "median_bound", 4: "weight_int16", 8: "mute", 16: "bits_error", 32: "past_window",
            64: "ring_underrun", 128: "partner_stopped"}
 

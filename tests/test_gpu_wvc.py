@@ -1,5 +1,6 @@
 """GPU: hybrid files with their .wvc correction files decode exactly (SURVEY §8f-4,
-beyond the reference; parity = round trip to the encoder's input, see test_wvc.py),
+beyond the reference; parity unpinned = round trip to the encoder's input, circular
+for stereo terms -1/-2 whose rule the encoder shares, see test_wvc.py),
 and the same .wv files without the correction decode exactly as the oracle."""
 import numpy as np
 import pytest

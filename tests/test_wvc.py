@@ -10,6 +10,9 @@ against); stereo terms -1/-2, which predict one channel from the other's output
 of the same pass, predict the exact value from the other channel's exact output.  No reference behaviour exists, so parity is unpinned and pinned
 instead by the round trip to the encoder's input PCM, plus the .wvc headers'
 CRC of the exact output; the .wv alone still decodes exactly as the oracle.
+For the -1/-2 rule that round trip is circular (synth/wv_encoder.cpp encodes
+with the same rule), so it stays unpinned until a WavPack-made .wvc with those
+terms can be checked.
 
 CPU: the device core built for the host (tests/emu).  GPU: test_gpu_wvc.py.
 """

@@ -725,7 +725,16 @@ __device__ __forceinline__ void pgroup(LState &s, const uint8_t *ring, uint32_t 
 // checked words at once (32-bit arithmetic), a fast group that met a longer word is
 // decoded again by them (they refill between a word's parts).  mm: the lanes' largest
 // median at the group's start.
-// (diagnostics) groups per path of one parser wave: wvg_batch_lane_counters
+// (diagnostics, builds with -DWV_LANE_COUNTERS=1) groups per path of one parser wave
+// and where its cycles go: wvg_batch_lane_counters.  Off in the product build: each
+// test of the counter pointer is a branch per group.
+#ifndef WV_LANE_COUNTERS
+#define WV_LANE_COUNTERS 0
+#endif
+#define LCNT(x)                                 \
+    do {                                        \
+        if constexpr (WV_LANE_COUNTERS != 0) x; \
+    } while (0)
 struct LCount {
     uint32_t groups, bulk, norun, split, fast, checked, replay;
     uint64_t wait_consumed, wait_loads;  // cycles in the group-start wait and the group-end load wait
@@ -735,15 +744,17 @@ template <bool FULL, bool MONO, bool HY>
 __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint32_t rb, int2 *res, uint32_t lane,
                                            uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin, uint32_t mm,
                                            LCount &cnt) {
-    cnt.groups++;
-    const bool live = g0 < nfr;
+    LCNT(cnt.groups++);
+    // (every wave-wide test below is one compare of a lane value -- a compound
+    // condition would go through SALU mask logic, ~20 cycles each way)
+    const uint32_t livem = (uint32_t)((int32_t)(g0 - nfr) >> 31);  // ~0: the lane's block has frames left
     s.slack = 0;
     // every live lane inside a zero run for the group's words (:304-316: while the
     // run's count is past 1 a word is a zero that reads nothing and changes no state
     // but the count): one bulk step -- the silence waves (the host's lane order)
     constexpr uint32_t WPG = MONO ? GF : 2 * GF;
-    const bool zrun = ((((uint32_t)(s.m[0][0] | s.m[1][0])) & ~1u) | ~s.keep | s.h1) == 0u && s.zacc > WPG;
-    if (lmask(live && !zrun) == 0ull) {
+    const uint32_t notrun = (((uint32_t)(s.m[0][0] | s.m[1][0])) & ~1u) | ~s.keep | s.h1 | (s.zacc <= WPG ? 1u : 0u);
+    if (lmask((notrun & livem) != 0u) == 0ull) {
 #pragma unroll
         for (int u = 0; u < GF; u++) {
             res[(((g0 + u) & (RF - 1)) << 6) + lane] = make_int2(0, 0);
@@ -753,21 +764,23 @@ __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint3
             }
         }
         s.zacc -= WPG;
-        if (!FULL && live && nfr <= g0 + GF) pfin = pverdict(s, u0);
-        cnt.bulk++;
+        if (!FULL && livem && nfr <= g0 + GF) pfin = pverdict(s, u0);
+        LCNT(cnt.bulk++);
         return;
     }
-    const bool m26 = lmask(live && mm >= (1u << 26)) != 0ull;  // (past the 24-bit products)
-    const bool norun = max(s.m[0][0], s.m[1][0]) >= 2 + 2 * GF && s.zacc == 0u;
+    const uint32_t mml = mm & livem;
+    const bool m26 = lmask(mml >= (1u << 26)) != 0ull;  // (past the 24-bit products)
+    // no lane can meet a zero run in the group: both median[0] >= 18, no run pending
+    const uint32_t runnable = ((uint32_t)(max(s.m[0][0], s.m[1][0]) - (2 + 2 * GF)) >> 31) | min(s.zacc, 1u);
 #ifndef WV_LANE_HY_PATH  // (diagnostic builds: 1 hybrid groups with large medians, 2 every hybrid group, checked)
 #define WV_LANE_HY_PATH 0
 #endif
-    const bool allnr = lmask(live && !norun) == 0ull &&
+    const bool allnr = lmask((runnable & livem) != 0u) == 0ull &&
                        !(HY && ((WV_LANE_HY_PATH == 1 && m26) || WV_LANE_HY_PATH == 2));
     if (__builtin_expect(m26 && !allnr, 0)) {
         pgroup<FULL, WK_CHECKED, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
         s.bad |= s.slack < 0 ? 32u : 0u;
-        cnt.checked++;
+        LCNT(cnt.checked++);
         return;
     }
     const LState s0 = s;
@@ -781,34 +794,34 @@ __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint3
         if (__builtin_expect(m26, 0)) {  // (medians below 2^29, none wraps in the group; or hybrid words)
             pgroup<FULL, WK_NORUN_SPLIT32, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
             lmerge(s, ring);
-            cnt.split++;
-        } else if (!HY && lmask(live && mm >= (1u << 17)) == 0ull) {
+            LCNT(cnt.split++);
+        } else if (!HY && lmask(mml >= (1u << 17)) == 0ull) {
             pgroup<FULL, WK_NORUN, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
-            cnt.norun++;
+            LCNT(cnt.norun++);
         } else {
             pgroup<FULL, WK_NORUN_SPLIT, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
             lmerge(s, ring);  // (the next group's words start from >= 33 bits)
-            cnt.split++;
+            LCNT(cnt.split++);
         }
         s.rare = s.rmax >> 4;  // (an escape: the checked words)
     } else if constexpr (HY) {  // (no run-aware fast words for hybrid blocks: the checked words)
         s.slack = 0;
         pgroup<FULL, WK_CHECKED, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
         s.bad |= s.slack < 0 ? 32u : 0u;
-        cnt.checked++;
+        LCNT(cnt.checked++);
         return;
     } else {
         s.rare = 0u;
         pgroup<FULL, WK_FAST, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
-        cnt.fast++;
+        LCNT(cnt.fast++);
     }
-    if (__builtin_expect(lmask((s.rare != 0u || s.slack < 0) && live) != 0ull, 0)) {
+    if (__builtin_expect(lmask(((s.rare | ((uint32_t)s.slack >> 31)) & livem) != 0u) != 0ull, 0)) {
         s = s0;
         pfin = pfin0;
         s.slack = 0;
         pgroup<FULL, WK_CHECKED, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
         s.bad |= s.slack < 0 ? 32u : 0u;
-        cnt.replay++;
+        LCNT(cnt.replay++);
     }
 }
 
@@ -952,7 +965,7 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
                                             uint8_t *ringm, uint32_t pair, uint32_t grp, uint32_t lane,
                                             uint32_t *__restrict__ dbg) {
     using namespace wvf;
-    const uint64_t t_start = __builtin_readcyclecounter();
+    const uint64_t t_start = WV_LANE_COUNTERS ? __builtin_readcyclecounter() : 0;
     LCount cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const LBlock lb = lane_block<MONO, HY, Ts...>(descs, list, n, grp, lane);
     const BlockDesc &d = descs[lb.bi];
@@ -967,12 +980,13 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
     const uint32_t e = lb.ok ? skip + d.bits_len : 0u;
     const uint32_t eu = (e + 15u) >> 4;
     const uint32_t ulast = eu > 0u ? eu - 1u : 0u;
+    const uint32_t euk = lb.ok ? eu : 0xFFFFFF00u;  // (the stream-end test as one compare)
     // (units past the stream re-read its last one and read as 0xFF; the 0xFF fill
     // only where some lane's stream ends: a wave-uniform branch)
 #pragma unroll 4
     for (uint32_t u = 0; u < (uint32_t)RU; u++) {
         uint4 v = src[min(u, ulast)];
-        if (lmask(lb.ok && u + 1u >= eu) != 0ull) v = ff_unit(v, u, e);
+        if (lmask(u + 1u >= euk) != 0ull) v = ff_unit(v, u, e);
         put_unit(ringm, rb, u, v);
     }
     uint32_t fu = RU;  // next unit to load
@@ -1012,9 +1026,9 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), lgkm/exp untouched: the loop's waits count only its own loads
     for (uint32_t g0 = 0; g0 < lb.nmax; g0 += GF) {
         // the recon wave has taken the frames this group overwrites
-        const uint64_t tw0 = dbg ? __builtin_readcyclecounter() : 0;
+        const uint64_t tw0 = (WV_LANE_COUNTERS && dbg) ? __builtin_readcyclecounter() : 0;
         if (!lwait(&sh.consumed, g0 + GF > (uint32_t)RF ? g0 + GF - RF : 0u, &sh.abort)) return;
-        if (dbg) cnt.wait_consumed += __builtin_readcyclecounter() - tw0;
+        if (WV_LANE_COUNTERS && dbg) cnt.wait_consumed += __builtin_readcyclecounter() - tw0;
         // a bound that keeps the group exact (else the two-wave kernel redoes the block;
         // the reason lands in status bits 16-23 beside ST_REDO, for diagnostics)
         // (unsigned: a median that wrapped negative counts as past every bound)
@@ -1033,27 +1047,27 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
         uint4 st0 = src[min(u0, ulast)], st1 = src[min(u0 + 1u, ulast)];
         uint4 st2 = src[min(u0 + 2u, ulast)], st3 = src[min(u0 + 3u, ulast)];
         fu = u0 + nld;
-        const uint64_t tg0 = dbg ? __builtin_readcyclecounter() : 0;
+        const uint64_t tg0 = (WV_LANE_COUNTERS && dbg) ? __builtin_readcyclecounter() : 0;
         if (g0 + GF < lb.nmin)  // (strict: the group holding a block's last frame records its verdict)
             pgroup_try<true, MONO, HY>(s, ring, rb, sh.res, lane, g0, nfr, u0, pfin, mm, cnt);
         else
             pgroup_try<false, MONO, HY>(s, ring, rb, sh.res, lane, g0, nfr, u0, pfin, mm, cnt);
-        if (dbg) cnt.words += __builtin_readcyclecounter() - tg0;
+        if (WV_LANE_COUNTERS && dbg) cnt.words += __builtin_readcyclecounter() - tg0;
         // the reader stayed inside the units written before this group
         s.rp = rpos(s);
         s.ra0 = s.ra;
         if (s.rp >= u0 * 4u) s.bad |= 64u;
         if (!s.bad0) s.bad0 = s.bad | (s.pmax >= 17u ? 16u : 0u);
         // the loads land in the ring (the unit holding the stream end gets its 0xFF tail)
-        if (dbg) {
+        if (WV_LANE_COUNTERS && dbg) {
             const uint64_t tl0 = __builtin_readcyclecounter();
             __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
             cnt.wait_loads += __builtin_readcyclecounter() - tl0;
         }
-        const uint64_t ts0 = dbg ? __builtin_readcyclecounter() : 0;
+        const uint64_t ts0 = (WV_LANE_COUNTERS && dbg) ? __builtin_readcyclecounter() : 0;
         // (branch-free: the 0xFF fill in the groups where some lane's stream ends, a
         // wave-uniform test; a unit without room in the lane's ring to the dummy slots)
-        if (lmask(lb.ok && u0 + (uint32_t)NLD >= eu) != 0ull) {
+        if (lmask(u0 + (uint32_t)NLD >= euk) != 0ull) {
             st0 = ff_unit(st0, u0, e);
             st1 = ff_unit(st1, u0 + 1u, e);
             st2 = ff_unit(st2, u0 + 2u, e);
@@ -1064,12 +1078,12 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
         put_unit_at(ringm, nld > 1u ? unit_addr(rb, u0 + 1u) : dcol, st1);
         put_unit_at(ringm, nld > 2u ? unit_addr(rb, u0 + 2u) : dcol, st2);
         put_unit_at(ringm, nld > 3u ? unit_addr(rb, u0 + 3u) : dcol, st3);
-        if (dbg) cnt.stage += __builtin_readcyclecounter() - ts0;
+        if (WV_LANE_COUNTERS && dbg) cnt.stage += __builtin_readcyclecounter() - ts0;
         // publish the group: residuals and verdicts first, then the count
         sh.pflag[lane] = pfin;
         w2::lds_publish(&sh.produced, g0 + GF);
     }
-    if (dbg && lane == 0u) {  // (diagnostics: cycles and groups per path of this wave)
+    if (WV_LANE_COUNTERS && dbg && lane == 0u) {  // (diagnostics: cycles and groups per path of this wave)
         uint32_t *o = dbg + grp * 16u;
         o[0] = (uint32_t)(__builtin_readcyclecounter() - t_start);
         o[1] = cnt.groups;
