@@ -390,6 +390,15 @@ __device__ __forceinline__ int32_t lhy_decay(int32_t slow) {  // a zero-run zero
     return sub32(slow, add32(slow, SLO) >> SLS);
 }
 
+// A word's result: its value v, and what the reconstruction wave needs to compute it
+// itself (CODES, lane_blocks): x, the 32 window bits after the unary part, the bucket's
+// low and high - low (mc).  v = (low + read_code(mc) from x) ^ (its sign bit) (rdecode);
+// a zero word is x = low = mc = 0, which decodes to 0.
+struct LW {
+    uint32_t x, low, mc;
+    int32_t v;
+};
+
 // get_words for one residual of channel C (WordsUtils.cs:290-503, lossless:
 // error_limit 0): the word as branch-free selects on lane masks.  Two rare
 // parts branch, taken when some lane needs them: the zero-run mode's entry (a
@@ -401,7 +410,7 @@ __device__ __forceinline__ int32_t lhy_decay(int32_t slow) {  // a zero-run zero
 // nothing, which leaves its state as it was -- and the checks it feeds are those
 // of the word that ends the run, which reads the same window with the same state.
 template <int C, bool HY = false>
-__device__ __forceinline__ int32_t lword(LState &s, const uint8_t *ring, uint32_t rbase) {
+__device__ __forceinline__ LW lword(LState &s, const uint8_t *ring, uint32_t rbase) {
     using namespace wvf;
     // zero-run mode (:304-352): both channels' median[0] < 2, nothing held
     const uint64_t h0m0 = lmask(s.keep == 0u), h1m0 = lmask(s.h1 != 0u);
@@ -486,10 +495,14 @@ __device__ __forceinline__ int32_t lword(LState &s, const uint8_t *ring, uint32_
     }
     const int32_t sg = __builtin_amdgcn_sbfe((int32_t)x, used, 1);  // 0 or -1
     lskip(s, vselm(zm, 0u, used + 1u));
-    const int32_t out = (int32_t)vselm(zm, 0u, mid ^ (uint32_t)sg);
+    LW w;
+    w.v = (int32_t)vselm(zm, 0u, mid ^ (uint32_t)sg);
+    w.x = vselm(zm, 0u, x);
+    w.low = vselm(zm, 0u, low);
+    w.mc = vselm(zm, 0u, mc);
     if constexpr (HY) s.slow[C] = zskip ? s.slow[C] : lhy_slow(s.slow[C], mid, ring);
     lrefill(s, ring, rbase);
-    return out;
+    return w;
 }
 
 // The fast word: lword without its two rare branches, VALU only.  A lane inside
@@ -497,7 +510,7 @@ __device__ __forceinline__ int32_t lword(LState &s, const uint8_t *ring, uint32_
 // escaped unary count only sets s.rare, and the group it is in is decoded again
 // from its starting state by lword (lane_parser).
 template <int C>
-__device__ __forceinline__ int32_t lword_fast(LState &s, const uint8_t *ring, uint32_t rbase) {
+__device__ __forceinline__ LW lword_fast(LState &s, const uint8_t *ring, uint32_t rbase) {
     using namespace wvf;
     // zero-run mode (:304-352): a pending run counts down; its entry is rare.  All
     // as 0/1 lane values (a compound condition would go through SALU mask logic)
@@ -545,9 +558,13 @@ __device__ __forceinline__ int32_t lword_fast(LState &s, const uint8_t *ring, ui
     s.win >>= len;
     s.nb -= (int32_t)len;
     s.slack = min(s.slack, s.nb);
-    const int32_t out = (int32_t)((mid ^ (uint32_t)sg) & (zsk - 1u));
+    LW w;
+    w.v = (int32_t)((mid ^ (uint32_t)sg) & (zsk - 1u));
+    w.x = x & (zsk - 1u);
+    w.low = low & (zsk - 1u);
+    w.mc = mc & (zsk - 1u);
     lrefill(s, ring, rbase);
-    return out;
+    return w;
 }
 
 // The no-run word: lword_fast for a group in which no lane can enter the zero-run
@@ -579,7 +596,7 @@ __device__ __forceinline__ void lmerge(LState &s, const uint8_t *ring) {
 // W32: 32-bit products (C#'s int wrap) for groups whose medians pass the 24-bit
 // operands (pgroup_try: below 2^29 at the group's start, so none wraps in the group)
 template <int C, bool SPLIT, bool HY = false, bool W32 = false>
-__device__ __forceinline__ int32_t lword_nz(LState &s, const uint8_t *ring, uint32_t rbase) {
+__device__ __forceinline__ LW lword_nz(LState &s, const uint8_t *ring, uint32_t rbase) {
     static_assert(!HY || SPLIT, "a hybrid word's bisection bits follow a refill");
     using namespace wvf;
     const uint32_t lo = (uint32_t)s.win, hi = (uint32_t)(s.win >> 32);
@@ -651,7 +668,7 @@ __device__ __forceinline__ int32_t lword_nz(LState &s, const uint8_t *ring, uint
     s.slack = min(s.slack, s.nb);
     if constexpr (!SPLIT) lmerge(s, ring);
     if constexpr (HY) s.slow[C] = lhy_slow(s.slow[C], mid, ring);
-    return (int32_t)(mid ^ (uint32_t)sg);
+    return LW{x, low, mc, (int32_t)(mid ^ (uint32_t)sg)};
 }
 
 // ---------------------------------------------------------------------------
@@ -664,11 +681,14 @@ __device__ __forceinline__ int32_t lword_nz(LState &s, const uint8_t *ring, uint
 // waits: a wait that runs out hands every block of the pair to the two-wave
 // kernel (ST_REDO).
 // ---------------------------------------------------------------------------
-constexpr int RF = 32;                     // residual frames in flight per lane
+constexpr int RF = 16;                     // frames in flight per lane (parser -> recon)
 constexpr uint32_t LSPIN = 1u << 24;       // bounded waits (polls)
 
 struct LShared {
-    int2 res[RF * 64];                     // parser -> recon: residuals of frame t at [(t % RF) * 64 + lane]
+    // parser -> recon, frame t at [(t % RF) * 64 + lane]: CODES, (x, low) of both words in
+    // rq and (mc, mc) in rm; else the two residuals in rm
+    int4 rq[RF * 64];
+    int2 rm[RF * 64];
     uint32_t pflag[64];                    // parser -> recon: the block's parse verdict (bit 31: final)
     uint32_t produced, consumed, abort;    // frames; abort: a wait ran out
 };
@@ -685,35 +705,40 @@ __device__ __forceinline__ uint32_t pverdict(const LState &s, uint32_t u0) {
 // word kinds: WK_CHECKED lword, WK_FAST lword_fast, WK_NORUN / WK_NORUN_SPLIT lword_nz
 enum { WK_CHECKED = 0, WK_FAST = 1, WK_NORUN = 2, WK_NORUN_SPLIT = 3, WK_NORUN_SPLIT32 = 4 };
 template <int K, int C, bool HY>
-__device__ __forceinline__ int32_t lword_k(LState &s, const uint8_t *ring, uint32_t rb) {
+__device__ __forceinline__ LW lword_k(LState &s, const uint8_t *ring, uint32_t rb) {
     if constexpr (K == WK_NORUN) return lword_nz<C, false, false>(s, ring, rb);  // (not HY: pgroup_try)
     else if constexpr (K == WK_NORUN_SPLIT) return lword_nz<C, true, HY>(s, ring, rb);
     else if constexpr (K == WK_NORUN_SPLIT32) return lword_nz<C, true, HY, true>(s, ring, rb);
     else if constexpr (K == WK_FAST) return lword_fast<C>(s, ring, rb);
     else return lword<C, HY>(s, ring, rb);
 }
-template <int U, bool FULL, int FAST, bool MONO, bool HY>
-__device__ __forceinline__ void pframe(LState &s, const uint8_t *ring, uint32_t rb, int2 *res, uint32_t lane,
+template <int U, bool FULL, int FAST, bool MONO, bool HY, bool CODES>
+__device__ __forceinline__ void pframe(LState &s, const uint8_t *ring, uint32_t rb, LShared &sh, uint32_t lane,
                                        uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin) {
     const uint32_t t = g0 + U;
-    int2 r;
-    r.x = lword_k<FAST, 0, HY>(s, ring, rb);
-    if constexpr (MONO) r.y = 0;
-    else r.y = lword_k<FAST, 1, HY>(s, ring, rb);
-    res[((t & (RF - 1)) << 6) + lane] = r;
+    const uint32_t slot = ((t & (RF - 1)) << 6) + lane;
+    const LW w0 = lword_k<FAST, 0, HY>(s, ring, rb);
+    LW w1 = {0u, 0u, 0u, 0};
+    if constexpr (!MONO) w1 = lword_k<FAST, 1, HY>(s, ring, rb);
+    if constexpr (CODES) {
+        sh.rq[slot] = make_int4((int32_t)w0.x, (int32_t)w0.low, (int32_t)w1.x, (int32_t)w1.low);
+        sh.rm[slot] = make_int2((int32_t)w0.mc, (int32_t)w1.mc);
+    } else {
+        sh.rm[slot] = make_int2(w0.v, w1.v);
+    }
     if (!FULL && t + 1u == nfr) pfin = pverdict(s, u0);
 }
-template <bool FULL, int FAST, bool MONO, bool HY>
-__device__ __forceinline__ void pgroup(LState &s, const uint8_t *ring, uint32_t rb, int2 *res, uint32_t lane,
+template <bool FULL, int FAST, bool MONO, bool HY, bool CODES>
+__device__ __forceinline__ void pgroup(LState &s, const uint8_t *ring, uint32_t rb, LShared &sh, uint32_t lane,
                                        uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin) {
-    pframe<0, FULL, FAST, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
-    pframe<1, FULL, FAST, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
-    pframe<2, FULL, FAST, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
-    pframe<3, FULL, FAST, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
-    pframe<4, FULL, FAST, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
-    pframe<5, FULL, FAST, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
-    pframe<6, FULL, FAST, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
-    pframe<7, FULL, FAST, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+    pframe<0, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
+    pframe<1, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
+    pframe<2, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
+    pframe<3, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
+    pframe<4, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
+    pframe<5, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
+    pframe<6, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
+    pframe<7, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
 }
 // a group: the fast words first -- the no-run words when no live lane can meet a
 // zero run in it (lword_nz), else lword_fast; if a live lane met a rare word, the
@@ -740,8 +765,8 @@ struct LCount {
     uint64_t wait_consumed, wait_loads;  // cycles in the group-start wait and the group-end load wait
     uint64_t words, stage;               // cycles in the group's words (pgroup_try) and in its ring stores
 };
-template <bool FULL, bool MONO, bool HY>
-__device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint32_t rb, int2 *res, uint32_t lane,
+template <bool FULL, bool MONO, bool HY, bool CODES>
+__device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint32_t rb, LShared &sh, uint32_t lane,
                                            uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin, uint32_t mm,
                                            LCount &cnt) {
     LCNT(cnt.groups++);
@@ -757,7 +782,9 @@ __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint3
     if (lmask((notrun & livem) != 0u) == 0ull) {
 #pragma unroll
         for (int u = 0; u < GF; u++) {
-            res[(((g0 + u) & (RF - 1)) << 6) + lane] = make_int2(0, 0);
+            const uint32_t slot = (((g0 + u) & (RF - 1)) << 6) + lane;
+            if constexpr (CODES) sh.rq[slot] = make_int4(0, 0, 0, 0);
+            sh.rm[slot] = make_int2(0, 0);
             if constexpr (HY) {  // every zero of a run decays its channel's slow_level
                 s.slow[0] = lhy_decay(s.slow[0]);
                 if constexpr (!MONO) s.slow[1] = lhy_decay(s.slow[1]);
@@ -778,7 +805,7 @@ __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint3
     const bool allnr = lmask((runnable & livem) != 0u) == 0ull &&
                        !(HY && ((WV_LANE_HY_PATH == 1 && m26) || WV_LANE_HY_PATH == 2));
     if (__builtin_expect(m26 && !allnr, 0)) {
-        pgroup<FULL, WK_CHECKED, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+        pgroup<FULL, WK_CHECKED, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
         s.bad |= s.slack < 0 ? 32u : 0u;
         LCNT(cnt.checked++);
         return;
@@ -792,34 +819,34 @@ __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint3
         // between a word's parts (a group with a longer word goes to the checked words)
         s.rmax = 0u;
         if (__builtin_expect(m26, 0)) {  // (medians below 2^29, none wraps in the group; or hybrid words)
-            pgroup<FULL, WK_NORUN_SPLIT32, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+            pgroup<FULL, WK_NORUN_SPLIT32, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
             lmerge(s, ring);
             LCNT(cnt.split++);
         } else if (!HY && lmask(mml >= (1u << 17)) == 0ull) {
-            pgroup<FULL, WK_NORUN, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+            pgroup<FULL, WK_NORUN, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
             LCNT(cnt.norun++);
         } else {
-            pgroup<FULL, WK_NORUN_SPLIT, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+            pgroup<FULL, WK_NORUN_SPLIT, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
             lmerge(s, ring);  // (the next group's words start from >= 33 bits)
             LCNT(cnt.split++);
         }
         s.rare = s.rmax >> 4;  // (an escape: the checked words)
     } else if constexpr (HY) {  // (no run-aware fast words for hybrid blocks: the checked words)
         s.slack = 0;
-        pgroup<FULL, WK_CHECKED, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+        pgroup<FULL, WK_CHECKED, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
         s.bad |= s.slack < 0 ? 32u : 0u;
         LCNT(cnt.checked++);
         return;
     } else {
         s.rare = 0u;
-        pgroup<FULL, WK_FAST, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+        pgroup<FULL, WK_FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
         LCNT(cnt.fast++);
     }
     if (__builtin_expect(lmask(((s.rare | ((uint32_t)s.slack >> 31)) & livem) != 0u) != 0ull, 0)) {
         s = s0;
         pfin = pfin0;
         s.slack = 0;
-        pgroup<FULL, WK_CHECKED, MONO, HY>(s, ring, rb, res, lane, g0, nfr, u0, pfin);
+        pgroup<FULL, WK_CHECKED, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
         s.bad |= s.slack < 0 ? 32u : 0u;
         LCNT(cnt.replay++);
     }
@@ -859,13 +886,35 @@ __device__ __forceinline__ int32_t lfix(int32_t x, uint32_t sh, const Fixup &fx)
     if constexpr (HY) return fixup_tail(fx, x);
     else return (int32_t)((uint32_t)x << sh);
 }
-template <int U, bool FULL, bool MONO, bool HY, int... Ts>
-__device__ __forceinline__ void rframe(LChain<Ts...> &ch, const int2 *res, uint32_t lane, uint32_t g0, uint32_t nfr,
+// a word's value from what the parser passed (LW, CODES): read_code(mc) on x
+// (WordsUtils.cs:546-570) plus low, then the sign bit after the code
+__device__ __forceinline__ int32_t rdecode(uint32_t x, uint32_t low, uint32_t mc) {
+    const uint32_t z = (uint32_t)__builtin_clz(mc | 1u);
+    const uint32_t ex = (0xFFFFFFFFu >> z) - mc;
+    const uint32_t nbt = z ^ 31u;
+    const uint32_t v = __builtin_amdgcn_ubfe(x, 0, nbt);
+    const bool big = v >= ex;
+    const uint32_t t = v + __builtin_amdgcn_ubfe(x, nbt, 1) - ex;  // code = v + t when big
+    const uint32_t used = nbt + (big ? 1u : 0u);
+    const int32_t sg = __builtin_amdgcn_sbfe((int32_t)x, used, 1);
+    return (int32_t)(add3(low, v, big ? t : 0u) ^ (uint32_t)sg);
+}
+template <int U, bool FULL, bool MONO, bool HY, bool CODES, int... Ts>
+__device__ __forceinline__ void rframe(LChain<Ts...> &ch, const LShared &shr, uint32_t lane, uint32_t g0, uint32_t nfr,
                                        bool joint, int32_t &mx, int32_t &mn, uint32_t &crc, uint32_t sh, int32_t *o,
                                        uint32_t rbad, const LEnd &e, bool fst, const Fixup &fx) {
     const uint32_t t = g0 + U;
-    const int2 r = res[((t & (RF - 1)) << 6) + lane];
-    int32_t L = r.x, R = r.y;
+    const uint32_t slot = ((t & (RF - 1)) << 6) + lane;
+    const int2 r = shr.rm[slot];
+    int32_t L, R;
+    if constexpr (CODES) {
+        const int4 q = shr.rq[slot];
+        L = rdecode((uint32_t)q.x, (uint32_t)q.y, (uint32_t)r.x);
+        R = MONO ? 0 : rdecode((uint32_t)q.z, (uint32_t)q.w, (uint32_t)r.y);
+    } else {
+        L = r.x;
+        R = r.y;
+    }
     ch.template frame<U, MONO>(L, R);
     if constexpr (MONO) {
         mx = max(mx, L);
@@ -898,6 +947,14 @@ __device__ __forceinline__ void rframe(LChain<Ts...> &ch, const int2 *res, uint3
         if (t + 1u == nfr) lane_finish(rbad, e, mx, mn, crc);
     }
 }
+
+// CODES: the parser hands the reconstruction wave each word's (x, low, mc) and the
+// reconstruction computes the value (rdecode), taking ~13 instructions a word off
+// the parser's chain -- for term lists whose reconstruction has the room (the 16-term
+// lists' passes already load it more than the words load the parser); hybrid words
+// (bisection) hand over values
+template <bool HY, int... Ts>
+constexpr bool lane_codes() { return !HY && sizeof...(Ts) <= 5; }
 
 // can this lane decode block d exactly (else ST_REDO)?
 template <bool MONO, bool HY, int... Ts>
@@ -965,6 +1022,7 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
                                             uint8_t *ringm, uint32_t pair, uint32_t grp, uint32_t lane,
                                             uint32_t *__restrict__ dbg) {
     using namespace wvf;
+    constexpr bool CODES = lane_codes<HY, Ts...>();
     const uint64_t t_start = WV_LANE_COUNTERS ? __builtin_readcyclecounter() : 0;
     LCount cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const LBlock lb = lane_block<MONO, HY, Ts...>(descs, list, n, grp, lane);
@@ -1015,12 +1073,12 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
     for (int c = 0; c < 2; c++) {
 #pragma unroll
         for (int k = 0; k < 3; k++) s.m[c][k] = d.median[c][k];
-        if constexpr (HY) {
-            s.slow[c] = d.slow_level[c];
-            s.acc[c] = d.bitrate_acc[c];
-            s.dlt[c] = d.bitrate_delta[c];
-            s.el[c] = 0;
-        }
+        // (set in every instantiation: left undefined, the unused fields of the state
+        // copies stay memory, which the backend would place in LDS)
+        s.slow[c] = HY ? d.slow_level[c] : 0;
+        s.acc[c] = HY ? d.bitrate_acc[c] : 0;
+        s.dlt[c] = HY ? d.bitrate_delta[c] : 0;
+        s.el[c] = 0;
     }
     uint32_t pfin = 0u;
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), lgkm/exp untouched: the loop's waits count only its own loads
@@ -1032,9 +1090,9 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
         // a bound that keeps the group exact (else the two-wave kernel redoes the block;
         // the reason lands in status bits 16-23 beside ST_REDO, for diagnostics)
         // (unsigned: a median that wrapped negative counts as past every bound)
-        const uint32_t *um = (const uint32_t *)&s.m[0][0];
-        const uint32_t mm = MONO ? max(max(um[0], um[1]), um[2])
-                                 : max(max(max(um[0], um[1]), max(um[2], um[3])), max(um[4], um[5]));
+        const uint32_t u00 = (uint32_t)s.m[0][0], u01 = (uint32_t)s.m[0][1], u02 = (uint32_t)s.m[0][2];
+        const uint32_t u10 = (uint32_t)s.m[1][0], u11 = (uint32_t)s.m[1][1], u12 = (uint32_t)s.m[1][2];
+        const uint32_t mm = MONO ? max(max(u00, u01), u02) : max(max(max(u00, u01), max(u02, u10)), max(u11, u12));
         // (the checked words' int32 products hold to 2^31; a hybrid word checks its own
         // bounds -- lhy_code: any median, wrapped or not, is exact or handed back)
         if constexpr (!HY) s.bad |= (mm >= (1u << 29) ? 2u : 0u);
@@ -1049,9 +1107,9 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
         fu = u0 + nld;
         const uint64_t tg0 = (WV_LANE_COUNTERS && dbg) ? __builtin_readcyclecounter() : 0;
         if (g0 + GF < lb.nmin)  // (strict: the group holding a block's last frame records its verdict)
-            pgroup_try<true, MONO, HY>(s, ring, rb, sh.res, lane, g0, nfr, u0, pfin, mm, cnt);
+            pgroup_try<true, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, mm, cnt);
         else
-            pgroup_try<false, MONO, HY>(s, ring, rb, sh.res, lane, g0, nfr, u0, pfin, mm, cnt);
+            pgroup_try<false, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, mm, cnt);
         if (WV_LANE_COUNTERS && dbg) cnt.words += __builtin_readcyclecounter() - tg0;
         // the reader stayed inside the units written before this group
         s.rp = rpos(s);
@@ -1105,6 +1163,7 @@ __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, 
                                            uint32_t n, int32_t *__restrict__ out, uint32_t *__restrict__ status,
                                            LShared &sh, uint32_t grp, uint32_t lane) {
     using namespace wvf;
+    constexpr bool CODES = lane_codes<HY, Ts...>();
     const LBlock lb = lane_block<MONO, HY, Ts...>(descs, list, n, grp, lane);
     const BlockDesc &d = descs[lb.bi];
     const uint32_t nfr = lb.nfr;
@@ -1131,23 +1190,23 @@ __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, 
         }
         rbad |= ch.wbad() ? 4u : 0u;
         if (g0 + GF < lb.nmin) {
-            rframe<0, true, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<1, true, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<2, true, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<3, true, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<4, true, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<5, true, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<6, true, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<7, true, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<0, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<1, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<2, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<3, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<4, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<5, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<6, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<7, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
         } else {
-            rframe<0, false, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<1, false, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<2, false, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<3, false, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<4, false, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<5, false, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<6, false, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<7, false, MONO, HY>(ch, sh.res, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<0, false, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<1, false, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<2, false, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<3, false, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<4, false, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<5, false, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<6, false, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<7, false, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
         }
         // the group's residuals are read (DS ops of one wave complete in order)
         w2::lds_publish(&sh.consumed, g0 + GF);
