@@ -668,6 +668,9 @@ __device__ __forceinline__ LW lword_nz(LState &s, const uint8_t *ring, uint32_t 
     s.slack = min(s.slack, s.nb);
     if constexpr (!SPLIT) lmerge(s, ring);
     if constexpr (HY) s.slow[C] = lhy_slow(s.slow[C], mid, ring);
+#ifdef WV_LANE_WORD_BARRIER  // (experiment: words in program order, the ring read a word ahead of its use)
+    __builtin_amdgcn_sched_barrier(WV_LANE_WORD_BARRIER);
+#endif
     return LW{x, low, mc, (int32_t)(mid ^ (uint32_t)sg)};
 }
 
@@ -681,7 +684,8 @@ __device__ __forceinline__ LW lword_nz(LState &s, const uint8_t *ring, uint32_t 
 // waits: a wait that runs out hands every block of the pair to the two-wave
 // kernel (ST_REDO).
 // ---------------------------------------------------------------------------
-constexpr int RF = 16;                     // frames in flight per lane (parser -> recon)
+constexpr int RF = 24;                     // frames in flight per lane (parser -> recon): three groups
+static_assert(RF % GF == 0, "a group's frames never wrap the frame ring");
 constexpr uint32_t LSPIN = 1u << 24;       // bounded waits (polls)
 
 struct LShared {
@@ -716,7 +720,7 @@ template <int U, bool FULL, int FAST, bool MONO, bool HY, bool CODES>
 __device__ __forceinline__ void pframe(LState &s, const uint8_t *ring, uint32_t rb, LShared &sh, uint32_t lane,
                                        uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin) {
     const uint32_t t = g0 + U;
-    const uint32_t slot = ((t & (RF - 1)) << 6) + lane;
+    const uint32_t slot = (((g0 % (uint32_t)RF) + U) << 6) + lane;  // (GF divides RF: no wrap inside a group)
     const LW w0 = lword_k<FAST, 0, HY>(s, ring, rb);
     LW w1 = {0u, 0u, 0u, 0};
     if constexpr (!MONO) w1 = lword_k<FAST, 1, HY>(s, ring, rb);
@@ -782,7 +786,7 @@ __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint3
     if (lmask((notrun & livem) != 0u) == 0ull) {
 #pragma unroll
         for (int u = 0; u < GF; u++) {
-            const uint32_t slot = (((g0 + u) & (RF - 1)) << 6) + lane;
+            const uint32_t slot = (((g0 % (uint32_t)RF) + u) << 6) + lane;
             if constexpr (CODES) sh.rq[slot] = make_int4(0, 0, 0, 0);
             sh.rm[slot] = make_int2(0, 0);
             if constexpr (HY) {  // every zero of a run decays its channel's slow_level
@@ -904,7 +908,7 @@ __device__ __forceinline__ void rframe(LChain<Ts...> &ch, const LShared &shr, ui
                                        bool joint, int32_t &mx, int32_t &mn, uint32_t &crc, uint32_t sh, int32_t *o,
                                        uint32_t rbad, const LEnd &e, bool fst, const Fixup &fx) {
     const uint32_t t = g0 + U;
-    const uint32_t slot = ((t & (RF - 1)) << 6) + lane;
+    const uint32_t slot = (((g0 % (uint32_t)RF) + U) << 6) + lane;
     const int2 r = shr.rm[slot];
     int32_t L, R;
     if constexpr (CODES) {
@@ -1081,11 +1085,14 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
         s.el[c] = 0;
     }
     uint32_t pfin = 0u;
+    uint32_t cpre = 0u;  // the recon's consumed count, read a group ahead (a lower bound: it only grows)
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), lgkm/exp untouched: the loop's waits count only its own loads
     for (uint32_t g0 = 0; g0 < lb.nmax; g0 += GF) {
-        // the recon wave has taken the frames this group overwrites
+        // the recon wave has taken the frames this group overwrites (RF = 3 groups: the
+        // count read at the last group's end nearly always suffices; else wait for it)
         const uint64_t tw0 = (WV_LANE_COUNTERS && dbg) ? __builtin_readcyclecounter() : 0;
-        if (!lwait(&sh.consumed, g0 + GF > (uint32_t)RF ? g0 + GF - RF : 0u, &sh.abort)) return;
+        const uint32_t need = g0 + GF > (uint32_t)RF ? g0 + GF - RF : 0u;
+        if (w2::uni(cpre) < need && !lwait(&sh.consumed, need, &sh.abort)) return;
         if (WV_LANE_COUNTERS && dbg) cnt.wait_consumed += __builtin_readcyclecounter() - tw0;
         // a bound that keeps the group exact (else the two-wave kernel redoes the block;
         // the reason lands in status bits 16-23 beside ST_REDO, for diagnostics)
@@ -1122,6 +1129,12 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
             __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
             cnt.wait_loads += __builtin_readcyclecounter() - tl0;
         }
+        // publish the group: residuals and verdicts first, then the count (before the
+        // ring stores, which only this wave reads: the publish waits for no more than
+        // the group's residual stores)
+        sh.pflag[lane] = pfin;
+        w2::lds_publish(&sh.produced, g0 + GF);
+        cpre = __hip_atomic_load(&sh.consumed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const uint64_t ts0 = (WV_LANE_COUNTERS && dbg) ? __builtin_readcyclecounter() : 0;
         // (branch-free: the 0xFF fill in the groups where some lane's stream ends, a
         // wave-uniform test; a unit without room in the lane's ring to the dummy slots)
@@ -1137,9 +1150,6 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
         put_unit_at(ringm, nld > 2u ? unit_addr(rb, u0 + 2u) : dcol, st2);
         put_unit_at(ringm, nld > 3u ? unit_addr(rb, u0 + 3u) : dcol, st3);
         if (WV_LANE_COUNTERS && dbg) cnt.stage += __builtin_readcyclecounter() - ts0;
-        // publish the group: residuals and verdicts first, then the count
-        sh.pflag[lane] = pfin;
-        w2::lds_publish(&sh.produced, g0 + GF);
     }
     if (WV_LANE_COUNTERS && dbg && lane == 0u) {  // (diagnostics: cycles and groups per path of this wave)
         uint32_t *o = dbg + grp * 16u;
