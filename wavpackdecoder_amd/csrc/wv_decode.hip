@@ -1201,6 +1201,10 @@ int term_set_of(const BlockDesc &d, int prefer_pipe) {
     if (d.wvx_state & 0x100) return -1;  // int32 + wvx fixup reads a second stream
     if (d.wvc_len) return -1;            // .wvc correction: a second stream read per hybrid word
     if (d.xfloat) return -1;             // exact float: WavPack 4's float_values over the wvx stream
+    // FALSE_STEREO with MONO_FLAG, or a block whose ints a frame differ from the file's:
+    // the layout rules of decode_pcm_run (malformed files only)
+    if ((d.flags & FALSE_STEREO) && (d.flags & MONO_FLAG)) return -1;
+    if ((((d.flags & MONO_FLAG) && !(d.flags & FALSE_STEREO)) ? 1u : 2u) != d.out_nch) return -1;
     const bool mono = (d.flags & MONO_DATA) != 0;
     if (d.num_terms < 0 || d.num_terms > MAXP) return -1;
     bool neg12 = false;

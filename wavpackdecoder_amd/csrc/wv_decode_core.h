@@ -157,6 +157,31 @@ struct BitReader {
         skip(n);
         return v;
     }
+    // BitsUtils.getbits for n > 32 (INT32 sent_bits of a malformed ID_INT32_INFO, up to
+    // 255): the reference loads bytes into its 32-bit register at shift bc & 31 until bc
+    // reaches n -- bytes past 32 bits wrap onto the low ones (C#'s masked int shift) --
+    // and returns the register; afterwards its state is that of n bits consumed.
+    WVF_HD uint32_t getbits_big(int n) {
+        const uint64_t p = consumed();
+        uint32_t bc = (8u - (uint32_t)(p & 7u)) & 7u;  // bits left of the byte in the register
+        uint64_t nb8 = (p + 7u) >> 3;                 // the next byte the reference loads
+        auto byte_at = [&](uint64_t i) -> uint32_t { return start + i < end ? base[start + i] : 0xFFu; };
+        uint32_t sr = bc ? byte_at(nb8 - 1u) >> (8u - bc) : 0u;
+        while ((int)bc < n) {
+            sr |= byte_at(nb8) << (bc & 31u);
+            bc += 8u;
+            nb8++;
+        }
+        int left = n;
+        while (left > 32) {
+            need(32);
+            skip(32);
+            left -= 32;
+        }
+        need(left);
+        skip(left);
+        return sr;
+    }
     // consume a run of one bits the way the reference's getbit loops do
     // (WordsUtils.cs:321, 381, 391): up to `cap` ones, plus the terminating
     // zero when fewer than `cap` were found.  cap <= 40.
@@ -670,7 +695,7 @@ WVF_HD int32_t fixup_wvx(const Fixup &f, BitReader &xb, uint32_t xlen, int32_t x
         }
         if (read) {
             if (xb.consumed() + (uint64_t)bits_to_read > 8ull * xlen) exc = 1;
-            const uint32_t data = xb.getbits_reg(bits_to_read) & f.mask;
+            const uint32_t data = (bits_to_read > 32 ? xb.getbits_big(bits_to_read) : xb.getbits_reg(bits_to_read)) & f.mask;
             x = shl32((int32_t)((uint32_t)shl32(x, bits_to_read) | data), f.sent_bits - bits_to_read);
         } else
             x = shl32(x, f.sent_bits);
@@ -872,6 +897,30 @@ WVF_HD uint32_t decode_pcm_run(PcmState &s, const BlockDesc &d, Store &out, uint
     const int nt = d.num_terms;
     const uint32_t nfr = d.nframes;
     const int och = mono_out ? 1 : 2;
+    // where a call's values land (UnpackUtils.cs:510-686 writes `wch` ints a frame from the
+    // call's buffer position; the caller advances out_nch a frame, WavPackUtils.cs:263-268):
+    // wch = 1 for MONO_FLAG without FALSE_STEREO, else 2 (FALSE_STEREO's copy, :655-664).
+    // When they differ, a 2-int block in a 1-int file shows the first n of its 2n ints
+    // (the next block of the call writes over the rest, or the call ends there; the
+    // framing raises the call's exception when 2n pass the caller's buffer), and a 1-int
+    // block in a 2-int file fills the first n of its 2n slots (the rest keep the caller's
+    // stale buffer: ST_NONDET from the framing)
+    // (a call that starts muted zero-fills MONO_FLAG ? n : 2n ints and returns before the
+    // FALSE_STEREO copy, :527-543: width och)
+    const uint32_t wch = (mono_out && !fstereo) ? 1u : 2u, sch = d.out_nch;
+    auto store = [&](uint32_t wch, uint32_t f0, uint32_t j, uint32_t n, int32_t a, int32_t b) {
+        if (wch == sch) {
+            const uint64_t o = (uint64_t)(f0 + j) * sch;
+            out.put(o, a);
+            if (wch == 2) out.put(o + 1, b);
+        } else if (wch == 2) {  // sch == 1
+            const uint32_t p = 2u * j;
+            if (p < n) out.put((uint64_t)f0 + p, a);
+            if (p + 1u < n) out.put((uint64_t)f0 + p + 1u, b);
+        } else {  // wch == 1, sch == 2
+            out.put((uint64_t)f0 * 2u + j, a);
+        }
+    };
     BitReader &bs = s.bs;
     BitReader &xb = s.xb;
     Entropy &w = s.w;
@@ -893,8 +942,7 @@ WVF_HD uint32_t decode_pcm_run(PcmState &s, const BlockDesc &d, Store &out, uint
         uint32_t n = chunk_len;
         if (n > nfr - f) n = nfr - f;
         if (s.muted) {  // mute_error set: unpack_samples zero-fills (UnpackUtils.cs:527-543)
-            for (uint32_t j = 0; j < n; j++)
-                for (int c = 0; c < och; c++) out.put((uint64_t)(f + j) * och + c, 0);
+            for (uint32_t j = 0; j < n; j++) store((uint32_t)och, f, j, n, 0, 0);
             f += n;
             chunk_len = next_call_len(d, f);
             bsp = 0;
@@ -986,16 +1034,7 @@ WVF_HD uint32_t decode_pcm_run(PcmState &s, const BlockDesc &d, Store &out, uint
                 oL = fixup_tail(fx, L);
                 oR = mono ? 0 : fixup_tail(fx, R);
             }
-            uint64_t o = (uint64_t)t * och;
-            if (mono_out) {
-                out.put(o, oL);
-            } else if (fstereo) {
-                out.put(o, oL);
-                out.put(o + 1, oL);
-            } else {
-                out.put(o, oL);
-                out.put(o + 1, oR);
-            }
+            store(wch, f, j, n, oL, fstereo ? oL : oR);
         }
         if (CHAIN && mute_at >= 0) {
             if (words_short) {
@@ -1056,16 +1095,7 @@ WVF_HD uint32_t decode_pcm_run(PcmState &s, const BlockDesc &d, Store &out, uint
                     z0 = fixup_tail(fx, 0);
                     z1 = mono ? 0 : fixup_tail(fx, 0);
                 }
-                uint64_t o = (uint64_t)(f + j) * och;
-                if (mono_out) {
-                    out.put(o, z0);
-                } else if (fstereo) {
-                    out.put(o, z0);
-                    out.put(o + 1, z0);
-                } else {
-                    out.put(o, z0);
-                    out.put(o + 1, z1);
-                }
+                store(wch, f, j, n, z0, fstereo ? z0 : z1);
             }
         }
         f += n;

@@ -881,9 +881,9 @@ class Framer {
                 out.jobs.push_back(j);
             }
             if (num_terms < 0 || num_terms > 16) status |= ST_UNSUPPORTED;
-            // FALSE_STEREO together with MONO_FLAG writes 2 ints/frame at a 1-int stride
-            if ((flags & FALSE_STEREO) && (flags & MONO_FLAG)) status |= ST_UNSUPPORTED;
-            if (int32_sent_bits > 32 || int32_sent_bits < 0) status |= ST_UNSUPPORTED;
+            // (FALSE_STEREO with MONO_FLAG: 2 ints a frame, the layout rule at the call loop)
+            // INT32 sent_bits past 32 with a wvx stream read: getbits past 32 bits
+            // (BitsUtils.cs:37-68 on a 32-bit register) -- BitReader::getbits_big
         }
         if (d.kind == KIND_PCM) {
             d.inherit = inh;
@@ -1298,9 +1298,13 @@ void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t ou
                 int64_t n = hh.block_index + hh.block_samples - F.sample_index;
                 if (n > samples) n = samples;
                 // one unpack_samples / unpack_dsd_samples call of n frames at buf_idx
-                const int bch = (hh.flags & MONO_FLAG) ? 1 : 2;  // ints each frame writes
-                if (bch != nch) {
-                    // a layout the reference writes inconsistently (and may overrun): not decoded here
+                // ints each frame writes: PCM 1 for MONO_FLAG without FALSE_STEREO
+                // (UnpackUtils.cs:655-664 copies a false-stereo frame), DSD 1 for MONO_FLAG
+                const bool pcm_blk = !(hh.flags & DSD_FLAG);
+                const int bch = ((hh.flags & MONO_FLAG) && !(pcm_blk && (hh.flags & FALSE_STEREO))) ? 1 : 2;
+                const int64_t buf_len = (int64_t)(disc_call ? 4096 : (int64_t)chunk * nch);
+                if (bch != nch && !pcm_blk) {
+                    // a DSD layout the reference writes inconsistently (and may overrun): not decoded here
                     info.nondet = 1;
                 }
                 if (cur_idx < 0) {
@@ -1320,11 +1324,14 @@ void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t ou
                         d.pre_chunk = (uint32_t)dchunk;
                         d.out_off = out_base_ints + (uint64_t)(out_frames * nch) - (uint64_t)(rem * nch);
                     }
-                    if (bch != nch) {
+                    if (bch != nch && !pcm_blk) {
                         d.kind = KIND_SKIP;
                         d.fstatus |= ST_UNSUPPORTED;
                         d.inherit = d.inherit_passes = 0;
                     }
+                    // a PCM block of 1 int a frame in a 2-int file leaves every other slot of
+                    // its calls with the caller's stale buffer (decode_pcm_run's store)
+                    if (bch != nch && pcm_blk && bch == 1) d.fstatus |= ST_NONDET;
                     if ((hh.flags & DSD_FLAG) && F.dsd.mode == 0 && (hh.flags & FALSE_STEREO)) {
                         // DsdUtils.cs:81 advances bufferStartPos, then :119-131 duplicates
                         // from past it: the reference overruns or emits caller-buffer garbage.
@@ -1337,6 +1344,9 @@ void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t ou
                     F.mark_adapted();
                 }
                 cur = &out.descs[(size_t)cur_idx];
+                // a 2-int PCM block in a 1-int file writes 2n ints from buf_idx: past the
+                // caller's buffer the C# array store throws (in this call)
+                if (pcm_blk && bch == 2 && nch == 1 && buf_idx + 2 * n > buf_len) info.exception = 1;
                 cur->nframes += (uint32_t)n;
                 F.sample_index += n;
                 buf_idx += n * nch;
