@@ -70,3 +70,28 @@ def test_c5_batch_matches_oracle(gpu_batch_cls, c5_corpus, framing, kernel):
         got = out[info.out_offset: info.out_offset + ref.frames * ref.nch]
         np.testing.assert_array_equal(got, ref.samples, err_msg=f"file {k} ({kind}, {framing}-framed)")
     b.close()
+
+
+def test_c5_batches_in_flight_match_oracle(gpu_batch_cls, c5_corpus):
+    """Two mixed batches decoded back to back: the second is issued while the first
+    runs, so it keeps all its launch groups (DSD modes 1/3, the PCM term sets) on one
+    stream (wv_api.cpp wvg_batch_decode); both must still equal the oracle."""
+    files, refs = c5_corpus
+    halves = [(0, N_FILES // 2), (N_FILES // 2, N_FILES)]
+    batches = []
+    for lo, hi in halves:
+        b = gpu_batch_cls(4096)
+        b.add_files(files[lo:hi], threads=8)
+        b.upload()
+        batches.append(b)
+    for b in batches:
+        b.decode()
+    for (lo, hi), b in zip(halves, batches):
+        out = b.download()
+        for k in range(hi - lo):
+            ref, info, r = refs[lo + k], b.infos[k], b.result(k)
+            assert not (r.status_or & WVG_ST_TIMEOUT), lo + k
+            assert r.exception == 0 and r.crc_errors == 0 and r.frames == ref.frames, lo + k
+            got = out[info.out_offset: info.out_offset + ref.frames * ref.nch]
+            np.testing.assert_array_equal(got, ref.samples, err_msg=f"file {lo + k}")
+        b.close()

@@ -8,6 +8,7 @@
 #include <cstddef>
 #include <chrono>
 #include <cstdio>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -54,7 +55,14 @@ using namespace wvg;
 // Every batch owns its streams, so batches of one context (or of several host
 // threads) run concurrently on the device; nothing synchronises the whole device.
 constexpr int kSide = kMaxTermSets + 3;  // term sets, generic PCM, DSD, DSD mode 1
-constexpr int kLanes = kSide;  // streams one decode launches on, at most (WVG_LANES: fewer)
+// streams one decode launches on, at most (WVG_LANES: fewer): its batch's stream and the
+// context's side streams.  Every stream takes one of the process's few hardware queues
+// (GPU_MAX_HW_QUEUES), and two busy streams on one queue run one after another, so the
+// side streams are few and shared by the context's batches (a decode uses them only
+// when no other batch of the context is running): with N batches in flight the process
+// holds N + 2 streams.  Three lanes give a mixed batch its latency (C5: DSD mode 3,
+// DSD mode 1 and the PCM groups side by side, 54.6 ms, as with a lane per group).
+constexpr int kLanes = 3;
 // The part of a device-framed descriptor the host reads (kind, flags, frames, the
 // call schedule, status, terms): everything up to and including term[].  The rest
 // (weights, histories, DSD, seek, sticky, .wvc, exact float) is zero or unused on
@@ -63,9 +71,13 @@ constexpr size_t kDescHead = offsetof(BlockDesc, term) + sizeof(((BlockDesc *)nu
 constexpr int SAMPLE_BUFFER_SIZE = 4096;  // Defines.cs:18, the request size WvDemo uses
 constexpr size_t kTimingPending = 64;  // timing pairs left pending before the oldest is folded
 
+struct wvg_batch;
 struct wvg_ctx {
     int device = 0;
     std::string err;
+    std::mutex mu;                   // guards `batches` and `side`
+    std::vector<wvg_batch *> batches;  // live batches (a decode counts those still running)
+    hipStream_t side[kLanes - 1] = {nullptr};  // side streams: lanes 1 .. kLanes - 1 of a decode
 };
 
 // Page-locked, grow-only host buffer: the batch's file bytes live here from
@@ -119,8 +131,7 @@ struct wvg_batch {
     wvg_ctx *ctx = nullptr;
     int chunk = 4096;
     hipStream_t stream = nullptr;          // the batch's own stream (default for decode/format/download)
-    hipStream_t side[kSide] = {nullptr};   // side streams: lanes 1 .. kLanes - 1 of a decode
-    hipEvent_t fork = nullptr, join[kSide] = {nullptr};
+    hipEvent_t fork = nullptr, join[kLanes - 1] = {nullptr};  // lanes 1 .. (the context's side streams)
     hipEvent_t done = nullptr;             // end of the last decode/format, on whatever stream it ran
     bool timing = false;                   // wvg_batch_set_timing: an event pair around every decode
     std::vector<hipEvent_t> tev;           // pending (start, end) pairs, folded into t_sum/t_cnt
@@ -160,6 +171,7 @@ struct wvg_batch {
     int force_lane = 0;                                 // WVG_FORCE_LANE=1: every PCM block on the generic kernel
     int prefer_pipe = 0;                                // WVG_PIPE=2: every PCM list on the pipelined kernel (A/B)
     int lanes = kLanes;                                 // WVG_LANES: streams per decode (A/B of the queue mapping)
+    bool lanes_env = false;                             // WVG_LANES given: no in-flight policy (wvg_batch_decode)
     int lane_mode = 1;                                  // term-set groups on the lane-per-block kernel (wvg_batch_set_kernel)
     std::vector<uint32_t> h_status, h_aux;
     int64_t bytes_in = 0, frames = 0;
@@ -245,15 +257,22 @@ wvg_ctx *wvg_open(int device) {
     return c;
 }
 
-void wvg_close(wvg_ctx *c) { delete c; }
+void wvg_close(wvg_ctx *c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    for (hipStream_t &st : c->side)
+        if (st) {
+            hipStreamSynchronize(st);
+            hipStreamDestroy(st);
+        }
+    delete c;
+}
 
 const char *wvg_last_error(wvg_ctx *c) { return c ? c->err.c_str() : "no context"; }
 
 static void free_streams(wvg_batch *b) {
-    for (int i = 0; i < kSide; i++) {
-        if (b->side[i]) hipStreamDestroy(b->side[i]);
+    for (int i = 0; i < kLanes - 1; i++)
         if (b->join[i]) hipEventDestroy(b->join[i]);
-    }
     if (b->fork) hipEventDestroy(b->fork);
     if (b->done) hipEventDestroy(b->done);
     if (b->stream) hipStreamDestroy(b->stream);
@@ -289,7 +308,10 @@ wvg_batch *wvg_batch_new(wvg_ctx *c, int chunk_frames) {
     // the decorr/entropy values of each block are parsed on the device (wv_meta_parse);
     // WVG_HOST_META=1 keeps them on the host framing (A/B comparisons)
     const char *ln = getenv("WVG_LANES");
-    if (ln && atoi(ln) >= 1) b->lanes = atoi(ln) < kLanes ? atoi(ln) : kLanes;
+    if (ln && atoi(ln) >= 1) {
+        b->lanes = atoi(ln) < kLanes ? atoi(ln) : kLanes;
+        b->lanes_env = true;
+    }
     const char *lk = getenv("WVG_LANE_KERNEL");
     b->lane_mode = lk ? atoi(lk) : 1;  // (default: the lane kernels, wvg_batch_set_kernel)
     const char *rm = getenv("WVG_DFRAME_RANK_MIN");
@@ -301,6 +323,10 @@ wvg_batch *wvg_batch_new(wvg_ctx *c, int chunk_frames) {
         const size_t bytes = sizeof(uint32_t) * 16u * kLaneDbgWaves * kMaxTermSets;
         if (hipMalloc(&b->d_lane_dbg, bytes) != hipSuccess || hipMemset(b->d_lane_dbg, 0, bytes) != hipSuccess)
             b->d_lane_dbg = nullptr;
+    }
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        c->batches.push_back(b);
     }
     return b;
 }
@@ -410,6 +436,11 @@ static hipError_t blob_push(wvg_batch *b, size_t upto = (size_t)-1) {
 
 void wvg_batch_free(wvg_batch *b) {
     if (!b) return;
+    {
+        std::lock_guard<std::mutex> g(b->ctx->mu);
+        auto &v = b->ctx->batches;
+        v.erase(std::remove(v.begin(), v.end(), b), v.end());
+    }
     hipSetDevice(b->ctx->device);
     quiesce(b);
     free_dev(b);
@@ -1068,6 +1099,14 @@ static hipError_t fold_timing(wvg_batch *b, int pairs) {
     return hipSuccess;
 }
 
+// another batch of b's context with a decode or format still running
+static bool others_running(wvg_batch *b) {
+    std::lock_guard<std::mutex> g(b->ctx->mu);
+    for (wvg_batch *o : b->ctx->batches)
+        if (o != b && o->done && hipEventQuery(o->done) == hipErrorNotReady) return true;
+    return false;
+}
+
 int wvg_batch_decode(wvg_batch *b, void *stream) {
     if (!b || !b->uploaded) return WVG_ERR_ARG;
     wvg_ctx *c = b->ctx;
@@ -1100,16 +1139,25 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
     for (int t = 0; t < kMaxTermSets; t++)
         if (!b->ts_list[t].empty()) used[n++] = t;
     int lane_of[kSide];
-    const int nlanes = b->lanes;
+    // With other batches of this context still running, a decode keeps its groups
+    // on its own stream (in order on it; the batches in flight fill the device);
+    // alone, it spreads them over the context's side streams for its own latency
+    // (kLanes).  C5 at 20 in flight: 10,600 Mframes/s on one stream per batch, 6,500
+    // on one per launch group (profiles/r04_c5_streams.txt).
+    int nlanes = b->lanes;
+    if (!b->lanes_env && nlanes > 1 && others_running(b)) nlanes = 1;
     const int nl = n < nlanes ? n : nlanes;
     if (n <= nlanes) {
         for (int i = 0; i < n; i++) lane_of[used[i]] = i;
     } else {
         int64_t load[kSide] = {0};
         int first = 0;  // lanes before it are reserved for the DSD groups
+        // (one lane left for the PCM groups; with a single lane everything is on it)
         for (int i = 0; i < n; i++)
-            if (used[i] == kDsd || used[i] == kDsd1) lane_of[used[i]] = first++;
-        if (first >= nl) first = 0;
+            if (used[i] == kDsd || used[i] == kDsd1) {
+                lane_of[used[i]] = first < nl - 1 ? first : 0;
+                if (first < nl - 1) first++;
+            }
         int pcm[kSide], np = 0;
         for (int i = 0; i < n; i++)
             if (used[i] != kDsd && used[i] != kDsd1) pcm[np++] = used[i];
@@ -1122,13 +1170,16 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
             load[best] += b->gframes[pcm[i]];
         }
     }
+    hipStream_t side[kLanes - 1] = {nullptr};
     for (int l = 1; l < nl; l++) {
-        if (!b->side[l - 1]) {
-            HIPCHK(c, hipStreamCreateWithFlags(&b->side[l - 1], hipStreamNonBlocking));
-            HIPCHK(c, hipEventCreateWithFlags(&b->join[l - 1], hipEventDisableTiming));
+        {
+            std::lock_guard<std::mutex> g(c->mu);
+            if (!c->side[l - 1]) HIPCHK(c, hipStreamCreateWithFlags(&c->side[l - 1], hipStreamNonBlocking));
+            side[l - 1] = c->side[l - 1];
         }
+        if (!b->join[l - 1]) HIPCHK(c, hipEventCreateWithFlags(&b->join[l - 1], hipEventDisableTiming));
     }
-    auto lane = [&](int l) -> hipStream_t { return l == 0 ? s : b->side[l - 1]; };
+    auto lane = [&](int l) -> hipStream_t { return l == 0 ? s : side[l - 1]; };
     auto slot = [&](int g) -> hipStream_t {
         for (int i = 0; i < n; i++)
             if (used[i] == g) return lane(lane_of[g]);
