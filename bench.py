@@ -411,6 +411,14 @@ def run_rank(args) -> None:
         other = {"kernel": "two_wave", "batches_in_flight": nb, "value": None, "dt": dt_o}
         for bb in batches[:nb]:
             bb.set_kernel(args.kernel)
+    # one batch alone on the kernel the library's default (WVG_KERNEL_AUTO) picks for a
+    # caller that decodes one batch at a time: the two-wave kernel (groups <= 2,048 blocks)
+    auto_ms = None
+    if not args.timed_only:
+        b.set_kernel("two_wave")
+        b.sync()
+        auto_ms = b.time(3)
+        b.set_kernel(args.kernel)
     # the timed decodes were real: every copy's output, CRCs and kernel routing
     ver = verify(batches, files, pcm)
     dt = _reduce(pg, t1 - t0, "max")
@@ -432,6 +440,7 @@ def run_rank(args) -> None:
     # a decode server's request on a warm batch: reset, frame the files on the host,
     # upload (page-locked), decode, download into page-locked memory; median of 3
     be = batches[-1]
+    be.set_kernel("two_wave")  # (one request at a time: WVG_KERNEL_AUTO's choice for such a caller)
     t_runs = []
     for _ in range(3):
         t_e2e = time.perf_counter()
@@ -455,6 +464,7 @@ def run_rank(args) -> None:
         t_runs.append(time.perf_counter() - t_d)
     t_e2e_dev = float(np.median(t_runs))
     dev_framed = be.framing_stats()
+    be.set_kernel(args.kernel)
     # the same request stream served by one host thread per batch copy, so one
     # batch's framing, upload, decode and download overlap the others' (ctypes
     # drops the GIL inside the library; each batch has its own stream)
@@ -542,12 +552,15 @@ def run_rank(args) -> None:
                         "WVG_KERNEL_TWO_WAVE) at its best depth, 3 batches in flight"},
             "hbm_gbs": round(node_gbs, 2),
             "launch_ms": {"in_flight_mean": round(kernel_ms, 4), "alone": round(solo_ms, 4),
+                          "alone_api_default": None if auto_ms is None else round(auto_ms, 4),
                           "host_issue_all_steps": round((t_issue - t0) * 1e3, 3),
                           "host_sync_all_steps": round((t1 - t_issue) * 1e3, 3),
                           "what": "device time of one decode launch (hipEvents on its stream): mean over the timed "
-                                  "region's launches, and with no other batch in flight"},
+                                  "region's launches, and with no other batch in flight (alone_api_default: the "
+                                  "kernel the library's default WVG_KERNEL_AUTO picks for a caller decoding one "
+                                  "batch at a time, the two-wave kernel)"},
             "pcie_inclusive": {"value": round(e2e, 2), "unit": "Msamples/s", "ms": round(t_e2e * 1e3, 3),
-                               "what": "warm batch: host framing + upload of the compressed batch (page-locked) + "
+                               "what": "warm batch on the two-wave kernel (WVG_KERNEL_AUTO's choice one request at a time): host framing + upload of the compressed batch (page-locked) + "
                                        "decode + download of int32 PCM into page-locked memory, rank 0, median of 3",
                                "device_framing": {"value": round(frames_rank / t_e2e_dev / 1e6, 2),
                                                   "ms": round(t_e2e_dev * 1e3, 3),

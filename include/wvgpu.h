@@ -174,17 +174,24 @@ int wvg_batch_decode(wvg_batch *b, void *stream);
 int wvg_batch_sync(wvg_batch *b);
 /* Which kernel decodes the batch's lossless PCM blocks whose decorr list has a
  * compile-time specialisation (no reference counterpart: a scheduling choice).
- * WVG_KERNEL_LANE (the default): one lane per block, 64 blocks per workgroup --
- * one SIMD issue slot moves 64 blocks, so batches in flight decode many times more
- * per second -- for lossless PCM blocks, hybrid stereo blocks of WavPack's default
- * list and DSD mode-3 blocks; blocks a lane cannot follow exactly are decoded again
- * by the two-wave kernel (the pipelined kernel for WavPack's 16-term 'high' list,
- * the wave-per-block kernel for DSD) within the same decode.  WVG_KERNEL_TWO_WAVE:
- * one workgroup per block (a scalar parser wave and a reconstruction wave), the
- * lowest latency for one small batch alone.  Results are identical either way
- * (WVG_LANE_KERNEL=0 in the environment selects the two-wave kernel for new batches). */
+ * WVG_KERNEL_LANE: one lane per block, 64 blocks per workgroup -- one SIMD issue
+ * slot moves 64 blocks, so batches in flight decode many times more per second --
+ * for lossless PCM blocks, hybrid stereo blocks of WavPack's default list and DSD
+ * mode-3 blocks; blocks a lane cannot follow exactly are decoded again by the
+ * two-wave kernel (the pipelined kernel for WavPack's 16-term 'high' list, the
+ * wave-per-block kernel for DSD) within the same decode.  WVG_KERNEL_TWO_WAVE: one
+ * workgroup per block (a scalar parser wave and a reconstruction wave; one wave
+ * per DSD block), the lowest latency for a batch alone.  WVG_KERNEL_AUTO (the
+ * default): the lane kernels once the context has had a decode issued while another
+ * of its batches was running; until then (one batch at a time) the two-wave /
+ * wave-per-block kernels for launch groups of at most 2,048 blocks (larger ones on
+ * lanes).  A decode issued while other batches
+ * run also keeps all its launch groups on its own stream (streams share the
+ * process's few hardware queues).  Results are identical in every mode
+ * (WVG_LANE_KERNEL=0/1 in the environment fixes the kernel for new batches). */
 #define WVG_KERNEL_TWO_WAVE 0
 #define WVG_KERNEL_LANE 1
+#define WVG_KERNEL_AUTO 2
 int wvg_batch_set_kernel(wvg_batch *b, int kernel);
 void *wvg_batch_stream(wvg_batch *b);  /* the batch's own hipStream_t */
 /* Device timing of every following decode (an event pair around each launch, on its

@@ -34,8 +34,7 @@ from wavpackdecoder_amd.api import DecodeBatch  # noqa: E402
 def run(name, files, pcm=None, iters=5, fmt=False):
     t0 = time.perf_counter()
     b = DecodeBatch(4096)
-    if KERNEL != "two_wave":
-        b.set_kernel(KERNEL)
+    b.set_kernel(KERNEL)
     b.add_files(files)  # host framing on worker threads
     t_frame = time.perf_counter() - t0
     b.upload()
@@ -76,8 +75,7 @@ def run(name, files, pcm=None, iters=5, fmt=False):
         copies = [b]
         for _ in range(INFLIGHT - 1):
             c = DecodeBatch(4096)
-            if KERNEL != "two_wave":
-                c.set_kernel(KERNEL)
+            c.set_kernel(KERNEL)
             c.add_files(files)
             c.upload()
             copies.append(c)
@@ -154,7 +152,7 @@ def main():
     ap.add_argument("--dsd-files", type=int, default=64, help="files per DSD mode batch (one block each)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="also time the oracle on this many host threads")
     ap.add_argument("--inflight", type=int, default=1, help="also time this many copies of each batch in flight")
-    ap.add_argument("--kernel", choices=("two_wave", "lane"), default="two_wave",
+    ap.add_argument("--kernel", choices=("two_wave", "lane", "auto"), default="two_wave",
                     help="PCM kernel for the term-set groups (wvg_batch_set_kernel)")
     a = ap.parse_args()
     global CPU_THREADS, INFLIGHT, KERNEL

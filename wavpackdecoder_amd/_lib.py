@@ -29,6 +29,7 @@ WVG_ERR_TIMEOUT = -5
 WVG_ERR_EXCEPTION = -6
 WVG_KERNEL_TWO_WAVE = 0
 WVG_KERNEL_LANE = 1
+WVG_KERNEL_AUTO = 2
 
 
 class WvgFileInfo(ctypes.Structure):

@@ -176,10 +176,13 @@ class DecodeBatch:
         self._check(self._L.wvg_batch_sync(self._b))
 
     def set_kernel(self, kernel: str):
-        """'lane' (the default: one lane per block, the most blocks per second with
-        batches in flight) or 'two_wave' (one workgroup per block: lowest latency for one
-        small batch alone) -- wvg_batch_set_kernel; results are identical either way."""
-        k = {"two_wave": _L.WVG_KERNEL_TWO_WAVE, "lane": _L.WVG_KERNEL_LANE}[kernel]
+        """'auto' (the default: the lane kernels once the context has had batches in
+        flight together, until then one workgroup per block for groups of up to 2,048
+        blocks), 'lane' (one lane per
+        block: the most blocks per second with batches in flight) or 'two_wave' (one
+        workgroup per block: lowest latency for a batch alone) -- wvg_batch_set_kernel;
+        results are identical in every mode."""
+        k = {"two_wave": _L.WVG_KERNEL_TWO_WAVE, "lane": _L.WVG_KERNEL_LANE, "auto": _L.WVG_KERNEL_AUTO}[kernel]
         self._check(self._L.wvg_batch_set_kernel(self._b, k))
 
     def set_timing(self, on: bool = True):

@@ -63,6 +63,7 @@ constexpr int kSide = kMaxTermSets + 3;  // term sets, generic PCM, DSD, DSD mod
 // holds N + 2 streams.  Three lanes give a mixed batch its latency (C5: DSD mode 3,
 // DSD mode 1 and the PCM groups side by side, 54.6 ms, as with a lane per group).
 constexpr int kLanes = 3;
+constexpr size_t kAutoLaneMin = 2048;  // WVG_KERNEL_AUTO: larger groups decode on lanes even alone
 // The part of a device-framed descriptor the host reads (kind, flags, frames, the
 // call schedule, status, terms): everything up to and including term[].  The rest
 // (weights, histories, DSD, seek, sticky, .wvc, exact float) is zero or unused on
@@ -78,6 +79,7 @@ struct wvg_ctx {
     std::mutex mu;                   // guards `batches` and `side`
     std::vector<wvg_batch *> batches;  // live batches (a decode counts those still running)
     hipStream_t side[kLanes - 1] = {nullptr};  // side streams: lanes 1 .. kLanes - 1 of a decode
+    std::atomic<bool> concurrent{false};  // a decode was once issued while another batch ran (WVG_KERNEL_AUTO)
 };
 
 // Page-locked, grow-only host buffer: the batch's file bytes live here from
@@ -173,6 +175,8 @@ struct wvg_batch {
     int lanes = kLanes;                                 // WVG_LANES: streams per decode (A/B of the queue mapping)
     bool lanes_env = false;                             // WVG_LANES given: no in-flight policy (wvg_batch_decode)
     int lane_mode = 1;                                  // term-set groups on the lane-per-block kernel (wvg_batch_set_kernel)
+    bool kernel_auto = true;                            // WVG_KERNEL_AUTO: lane_mode chosen per decode and group
+    bool log_decodes = false;                           // WVG_DECODE_LOG=1: each decode's streams and kernels on stderr
     std::vector<uint32_t> h_status, h_aux;
     int64_t bytes_in = 0, frames = 0;
     // format epilogue: per-file byte image of WavpackFormatSamples
@@ -313,7 +317,10 @@ wvg_batch *wvg_batch_new(wvg_ctx *c, int chunk_frames) {
         b->lanes_env = true;
     }
     const char *lk = getenv("WVG_LANE_KERNEL");
-    b->lane_mode = lk ? atoi(lk) : 1;  // (default: the lane kernels, wvg_batch_set_kernel)
+    b->lane_mode = lk ? atoi(lk) : 1;  // (default: WVG_KERNEL_AUTO, wvg_batch_set_kernel)
+    b->kernel_auto = !lk;
+    const char *dl = getenv("WVG_DECODE_LOG");
+    b->log_decodes = dl && dl[0] == '1';
     const char *rm = getenv("WVG_DFRAME_RANK_MIN");
     if (rm) b->rank_min = atoll(rm);
     const char *hm = getenv("WVG_HOST_META");
@@ -1144,8 +1151,26 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
     // alone, it spreads them over the context's side streams for its own latency
     // (kLanes).  C5 at 20 in flight: 10,600 Mframes/s on one stream per batch, 6,500
     // on one per launch group (profiles/r04_c5_streams.txt).
+    const bool running = (!b->lanes_env || b->kernel_auto) && others_running(b);
     int nlanes = b->lanes;
-    if (!b->lanes_env && nlanes > 1 && others_running(b)) nlanes = 1;
+    if (!b->lanes_env && nlanes > 1 && running) nlanes = 1;
+    // WVG_KERNEL_AUTO: in a context that has had batches in flight together, the lane
+    // kernels (throughput); in one that decodes a batch at a time, a group of at most
+    // kAutoLaneMin blocks on the one-workgroup / one-wave-per-block kernels, whose chains
+    // run faster than a lane's (C2 alone: 6.5 vs 7.5 ms; C4 15.4 vs 24.4; DSD mode 3 34 vs
+    // 56), larger ones on lanes (C3's 4,096 blocks: 24.8 vs 37.7 ms).  (Not per decode: a
+    // lane workgroup needs a whole CU's LDS, and a two-wave decode among lane decodes
+    // leaves CUs partly taken -- C4 at 20 in flight fell from 16,000 to 8,200 Mframes/s
+    // when the first decode of each round ran alone on the two-wave kernel.)
+    if (running) c->concurrent = true;
+    const bool lanes_now = c->concurrent;
+    auto mode_of = [&](size_t nblocks) -> int {
+        if (!b->kernel_auto) return b->lane_mode;
+        return (lanes_now || nblocks > kAutoLaneMin) ? 1 : 0;
+    };
+    if (b->log_decodes)
+        fprintf(stderr, "wvg decode %p: groups %d, others running %d, streams %d, auto %d\n", (void *)b, n,
+                (int)running, nlanes < n ? nlanes : n, (int)b->kernel_auto);
     const int nl = n < nlanes ? n : nlanes;
     if (n <= nlanes) {
         for (int i = 0; i < n; i++) lane_of[used[i]] = i;
@@ -1209,14 +1234,16 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
     };
     HIPCHK(c, launch_decode(b->d_descs, b->d_pcml, (uint32_t)b->pcm_list.size(), b->d_dsd, (uint32_t)b->dsd_list.size(),
                             b->dsd_fast_lo, b->dsd_fast_n, b->d_blob, b->d_tables, b->d_out, b->d_status, b->d_mute,
-                            slot(kPcm), slot(kDsd), slot(kDsd1), b->lane_mode, b->dsd_high_lo, b->dsd_high_mono));
+                            slot(kPcm), slot(kDsd), slot(kDsd1), mode_of(b->dsd_list.size() - b->dsd_high_lo),
+                            b->dsd_high_lo, b->dsd_high_mono));
     HIPCHK(c, mark(kDsd));
     HIPCHK(c, mark(kDsd1));
     HIPCHK(c, mark(kPcm));
     for (int t = 0; t < kMaxTermSets; t++)
         if (!b->ts_list[t].empty()) {
             HIPCHK(c, launch_2wave(t, b->d_descs, b->d_ts[t], (uint32_t)b->ts_list[t].size(), b->d_blob, b->d_out,
-                                   b->d_status, b->d_mute, slot(t), b->lane_mode, b->d_ts[t] + b->ts_list[t].size(),
+                                   b->d_status, b->d_mute, slot(t), mode_of(b->ts_list[t].size()),
+                                   b->d_ts[t] + b->ts_list[t].size(),
                                    (uint32_t)b->ts_lane[t].size(),
                                    b->d_lane_dbg && b->ts_lane[t].size() <= 64u * kLaneDbgWaves
                                        ? b->d_lane_dbg + (size_t)t * kLaneDbgWaves * 16u
@@ -1245,7 +1272,13 @@ int wvg_batch_sync(wvg_batch *b) {
 void *wvg_batch_stream(wvg_batch *b) { return b ? (void *)b->stream : nullptr; }
 
 int wvg_batch_set_kernel(wvg_batch *b, int kernel) {
-    if (!b || (kernel != WVG_KERNEL_TWO_WAVE && kernel != WVG_KERNEL_LANE)) return WVG_ERR_ARG;
+    if (!b || (kernel != WVG_KERNEL_TWO_WAVE && kernel != WVG_KERNEL_LANE && kernel != WVG_KERNEL_AUTO))
+        return WVG_ERR_ARG;
+    if (kernel == WVG_KERNEL_AUTO) {
+        b->kernel_auto = true;
+        return WVG_OK;
+    }
+    b->kernel_auto = false;
     b->lane_mode = kernel == WVG_KERNEL_LANE ? 1 : 0;
     return WVG_OK;
 }

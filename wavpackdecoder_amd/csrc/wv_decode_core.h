@@ -117,6 +117,24 @@ struct BitReader {
     WVF_HD uint64_t consumed() const { return (pos - start) * 8 - (uint64_t)nb; }
     // keep at least 33 valid bits in the window
     WVF_HD void refill() {
+#if defined(__HIP_DEVICE_COMPILE__)
+        // the device: the 8 bytes from pos out of three aligned dwords read together
+        // through the scalar cache (a decode here is wave-uniform) instead of one
+        // dependent byte load per byte; the byte loop only within 12 bytes of the end
+        if (nb <= 56 && pos + 12u <= end) {
+            typedef const __attribute__((address_space(4))) uint32_t *cdw;
+            const cdw w = (cdw)(base + (pos & ~(uint64_t)3));  // (base: the blob, 16-B aligned)
+            const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+            const uint32_t sh = (uint32_t)(pos & 3u) * 8u;
+            uint64_t v = ((uint64_t)w1 << 32) | w0;
+            if (sh) v = (v >> sh) | ((uint64_t)w2 << (64u - sh));
+            const int k = (64 - nb) >> 3;  // bytes taken: nb ends in 57..64, as the byte loop's
+            win |= (k >= 8 ? v : (v & ((1ull << (8 * k)) - 1ull))) << nb;
+            nb += 8 * k;
+            pos += (uint64_t)k;
+            return;
+        }
+#endif
         while (nb <= 56) {
             uint64_t b = pos < end ? (uint64_t)base[pos] : 0xFFull;
             win |= b << nb;
