@@ -33,30 +33,33 @@ constexpr int32_t kUp = 0x010000FE, kDown = 0x00010000;  // DsdUtils.cs UP / DOW
 __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
 
 // per-lane payload window: byte bp of the payload in bits 63..56 of win, `avail`
-// bytes valid, nxt = the dword after them (loaded one refill ahead)
+// bytes valid, nxt / nxt2 = the two dwords after them (loaded two refills ahead: a
+// refill comes every ~600 cycles, a global load can take longer)
 struct Win {
     const uint32_t *w;
     uint64_t win;
     int32_t avail;
-    uint32_t ni, nxt;
+    uint32_t ni, nxt, nxt2;
     __device__ __forceinline__ void init(const uint8_t *p) {
         const uint32_t sh = (uint32_t)((uintptr_t)p & 3u);
         w = (const uint32_t *)(p - sh);
         win = (uint64_t)bswap(w[0]) << (32u + 8u * sh);
         avail = 4 - (int32_t)sh;
         nxt = w[1];
-        ni = 2;
+        nxt2 = w[2];
+        ni = 3;
         refill();
     }
     // avail <= 4: four more bytes below the valid ones (branch-free: a lane with
-    // more keeps its window and its read-ahead dword)
+    // more keeps its window and its read-ahead dwords)
     __device__ __forceinline__ void refill() {
         const bool m = avail <= 4;
         const uint32_t sh = (uint32_t)(32 - 8 * (m ? avail : 0)) & 63u;
         win |= m ? (uint64_t)bswap(nxt) << sh : 0ull;
         avail += m ? 4 : 0;
         const uint32_t nn = w[ni];  // (read every time: the address is always inside the blob's tail)
-        nxt = m ? nn : nxt;
+        nxt = m ? nxt2 : nxt;
+        nxt2 = m ? nn : nxt2;
         ni += m ? 1u : 0u;
     }
 };
@@ -70,9 +73,11 @@ __device__ __forceinline__ int32_t decide(uint32_t &low, uint32_t &high, uint32_
     const bool zero = value <= split;
     high = zero ? split : high;
     low = zero ? low : split + 1u;
-    uint32_t n = (uint32_t)__builtin_clz((high ^ low) | 1u) >> 3;  // 0..3, 4 below: a zero xor
-    n = ((high ^ low) == 0u) ? 4u : n;
-    n = min(n, left);
+    // bytes to shift out: leading zero bytes of high ^ low (v_ffbh_u32 of 0 is ~0: 4 after
+    // the cap), at most the bytes left
+    uint32_t lz;
+    asm("v_ffbh_u32 %0, %1" : "=v"(lz) : "v"(high ^ low));
+    const uint32_t n = min(min(lz >> 3, 4u), left);
     const uint32_t s = n << 3;  // 0..32
     value = (uint32_t)(((((uint64_t)value << 32) | (src.win >> 32)) << s) >> 32);
     high = (uint32_t)(((((uint64_t)high << 32) | 0xFFFFFFFFull) << s) >> 32);
