@@ -62,9 +62,8 @@ struct DevStoreWave {
 // blocks in order, the PcmState of one handed to the next; a block that raises
 // the reference's exception ends the chain (the reference stops there).
 __device__ __noinline__ void decode_chain(const BlockDesc *__restrict__ descs, uint32_t head, const uint8_t *blob,
-                                          int32_t *out, uint32_t *status, uint32_t *aux) {
+                                          int32_t *out, uint32_t *status, uint32_t *aux, PcmState &s) {
     const bool lead = threadIdx.x == 0;
-    PcmState s;
     const uint32_t n = descs[head].chain_len;
     for (uint32_t k = 0; k < n; k++) {
         const uint32_t bi = head + k;
@@ -87,16 +86,19 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_pcm_wave(const BlockD
                                                                     int32_t *__restrict__ out,
                                                                     uint32_t *__restrict__ status,
                                                                     uint32_t *__restrict__ aux) {
+    // the decode state in LDS: every lane of the (wave-uniform) decode reads and writes
+    // the same values; in registers its run-time indexed pass rings went to scratch
+    __shared__ PcmState ps;
     const uint32_t bi = list[blockIdx.x];
     const BlockDesc &d = descs[bi];
     if (d.chain_len >= 2) {
-        decode_chain(descs, bi, blob, out, status, aux);
+        decode_chain(descs, bi, blob, out, status, aux, ps);
         return;
     }
     const bool lead = threadIdx.x == 0;
     DevStoreWave st{out + d.out_off, (uint64_t)d.pre_end * d.out_nch, lead};
     uint32_t exc = aux[bi];
-    const uint32_t s = d.fstatus | decode_pcm_block(d, blob, st, &exc);
+    const uint32_t s = d.fstatus | decode_pcm_block_in(ps, d, blob, st, &exc);
     if (lead) {
         status[bi] = s;
         aux[bi] = exc;

@@ -1134,12 +1134,19 @@ WVF_HD uint32_t decode_pcm_run(PcmState &s, const BlockDesc &d, Store &out, uint
     return status;
 }
 
-// one block from its descriptor alone
+// one block from its descriptor alone, its state in `s` (the device kernel passes a
+// wave's LDS copy: the pass rings and weights are indexed by run-time pass and slot
+// numbers, which in registers would live in scratch memory)
+template <class Store>
+WVF_HD uint32_t decode_pcm_block_in(PcmState &s, const BlockDesc &d, const uint8_t *blob, Store &out,
+                                    uint32_t *exc_frame = nullptr) {
+    pcm_state_load(s, d, blob);
+    return decode_pcm_run<Store, false>(s, d, out, exc_frame);
+}
 template <class Store>
 WVF_HD uint32_t decode_pcm_block(const BlockDesc &d, const uint8_t *blob, Store &out, uint32_t *exc_frame = nullptr) {
     PcmState s;
-    pcm_state_load(s, d, blob);
-    return decode_pcm_run<Store, false>(s, d, out, exc_frame);
+    return decode_pcm_block_in(s, d, blob, out, exc_frame);
 }
 
 // ---------------------------------------------------------------------------
