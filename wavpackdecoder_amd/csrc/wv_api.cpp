@@ -1151,7 +1151,10 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
     // alone, it spreads them over the context's side streams for its own latency
     // (kLanes).  C5 at 20 in flight: 10,600 Mframes/s on one stream per batch, 6,500
     // on one per launch group (profiles/r04_c5_streams.txt).
-    const bool running = (!b->lanes_env || b->kernel_auto) && others_running(b);
+    // (asked only when it decides something: a multi-group decode's streams, or the
+    // default kernel choice before the context has seen batches overlap)
+    const bool ask = (!b->lanes_env && b->lanes > 1 && n > 1) || (b->kernel_auto && !c->concurrent);
+    const bool running = ask && others_running(b);
     int nlanes = b->lanes;
     if (!b->lanes_env && nlanes > 1 && running) nlanes = 1;
     // WVG_KERNEL_AUTO: in a context that has had batches in flight together, the lane
