@@ -18,11 +18,13 @@ value  : frames decoded by all ranks / max-over-ranks wall time of the K steps.
          with its own device buffers and HIP stream, so consecutive steps overlap
          on the device as in a decode server with several batches in flight:
          every step is still one complete decode of the whole batch into its own
-         output.  The default kernel is the lane-per-block one (--kernel lane,
-         wv_lane.h): a block is one serial entropy chain, one lane decodes it, a
-         batch of 1,024 blocks is 8 workgroups of 4 waves (two parser/reconstruction
-         pairs of 64 blocks each, one workgroup per CU), so the chip holds many
-         batches at once -- the default keeps min(K, 20) in flight.  --kernel two_wave is the
+         output.  The measured kernel is the lane-per-block one (--kernel lane,
+         wv_lane.h; the library's default WVG_KERNEL_AUTO picks it once batches
+         overlap): a block is one serial entropy chain, one lane decodes it, a
+         batch of 1,024 blocks is 9 workgroups of 4 waves (two parser/reconstruction
+         pairs of 64 lane slots each, the lane order's gap slots included: SQ_WAVES
+         36; one workgroup per CU), so the chip holds many batches at once -- the
+         default keeps min(K, 20) in flight.  --kernel two_wave is the
          one-workgroup-per-block kernel (lowest latency for a batch alone; best at
          3 in flight), measured beside it in "two_wave".  The line also reports
          the same K steps run one batch at a time ("value_one_batch_at_a_time")
