@@ -470,7 +470,7 @@ def run_rank(args) -> None:
     # the same request stream served by one host thread per batch copy, so one
     # batch's framing, upload, decode and download overlap the others' (ctypes
     # drops the GIL inside the library; each batch has its own stream)
-    e2e_pipe = e2e_pcm = None
+    e2e_pipe = e2e_pcm = e2e_pcm2 = None
     if len(batches) > 1:
         import threading
         rounds = 4
@@ -504,6 +504,36 @@ def run_rank(args) -> None:
 
         e2e_pipe = pipelined(False)
         e2e_pcm = pipelined(True)
+
+        # the same 4 request threads, each with two batches: a request's framing, upload
+        # and decode are issued before the previous request's format + PCM download, so
+        # the host side of one overlaps the device side of the other
+        def serve2(b0, b1, rounds=rounds):
+            bb = (b0, b1)
+
+            def start(x):
+                x.reset()
+                x.add_files(files)
+                x.upload()
+                x.decode()
+            start(bb[0])
+            for k in range(rounds):
+                if k + 1 < rounds:
+                    start(bb[(k + 1) % 2])
+                bb[k % 2].format()
+                bb[k % 2].download_pcm(pinned=True)
+
+        if len(batches) >= 8:
+            pairs = [(batches[2 * i], batches[2 * i + 1]) for i in range(4)]
+            for b0, b1 in pairs:  # (page-locked landing buffers of the second batches: untimed)
+                serve2(b0, b1, 2)
+            th = [threading.Thread(target=serve2, args=p) for p in pairs]
+            t_p = time.perf_counter()
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            e2e_pcm2 = frames_rank * rounds * len(pairs) / (time.perf_counter() - t_p) / 1e6
 
     if kernel_ms <= 0:  # (timing off: the launch time of one batch alone stands in)
         kernel_ms = solo_ms if solo_ms > 0 else b.time(3)
@@ -571,10 +601,13 @@ def run_rank(args) -> None:
                                                           "on the GPU (wvg_batch_add_files_device)"},
                                "pipelined": None if e2e_pipe is None else round(e2e_pipe, 2),
                                "pipelined_pcm": None if e2e_pcm is None else round(e2e_pcm, 2),
+                               "pipelined_pcm_2buf": None if e2e_pcm2 is None else round(e2e_pcm2, 2),
                                "pipelined_what": "the same request served by one host thread per batch copy (at most 4) "
                                                  "(4 requests each), framing/copies/decode of different batches "
                                                  "overlapping; _pcm: formatted on the device (WavpackFormatSamples) "
-                                                 "and downloaded as PCM bytes"},
+                                                 "and downloaded as PCM bytes; _pcm_2buf: the 4 threads with two "
+                                                 "batches each, the next request framed, uploaded and decoding "
+                                                 "before the current one's PCM download"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": None if traffic is None else int(traffic),
