@@ -30,10 +30,13 @@ value  : frames decoded by all ranks / max-over-ranks wall time of the K steps.
          the same K steps run one batch at a time ("value_one_batch_at_a_time")
          and the per-launch device times (launch_ms).
 
-After the timed region every in-flight copy is downloaded and checked (C2): its
-int32 output must equal the generator's PCM bit for bit, every block's CRC must
-match (crc_errors == 0), and no block may have been handed back by the lane
-kernel to its fallback (WVG_ST_REDONE; reported as "redo_blocks").
+Before the timed region every copy's output is overwritten with 0x7F bytes and its
+block statuses marked unwritten (wvg_batch_poison); right after it every in-flight
+copy -- whose last decode is a timed one -- is downloaded and checked (C2): its int32
+output must equal the generator's PCM bit for bit, every block's status must have
+been stored by a decode, every block's CRC must match (crc_errors == 0), and the
+blocks handed back by the lane kernel to its fallback (WVG_ST_REDONE) are counted
+("redo_blocks").
 
 Also printed in the same JSON line:
   roofline     : algorithmic bytes per launch (compressed bytes in + int32
@@ -197,18 +200,20 @@ def verify(batches, files, pcm) -> dict:
     (WavPackUtils.cs:273-275), and no block went through the lane kernel's
     fallback (WVG_ST_REDONE).  Raises on any failure."""
     from wavpackdecoder_amd import _lib
-    crc = redo = blocks = 0
+    crc = redo = blocks = unwritten = 0
     for bb in batches:
         out = bb.download()
         if pcm is not None:
             assert np.array_equal(out, pcm.reshape(-1)), "decoded PCM differs from the generator's"
-        crc += sum(bb.result(i).crc_errors for i in range(len(files)) if bb.infos[i].open_ok)
         st = bb.block_status()
+        unwritten += int(np.count_nonzero(st & _lib.WVG_ST_UNWRITTEN))
+        crc += sum(bb.result(i).crc_errors for i in range(len(files)) if bb.infos[i].open_ok)
         redo += int(np.count_nonzero(st & _lib.WVG_ST_REDONE))
         blocks += int(st.size)
+    assert unwritten == 0, f"{unwritten} blocks whose status no decode stored"
     assert crc == 0, f"{crc} CRC errors in a synthetic corpus"
     return {"copies": len(batches), "blocks": blocks, "crc_errors": crc, "redo_blocks": redo,
-            "pcm_equal": pcm is not None}
+            "unwritten_blocks": unwritten, "pcm_equal": pcm is not None}
 
 
 # ---------------------------------------------------------------------------
@@ -362,6 +367,11 @@ def run_rank(args) -> None:
         bb.sync()
     if args.check:
         verify(batches, files, pcm)
+    # every copy's output and block statuses are overwritten (0x7F bytes, WVG_ST_UNWRITTEN)
+    # after the untimed decodes, so the check right after the timed region sees only what
+    # the timed launches wrote
+    for bb in batches:
+        bb.poison(0x7F)
 
     # device time of every launch in the timed region (an event pair around each
     # decode on the stream it runs on)
@@ -378,6 +388,10 @@ def run_rank(args) -> None:
         bb.sync()
     t1 = time.perf_counter()
     _barrier(pg)
+    # the timed decodes were real: every copy's output (poisoned before the timed region,
+    # and each copy's last decode is a timed one), CRCs and kernel routing
+    ver = verify(batches, files, pcm)
+    ver["checked"] = "right after the timed region; outputs poisoned (0x7F) before it"
     tsum = tn = 0.0
     for bb in batches:
         ms, n = bb.timed()
@@ -421,8 +435,6 @@ def run_rank(args) -> None:
         b.sync()
         auto_ms = b.time(3)
         b.set_kernel(args.kernel)
-    # the timed decodes were real: every copy's output, CRCs and kernel routing
-    ver = verify(batches, files, pcm)
     dt = _reduce(pg, t1 - t0, "max")
     frames_total = _reduce(pg, float(frames_rank), "sum")
     kms_all = _gather(pg, kernel_ms, ws)

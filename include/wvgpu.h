@@ -54,6 +54,8 @@ extern "C" {
 #define WVG_ST_REDONE 0x200u     /* wvg_batch_block_status only: the lane kernel handed this block back and the
                                     one-workgroup-per-block kernel decoded it (a cost, never a result: masked out
                                     of wvg_file_result.status_or) */
+#define WVG_ST_UNWRITTEN 0x40000000u /* wvg_batch_block_status only: no decode has stored this block's status since
+                                        wvg_batch_poison (a bench/test check that a decode really ran) */
 
 typedef struct wvg_ctx wvg_ctx;
 typedef struct wvg_batch wvg_batch;
@@ -194,6 +196,12 @@ int wvg_batch_sync(wvg_batch *b);
 #define WVG_KERNEL_AUTO 2
 int wvg_batch_set_kernel(wvg_batch *b, int kernel);
 void *wvg_batch_stream(wvg_batch *b);  /* the batch's own hipStream_t */
+/* Verification aid (no reference counterpart): overwrite the uploaded batch's int32
+ * output with `byte` in every byte and mark every decodable block WVG_ST_UNWRITTEN, so
+ * that what a download shows afterwards was written by the decodes issued after this
+ * call.  Waits for the batch's earlier work.  (Gaps the reference zero-fills are left
+ * poisoned until the next wvg_batch_upload.) */
+int wvg_batch_poison(wvg_batch *b, int byte);
 /* Device timing of every following decode (an event pair around each launch, on its
  * stream); wvg_batch_timed waits for them and returns the mean and the count. */
 int wvg_batch_set_timing(wvg_batch *b, int on);

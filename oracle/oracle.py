@@ -148,3 +148,21 @@ def read_code(buf: bytes, maxcode: int):
     used = ctypes.c_int(0)
     code = lib().wvo_read_code_bytes(buf, len(buf), maxcode, ctypes.byref(used))
     return int(code), int(used.value)
+
+
+def decode_many(files, chunk: int = 4096, threads: int | None = None) -> list:
+    """decode_file over many files on host threads (ctypes drops the GIL; one oracle
+    context per call) -- for parity runs at the BASELINE configs' own sizes."""
+    from concurrent.futures import ThreadPoolExecutor
+    if threads is None:
+        threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "8") or 8), os.cpu_count() or 1))
+
+    def one(f):
+        # frames bound from the headers (block_samples per block), not the generous default
+        i, fr = 0, 0
+        while i + 32 <= len(f) and f[i:i + 4] == b"wvpk":
+            fr += int.from_bytes(f[i + 20:i + 24], "little")
+            i += 8 + int.from_bytes(f[i + 4:i + 8], "little")
+        return decode_file(f, chunk=chunk, max_frames=max(fr, 1 << 16))
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        return list(ex.map(one, files))

@@ -61,12 +61,35 @@ def c2(nblocks: int = 1024, block: int = 22050, return_pcm: bool = False):
     return (d["pcm"], data) if return_pcm else data
 
 
+def _workers() -> int:
+    return max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "8") or 8), os.cpu_count() or 1))
+
+
+def _c3_part(job):
+    """Blocks [k0, k1) of C3: their PCM and their encoded stream (a run of whole
+    blocks that starts at block_index k0 * block, as encode_pcm_parallel's parts)."""
+    k0, k1, nblocks, block = job
+    pcm = np.concatenate([S.audio_like(block, 2, 24, seed=0xC3 + b, sigma=4096.0) for b in range(k0, k1)], axis=0)
+    p = S.EncParams(terms=S.TERMS_HIGH, bytes_per_sample=3, block_samples=block, config_flags=0x800 | 0x1000,
+                    block_index_start=k0 * block, total_override=nblocks * block)
+    return pcm, S.encode_pcm(pcm, p)
+
+
 def c3(nblocks: int = 4096, block: int = 44100, return_pcm: bool = False):
     def make():
-        parts = [S.audio_like(block, 2, 24, seed=0xC3 + b, sigma=4096.0) for b in range(nblocks)]
-        pcm = np.concatenate(parts, axis=0)
-        data = S.encode_pcm_parallel(pcm, S.EncParams(terms=S.TERMS_HIGH, bytes_per_sample=3, block_samples=block,
-                                                      config_flags=0x800 | 0x1000))
+        # the PCM and the encode of whole-block parts in worker processes (the same stream
+        # as encode_pcm_parallel over the concatenated PCM)
+        from concurrent.futures import ProcessPoolExecutor
+        w = _workers()
+        per = max(1, (nblocks + w - 1) // w)
+        jobs = [(k, min(k + per, nblocks), nblocks, block) for k in range(0, nblocks, per)]
+        if len(jobs) == 1:
+            parts = [_c3_part(jobs[0])]
+        else:
+            with ProcessPoolExecutor(max_workers=w) as ex:
+                parts = list(ex.map(_c3_part, jobs))
+        pcm = np.concatenate([p for p, _ in parts], axis=0)
+        data = b"".join(d for _, d in parts)
         return {"pcm": pcm, "wv": np.frombuffer(data, dtype=np.uint8)}
     d = _cached(f"c3-{nblocks}-{block}", make)
     data = d["wv"].tobytes()
@@ -166,8 +189,22 @@ def c5_cost(i: int) -> float:
     return C5_COST[kind] * frames
 
 
-def c5(nfiles: int, start: int = 0):
-    return [c5_file(i) for i in range(start, start + nfiles)]
+def _c5_range(job):
+    lo, hi = job
+    return [c5_file(i) for i in range(lo, hi)]
+
+
+def c5(nfiles: int, start: int = 0, workers: int | None = None):
+    """Files start .. start + nfiles - 1 of the mixed corpus (generated in worker
+    processes for large slices; the files do not depend on how they are split)."""
+    w = workers if workers is not None else _workers()
+    if nfiles < 64 or w <= 1:
+        return [c5_file(i) for i in range(start, start + nfiles)]
+    from concurrent.futures import ProcessPoolExecutor
+    step = max(16, (nfiles + 4 * w - 1) // (4 * w))
+    jobs = [(i, min(i + step, start + nfiles)) for i in range(start, start + nfiles, step)]
+    with ProcessPoolExecutor(max_workers=w) as ex:
+        return [f for part in ex.map(_c5_range, jobs) for f in part]
 
 
 def c2_shard(rank: int, nblocks: int = 1024, block: int = 22050) -> bytes:

@@ -128,3 +128,19 @@ def test_dsd_calls_and_seeks_match_oracle():
             _same(_oracle_calls(data, samples), _mirror_calls(data, samples), f"{name}/{samples}")
         for target in (3, 5001, 9999):
             _same(_oracle_calls(data, 4096, seek=target), _mirror_calls(data, 4096, seek=target), f"{name}@{target}")
+
+
+def test_overrun_layouts_calls_match_oracle():
+    """a block that writes 2 ints a frame into a 1-int file throws
+    in the call whose store runs past the caller's buffer (WavPackUtils.cs:261); that
+    call returns nothing, the calls before it their frames -- call by call against the
+    oracle, PCM (FALSE_STEREO + MONO_FLAG, a stereo block in a mono file) and DSD
+    (FALSE_STEREO in a mono file)."""
+    from tests.test_layout_quirks import dsd_fs_mono_cases, quirk_cases
+    names = ("fs_monoflag", "fs_monoflag_chunk500", "fs_monoflag_overrun", "mono_file_stereo_block",
+             "mono_file_stereo_block_chunk300")
+    cases = [(n, d, c) for n, d, c in quirk_cases() if n in names]
+    cases += [(n, d, c) for n, d, c in dsd_fs_mono_cases() if O.decode_file(d, chunk=c).status == -3]
+    for name, data, chunk in cases:
+        for samples in sorted({chunk, 4096, 1000}):
+            _same(_oracle_calls(data, samples), _mirror_calls(data, samples), f"{name}/{samples}")

@@ -109,3 +109,34 @@ def test_dsd3_lanes_with_other_kinds():
 def test_dsd_cases_lane_route(case):
     name, data, chunk = case
     _check([data], [name], chunk)
+
+
+def test_dsd3_false_stereo_mono_file_stays_in_range():
+    """a mode-3 block flagged FALSE_STEREO inside a mono DSD file once
+    reached the mono lane launch, which stored 2 ints a frame into a 1-int range.  The
+    framing now declines such blocks (and raises the reference's exception where the
+    expansion overruns the caller's buffer), and the lane kernel hands back any block
+    whose store width differs from the file's.  The files around it must decode exactly."""
+    from tests.test_layout_quirks import FALSE_STEREO, set_flags
+    dd = S.dsd_random_like(9000, 1, seed=77, density=0.3)
+    flipped = [set_flags(S.encode_dsd(dd, S.DsdParams(nch=1, mode=3, block_samples=b)), None, FALSE_STEREO)
+               for b in (1500, 3000)]
+    small = set_flags(S.encode_dsd(S.dsd_random_like(1500, 1, seed=78, density=0.3),
+                                   S.DsdParams(nch=1, mode=3, block_samples=1500)), None, FALSE_STEREO)
+    normal = [_dsd3(7000, 1, seed=79), _dsd3(5000, 2, seed=80), _dsd3(3000, 1, seed=81)]
+    files = [normal[0], flipped[0], normal[1], small, flipped[1], normal[2]]
+    out, res, infos, st = _run(files)
+    for k in (0, 2, 5):
+        ref = O.decode_file(files[k], chunk=4096)
+        r, info = res[k], infos[k]
+        assert r.exception == 0 and r.frames == ref.frames and r.crc_errors == ref.crc_errors, k
+        np.testing.assert_array_equal(out[info.out_offset: info.out_offset + ref.frames * ref.nch], ref.samples,
+                                      err_msg=str(k))
+    for k in (1, 3, 4):
+        ref = O.decode_file(files[k], chunk=4096)
+        r = res[k]
+        assert not (r.status_or & WVG_ST_TIMEOUT), k
+        if ref.status == -3:
+            assert r.exception == 1, k
+        else:
+            assert r.status_or & 0x20, k  # declined (WVG_ST_UNSUPPORTED)

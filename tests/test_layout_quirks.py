@@ -111,3 +111,29 @@ def test_quirk_layout_host_core_vs_oracle(name, data, chunk):
 def test_quirk_cases_cover_each_layout():
     kinds = {nm: O.decode_file(d, chunk=c).status for nm, d, c in CASES}
     assert kinds["fs_monoflag_overrun"] == -3 and kinds["fs_monoflag"] == 0
+
+
+def dsd_fs_mono_cases():
+    """Mono DSD files whose blocks carry FALSE_STEREO (MONO_DATA still set): the unmuted
+    call decodes n values and expands them to 2n ints (DsdUtils.cs:119-131) in a 1-int
+    file -- past the caller's buffer the C# store throws.  (the lane kernel
+    once wrote those 2n ints into the next block's range.)"""
+    out = []
+    for frames, block in ((9000, 3000), (9000, 5000), (1500, 1500)):
+        for mode in (0, 1, 3):
+            dd = S.dsd_random_like(frames, 1, seed=5 + mode, density=0.3)
+            f = S.encode_dsd(dd, S.DsdParams(nch=1, mode=mode, block_samples=block))
+            out.append((f"dsd_m{mode}_mono_fs_{frames}_{block}", set_flags(f, None, FALSE_STEREO), 4096))
+    return out
+
+
+@pytest.mark.parametrize("name,data,chunk", dsd_fs_mono_cases(), ids=[c[0] for c in dsd_fs_mono_cases()])
+def test_dsd_false_stereo_in_mono_file(name, data, chunk):
+    n, out, crc, st = E.decode(data, chunk)
+    ref = O.decode_file(data, chunk=chunk)
+    if ref.status == -3:  # the expansion overran the caller's buffer: the same call throws
+        assert n == -3, name
+        return
+    # a layout the device does not decode (the first n of the 2n expanded ints): declined
+    assert st & ST_UNSUPPORTED, name
+    assert n == ref.frames, name

@@ -23,6 +23,7 @@ WVG_ST_DSD_MUTE = 0x40
 WVG_ST_NONDET = 0x80
 WVG_ST_TIMEOUT = 0x100
 WVG_ST_REDONE = 0x200  # block status only: decoded by the lane kernel's fallback
+WVG_ST_UNWRITTEN = 0x40000000  # block status only: no decode stored it since wvg_batch_poison
 WVG_ERR_ARG = -2
 WVG_ERR_OPEN = -3
 WVG_ERR_TIMEOUT = -5
@@ -95,6 +96,7 @@ def lib():
         "wvg_batch_decode": (i32, [vp, vp]),
         "wvg_batch_sync": (i32, [vp]),
         "wvg_batch_stream": (vp, [vp]),
+        "wvg_batch_poison": (i32, [vp, i32]),
         "wvg_batch_set_timing": (i32, [vp, i32]),
         "wvg_batch_set_kernel": (i32, [vp, i32]),
         "wvg_batch_timed": (i32, [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]),
@@ -145,7 +147,7 @@ def lib():
 EXPORTED = ("wvg_open", "wvg_close", "wvg_last_error", "wvg_batch_new", "wvg_batch_free", "wvg_batch_add_file",
             "wvg_batch_add_file_at", "wvg_batch_add_files", "wvg_batch_add_files_device", "wvg_batch_file_info", "wvg_batch_add_file_wvc",
             "wvg_batch_framing_stats",
-            "wvg_batch_upload", "wvg_batch_reset", "wvg_batch_decode", "wvg_batch_sync", "wvg_batch_stream", "wvg_batch_set_timing", "wvg_batch_set_kernel",
+            "wvg_batch_upload", "wvg_batch_reset", "wvg_batch_decode", "wvg_batch_sync", "wvg_batch_stream", "wvg_batch_poison", "wvg_batch_set_timing", "wvg_batch_set_kernel",
             "wvg_batch_timed", "wvg_batch_group_times", "wvg_batch_out_ints", "wvg_batch_device_out",
             "wvg_batch_num_blocks", "wvg_batch_bytes_in", "wvg_batch_frames", "wvg_batch_download", "wvg_batch_host_out",
             "wvg_batch_file_result", "wvg_batch_block_status", "wvg_batch_lane_counters", "wvg_batch_file_blocks", "wvg_batch_time", "wvg_decode_file",

@@ -175,6 +175,14 @@ class DecodeBatch:
     def sync(self):
         self._check(self._L.wvg_batch_sync(self._b))
 
+    def poison(self, byte: int = 0x7F):
+        """Overwrite the output with `byte` and mark every decodable block's status
+        WVG_ST_UNWRITTEN (wvg_batch_poison): what a later download shows was written by
+        the decodes issued after this call."""
+        if not self._uploaded:
+            self.upload()
+        self._check(self._L.wvg_batch_poison(self._b, int(byte)))
+
     def set_kernel(self, kernel: str):
         """'auto' (the default: the lane kernels once the context has had batches in
         flight together, until then one workgroup per block for groups of up to 2,048

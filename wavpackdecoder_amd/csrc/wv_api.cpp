@@ -1027,9 +1027,11 @@ int wvg_batch_upload(wvg_batch *b) {
     HIPCHK(c, hipMemsetAsync(b->d_mute, 0, sizeof(uint32_t) * (nd ? nd : 1), s));
     // longest blocks first within a kind, so the long tail starts early (order is
     // free: every block writes its own output range; DSD fills follow on the same stream)
+    // (KIND_SKIP first: the mode-3 range [dsd_high_lo, end) then holds mode-3 blocks only)
+    auto kind_rank = [](uint32_t k) { return k == KIND_SKIP ? 0u : k + 1u; };
     auto by_kind_len = [&](uint32_t x, uint32_t y) {
         const BlockDesc &p = b->fo.descs[x], &q = b->fo.descs[y];
-        if (p.kind != q.kind) return p.kind < q.kind;
+        if (p.kind != q.kind) return kind_rank(p.kind) < kind_rank(q.kind);
         if (p.kind == KIND_DSD_HIGH) {  // stereo blocks before mono ones (one lane kernel each)
             const bool pm = (p.flags & wvf::MONO_DATA) != 0, qm = (q.flags & wvf::MONO_DATA) != 0;
             if (pm != qm) return qm;
@@ -1274,6 +1276,27 @@ int wvg_batch_sync(wvg_batch *b) {
 
 void *wvg_batch_stream(wvg_batch *b) { return b ? (void *)b->stream : nullptr; }
 
+int wvg_batch_poison(wvg_batch *b, int byte) {
+    if (!b || !b->uploaded) return WVG_ERR_ARG;
+    wvg_ctx *c = b->ctx;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, quiesce(b));
+    if (b->out_ints) HIPCHK(c, hipMemsetAsync(b->d_out, byte & 0xFF, sizeof(int32_t) * (size_t)b->out_ints, b->stream));
+    const size_t nd = b->fo.descs.size();
+    if (nd) {
+        // every block a kernel decodes gets WVG_ST_UNWRITTEN until a decode stores its status
+        // (KIND_SKIP blocks keep the framing's verdict: no kernel writes them)
+        std::vector<uint32_t> st(nd);
+        for (size_t k = 0; k < nd; k++)
+            st[k] = b->fo.descs[k].fstatus | (b->fo.descs[k].kind == KIND_SKIP ? 0u : (uint32_t)WVG_ST_UNWRITTEN);
+        HIPCHK(c, hipMemcpyAsync(b->d_status, st.data(), sizeof(uint32_t) * nd, hipMemcpyHostToDevice, b->stream));
+        HIPCHK(c, hipMemsetAsync(b->d_mute, 0, sizeof(uint32_t) * nd, b->stream));
+    }
+    HIPCHK(c, hipStreamSynchronize(b->stream));
+    b->downloaded = false;
+    return WVG_OK;
+}
+
 int wvg_batch_set_kernel(wvg_batch *b, int kernel) {
     if (!b || (kernel != WVG_KERNEL_TWO_WAVE && kernel != WVG_KERNEL_LANE && kernel != WVG_KERNEL_AUTO))
         return WVG_ERR_ARG;
@@ -1367,6 +1390,8 @@ int wvg_batch_lane_counters(wvg_batch *b, int ts, uint32_t *out, int64_t cap) {
     const size_t nw = (b->ts_lane[ts].size() + 63) / 64;
     if (nw > kLaneDbgWaves) return WVG_ERR_ARG;
     if (cap < (int64_t)(16 * nw)) return WVG_ERR_SPACE;
+    // (the decode may have run on a caller's stream or the context's side streams)
+    HIPCHK(b->ctx, hipEventSynchronize(b->done));
     HIPCHK(b->ctx, hipStreamSynchronize(b->stream));
     HIPCHK(b->ctx, hipMemcpy(out, b->d_lane_dbg + (size_t)ts * kLaneDbgWaves * 16u, sizeof(uint32_t) * 16 * nw,
                              hipMemcpyDeviceToHost));

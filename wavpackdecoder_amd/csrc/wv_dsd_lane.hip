@@ -121,6 +121,9 @@ __device__ __forceinline__ bool dsd3_ok(const BlockDesc &d) {
     if (d.kind != KIND_DSD_HIGH) return false;
     if (((d.flags & MONO_DATA) ? 1 : 2) != CH) return false;
     if (CH == 2 && (d.flags & FALSE_STEREO)) return false;
+    // the lane stores och ints a frame: they must be the file's (a FALSE_STEREO block in a
+    // 1-int file would write past its range)
+    if (((CH == 2 || (d.flags & FALSE_STEREO)) ? 2u : 1u) != d.out_nch) return false;
     if (d.inherit || d.chain_len >= 2 || d.pre_end || d.fstatus) return false;
     if (d.dsd_data_len < 4u) return false;
     return true;

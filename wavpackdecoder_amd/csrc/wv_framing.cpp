@@ -1303,7 +1303,11 @@ void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t ou
                 const bool pcm_blk = !(hh.flags & DSD_FLAG);
                 const int bch = ((hh.flags & MONO_FLAG) && !(pcm_blk && (hh.flags & FALSE_STEREO))) ? 1 : 2;
                 const int64_t buf_len = (int64_t)(disc_call ? 4096 : (int64_t)chunk * nch);
-                if (bch != nch && !pcm_blk) {
+                // a DSD block's unmuted call writes 2 ints a frame on FALSE_STEREO whatever
+                // MONO_FLAG says (DsdUtils.cs:119-131), its muted call MONO_FLAG ? 1 : 2
+                // (:106-113): both must be the file's width for the block to be decoded here
+                const int dsd_wch = (hh.flags & FALSE_STEREO) ? 2 : bch;
+                if (!pcm_blk && (bch != nch || dsd_wch != nch)) {
                     // a DSD layout the reference writes inconsistently (and may overrun): not decoded here
                     info.nondet = 1;
                 }
@@ -1324,7 +1328,7 @@ void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t ou
                         d.pre_chunk = (uint32_t)dchunk;
                         d.out_off = out_base_ints + (uint64_t)(out_frames * nch) - (uint64_t)(rem * nch);
                     }
-                    if (bch != nch && !pcm_blk) {
+                    if (!pcm_blk && (bch != nch || dsd_wch != nch)) {
                         d.kind = KIND_SKIP;
                         d.fstatus |= ST_UNSUPPORTED;
                         d.inherit = d.inherit_passes = 0;
@@ -1337,17 +1341,29 @@ void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t ou
                         // from past it: the reference overruns or emits caller-buffer garbage.
                         d.kind = KIND_SKIP;
                         d.fstatus |= ST_NONDET;
-                        if (buf_idx + 3 * n > (int64_t)chunk * nch) info.exception = 1;
                     }
                     out.descs.push_back(d);
                     cur_idx = (int64_t)out.descs.size() - 1;
                     F.mark_adapted();
                 }
                 cur = &out.descs[(size_t)cur_idx];
-                // a 2-int PCM block in a 1-int file writes 2n ints from buf_idx: past the
-                // caller's buffer the C# array store throws (in this call)
-                if (pcm_blk && bch == 2 && nch == 1 && buf_idx + 2 * n > buf_len) info.exception = 1;
+                // the C# array store past the caller's buffer throws in this call, which
+                // then returns nothing (the exception escapes WavpackUnpackSamples,
+                // WavPackUtils.cs:261): a 2-int PCM block in a 1-int file writes 2n ints
+                // from buf_idx; DSD mode 0 + FALSE_STEREO advances bufferStartPos by n
+                // (DsdUtils.cs:81) and then expands 2n ints past it (:119-131).  (The
+                // frames stay in the descriptor: the device decodes them, nobody reads them.)
+                // A DSD FALSE_STEREO block in a 1-int file (declined above) likewise expands 2n
+                // ints.  (Known divergence, malformed files only: a call that starts muted
+                // zero-fills n ints and returns before the copy, UnpackUtils.cs:527-543 /
+                // DsdUtils.cs:104-117, so the reference does not throw there; the framing
+                // cannot see the device's mute state and flags the throw.)
+                const int wch = pcm_blk ? bch : dsd_wch;  // ints a frame the unmuted call writes
+                const bool overrun =
+                    (wch == 2 && nch == 1 && buf_idx + 2 * n > buf_len) ||
+                    (!pcm_blk && F.dsd.mode == 0 && (hh.flags & FALSE_STEREO) && buf_idx + 3 * n > buf_len);
                 cur->nframes += (uint32_t)n;
+                if (overrun) throw CsException();
                 F.sample_index += n;
                 buf_idx += n * nch;
                 unpacked += n;
