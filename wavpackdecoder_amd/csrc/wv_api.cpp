@@ -22,7 +22,8 @@ namespace wvg {
 hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint32_t n_pcm, const uint32_t *dsd_list,
                          uint32_t n_dsd, uint32_t fast_lo, uint32_t n_fast, const uint8_t *blob, const uint8_t *tables,
                          int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s_pcm, hipStream_t s_dsd,
-                         hipStream_t s_fast, int lane_mode, uint32_t high_lo, uint32_t n_high_mono);
+                         hipStream_t s_fast, int lane_mode, uint32_t high_lo, uint32_t n_high_mono,
+                         int lane_mode_fast, uint32_t n_fast_mono);
 int term_set_of(const BlockDesc &d, int prefer_pipe);
 hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, uint32_t n, const uint8_t *blob,
                         int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s, int lane_mode,
@@ -164,6 +165,7 @@ struct wvg_batch {
     int64_t out_ints = 0;
     std::vector<uint32_t> pcm_list, dsd_list;           // wave-per-block kernels (generic PCM, DSD)
     uint32_t dsd_fast_lo = 0, dsd_fast_n = 0;          // the mode-1 range of dsd_list (sorted by kind)
+    uint32_t dsd_fast_mono = 0;                        // ... its mono blocks (after the stereo ones)
     uint32_t dsd_high_lo = 0, dsd_high_mono = 0;       // the mode-3 range [high_lo, end): stereo, then mono blocks
     std::vector<uint32_t> ts_list[kMaxTermSets];        // two-wave kernels per term set
     int64_t gframes[kSide] = {0};                       // frames per launch group (the lane assignment's load)
@@ -1032,7 +1034,7 @@ int wvg_batch_upload(wvg_batch *b) {
     auto by_kind_len = [&](uint32_t x, uint32_t y) {
         const BlockDesc &p = b->fo.descs[x], &q = b->fo.descs[y];
         if (p.kind != q.kind) return kind_rank(p.kind) < kind_rank(q.kind);
-        if (p.kind == KIND_DSD_HIGH) {  // stereo blocks before mono ones (one lane kernel each)
+        if (p.kind == KIND_DSD_HIGH || p.kind == KIND_DSD_FAST) {  // stereo before mono (one lane kernel each)
             const bool pm = (p.flags & wvf::MONO_DATA) != 0, qm = (q.flags & wvf::MONO_DATA) != 0;
             if (pm != qm) return qm;
         }
@@ -1041,7 +1043,7 @@ int wvg_batch_upload(wvg_batch *b) {
     std::sort(b->pcm_list.begin(), b->pcm_list.end(), by_kind_len);
     std::sort(b->dsd_list.begin(), b->dsd_list.end(), by_kind_len);
     // the mode-1 blocks are one range of the kind-sorted list (their own kernel)
-    b->dsd_fast_lo = b->dsd_fast_n = 0;
+    b->dsd_fast_lo = b->dsd_fast_n = b->dsd_fast_mono = 0;
     b->dsd_high_lo = (uint32_t)b->dsd_list.size();
     b->dsd_high_mono = 0;
     for (size_t k = 0; k < b->dsd_list.size(); k++) {
@@ -1053,6 +1055,7 @@ int wvg_batch_upload(wvg_batch *b) {
         if (d.kind != KIND_DSD_FAST) continue;
         if (!b->dsd_fast_n) b->dsd_fast_lo = (uint32_t)k;
         b->dsd_fast_n++;
+        if (d.flags & wvf::MONO_DATA) b->dsd_fast_mono++;
     }
     const size_t np = b->pcm_list.size(), ns = b->dsd_list.size();
     HIPCHK(c, ensure(b->d_pcml, b->cap_pcml, sizeof(uint32_t) * (np ? np : 1)));
@@ -1240,7 +1243,7 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
     HIPCHK(c, launch_decode(b->d_descs, b->d_pcml, (uint32_t)b->pcm_list.size(), b->d_dsd, (uint32_t)b->dsd_list.size(),
                             b->dsd_fast_lo, b->dsd_fast_n, b->d_blob, b->d_tables, b->d_out, b->d_status, b->d_mute,
                             slot(kPcm), slot(kDsd), slot(kDsd1), mode_of(b->dsd_list.size() - b->dsd_high_lo),
-                            b->dsd_high_lo, b->dsd_high_mono));
+                            b->dsd_high_lo, b->dsd_high_mono, mode_of(b->dsd_fast_n), b->dsd_fast_mono));
     HIPCHK(c, mark(kDsd));
     HIPCHK(c, mark(kDsd1));
     HIPCHK(c, mark(kPcm));
@@ -1861,7 +1864,11 @@ int64_t wvg_stream_unpack(wvg_stream *s, int32_t *buffer, int64_t samples) {
         s->schedule_changed = 1;  // later calls of another size: served from the first schedule
     }
     if (s->pos >= s->limit) return s->throws ? WVG_ERR_EXCEPTION : 0;
-    const int64_t n = std::min(samples, s->limit - s->pos);
+    int64_t n = std::min(samples, s->limit - s->pos);
+    // a call the reference ends early (its loop breaks on a header / unpack_init failure)
+    const std::vector<int64_t> &cuts = s->b->finfo[0].call_cuts;
+    auto cut = std::upper_bound(cuts.begin(), cuts.end(), s->pos);
+    if (cut != cuts.end() && *cut - s->pos < n) n = *cut - s->pos;
     wvg_ctx *c = s->ctx;
     int64_t done = 0;
     while (done < n) {

@@ -125,6 +125,9 @@ hipError_t launch_dsd3_lane(const BlockDesc *descs, const uint32_t *list, uint32
                             const int32_t *ptables, int32_t *out, uint32_t *status, uint32_t *mute_chunk,
                             uint32_t n_mono, hipStream_t s);
 
+hipError_t launch_dsd1_lane(const BlockDesc *descs, const uint32_t *list, uint32_t n, const uint8_t *blob,
+                            int32_t *out, uint32_t *status, uint32_t *mute_chunk, uint32_t n_mono, hipStream_t s);
+
 hipError_t upload_dsd_ptables() {
     std::vector<int32_t> t(256 * 256);
     for (int r = 0; r < 256; r++) dsd_ptable_init(r, t.data() + (size_t)r * 256, 0, 1);
@@ -988,11 +991,14 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_fast(const BlockD
                                                                     const uint8_t *__restrict__ tables,
                                                                     int32_t *__restrict__ out,
                                                                     uint32_t *__restrict__ status,
-                                                                    uint32_t *__restrict__ mute_chunk) {
+                                                                    uint32_t *__restrict__ mute_chunk,
+                                                                    uint32_t mode) {
     __shared__ uint32_t tab[kDsdFastLds / 4];
     static_assert(kDsdStageAt * 4u + kDsdProbStage <= kDsdFastLds, "the stage lives in the row region");
     const uint32_t bi = list[blockIdx.x];
     const BlockDesc &d = descs[bi];
+    // mode bit 2: only the blocks the row kernel (wv_dsd1_lane.hip) handed back (ST_REDO)
+    if ((mode & 4u) && !(status[bi] & lane::ST_REDO)) return;
     const bool lead = threadIdx.x == 0;
     const uint32_t bins = (uint32_t)d.dsd_history_bins;
     DevStoreWave st{out + d.out_off, (uint64_t)d.pre_end * d.out_nch, lead};
@@ -1025,7 +1031,7 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_fast(const BlockD
         r = (d.flags & wvf::MONO_DATA) ? dsd_fast_v2<1>(d, blob, tab, vmag, vsh1, vsh2, st)
                                        : dsd_fast_v2<2>(d, blob, tab, vmag, vsh1, vsh2, st);
     if (lead) {
-        status[bi] = d.fstatus | r.status;
+        status[bi] = d.fstatus | r.status | ((mode & 4u) ? (uint32_t)ST_REDONE : 0u);
         mute_chunk[bi] = r.mute_chunk;
     }
 }
@@ -1317,11 +1323,14 @@ namespace wvg {
 // wv_decode_dsd_wave launch on s_dsd (mute fills: launch_dsd_fill, after the join)
 // With lane_mode, the mode-3 range [high_lo, n_dsd) (stereo first, then n_high_mono
 // mono blocks) goes to the lane-per-block kernel (wv_dsd_lane.hip) after the wave
-// kernel's other blocks, and the wave kernel then decodes what it handed back.
+// kernel's other blocks, and the wave kernel then decodes what it handed back; with
+// lane_mode_fast, the mode-1 range (stereo first, then n_fast_mono mono blocks) to the
+// 16-lane row kernel (wv_dsd1_lane.hip), its hand-backs to wv_decode_dsd_fast.
 hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint32_t n_pcm, const uint32_t *dsd_list,
                          uint32_t n_dsd, uint32_t fast_lo, uint32_t n_fast, const uint8_t *blob, const uint8_t *tables,
                          int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s_pcm, hipStream_t s_dsd,
-                         hipStream_t s_fast, int lane_mode, uint32_t high_lo, uint32_t n_high_mono) {
+                         hipStream_t s_fast, int lane_mode, uint32_t high_lo, uint32_t n_high_mono,
+                         int lane_mode_fast, uint32_t n_fast_mono) {
     // the DSD kernels first: their blocks are the batch's longest serial chains
     const uint32_t skip = n_fast ? 1u : 0u;
     const uint32_t n_high = lane_mode ? n_dsd - high_lo : 0u;
@@ -1340,8 +1349,18 @@ hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint3
     }
     if (n_fast) {
         const uint32_t *fl = dsd_list + fast_lo;
-        hipLaunchKernelGGL(wv_decode_dsd_fast, dim3(n_fast), dim3(64), 0, s_fast, descs, fl, blob, tables, out, status,
-                           aux);
+        if (lane_mode_fast) {
+            // mode 1 on rows of 16 lanes (wv_dsd1_lane.hip), then its hand-backs one wave per block
+            if (hipError_t e = launch_dsd1_lane(descs, fl, n_fast, blob, out, status, aux, n_fast_mono, s_fast);
+                e != hipSuccess)
+                return e;
+            if (lane_mode_fast != 2)  // 2: the row kernel alone (diagnostics: ST_REDO stays in the status)
+                hipLaunchKernelGGL(wv_decode_dsd_fast, dim3(n_fast), dim3(64), 0, s_fast, descs, fl, blob, tables, out,
+                                   status, aux, 4u);
+        } else {
+            hipLaunchKernelGGL(wv_decode_dsd_fast, dim3(n_fast), dim3(64), 0, s_fast, descs, fl, blob, tables, out,
+                               status, aux, 0u);
+        }
     }
     if (n_pcm)
         hipLaunchKernelGGL(wv_decode_pcm_wave, dim3(n_pcm), dim3(64), 0, s_pcm, descs, pcm_list, blob, out, status, aux);

@@ -1382,6 +1382,7 @@ void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t ou
             if (info.first_call_frames < 0) info.first_call_frames = unpacked;
             if (unpacked == 0) break;
             out_frames += unpacked;
+            if (unpacked < (int64_t)chunk) info.call_cuts.push_back(out_frames);
             if (info.exception) break;
             // a descriptor whose block stopped exactly at a call boundary stays open:
             // the next call continues it (cur_idx kept)

@@ -36,6 +36,10 @@ struct FileInfo {
     int32_t out_nch = 0;        // ints per frame
     int64_t out_frames = 0;     // frames all calls return
     int64_t first_call_frames = -1;  // frames the first call returns (-1: it threw)
+    // output frame counts at which a call returned fewer frames than it asked for (the
+    // reference's loop breaks on a header or unpack_init failure, WavPackUtils.cs:215-221;
+    // and the file's last call): the stream API ends its calls there too
+    std::vector<int64_t> call_cuts;
     int32_t seek_result = 0;    // SetSample: 1 positioned, 0 false, -1 exception (0 when no seek was asked)
     int64_t sample_index0 = 0;  // stream.sample_index when the caller's first (non-discard) call starts
     uint64_t blob_base = 0;     // the file's first byte inside the batch blob (header/trailer offsets are file-relative)
