@@ -38,6 +38,21 @@
 namespace wvg {
 namespace d1lane {
 
+#ifndef WV_D1_PF  // (A/B builds) the window's load consumed a refill after it is issued
+#define WV_D1_PF 0
+#endif
+#ifndef WV_D1_PRE  // (A/B builds) stereo: the next symbol's bin read while this one decodes
+#define WV_D1_PRE 0
+#endif
+#ifndef WV_D1_SEGLDS  // (A/B builds) the segment's start read from LDS, not a row max (slower: an LDS
+#define WV_D1_SEGLDS 0  // round trip on the chain, where the row max overlaps the probability read)
+#endif
+#ifndef WV_D1_BPERM  // (A/B builds) low / high from lanes cnt - 1 / cnt by ds_bpermute, not row max / min
+#define WV_D1_BPERM 0   // (slower: the permute's LDS latency on the chain)
+#endif
+#ifndef WV_D1_UFLUSH  // (A/B builds) stereo: the output staged and stored at uniform points
+#define WV_D1_UFLUSH 1
+#endif
 constexpr uint32_t ST_REDO = 1u << 15;  // as wv_lane.h: decode this block again (wave kernel)
 constexpr uint32_t kBins = 32;          // init_dsd_block_fast: history_bits <= MAX_HISTORY_BITS (5)
 
@@ -89,32 +104,43 @@ __device__ __forceinline__ uint32_t gm_div(uint32_t mag, uint32_t sh, uint32_t n
     return (t1 + ((n - t1) >> (sh & 0xFFu))) >> (sh >> 8);
 }
 
-// per-lane payload window (as wv_dsd_lane.hip): byte 0 in bits 63..56 of win, avail
-// bytes valid (>= 4 between symbols), nxt / nxt2 the two dwords after them
+// per-lane payload window: byte 0 in bits 63..56 of win, avail bytes valid (>= 4
+// between symbols), q0 / q1 the two dwords after them, ld the load of the dword after
+// those, issued at the previous refill: a refill consumes only a load issued a symbol
+// (hundreds of cycles) earlier, so no symbol waits on memory -- a select on a load issued
+// in the same refill would wait for it there (the compiler's vmcnt)
 struct Win {
     const uint32_t *w;
     uint64_t win;
     int32_t avail;
-    uint32_t ni, nxt, nxt2;
+    uint32_t ni, q0, q1, ld;
     __device__ __forceinline__ void init(const uint8_t *p) {
         const uint32_t sh = (uint32_t)((uintptr_t)p & 3u);
         w = (const uint32_t *)(p - sh);
         win = (uint64_t)bswap(w[0]) << (32u + 8u * sh);
         avail = 4 - (int32_t)sh;
-        nxt = w[1];
-        nxt2 = w[2];
+        q0 = w[1];
+        q1 = w[2];
+        ld = w[3];
         ni = 3;
         refill();
     }
     __device__ __forceinline__ void refill() {  // branch-free: a lane with more than 4 bytes keeps its window
         const bool m = avail <= 4;
         const uint32_t sh = (uint32_t)(32 - 8 * (m ? avail : 0)) & 63u;
-        win |= m ? (uint64_t)bswap(nxt) << sh : 0ull;
+        win |= m ? (uint64_t)bswap(q0) << sh : 0ull;
         avail += m ? 4 : 0;
-        const uint32_t nn = w[ni];  // (always inside the blob's 64-B tail: at most 12 bytes ahead)
-        nxt = m ? nxt2 : nxt;
-        nxt2 = m ? nn : nxt2;
+#if WV_D1_PF
+        q0 = m ? q1 : q0;
+        q1 = m ? ld : q1;
         ni += m ? 1u : 0u;
+        ld = w[ni];  // (reads stay within 16 bytes past the consumed ones: the blob's 64-B tail)
+#else
+        const uint32_t nn = w[ni];
+        q0 = m ? q1 : q0;
+        q1 = m ? nn : q1;
+        ni += m ? 1u : 0u;
+#endif
     }
 };
 
@@ -167,7 +193,7 @@ __device__ __forceinline__ void build(const BlockDesc &d, const uint8_t *__restr
     } else {
         const uint32_t sh = (uint32_t)(d.dsd_prob_off & 3u);
         const uint32_t *g = (const uint32_t *)(src - sh);
-        for (uint32_t i = lane; i < ne / 4u; i += 64) pw[i] = __builtin_amdgcn_alignbyte(g[i + 1u], g[i], sh * 8u);
+        for (uint32_t i = lane; i < ne / 4u; i += 64) pw[i] = __builtin_amdgcn_alignbyte(g[i + 1u], g[i], sh);
     }
     __syncthreads();
     uint32_t my_tot = 0;
@@ -240,10 +266,19 @@ __device__ __forceinline__ void m1_rows(const BlockDesc *__restrict__ descs, con
     int32_t *o = out + d.out_off;
     uint32_t nst = 0u, obase = 0u;
     int32_t stg = 0;
+    // a bin's reciprocal and this lane's segment end: read a symbol ahead for stereo (the
+    // next symbol's bin is p1 before this one decodes: each channel's history is its own
+    // previous symbol, DsdUtils.cs:290-292), after the symbol for mono (its own code)
+    struct Pre {
+        uint32_t mag, gsh, be;
+    };
+    auto pre = [&](uint32_t pa) -> Pre { return Pre{S.gm[pa][0], S.gm[pa][1], (uint32_t)S.base[pa * 16u + j]}; };
+    Pre cur = pre(0u);
     auto symbol = [&](bool act) {
         const uint32_t pa = p0;
-        const uint32_t mag = S.gm[pa][0], gsh = S.gm[pa][1];
-        const uint32_t be = S.base[pa * 16u + j];
+        const uint32_t mag = cur.mag, gsh = cur.gsh, be = cur.be;
+        Pre nx;
+        if (CH == 2 && WV_D1_PRE) nx = pre(p1);
         uint32_t mult = gm_div(mag, gsh, high - low);
         if (__builtin_expect(__ballot(act && mult == 0u) != 0ull, 0)) {
             // DsdUtils.cs:262-274: four more value bytes (when there are), the full range
@@ -260,31 +295,56 @@ __device__ __forceinline__ void m1_rows(const BlockDesc *__restrict__ descs, con
         }
         const uint32_t x = value - low;
         // the segment: entries 16 seg .. 16 seg + 15 hold index = x / mult
-        const bool c1 = be * mult <= x;
+        const uint32_t q1 = be * mult;
+        const bool c1 = q1 <= x;
         const uint32_t seg = row_count(__ballot(c1), rsh);
         bad |= (act && seg >= 16u) ? 2u : 0u;  // index >= tot (or an empty bin)
+        const uint32_t sg = min(seg, 15u);
+#if WV_D1_SEGLDS
+        // the running sum before the segment: the previous segment's end, read beside the
+        // segment's probabilities
+        const uint32_t segstart = seg ? (uint32_t)S.base[pa * 16u + sg - 1u] : 0u;
+#else
         const uint32_t segstart = row_max(c1 ? be : 0u);  // running sum before the segment
-        const uint32_t pbv = S.prob[pa * 256u + (min(seg, 15u) << 4) + j];
+#endif
+        const uint32_t pbv = S.prob[pa * 256u + (sg << 4) + j];
         const uint32_t q2 = (segstart + row_scan(pbv)) * mult;
         const bool c2 = q2 <= x;
-        const uint32_t code = (seg << 4) + row_count(__ballot(c2), rsh);
+        const uint32_t cnt = row_count(__ballot(c2), rsh);
+        const uint32_t code = (seg << 4) + cnt;
         // low += summed[code - 1] * mult; high = low + prob[code] * mult - 1 (:281-284)
-        const uint32_t lo = row_max(c2 ? q2 : segstart * mult);
+#if WV_D1_BPERM
+        // the products of entries code - 1 and code: lanes cnt - 1 and cnt of the row
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((rsh + cnt) << 2), (int)q2);
+        const uint32_t lq = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((rsh + cnt - 1u) << 2), (int)q2);
+        const uint32_t lo = cnt ? lq : segstart * mult;
+#else
+        // (entry code - 1's product is the largest at or below x: a lane of the segment, or
+        // for cnt == 0 the previous segment's end, lane seg - 1's q1)
+        const uint32_t lo = row_max(c2 ? q2 : (c1 ? q1 : 0u));
         const uint32_t hi = row_min(c2 ? 0xFFFFFFFFu : q2);
-        high = act ? low + hi - 1u : high;
-        low = act ? low + lo : low;
-        crc = act ? crc * 3u + code : crc;
+#endif
+        // (a row past its block's end decodes on, unobserved: its reads stay inside its
+        // data -- `left` -- and its table; the crc, the verdicts and the stores are gated)
+        high = low + hi - 1u;
+        low = low + lo;
+        uint32_t c3;  // crc * 3 (full-rate; the compiler's choice is a 64-bit multiply-add)
+        asm("v_lshl_add_u32 %0, %1, 1, %1" : "=v"(c3) : "v"(crc));
+        crc = act ? c3 + code : crc;
         if (CH == 2) {
-            p0 = act ? p1 : p0;
-            p1 = act ? (code & bmask) : p1;
+            p0 = p1;
+            p1 = code & bmask;
+            if (WV_D1_PRE) cur = nx;
+            else cur = pre(p0);
         } else {
-            p0 = act ? (code & bmask) : p0;
+            p0 = code & bmask;
+            cur = pre(p0);
         }
         // the byte loop (:295-300) as one shift by the leading zero bytes of high ^ low,
         // capped by the bytes left
         uint32_t lz;
         asm("v_ffbh_u32 %0, %1" : "=v"(lz) : "v"(high ^ low));
-        const uint32_t nb = act ? min(min(lz >> 3, 4u), left) : 0u;
+        const uint32_t nb = min(min(lz >> 3, 4u), left);
         const uint32_t s = nb << 3;
         value = (uint32_t)(((((uint64_t)value << 32) | (src.win >> 32)) << s) >> 32);
         high = (uint32_t)(((((uint64_t)high << 32) | 0xFFFFFFFFull) << s) >> 32);
@@ -292,25 +352,42 @@ __device__ __forceinline__ void m1_rows(const BlockDesc *__restrict__ descs, con
         src.win <<= s;
         src.avail -= (int32_t)nb;
         left -= nb;
-        dry = min(dry, src.avail);
+        dry = act ? min(dry, src.avail) : dry;
         src.refill();
         // stage the symbol's int(s); a row's 16 ints go out in one store
-        if (act) {
-            stg = (j == nst || (wps == 2u && j == nst + 1u)) ? (int32_t)code : stg;
-            nst += wps;
-        }
-        if (nst == 16u) {
-            o[obase + j] = stg;
-            obase += 16u;
-            nst = 0u;
+        if (CH == 2 && WV_D1_UFLUSH) {
+            // stereo: int k of a frame run is symbol k (every row at the same position)
+            stg = (act && j == nst) ? (int32_t)code : stg;
+            nst = (nst + 1u) & 15u;
+        } else {
+            if (act) {
+                stg = (j == nst || (wps == 2u && j == nst + 1u)) ? (int32_t)code : stg;
+                nst += wps;
+            }
+            if (nst == 16u) {
+                o[obase + j] = stg;
+                obase += 16u;
+                nst = 0u;
+            }
         }
     };
+    const uint32_t nint = nfr * (CH == 2 ? 2u : wps);  // the row's ints
     for (uint32_t t = 0; t < nmax; t++) {
         const bool act = t < nfr;
         symbol(act);
-        if (CH == 2) symbol(act);
+        if (CH == 2) {
+            symbol(act);
+            if (WV_D1_UFLUSH && (t & 7u) == 7u) {  // (uniform) every 8 frames: each row's 16 ints, or its last ones
+                if (obase + j < nint) o[obase + j] = stg;
+                obase += 16u;
+            }
+        }
     }
-    if (ok && j < nst) o[obase + j] = stg;
+    if (CH == 2 && WV_D1_UFLUSH) {
+        if (obase + j < nint) o[obase + j] = stg;
+    } else if (ok && j < nst) {
+        o[obase + j] = stg;
+    }
     if (!ok || j != 0u) return;
     if (bad || dry < 0) {
         status[bi] = ST_REDO | ((bad ? 2u : 64u) << 16);
