@@ -194,7 +194,7 @@ def pmc_traffic(kernel_substr: str = "wv_pcm_2wave<17, 17>"):
 KERNEL_NAMES = {"lane": "wv_pcm_lane<false, false, 17, 17>", "two_wave": "wv_pcm_2wave<17, 17>"}
 
 
-def verify(batches, files, pcm) -> dict:
+def verify(batches, pcm) -> dict:
     """Download every batch copy and check what its last decode produced: C2's
     int32 output equals the generator's PCM, no CRC error in any file
     (WavPackUtils.cs:273-275), and no block went through the lane kernel's
@@ -207,7 +207,7 @@ def verify(batches, files, pcm) -> dict:
             assert np.array_equal(out, pcm.reshape(-1)), "decoded PCM differs from the generator's"
         st = bb.block_status()
         unwritten += int(np.count_nonzero(st & _lib.WVG_ST_UNWRITTEN))
-        crc += sum(bb.result(i).crc_errors for i in range(len(files)) if bb.infos[i].open_ok)
+        crc += sum(bb.result(i).crc_errors for i in range(len(bb.infos)) if bb.infos[i].open_ok)
         redo += int(np.count_nonzero(st & _lib.WVG_ST_REDONE))
         blocks += int(st.size)
     assert unwritten == 0, f"{unwritten} blocks whose status no decode stored"
@@ -262,6 +262,29 @@ def cpu_decode_rate(data: bytes, threads: int, reps: int):
             assert all(r.crc_errors == 0 for r in res)
     t = float(np.median(times))
     return frames / t / 1e6, t, frames
+
+
+def cpu_baseline_c5(files, force_threads: int | None, sample: int = 400):
+    """C5's CPU baseline: the oracle over a bounded sample of the rank's files (the
+    first `sample`) on the lease's threads, one decoder context per file."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import oracle as O
+    topo = cpu_topology()
+    cps = topo["cores_per_socket"] or topo["affinity_cpus"]
+    usable = min(topo["affinity_cpus"], topo["lease_threads"] or topo["affinity_cpus"])
+    threads = force_threads or max(1, min(cps, usable))
+    part = files[:sample]
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        t0 = time.perf_counter()
+        res = list(ex.map(lambda f: O.decode_file(f, chunk=4096, max_frames=len(f) * 8), part))
+        dt = time.perf_counter() - t0
+    fr = sum(r.frames for r in res)
+    v = fr / dt / 1e6
+    return {"value": round(v, 2), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"oracle over the rank's first {len(part)} C5 files ({fr} frames) on {threads} threads, "
+                      "4096-frame calls",
+            "socket_scaled": round(v / threads * cps, 2), "cores_per_socket": cps}
 
 
 def cpu_baseline(data: bytes, reps: int, force_threads: int | None):
@@ -328,9 +351,17 @@ def run_rank(args) -> None:
         from wavpackdecoder_amd import shard
         costs = [corpora.c5_cost(i) for i in range(args.c5_files)]
         mine = shard.partition([int(c) for c in costs], ws)[rank]
-        files = [corpora.c5_file(i) for i in mine]
+        t_gen = time.perf_counter()
+        files = corpora.c5_files(mine, progress=rank == 0)
+        print(f"bench: C5 rank {rank}: {len(files)} files generated in {time.perf_counter() - t_gen:.1f} s",
+              file=sys.stderr, flush=True)
         workload = f"C5: files 0..{args.c5_files - 1} of the mixed corpus, LPT file partition over {ws} GPU(s)"
         scaling = "strong"
+    # the rank's files in slices of at most --c5-batch files (one batch each); a single
+    # slice is decoded as `inflight` copies, several slices are all decoded every step
+    slices = [files[k:k + args.c5_batch] for k in range(0, len(files), args.c5_batch)] if args.workload == "c5" \
+        else [files]
+    multi = len(slices) > 1
 
     L = _lib.lib()
     api._ctx = L.wvg_open(local)
@@ -344,15 +375,24 @@ def run_rank(args) -> None:
     inflight = args.inflight if args.inflight else (20 if args.kernel == "lane" else 3)
     inflight = max(1, min(inflight, args.steps))
     batches = []
-    for _ in range(inflight):
+    for k in range(len(slices) if multi else inflight):
         bb = DecodeBatch(4096)
         bb.set_kernel(args.kernel)
-        bb.add_files(files)  # host framing on worker threads
+        bb.add_files(slices[k] if multi else files)  # host framing on worker threads
         bb.upload()
         batches.append(bb)
     b = batches[0]
-    frames_rank = b.frames
+    frames_rank = sum(bb.frames for bb in batches) if multi else b.frames
     alg_bytes = sum(algorithmic_bytes(f) for f in files)
+    # (several slices: a step decodes every slice, all issued back to back; else step k
+    # decodes copy k % inflight)
+    def step(k):
+        if multi:
+            for bb in batches:
+                bb.decode()
+        else:
+            batches[k % len(batches)].decode()
+    extras = not multi and not args.timed_only  # the one-batch legs beside `value`
 
     # setup, untimed: one decode of every copy binds its stream to a hardware queue
     # (a copy's first decode also pays one-time costs: the queue's creation, the code
@@ -362,11 +402,11 @@ def run_rank(args) -> None:
     for bb in batches:
         bb.sync()
     for k in range(args.warmup):
-        batches[k % len(batches)].decode()
+        step(k)
     for bb in batches:
         bb.sync()
     if args.check:
-        verify(batches, files, pcm)
+        verify(batches, pcm)
     # every copy's output and block statuses are overwritten (0x7F bytes, WVG_ST_UNWRITTEN)
     # after the untimed decodes, so the check right after the timed region sees only what
     # the timed launches wrote
@@ -382,7 +422,7 @@ def run_rank(args) -> None:
         bb.sync()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        batches[k % len(batches)].decode()
+        step(k)
     t_issue = time.perf_counter()
     for bb in batches:
         bb.sync()
@@ -390,7 +430,7 @@ def run_rank(args) -> None:
     _barrier(pg)
     # the timed decodes were real: every copy's output (poisoned before the timed region,
     # and each copy's last decode is a timed one), CRCs and kernel routing
-    ver = verify(batches, files, pcm)
+    ver = verify(batches, pcm)
     ver["checked"] = "right after the timed region; outputs poisoned (0x7F) before it"
     tsum = tn = 0.0
     for bb in batches:
@@ -399,10 +439,10 @@ def run_rank(args) -> None:
         tn += n
         bb.set_timing(False)
     kernel_ms = tsum / max(tn, 1)
-    solo_ms = b.time(3) if len(batches) > 1 and not args.timed_only else kernel_ms  # nothing else in flight
+    solo_ms = b.time(3) if len(batches) > 1 and extras else kernel_ms  # nothing else in flight
     # the same K steps one batch at a time (reported beside `value`)
     serial_dt = None
-    if len(batches) > 1 and not args.timed_only:
+    if len(batches) > 1 and extras:
         _barrier(pg)
         b.sync()
         t2 = time.perf_counter()
@@ -412,7 +452,7 @@ def run_rank(args) -> None:
         serial_dt = _reduce(pg, time.perf_counter() - t2, "max")
     # the other kernel on the same batches, at its own best depth (reported beside `value`)
     other = None
-    if not args.timed_only and args.kernel == "lane":
+    if extras and args.kernel == "lane":
         nb = min(3, len(batches))
         for bb in batches[:nb]:
             bb.set_kernel("two_wave")
@@ -430,7 +470,7 @@ def run_rank(args) -> None:
     # one batch alone on the kernel the library's default (WVG_KERNEL_AUTO) picks for a
     # caller that decodes one batch at a time: the two-wave kernel (groups <= 2,048 blocks)
     auto_ms = None
-    if not args.timed_only:
+    if extras:
         b.set_kernel("two_wave")
         b.sync()
         auto_ms = b.time(3)
@@ -442,10 +482,27 @@ def run_rank(args) -> None:
 
     # PCIe-inclusive rate (host bytes in -> host int32 out, framing included),
     # reported beside `value`, never as it
-    if args.timed_only:  # profiling runs: only the timed region's launches reach the profiler
+    if args.timed_only or multi:  # profiling runs: only the timed region's launches reach the profiler
+        cpu = None
+        if multi and rank == 0 and not args.no_cpu:
+            cpu = cpu_baseline_c5(files, args.cpu_threads)
         if rank == 0:
-            print(json.dumps({"metric": METRIC, "value": round(value, 2), "kernel_ms": round(kernel_ms, 4),
-                              "batches_in_flight": len(batches), "verified": ver}), flush=True)
+            line = {"metric": METRIC, "value": round(value, 2), "unit": "Msamples/s", "n_gpus": ws,
+                    "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+                    "higher_is_better": True, "scaling": scaling, "dtype": "int32",
+                    "data": "synthetic (repo encoder; C5 seeds per file index)",
+                    "config": {"workload": workload, "files_rank0": len(files), "slices_rank0": len(slices),
+                               "blocks_rank0": sum(bb.num_blocks for bb in batches), "frames_rank0": int(frames_rank),
+                               "frames_total": int(frames_total),
+                               "parallelism": f"file-shard x{ws}, no collectives"},
+                    "kernel_ms": round(kernel_ms, 4), "per_rank_kernel_ms": [round(x, 4) for x in kms_all],
+                    "batches_in_flight": len(batches), "kernel": args.kernel, "verified": ver,
+                    "cpu_baseline": cpu}
+            if multi:
+                line["vs_cpu"] = None if cpu is None else {
+                    "measured": round(value / cpu["value"], 2),
+                    "per_gpu_vs_socket_scaled": round(value / ws / cpu["socket_scaled"], 2)}
+            print(json.dumps(line), flush=True)
         for bb in batches:
             bb.close()
         if pg is not None:
@@ -650,6 +707,8 @@ def main():
     ap.add_argument("--blocks", type=int, default=1024)
     ap.add_argument("--block-frames", type=int, default=22050)
     ap.add_argument("--c5-files", type=int, default=4000)
+    ap.add_argument("--c5-batch", type=int, default=4000,
+                    help="C5: files per batch; a rank with more files decodes all its batches every step")
     ap.add_argument("--inflight", type=int, default=None,
                     help="batch copies decoding concurrently (own buffers and streams); 1 = one batch at a time "
                          "(default: 20 for the lane kernel, 3 for the two-wave kernel, at most --steps)")

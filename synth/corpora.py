@@ -162,7 +162,9 @@ def c5_file(i: int) -> bytes:
 
 # relative device cost per frame of a block of each C5 kind (one serial chain per
 # block; DESIGN.md §6 per-mode timings): used to balance a strong-scaling split
-C5_COST = {"stereo16": 1.0, "mono16": 0.6, "stereo24": 1.6, "mono24": 1.0, "dsd0": 1.0, "dsd1": 4.5, "dsd3": 12.5}
+# (round 5: from the kinds' in-flight rates on the lane kernels -- C2 56,000, C3 57,000,
+# DSD mode 0 212,000, mode 1 7,350, mode 3 9,330 Mframes/s; mono about twice stereo)
+C5_COST = {"stereo16": 1.0, "mono16": 0.5, "stereo24": 1.0, "mono24": 0.6, "dsd0": 0.3, "dsd1": 7.6, "dsd3": 6.0}
 
 
 def c5_meta(i: int):
@@ -192,6 +194,30 @@ def c5_cost(i: int) -> float:
 def _c5_range(job):
     lo, hi = job
     return [c5_file(i) for i in range(lo, hi)]
+
+
+def c5_files(indices, progress: bool = False, workers: int | None = None):
+    """The corpus files with the given indices (worker processes; progress lines on
+    stderr for long lists)."""
+    import sys
+    idx = list(indices)
+    w = workers if workers is not None else _workers()
+    if len(idx) < 64 or w <= 1:
+        return [c5_file(i) for i in idx]
+    from concurrent.futures import ProcessPoolExecutor
+    step = 256
+    jobs = [idx[k:k + step] for k in range(0, len(idx), step)]
+    out = []
+    with ProcessPoolExecutor(max_workers=w) as ex:
+        for n, part in enumerate(ex.map(_c5_list, jobs)):
+            out += part
+            if progress and n % 40 == 39:
+                print(f"c5: {len(out)} of {len(idx)} files", file=sys.stderr, flush=True)
+    return out
+
+
+def _c5_list(ids):
+    return [c5_file(i) for i in ids]
 
 
 def c5(nfiles: int, start: int = 0, workers: int | None = None):
