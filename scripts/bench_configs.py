@@ -103,19 +103,44 @@ def run(name, files, pcm=None, iters=5, fmt=False):
     b.close()
 
 
-def run_wvc(name, wv, wvc, iters=5):
-    """A hybrid file with its .wvc: device time of the exact decode."""
-    b = DecodeBatch(4096)
-    b.add_file(wv, wvc=wvc)
-    b.upload()
+def run_wvc(name, wv, wvc, iters=5, exact=None):
+    """A hybrid file with its .wvc: device time of the exact decode (one batch; and
+    INFLIGHT copies in flight), the output checked against `exact` when given."""
+    def mk():
+        c = DecodeBatch(4096)
+        c.set_kernel(KERNEL)
+        c.add_file(wv, wvc=wvc)
+        c.upload()
+        return c
+    b = mk()
     b.decode()
     b.sync()
     ms = b.time(iters)
-    b.download()
+    out = b.download()
     r = b.result(0)
-    print(json.dumps({"config": name, "files": 1, "blocks": b.num_blocks, "frames": b.frames,
-                      "compressed_bytes": b.bytes_in, "kernel_ms": round(ms, 3),
-                      "Mframes_per_s": round(b.frames / ms / 1e3, 1), "crc_errors": int(r.crc_errors)}), flush=True)
+    st = b.block_status()
+    line = {"config": name, "files": 1, "blocks": b.num_blocks, "frames": b.frames,
+            "compressed_bytes": b.bytes_in, "kernel": KERNEL, "kernel_ms": round(ms, 3),
+            "Mframes_per_s": round(b.frames / ms / 1e3, 1), "crc_errors": int(r.crc_errors),
+            "redone_blocks": int(((st & 0x200) != 0).sum()),
+            "exact": None if exact is None else bool(np.array_equal(out[: exact.size], exact))}
+    if INFLIGHT > 1:
+        copies = [b] + [mk() for _ in range(INFLIGHT - 1)]
+        steps = 4 * INFLIGHT
+        for c in copies:
+            c.decode()
+        for c in copies:
+            c.sync()
+        t = time.perf_counter()
+        for k in range(steps):
+            copies[k % INFLIGHT].decode()
+        for c in copies:
+            c.sync()
+        line["inflight"] = INFLIGHT
+        line["Mframes_per_s_inflight"] = round(b.frames * steps / (time.perf_counter() - t) / 1e6, 1)
+        for c in copies[1:]:
+            c.close()
+    print(json.dumps(line), flush=True)
     b.close()
 
 
@@ -176,8 +201,9 @@ def main():
         elif c == "c4":
             run("C4 1024 x 22050 float32 hybrid+bitrate", [corpora.c4()])
         elif c == "c4wvc":  # C4 with its .wvc correction files: the exact decode (generic kernel)
-            wv, wvc, _ = corpora.c4_wvc()
-            run_wvc("C4 1024 x 22050 float32 hybrid+bitrate + .wvc (exact)", wv, wvc)
+            wv, wvc, ll = corpora.c4_wvc()
+            from oracle import oracle as O  # (the exactness check: the lossless encode's decode)
+            run_wvc("C4 1024 x 22050 float32 hybrid+bitrate + .wvc (exact)", wv, wvc, exact=O.decode_file(ll).samples)
         elif c == "c5":
             run(f"C5 mixed corpus, files 0..{a.c5_files - 1}", corpora.c5(a.c5_files))
         elif c.startswith("dsd"):  # dsd0 / dsd1 / dsd3: N stereo files of one 22,050-frame block in one mode

@@ -23,7 +23,8 @@ hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint3
                          uint32_t n_dsd, uint32_t fast_lo, uint32_t n_fast, const uint8_t *blob, const uint8_t *tables,
                          int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s_pcm, hipStream_t s_dsd,
                          hipStream_t s_fast, int lane_mode, uint32_t high_lo, uint32_t n_high_mono,
-                         int lane_mode_fast, uint32_t n_fast_mono);
+                         int lane_mode_fast, uint32_t n_fast_mono, int lane_mode_wvc, uint32_t n_pcm_wvc);
+bool wvc_lane_candidate(const BlockDesc &d);
 int term_set_of(const BlockDesc &d, int prefer_pipe);
 hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, uint32_t n, const uint8_t *blob,
                         int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s, int lane_mode,
@@ -166,6 +167,7 @@ struct wvg_batch {
     std::vector<uint32_t> pcm_list, dsd_list;           // wave-per-block kernels (generic PCM, DSD)
     uint32_t dsd_fast_lo = 0, dsd_fast_n = 0;          // the mode-1 range of dsd_list (sorted by kind)
     uint32_t dsd_fast_mono = 0;                        // ... its mono blocks (after the stereo ones)
+    uint32_t pcm_wvc_n = 0;                            // pcm_list's tail: .wvc lane candidates
     uint32_t dsd_high_lo = 0, dsd_high_mono = 0;       // the mode-3 range [high_lo, end): stereo, then mono blocks
     std::vector<uint32_t> ts_list[kMaxTermSets];        // two-wave kernels per term set
     int64_t gframes[kSide] = {0};                       // frames per launch group (the lane assignment's load)
@@ -1041,6 +1043,11 @@ int wvg_batch_upload(wvg_batch *b) {
         return p.nframes != q.nframes ? p.nframes > q.nframes : x < y;
     };
     std::sort(b->pcm_list.begin(), b->pcm_list.end(), by_kind_len);
+    // the .wvc lane kernel's candidates at the tail (longest first there too)
+    b->pcm_wvc_n = (uint32_t)(b->pcm_list.end() -
+                              std::stable_partition(b->pcm_list.begin(), b->pcm_list.end(), [&](uint32_t k) {
+                                  return !wvc_lane_candidate(b->fo.descs[k]);
+                              }));
     std::sort(b->dsd_list.begin(), b->dsd_list.end(), by_kind_len);
     // the mode-1 blocks are one range of the kind-sorted list (their own kernel)
     b->dsd_fast_lo = b->dsd_fast_n = b->dsd_fast_mono = 0;
@@ -1243,7 +1250,8 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
     HIPCHK(c, launch_decode(b->d_descs, b->d_pcml, (uint32_t)b->pcm_list.size(), b->d_dsd, (uint32_t)b->dsd_list.size(),
                             b->dsd_fast_lo, b->dsd_fast_n, b->d_blob, b->d_tables, b->d_out, b->d_status, b->d_mute,
                             slot(kPcm), slot(kDsd), slot(kDsd1), mode_of(b->dsd_list.size() - b->dsd_high_lo),
-                            b->dsd_high_lo, b->dsd_high_mono, mode_of(b->dsd_fast_n), b->dsd_fast_mono));
+                            b->dsd_high_lo, b->dsd_high_mono, mode_of(b->dsd_fast_n), b->dsd_fast_mono,
+                            mode_of(b->pcm_wvc_n), b->pcm_wvc_n));
     HIPCHK(c, mark(kDsd));
     HIPCHK(c, mark(kDsd1));
     HIPCHK(c, mark(kPcm));

@@ -85,24 +85,42 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_pcm_wave(const BlockD
                                                                     const uint8_t *__restrict__ blob,
                                                                     int32_t *__restrict__ out,
                                                                     uint32_t *__restrict__ status,
-                                                                    uint32_t *__restrict__ aux) {
+                                                                    uint32_t *__restrict__ aux, uint32_t mode) {
     // the decode state in LDS: every lane of the (wave-uniform) decode reads and writes
     // the same values; in registers its run-time indexed pass rings went to scratch
     __shared__ PcmState ps;
     const uint32_t bi = list[blockIdx.x];
     const BlockDesc &d = descs[bi];
+    // mode bit 2: only the blocks the .wvc lane kernel handed back (ST_REDO)
+    if ((mode & 4u) && !(status[bi] & lane::ST_REDO)) return;
     if (d.chain_len >= 2) {
         decode_chain(descs, bi, blob, out, status, aux, ps);
         return;
     }
     const bool lead = threadIdx.x == 0;
     DevStoreWave st{out + d.out_off, (uint64_t)d.pre_end * d.out_nch, lead};
-    uint32_t exc = aux[bi];
-    const uint32_t s = d.fstatus | decode_pcm_block_in(ps, d, blob, st, &exc);
+    uint32_t exc = (mode & 4u) ? 0u : aux[bi];
+    const uint32_t s = d.fstatus | decode_pcm_block_in(ps, d, blob, st, &exc) | ((mode & 4u) ? (uint32_t)ST_REDONE : 0u);
     if (lead) {
         status[bi] = s;
         aux[bi] = exc;
     }
+}
+
+// hybrid stereo blocks of WavPack's default list with their .wvc stream (HYBRID_BITRATE,
+// no HYBRID_BALANCE, not int32; no sticky state, seek or exact float): the .wvc lane
+// kernel's candidates (wv_lane.h, HY == 2), the tail of the generic kernel's list
+bool wvc_lane_candidate(const BlockDesc &d) {
+    using namespace wvf;
+    if (d.kind != KIND_PCM || !d.wvc_len || (d.flags & MONO_DATA) || d.out_nch != 2) return false;
+    if ((d.flags & (HYBRID_FLAG | HYBRID_BITRATE | HYBRID_BALANCE | INT32_DATA)) != (HYBRID_FLAG | HYBRID_BITRATE))
+        return false;
+    if (d.chain_len >= 2 || d.inherit || d.xfloat || d.wvx_state || d.pre_end || d.fstatus) return false;
+    static const int8_t def[5] = {WVG_TS_DEFAULT};
+    if (d.num_terms != 5) return false;
+    for (int i = 0; i < 5; i++)
+        if (d.term[i] != def[i]) return false;
+    return true;
 }
 
 // Mode 3's starting probability table for every rate_i (init_ptable,
@@ -1330,7 +1348,7 @@ hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint3
                          uint32_t n_dsd, uint32_t fast_lo, uint32_t n_fast, const uint8_t *blob, const uint8_t *tables,
                          int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s_pcm, hipStream_t s_dsd,
                          hipStream_t s_fast, int lane_mode, uint32_t high_lo, uint32_t n_high_mono,
-                         int lane_mode_fast, uint32_t n_fast_mono) {
+                         int lane_mode_fast, uint32_t n_fast_mono, int lane_mode_wvc, uint32_t n_pcm_wvc) {
     // the DSD kernels first: their blocks are the batch's longest serial chains
     const uint32_t skip = n_fast ? 1u : 0u;
     const uint32_t n_high = lane_mode ? n_dsd - high_lo : 0u;
@@ -1362,8 +1380,25 @@ hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint3
                                status, aux, 0u);
         }
     }
-    if (n_pcm)
-        hipLaunchKernelGGL(wv_decode_pcm_wave, dim3(n_pcm), dim3(64), 0, s_pcm, descs, pcm_list, blob, out, status, aux);
+    if (n_pcm && lane_mode_wvc && n_pcm_wvc) {
+        // the list's tail: hybrid default-list blocks with a .wvc stream on the .wvc lane
+        // kernel, then what it handed back on the generic kernel (the head as usual)
+        const uint32_t nh = n_pcm - n_pcm_wvc;
+        const uint32_t *tl = pcm_list + nh;
+        dim3 gl((n_pcm_wvc + 64 * lane::LPAIRS - 1) / (64 * lane::LPAIRS)), bl(64 * lane::LPAIRS * 2);
+        if (hipError_t e = launch_lane(LANE_HY_WVC, gl, bl, s_pcm, descs, tl, n_pcm_wvc, blob, out, status, nullptr);
+            e != hipSuccess)
+            return e;
+        if (nh)
+            hipLaunchKernelGGL(wv_decode_pcm_wave, dim3(nh), dim3(64), 0, s_pcm, descs, pcm_list, blob, out, status, aux,
+                               0u);
+        if (lane_mode_wvc != 2)  // 2: the lane kernel alone (diagnostics: ST_REDO stays in the status)
+            hipLaunchKernelGGL(wv_decode_pcm_wave, dim3(n_pcm_wvc), dim3(64), 0, s_pcm, descs, tl, blob, out, status,
+                               aux, 4u);
+    } else if (n_pcm) {
+        hipLaunchKernelGGL(wv_decode_pcm_wave, dim3(n_pcm), dim3(64), 0, s_pcm, descs, pcm_list, blob, out, status, aux,
+                           0u);
+    }
     return hipGetLastError();
 }
 

@@ -122,6 +122,25 @@ struct LPass {
             R = sb;
         }
     }
+    // .wvc (HY == 2): the frame with the exact-minus-lossy differences cL / cR carried
+    // along (pass_stereo_wvc, wv_decode_core.h): a pass predicting from history moves
+    // both values alike; -1 / -2 predict one channel from the other's output of this
+    // pass, the exact one from the exact output with the same (not yet updated) weight
+    template <int U, bool MONO>
+    __device__ __forceinline__ void frame_wvc(int32_t &L, int32_t &R, int32_t &cL, int32_t &cR) {
+        using namespace wvf;
+        if constexpr (T == -1) {
+            const int32_t w0 = wB;
+            frame<U, MONO>(L, R);
+            cR = add32(cR, sub32(aw(w0, add32(L, cL)), aw(w0, L)));
+        } else if constexpr (T == -2) {
+            const int32_t w0 = wA;
+            frame<U, MONO>(L, R);
+            cL = add32(cL, sub32(aw(w0, add32(R, cR)), aw(w0, R)));
+        } else {
+            frame<U, MONO>(L, R);
+        }
+    }
     // could a weight leave int16 within the next group?  (the (short) stores at
     // pass-call seams, B-4, are the identity while it cannot; negative terms stay
     // within +-1024)
@@ -139,6 +158,8 @@ struct LChain<> {
     __device__ __forceinline__ void init(const BlockDesc &, int) {}
     template <int U, bool MONO>
     __device__ __forceinline__ void frame(int32_t &, int32_t &) {}
+    template <int U, bool MONO>
+    __device__ __forceinline__ void frame_wvc(int32_t &, int32_t &, int32_t &, int32_t &) {}
     __device__ __forceinline__ bool wbad() const { return false; }
 };
 template <int T, int... Ts>
@@ -153,6 +174,11 @@ struct LChain<T, Ts...> {
     __device__ __forceinline__ void frame(int32_t &L, int32_t &R) {
         p.template frame<U, MONO>(L, R);
         rest.template frame<U, MONO>(L, R);
+    }
+    template <int U, bool MONO>
+    __device__ __forceinline__ void frame_wvc(int32_t &L, int32_t &R, int32_t &cL, int32_t &cR) {
+        p.template frame_wvc<U, MONO>(L, R, cL, cR);
+        rest.template frame_wvc<U, MONO>(L, R, cL, cR);
     }
     __device__ __forceinline__ bool wbad() const { return p.wbad() || rest.wbad(); }
 };
@@ -207,6 +233,17 @@ __device__ __forceinline__ uint4 ff_unit(uint4 v, uint32_t u, uint32_t e) {
     v.w = ff_tail(v.w, b + 12, e);
     return v;
 }
+
+// .wvc correction stream window (HY == 2; cwin_init / cwin_merge / cwin_corr below)
+struct CWin {
+    const uint32_t *w;  // the stream's dword-aligned base
+    uint64_t win;       // LSB = next bit
+    int32_t nb;         // valid bits (>= 33 at every word start)
+    uint32_t q0, ld;    // the next dword, and the load of the one after (consumed a refill later)
+    uint32_t ni;        // index of the dword in ld
+    uint32_t used;      // bits consumed (checked against end at the block's end)
+    uint32_t end;       // the stream's bits (from its first bit)
+};
 
 struct LState {
     uint64_t win;  // bit window, LSB = next bit; bits at or above nb are zero
@@ -347,7 +384,7 @@ __device__ __forceinline__ void lhy_errlim(LState &s, const uint8_t *ring, bool 
 // lane that is done idles through them).  The reference's 64-bit bounds: the lane
 // hands back a word whose high reaches 2^31, and a bisection past the 31 bits of x.
 __device__ __forceinline__ void lhy_code(uint32_t x, uint32_t low, uint32_t mc, int32_t el, uint32_t &mid,
-                                         uint32_t &used, uint32_t &bad) {
+                                         uint32_t &used, uint32_t &bad, uint32_t &lo_f, uint32_t &n_f) {
     const uint32_t z = (uint32_t)__builtin_clz(mc | 1u);
     const uint32_t ex = (0xFFFFFFFFu >> z) - mc;
     const uint32_t nbt = z ^ 31u;
@@ -374,6 +411,59 @@ __device__ __forceinline__ void lhy_code(uint32_t x, uint32_t low, uint32_t mc, 
     bad |= ((low | (low + mc)) >= 0x80000000u || ub > 31u) ? 2u : 0u;
     mid = el == 0 ? mid_rc : lo + (n >> 1);
     used = el == 0 ? used_rc : min(ub, 31u);
+    lo_f = lo;  // the final interval [lo, lo + n - 1] (the .wvc code's range)
+    n_f = n;
+}
+
+// ---- .wvc correction stream (HY == 2; beyond the reference: WavPack 4's get_word) ----
+// A hybrid word the error limit left inexact (el != 0) reads its exact magnitude as
+// read_code(wvcbits, high - low) + low from the block's ID_WVC_BITSTREAM; the
+// parser hands the reconstruction exact-minus-lossy (corr), which it carries through
+// the passes (LPass::frame_wvc).  Each lane reads its correction stream through a
+// 64-bit register window merged from dwords loaded a refill ahead (global loads: the
+// stream is sparse beside the main one); a lane whose reads pass the stream's end
+// hands its block back (its bytes past the end would read 0xFF there).
+
+__device__ __forceinline__ void cwin_init(CWin &c, const uint8_t *blob, uint64_t off, uint32_t len) {
+    const uint32_t sh = (uint32_t)(off & 3u);
+    c.w = (const uint32_t *)(blob + (off - sh));
+    c.win = ((uint64_t)c.w[0] | ((uint64_t)c.w[1] << 32)) >> (8u * sh);
+    c.nb = 64 - 8 * (int32_t)sh;
+    c.q0 = c.w[2];
+    c.ld = c.w[3];
+    c.ni = 4;
+    c.used = 0;
+    c.end = len * 8u;
+}
+__device__ __forceinline__ void cwin_merge(CWin &c) {  // keep >= 33 bits: merge q0 when 32 or fewer are left
+    const uint32_t mg = (uint32_t)((c.nb - 33) >> 31);  // ~0: merge
+    const uint32_t sh = (uint32_t)c.nb;
+    __builtin_assume(sh < 64u);
+    c.win |= (uint64_t)(c.q0 & mg) << sh;
+    c.nb += (int32_t)(mg & 32u);
+    c.q0 = mg ? c.ld : c.q0;
+    c.ni += mg & 1u;
+    c.ld = c.w[c.ni];  // (reads stay within 12 bytes past the stream: the blob's tail)
+}
+// exact - lossy for a word of sign sg (0 / -1), lossy magnitude mid, final interval
+// (lo, n), error limit el (0: the word was exact, nothing is read)
+__device__ __forceinline__ int32_t cwin_corr(CWin &c, int32_t el, uint32_t mid, int32_t sg, uint32_t lo, uint32_t n) {
+    const uint32_t mc = n - 1u;  // high - low
+    const uint32_t x = (uint32_t)c.win;
+    const uint32_t z = (uint32_t)__builtin_clz(mc | 1u);
+    const uint32_t ex = (0xFFFFFFFFu >> z) - mc;
+    const uint32_t nbt = z ^ 31u;
+    const uint32_t v = __builtin_amdgcn_ubfe(x, 0, nbt);
+    const bool big = v >= ex;
+    const uint32_t code = big ? 2u * v + __builtin_amdgcn_ubfe(x, nbt, 1) - ex : v;
+    const uint32_t used = el != 0 ? nbt + (big ? 1u : 0u) : 0u;
+    c.win >>= used;
+    c.nb -= (int32_t)used;
+    c.used += used;
+    cwin_merge(c);
+    const uint32_t value = lo + code;
+    const uint32_t d = sg ? mid - value : value - mid;
+    return el != 0 ? (int32_t)d : 0;
 }
 // slow_level after a word (HYBRID_BITRATE, :501-502): slow - (slow + SLO) >> SLS + mylog2(mid)
 // (mylog2, WordsUtils.cs:588-608: the 8 bits below the leading one index the table)
@@ -397,6 +487,7 @@ __device__ __forceinline__ int32_t lhy_decay(int32_t slow) {  // a zero-run zero
 struct LW {
     uint32_t x, low, mc;
     int32_t v;
+    int32_t corr;  // HY == 2: the .wvc's exact minus this lossy value
 };
 
 // get_words for one residual of channel C (WordsUtils.cs:290-503, lossless:
@@ -409,8 +500,8 @@ struct LW {
 // run (zskip) runs the word as a held zero over all-zero medians that consumes
 // nothing, which leaves its state as it was -- and the checks it feeds are those
 // of the word that ends the run, which reads the same window with the same state.
-template <int C, bool HY = false>
-__device__ __forceinline__ LW lword(LState &s, const uint8_t *ring, uint32_t rbase) {
+template <int C, int HY = false>
+__device__ __forceinline__ LW lword(LState &s, const uint8_t *ring, uint32_t rbase, CWin &cw) {
     using namespace wvf;
     // zero-run mode (:304-352): both channels' median[0] < 2, nothing held
     const uint64_t h0m0 = lmask(s.keep == 0u), h1m0 = lmask(s.h1 != 0u);
@@ -478,9 +569,9 @@ __device__ __forceinline__ LW lword(LState &s, const uint8_t *ring, uint32_t rba
                                 vselmi(ob, 0, csel<-2, 5>(o2))));
     // read_code(high - low = mc) (WordsUtils.cs:546-570), then the sign bit
     const uint32_t x = (uint32_t)s.win;
-    uint32_t mid, used;
+    uint32_t mid, used, lo_f = 0u, n_f = 1u;
     if constexpr (HY) {
-        lhy_code(x, low, mc, s.el[C], mid, used, s.bad);
+        lhy_code(x, low, mc, s.el[C], mid, used, s.bad, lo_f, n_f);
         s.slack = min(s.slack, 31 - (int32_t)used);  // (the sign must lie in x)
     } else {
         const uint32_t z = (uint32_t)__builtin_clz(mc | 1u);
@@ -500,6 +591,8 @@ __device__ __forceinline__ LW lword(LState &s, const uint8_t *ring, uint32_t rba
     w.x = vselm(zm, 0u, x);
     w.low = vselm(zm, 0u, low);
     w.mc = vselm(zm, 0u, mc);
+    w.corr = 0;
+    if constexpr (HY == 2) w.corr = cwin_corr(cw, zskip ? 0 : s.el[C], mid, sg, lo_f, n_f);
     if constexpr (HY) s.slow[C] = zskip ? s.slow[C] : lhy_slow(s.slow[C], mid, ring);
     lrefill(s, ring, rbase);
     return w;
@@ -563,6 +656,7 @@ __device__ __forceinline__ LW lword_fast(LState &s, const uint8_t *ring, uint32_
     w.x = x & (zsk - 1u);
     w.low = low & (zsk - 1u);
     w.mc = mc & (zsk - 1u);
+    w.corr = 0;
     lrefill(s, ring, rbase);
     return w;
 }
@@ -595,8 +689,8 @@ __device__ __forceinline__ void lmerge(LState &s, const uint8_t *ring) {
 // past it shows as slack < 0, and the group is replayed by the checked words)
 // W32: 32-bit products (C#'s int wrap) for groups whose medians pass the 24-bit
 // operands (pgroup_try: below 2^29 at the group's start, so none wraps in the group)
-template <int C, bool SPLIT, bool HY = false, bool W32 = false>
-__device__ __forceinline__ LW lword_nz(LState &s, const uint8_t *ring, uint32_t rbase) {
+template <int C, bool SPLIT, int HY = false, bool W32 = false>
+__device__ __forceinline__ LW lword_nz(LState &s, const uint8_t *ring, uint32_t rbase, CWin &cw) {
     static_assert(!HY || SPLIT, "a hybrid word's bisection bits follow a refill");
     using namespace wvf;
     const uint32_t lo = (uint32_t)s.win, hi = (uint32_t)(s.win >> 32);
@@ -646,9 +740,9 @@ __device__ __forceinline__ LW lword_nz(LState &s, const uint8_t *ring, uint32_t 
     } else {
         x = __builtin_amdgcn_alignbit(hi, lo, q);
     }
-    uint32_t mid, used;
+    uint32_t mid, used, lo_f = 0u, n_f = 1u;
     if constexpr (HY) {
-        lhy_code(x, low, mc, s.el[C], mid, used, s.bad);
+        lhy_code(x, low, mc, s.el[C], mid, used, s.bad, lo_f, n_f);
         s.slack = min(s.slack, 31 - (int32_t)used);  // (the sign must lie in x)
     } else {
         const uint32_t z = (uint32_t)__builtin_clz(mc | 1u);
@@ -671,7 +765,9 @@ __device__ __forceinline__ LW lword_nz(LState &s, const uint8_t *ring, uint32_t 
 #ifdef WV_LANE_WORD_BARRIER  // (experiment: words in program order, the ring read a word ahead of its use)
     __builtin_amdgcn_sched_barrier(WV_LANE_WORD_BARRIER);
 #endif
-    return LW{x, low, mc, (int32_t)(mid ^ (uint32_t)sg)};
+    int32_t corr = 0;
+    if constexpr (HY == 2) corr = cwin_corr(cw, s.el[C], mid, sg, lo_f, n_f);
+    return LW{x, low, mc, (int32_t)(mid ^ (uint32_t)sg), corr};
 }
 
 // ---------------------------------------------------------------------------
@@ -701,48 +797,51 @@ struct LShared {
 __device__ __forceinline__ uint32_t rpos(const LState &s) { return s.rp + (((s.ra0 - s.ra) & RSLOT) >> 8); }
 
 // the parser's verdict for its lane now (after the block's last frame)
-__device__ __forceinline__ uint32_t pverdict(const LState &s, uint32_t u0) {
-    const uint32_t r = s.bad | (s.pmax >= 17u ? 16u : 0u) | (s.slack < 0 ? 32u : 0u) | (rpos(s) >= u0 * 4u ? 64u : 0u);
+template <int HY>
+__device__ __forceinline__ uint32_t pverdict(const LState &s, uint32_t u0, const CWin &cw) {
+    uint32_t r = s.bad | (s.pmax >= 17u ? 16u : 0u) | (s.slack < 0 ? 32u : 0u) | (rpos(s) >= u0 * 4u ? 64u : 0u);
+    if constexpr (HY == 2) r |= cw.used > cw.end ? 1u : 0u;  // (a correction read past its stream)
     return 0x80000000u | r | ((s.bad0 ? s.bad0 : r) << 8);
 }
 
 // word kinds: WK_CHECKED lword, WK_FAST lword_fast, WK_NORUN / WK_NORUN_SPLIT lword_nz
 enum { WK_CHECKED = 0, WK_FAST = 1, WK_NORUN = 2, WK_NORUN_SPLIT = 3, WK_NORUN_SPLIT32 = 4 };
-template <int K, int C, bool HY>
-__device__ __forceinline__ LW lword_k(LState &s, const uint8_t *ring, uint32_t rb) {
-    if constexpr (K == WK_NORUN) return lword_nz<C, false, false>(s, ring, rb);  // (not HY: pgroup_try)
-    else if constexpr (K == WK_NORUN_SPLIT) return lword_nz<C, true, HY>(s, ring, rb);
-    else if constexpr (K == WK_NORUN_SPLIT32) return lword_nz<C, true, HY, true>(s, ring, rb);
+template <int K, int C, int HY>
+__device__ __forceinline__ LW lword_k(LState &s, const uint8_t *ring, uint32_t rb, CWin &cw) {
+    if constexpr (K == WK_NORUN) return lword_nz<C, false, false>(s, ring, rb, cw);  // (not HY: pgroup_try)
+    else if constexpr (K == WK_NORUN_SPLIT) return lword_nz<C, true, HY>(s, ring, rb, cw);
+    else if constexpr (K == WK_NORUN_SPLIT32) return lword_nz<C, true, HY, true>(s, ring, rb, cw);
     else if constexpr (K == WK_FAST) return lword_fast<C>(s, ring, rb);
-    else return lword<C, HY>(s, ring, rb);
+    else return lword<C, HY>(s, ring, rb, cw);
 }
-template <int U, bool FULL, int FAST, bool MONO, bool HY, bool CODES>
+template <int U, bool FULL, int FAST, bool MONO, int HY, bool CODES>
 __device__ __forceinline__ void pframe(LState &s, const uint8_t *ring, uint32_t rb, LShared &sh, uint32_t lane,
-                                       uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin) {
+                                       uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin, CWin &cw) {
     const uint32_t t = g0 + U;
     const uint32_t slot = (((g0 % (uint32_t)RF) + U) << 6) + lane;  // (GF divides RF: no wrap inside a group)
-    const LW w0 = lword_k<FAST, 0, HY>(s, ring, rb);
+    const LW w0 = lword_k<FAST, 0, HY>(s, ring, rb, cw);
     LW w1 = {0u, 0u, 0u, 0};
-    if constexpr (!MONO) w1 = lword_k<FAST, 1, HY>(s, ring, rb);
+    if constexpr (!MONO) w1 = lword_k<FAST, 1, HY>(s, ring, rb, cw);
     if constexpr (CODES) {
         sh.rq[slot] = make_int4((int32_t)w0.x, (int32_t)w0.low, (int32_t)w1.x, (int32_t)w1.low);
         sh.rm[slot] = make_int2((int32_t)w0.mc, (int32_t)w1.mc);
     } else {
         sh.rm[slot] = make_int2(w0.v, w1.v);
+        if constexpr (HY == 2) *(int2 *)&sh.rq[slot] = make_int2(w0.corr, w1.corr);  // (rq is free without CODES)
     }
-    if (!FULL && t + 1u == nfr) pfin = pverdict(s, u0);
+    if (!FULL && t + 1u == nfr) pfin = pverdict<HY>(s, u0, cw);
 }
-template <bool FULL, int FAST, bool MONO, bool HY, bool CODES>
+template <bool FULL, int FAST, bool MONO, int HY, bool CODES>
 __device__ __forceinline__ void pgroup(LState &s, const uint8_t *ring, uint32_t rb, LShared &sh, uint32_t lane,
-                                       uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin) {
-    pframe<0, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
-    pframe<1, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
-    pframe<2, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
-    pframe<3, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
-    pframe<4, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
-    pframe<5, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
-    pframe<6, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
-    pframe<7, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
+                                       uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin, CWin &cw) {
+    pframe<0, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
+    pframe<1, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
+    pframe<2, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
+    pframe<3, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
+    pframe<4, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
+    pframe<5, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
+    pframe<6, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
+    pframe<7, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
 }
 // a group: the fast words first -- the no-run words when no live lane can meet a
 // zero run in it (lword_nz), else lword_fast; if a live lane met a rare word, the
@@ -769,10 +868,10 @@ struct LCount {
     uint64_t wait_consumed, wait_loads;  // cycles in the group-start wait and the group-end load wait
     uint64_t words, stage;               // cycles in the group's words (pgroup_try) and in its ring stores
 };
-template <bool FULL, bool MONO, bool HY, bool CODES>
+template <bool FULL, bool MONO, int HY, bool CODES>
 __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint32_t rb, LShared &sh, uint32_t lane,
                                            uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin, uint32_t mm,
-                                           LCount &cnt) {
+                                           LCount &cnt, CWin &cw) {
     LCNT(cnt.groups++);
     // (every wave-wide test below is one compare of a lane value -- a compound
     // condition would go through SALU mask logic, ~20 cycles each way)
@@ -788,6 +887,7 @@ __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint3
         for (int u = 0; u < GF; u++) {
             const uint32_t slot = (((g0 % (uint32_t)RF) + u) << 6) + lane;
             if constexpr (CODES) sh.rq[slot] = make_int4(0, 0, 0, 0);
+            if constexpr (HY == 2) *(int2 *)&sh.rq[slot] = make_int2(0, 0);
             sh.rm[slot] = make_int2(0, 0);
             if constexpr (HY) {  // every zero of a run decays its channel's slow_level
                 s.slow[0] = lhy_decay(s.slow[0]);
@@ -795,7 +895,7 @@ __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint3
             }
         }
         s.zacc -= WPG;
-        if (!FULL && livem && nfr <= g0 + GF) pfin = pverdict(s, u0);
+        if (!FULL && livem && nfr <= g0 + GF) pfin = pverdict<HY>(s, u0, cw);
         LCNT(cnt.bulk++);
         return;
     }
@@ -809,12 +909,14 @@ __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint3
     const bool allnr = lmask((runnable & livem) != 0u) == 0ull &&
                        !(HY && ((WV_LANE_HY_PATH == 1 && m26) || WV_LANE_HY_PATH == 2));
     if (__builtin_expect(m26 && !allnr, 0)) {
-        pgroup<FULL, WK_CHECKED, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
+        pgroup<FULL, WK_CHECKED, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
         s.bad |= s.slack < 0 ? 32u : 0u;
         LCNT(cnt.checked++);
         return;
     }
     const LState s0 = s;
+    CWin cw0;  // (copied only where it is used: a copy of the unused window went to scratch)
+    if constexpr (HY == 2) cw0 = cw;
     const uint32_t pfin0 = pfin;
     if (allnr) {
         // a word may count on 33 bits: 17 of unary count (16 ones are an escape) and a
@@ -823,34 +925,35 @@ __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint3
         // between a word's parts (a group with a longer word goes to the checked words)
         s.rmax = 0u;
         if (__builtin_expect(m26, 0)) {  // (medians below 2^29, none wraps in the group; or hybrid words)
-            pgroup<FULL, WK_NORUN_SPLIT32, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
+            pgroup<FULL, WK_NORUN_SPLIT32, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
             lmerge(s, ring);
             LCNT(cnt.split++);
         } else if (!HY && lmask(mml >= (1u << 17)) == 0ull) {
-            pgroup<FULL, WK_NORUN, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
+            pgroup<FULL, WK_NORUN, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
             LCNT(cnt.norun++);
         } else {
-            pgroup<FULL, WK_NORUN_SPLIT, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
+            pgroup<FULL, WK_NORUN_SPLIT, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
             lmerge(s, ring);  // (the next group's words start from >= 33 bits)
             LCNT(cnt.split++);
         }
         s.rare = s.rmax >> 4;  // (an escape: the checked words)
     } else if constexpr (HY) {  // (no run-aware fast words for hybrid blocks: the checked words)
         s.slack = 0;
-        pgroup<FULL, WK_CHECKED, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
+        pgroup<FULL, WK_CHECKED, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
         s.bad |= s.slack < 0 ? 32u : 0u;
         LCNT(cnt.checked++);
         return;
     } else {
         s.rare = 0u;
-        pgroup<FULL, WK_FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
+        pgroup<FULL, WK_FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
         LCNT(cnt.fast++);
     }
     if (__builtin_expect(lmask(((s.rare | ((uint32_t)s.slack >> 31)) & livem) != 0u) != 0ull, 0)) {
         s = s0;
+        if constexpr (HY == 2) cw = cw0;
         pfin = pfin0;
         s.slack = 0;
-        pgroup<FULL, WK_CHECKED, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
+        pgroup<FULL, WK_CHECKED, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
         s.bad |= s.slack < 0 ? 32u : 0u;
         LCNT(cnt.replay++);
     }
@@ -885,7 +988,7 @@ __device__ __forceinline__ void st2(int32_t *p, int2 v) {
 // MONO: one sample per frame (UnpackUtils.cs:571-588: crc = 3 crc + v), stored once, or
 // twice for FALSE_STEREO (fst; :655-664, after the fixup)
 // HY: the whole fixup (fixup_tail: float_values, or the lossy clip and shift), else the shift
-template <bool HY>
+template <int HY>
 __device__ __forceinline__ int32_t lfix(int32_t x, uint32_t sh, const Fixup &fx) {
     if constexpr (HY) return fixup_tail(fx, x);
     else return (int32_t)((uint32_t)x << sh);
@@ -903,7 +1006,7 @@ __device__ __forceinline__ int32_t rdecode(uint32_t x, uint32_t low, uint32_t mc
     const int32_t sg = __builtin_amdgcn_sbfe((int32_t)x, used, 1);
     return (int32_t)(add3(low, v, big ? t : 0u) ^ (uint32_t)sg);
 }
-template <int U, bool FULL, bool MONO, bool HY, bool CODES, int... Ts>
+template <int U, bool FULL, bool MONO, int HY, bool CODES, int... Ts>
 __device__ __forceinline__ void rframe(LChain<Ts...> &ch, const LShared &shr, uint32_t lane, uint32_t g0, uint32_t nfr,
                                        bool joint, int32_t &mx, int32_t &mn, uint32_t &crc, uint32_t sh, int32_t *o,
                                        uint32_t rbad, const LEnd &e, bool fst, const Fixup &fx) {
@@ -919,7 +1022,15 @@ __device__ __forceinline__ void rframe(LChain<Ts...> &ch, const LShared &shr, ui
         L = r.x;
         R = r.y;
     }
-    ch.template frame<U, MONO>(L, R);
+    if constexpr (HY == 2) {  // the exact values; the passes keep the lossy history
+        const int2 c = *(const int2 *)&shr.rq[slot];
+        int32_t cL = c.x, cR = c.y;
+        ch.template frame_wvc<U, MONO>(L, R, cL, cR);
+        L = wvf::add32(L, cL);
+        R = wvf::add32(R, cR);
+    } else {
+        ch.template frame<U, MONO>(L, R);
+    }
     if constexpr (MONO) {
         mx = max(mx, L);
         mn = min(mn, L);
@@ -957,11 +1068,11 @@ __device__ __forceinline__ void rframe(LChain<Ts...> &ch, const LShared &shr, ui
 // the parser's chain -- for term lists whose reconstruction has the room (the 16-term
 // lists' passes already load it more than the words load the parser); hybrid words
 // (bisection) hand over values
-template <bool HY, int... Ts>
+template <int HY, int... Ts>
 constexpr bool lane_codes() { return !HY && sizeof...(Ts) <= 5; }
 
 // can this lane decode block d exactly (else ST_REDO)?
-template <bool MONO, bool HY, int... Ts>
+template <bool MONO, int HY, int... Ts>
 __device__ __forceinline__ bool lane_ok(const BlockDesc &d) {
     using namespace wvf;
     if (d.kind != KIND_PCM) return false;
@@ -973,7 +1084,8 @@ __device__ __forceinline__ bool lane_ok(const BlockDesc &d) {
         return false;
     }
     if (((d.flags & MONO_DATA) != 0) != MONO) return false;
-    if (d.inherit || d.chain_len >= 2 || d.wvx_state || d.wvc_len || d.xfloat || d.pre_end || d.fstatus) return false;
+    if ((d.wvc_len != 0) != (HY == 2)) return false;  // HY 2: hybrid blocks with their .wvc stream
+    if (d.inherit || d.chain_len >= 2 || d.wvx_state || d.xfloat || d.pre_end || d.fstatus) return false;
     if (d.num_terms != (int32_t)sizeof...(Ts)) return false;
     constexpr int8_t terms[sizeof...(Ts) + 1] = {(int8_t)Ts..., 0};
     for (int i = 0; i < (int)sizeof...(Ts); i++)
@@ -986,7 +1098,7 @@ struct LBlock {
     uint32_t bi, nfr, nmax, nmin;
     bool ok, inl;
 };
-template <bool MONO, bool HY, int... Ts>
+template <bool MONO, int HY, int... Ts>
 __device__ __forceinline__ LBlock lane_block(const BlockDesc *descs, const uint32_t *list, uint32_t n, uint32_t grp,
                                              uint32_t lane) {
     LBlock b;
@@ -1020,7 +1132,7 @@ __device__ __forceinline__ bool lwait(uint32_t *ctr, uint32_t v, uint32_t *abort
     return false;
 }
 
-template <bool MONO, bool HY, int... Ts>
+template <bool MONO, int HY, int... Ts>
 __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
                                             uint32_t n, const uint8_t *__restrict__ blob, LShared &sh,
                                             uint8_t *ringm, uint32_t pair, uint32_t grp, uint32_t lane,
@@ -1084,6 +1196,10 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
         s.dlt[c] = HY ? d.bitrate_delta[c] : 0;
         s.el[c] = 0;
     }
+    // (every field set in every instantiation: left undefined, they stay memory -- scratch)
+    CWin cw;  // the .wvc stream (HY == 2; a local of its own: in LState it went to scratch)
+    if constexpr (HY == 2) cwin_init(cw, blob, lb.ok ? d.wvc_off : 0u, lb.ok ? d.wvc_len : 0u);
+    else cw = CWin{(const uint32_t *)blob, 0ull, 0, 0u, 0u, 0u, 0u, 0u};
     uint32_t pfin = 0u;
     uint32_t cpre = 0u;  // the recon's consumed count, read a group ahead (a lower bound: it only grows)
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), lgkm/exp untouched: the loop's waits count only its own loads
@@ -1114,9 +1230,9 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
         fu = u0 + nld;
         const uint64_t tg0 = (WV_LANE_COUNTERS && dbg) ? __builtin_readcyclecounter() : 0;
         if (g0 + GF < lb.nmin)  // (strict: the group holding a block's last frame records its verdict)
-            pgroup_try<true, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, mm, cnt);
+            pgroup_try<true, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, mm, cnt, cw);
         else
-            pgroup_try<false, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, mm, cnt);
+            pgroup_try<false, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, mm, cnt, cw);
         if (WV_LANE_COUNTERS && dbg) cnt.words += __builtin_readcyclecounter() - tg0;
         // the reader stayed inside the units written before this group
         s.rp = rpos(s);
@@ -1168,7 +1284,7 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
     }
 }
 
-template <bool MONO, bool HY, int... Ts>
+template <bool MONO, int HY, int... Ts>
 __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
                                            uint32_t n, int32_t *__restrict__ out, uint32_t *__restrict__ status,
                                            LShared &sh, uint32_t grp, uint32_t lane) {
@@ -1233,7 +1349,7 @@ __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, 
 // waves on one SIMD: measured with 20 batches in flight, 16-unit rings (68 KiB per
 // workgroup, two per CU possible) ran at ~30,000 Msamples/s on most runs and
 // ~47,000 on some; a workgroup per CU keeps every launch at its one-batch time.
-template <bool MONO, bool HY, int... Ts>
+template <bool MONO, int HY, int... Ts>
 __device__ __forceinline__ void lane_blocks(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
                                             uint32_t n, const uint8_t *__restrict__ blob, int32_t *__restrict__ out,
                                             uint32_t *__restrict__ status, uint32_t *__restrict__ dbg) {
@@ -1273,7 +1389,7 @@ __device__ __forceinline__ void lane_blocks(const BlockDesc *__restrict__ descs,
 #define WVG_TS_M5 18, 3, 2, 18, 18
 #define WVG_TS_HIGH16 2, 18, -1, 8, 6, 3, 5, 7, 4, 2, 18, -2, 3, 2, 18, 18
 #define WVG_TS_MONO_HIGH16 1, 17, 2, 18, 8, 6, 3, 5, 7, 4, 2, 18, 3, 2, 18, 18
-enum LaneList { LANE_FAST = 0, LANE_DEFAULT, LANE_M5, LANE_HIGH16, LANE_MONO_HIGH16, LANE_HY_DEFAULT };
+enum LaneList { LANE_FAST = 0, LANE_DEFAULT, LANE_M5, LANE_HIGH16, LANE_MONO_HIGH16, LANE_HY_DEFAULT, LANE_HY_WVC };
 // the lane kernel of one list over n blocks (wv_lane.hip)
 // dbg (nullptr: off): per parser wave 16 words (cycles, groups by path, wait cycles: LCount)
 hipError_t launch_lane(int which, dim3 grid, dim3 block, hipStream_t s, const BlockDesc *descs, const uint32_t *list,
