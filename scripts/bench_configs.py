@@ -202,8 +202,13 @@ def main():
             run("C4 1024 x 22050 float32 hybrid+bitrate", [corpora.c4()])
         elif c == "c4wvc":  # C4 with its .wvc correction files: the exact decode (generic kernel)
             wv, wvc, ll = corpora.c4_wvc()
-            from oracle import oracle as O  # (the exactness check: the lossless encode's decode)
-            run_wvc("C4 1024 x 22050 float32 hybrid+bitrate + .wvc (exact)", wv, wvc, exact=O.decode_file(ll).samples)
+            # (the exactness check: the same mantissas encoded losslessly, decoded here too)
+            r = DecodeBatch(4096)
+            r.add_file(ll)
+            r.decode()
+            ref = r.download().copy()
+            r.close()
+            run_wvc("C4 1024 x 22050 float32 hybrid+bitrate + .wvc (exact)", wv, wvc, exact=ref)
         elif c == "c5":
             run(f"C5 mixed corpus, files 0..{a.c5_files - 1}", corpora.c5(a.c5_files))
         elif c.startswith("dsd"):  # dsd0 / dsd1 / dsd3: N stereo files of one 22,050-frame block in one mode
