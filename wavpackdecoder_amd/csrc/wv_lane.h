@@ -431,7 +431,7 @@ __device__ __forceinline__ void cwin_init(CWin &c, const uint8_t *blob, uint64_t
     c.nb = 64 - 8 * (int32_t)sh;
     c.q0 = c.w[2];
     c.ld = c.w[3];
-    c.ni = 4;
+    c.ni = 3;
     c.used = 0;
     c.end = len * 8u;
 }
