@@ -84,6 +84,7 @@ int64_t emu_decode_from(const uint8_t *file, size_t len, int64_t seek_to, int ch
     bool exception = info.exception != 0;
     std::vector<std::pair<int64_t, int64_t>> fills;
     PcmState chain;  // the state a chain carries from block to block (wv_decode_chain)
+    DsdState dchain;  // ... and a DSD chain (decode_dsd_chain)
     for (auto &d : fo.descs) {
         uint32_t st = d.fstatus;
         HostStore hs{out, d.out_off, (uint64_t)d.pre_end * d.out_nch};
@@ -93,7 +94,9 @@ int64_t emu_decode_from(const uint8_t *file, size_t len, int64_t seek_to, int ch
         } else if (d.kind == KIND_PCM) {
             st |= decode_pcm_block(d, file, hs);
         } else if (d.kind != KIND_SKIP) {
-            DsdResult r = decode_dsd_block(d, file, fo.tables.data(), ptable.data(), hs);
+            DsdResult r = (d.chain_len || (d.inherit & INH_MEMBER))
+                              ? decode_dsd_chained(dchain, d, d.chain_len != 0, file, fo.tables.data(), ptable.data(), hs)
+                              : decode_dsd_block(d, file, fo.tables.data(), ptable.data(), hs);
             st |= r.status;
             if (r.status & ST_DSD_MUTE) {
                 // chunks from mute_chunk on: fill n*call_nch from the call start (a false-stereo

@@ -140,3 +140,25 @@ def test_dsd3_false_stereo_mono_file_stays_in_range():
             assert r.exception == 1, k
         else:
             assert r.status_or & 0x20, k  # declined (WVG_ST_UNSUPPORTED)
+
+
+@pytest.mark.parametrize("kernel", ["lane", "two_wave"])
+def test_dsd_sticky_chains(kernel):
+    """DSD blocks continuing the DSD (and crc / mute) state of the block before them,
+    one chain per file decoded in order by the wave kernel (decode_dsd_chain; the lane
+    kernels hand chain blocks back), against the oracle in one batch."""
+    cases = V.dsd_sticky_cases()
+    for chunk in (4096, 1000):
+        sub = [c for c in cases if c[2] == chunk]
+        out, res, infos, st = _run([d for _, d, _ in sub], chunk, kernel)
+        for (name, data, _), r, info in zip(sub, res, infos):
+            ref = O.decode_file(data, chunk=chunk)
+            assert r is not None and not (r.status_or & WVG_ST_TIMEOUT), name
+            assert not (r.status_or & 0x20), name  # decoded, not declined
+            if ref.status == -3:
+                assert r.exception == 1, name
+                continue
+            assert r.frames == ref.frames and r.crc_errors == ref.crc_errors, name
+            if not (r.status_or & WVG_ST_NONDET):
+                got = out[info.out_offset: info.out_offset + ref.frames * ref.nch]
+                np.testing.assert_array_equal(got, ref.samples, err_msg=name)

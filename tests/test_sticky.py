@@ -75,3 +75,31 @@ def test_stereo_term0_matches_oracle(case):
     assert n == r.frames and crc == r.crc_errors, name
     if not (st & ST_NONDET):
         np.testing.assert_array_equal(out, r.samples, err_msg=name)
+
+
+@pytest.mark.parametrize("case", V.dsd_sticky_cases(), ids=lambda c: c[0])
+def test_dsd_chain_matches_oracle(case):
+    """DSD chains (decode_dsd_chained): blocks without ID_DSD_BLOCK, or read without
+    unpack_init, continue the DSD state -- formerly declined (ST_UNSUPPORTED).  Samples
+    are compared unless the reference reads its caller's stale buffer (ST_NONDET: a
+    continuing mode-0 block past its data, a failed mode-1 symbol)."""
+    name, data, chunk = case
+    r = O.decode_file(data, chunk=chunk)
+    n, out, crc, st = E.decode(data, chunk)
+    assert not (st & ST_UNSUPPORTED), name
+    if r.status != 0:
+        assert n == r.status, name
+        return
+    assert n == r.frames and crc == r.crc_errors, name
+    if not (st & ST_NONDET):
+        np.testing.assert_array_equal(out, r.samples, err_msg=name)
+
+
+def test_dsd_chain_cases_cover_kinds():
+    """the DSD chain cases compare samples in every mode (not all NONDET)"""
+    seen = set()
+    for name, data, chunk in V.dsd_sticky_cases():
+        n, out, crc, st = E.decode(data, chunk)
+        if not (st & ST_NONDET) and n > 0:
+            seen.add(name.split("_")[2])
+    assert seen == {"m0", "m1", "m3"} or seen >= {"m1", "m3"}

@@ -534,7 +534,9 @@ static int commit_file(wvg_batch *b, const FileInfo &fi, size_t len, wvg_file_in
     for (int64_t k = fi.first_desc; k < fi.first_desc + fi.num_desc; k++) {
         const BlockDesc &d = b->fo.descs[(size_t)k];
         b->frames += d.nframes;
-        if (d.inherit & INH_MEMBER) continue;  // decoded by its chain's first block (wv_decode_pcm_wave)
+        // a chain member is decoded by its chain's first block (wv_decode_pcm_wave /
+        // wv_decode_dsd_wave); DSD members stay in the DSD list for the mute fills (wv_dsd_fill)
+        if ((d.inherit & INH_MEMBER) && d.kind == KIND_PCM) continue;
         int ts = (d.kind == KIND_PCM && !b->force_lane) ? term_set_of(d, b->prefer_pipe) : -1;
         if (ts >= 0) b->ts_list[ts].push_back((uint32_t)k);
         else if (d.kind == KIND_PCM) b->pcm_list.push_back((uint32_t)k);
@@ -1251,7 +1253,9 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
                             b->dsd_fast_lo, b->dsd_fast_n, b->d_blob, b->d_tables, b->d_out, b->d_status, b->d_mute,
                             slot(kPcm), slot(kDsd), slot(kDsd1), mode_of(b->dsd_list.size() - b->dsd_high_lo),
                             b->dsd_high_lo, b->dsd_high_mono, mode_of(b->dsd_fast_n), b->dsd_fast_mono,
-                            mode_of(b->pcm_wvc_n), b->pcm_wvc_n));
+                            // (.wvc blocks: the lane kernel even alone -- 35.8 against the generic
+                            // kernel's 130 ms for C4's 1,024 blocks, profiles/r05_c4wvc_rates.jsonl)
+                            b->kernel_auto ? 1 : b->lane_mode, b->pcm_wvc_n));
     HIPCHK(c, mark(kDsd));
     HIPCHK(c, mark(kDsd1));
     HIPCHK(c, mark(kPcm));

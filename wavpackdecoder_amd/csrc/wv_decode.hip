@@ -730,6 +730,28 @@ __device__ __forceinline__ DsdResult dsd_raw_lanes(const BlockDesc &d, const uin
     return res;
 }
 
+// A chain of DSD blocks continuing each other's DSD state (Appendix B-8 for DSD:
+// a block without ID_DSD_BLOCK, or read without unpack_init): the blocks in order,
+// the DsdState of one handed to the next (decode_dsd_chained, wv_decode_core.h);
+// each block's status and first muted chunk are its own (wv_dsd_fill reads them)
+__device__ __noinline__ void decode_dsd_chain(const BlockDesc *__restrict__ descs, uint32_t head,
+                                              const uint8_t *blob, const uint8_t *tables, int32_t *ptable,
+                                              int32_t *out, uint32_t *status, uint32_t *mute_chunk, uint32_t mode) {
+    const bool lead = threadIdx.x == 0;
+    const uint32_t n = descs[head].chain_len;
+    DsdState S;
+    for (uint32_t k = 0; k < n; k++) {
+        const uint32_t bi = head + k;
+        const BlockDesc &d = descs[bi];
+        DevStoreWave st{out + d.out_off, (uint64_t)d.pre_end * d.out_nch, lead};
+        const DsdResult r = decode_dsd_chained(S, d, k == 0, blob, tables, ptable, st, g_dsd_ptables);
+        if (lead) {
+            status[bi] = d.fstatus | r.status | ((k == 0 && (mode & 4u)) ? (uint32_t)ST_REDONE : 0u);
+            mute_chunk[bi] = r.mute_chunk;
+        }
+    }
+}
+
 extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_wave(const BlockDesc *__restrict__ descs,
                                                                     const uint32_t *__restrict__ list,
                                                                     const uint8_t *__restrict__ blob,
@@ -747,6 +769,11 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_wave(const BlockD
     if ((mode & 1u) && d.kind == KIND_DSD_FAST) return;
     if ((mode & 2u) && d.kind == KIND_DSD_HIGH) return;
     if ((mode & 4u) && !(status[bi] & lane::ST_REDO)) return;
+    if (d.inherit & INH_MEMBER) return;  // decoded by its chain's first block
+    if (d.chain_len >= 2) {
+        decode_dsd_chain(descs, bi, blob, tables, pt_lds, out, status, mute_chunk, mode);
+        return;
+    }
     const bool lead = threadIdx.x == 0;
     DevStoreWave st{out + d.out_off, (uint64_t)d.pre_end * d.out_nch, lead};
     DsdResult r;
@@ -1017,6 +1044,11 @@ extern "C" __global__ void __launch_bounds__(64) wv_decode_dsd_fast(const BlockD
     const BlockDesc &d = descs[bi];
     // mode bit 2: only the blocks the row kernel (wv_dsd1_lane.hip) handed back (ST_REDO)
     if ((mode & 4u) && !(status[bi] & lane::ST_REDO)) return;
+    if (d.inherit & INH_MEMBER) return;  // decoded by its chain's first block
+    if (d.chain_len >= 2) {  // (the generic decode with the host's tables; tab: the ptable scratch)
+        decode_dsd_chain(descs, bi, blob, tables, (int32_t *)tab, out, status, mute_chunk, mode);
+        return;
+    }
     const bool lead = threadIdx.x == 0;
     const uint32_t bins = (uint32_t)d.dsd_history_bins;
     DevStoreWave st{out + d.out_off, (uint64_t)d.pre_end * d.out_nch, lead};

@@ -1181,35 +1181,51 @@ WVF_HD void dsd_ptable_init(int32_t rate_i, int32_t *pt, uint32_t lane, uint32_t
     }
 }
 
-template <class Store>
-WVF_HD DsdResult decode_dsd_block(const BlockDesc &d, const uint8_t *blob, const uint8_t *tables, int32_t *ptable,
-                                  Store &out, const int32_t *ptables_all = nullptr) {
-    using namespace wvf;
-    const uint32_t flags = d.flags;
-    const bool mono = (flags & MONO_DATA) != 0;
-    const bool fstereo = (flags & FALSE_STEREO) != 0;
-    const int wch = mono ? 1 : 2;
-    const int och = (flags & MONO_FLAG) ? 1 : 2;
-    const uint8_t *data = blob + d.bits_off;  // data[byteptr] with byteptr == 0 here
-    const uint32_t dlen = d.dsd_data_len;
-    uint32_t bp = 0;
-    int32_t crc = -1;
-    DsdResult res = {0, 0};
-    bool mute = false;
-
-    // mode 1 state
-    const int bins = d.dsd_history_bins;
-    const uint8_t *prob = tables + d.dsd_table_off;
-    const uint16_t *summed = (const uint16_t *)(tables + d.dsd_table_off + (size_t)bins * 256);
-    const uint8_t *lookup = tables + d.dsd_table_off + (size_t)bins * 768;
-    const int32_t *vlook = (const int32_t *)(tables + d.dsd_table_off + (size_t)bins * 2048);
-    uint32_t low = 0, high = 0xFFFFFFFFu, value = 0;
-    int p0 = 0, p1 = 0;
-    // mode 3 state
+// The DSD decode state of WavpackStream.dsds (and the crc / mute_error unpack_init
+// resets): per block from its descriptor, or -- a block without ID_DSD_BLOCK, or a
+// header read without unpack_init (DsdUtils.cs:17-54, UnpackUtils.cs:24-68,
+// WavPackUtils.cs:219-251) -- carried on from the block decoded before it (a chain,
+// chain_blocks in wv_framing.cpp; Appendix B-8 for DSD).
+struct DsdState {
+    const uint8_t *data;  // the metadata sub-block the bytes come from, from its payload start
+    uint32_t dlen, bp;    // its bytes from there (data.Length - byteptr at the payload start), bytes read
+    uint32_t kind;        // the mode (KIND_DSD_*) of the sub-block
+    // mode 1 (init_dsd_block_fast's tables, host-built)
+    int bins;
+    const uint8_t *prob;
+    const uint16_t *summed;
+    const uint8_t *lookup;
+    const int32_t *vlook;
+    uint32_t low, high, value;
+    int p0, p1;
+    // mode 3 (the ptable itself lives in the caller's 256-int scratch)
     int32_t F[2][9];  // value, filter0..6, factor
-    int32_t bytei[2] = {0, 0};
+    int32_t bytei[2];
+    int32_t crc;
+    bool mute;
+};
+
+// the state init_dsd_block leaves for block d (ptable: 256 ints of scratch, mode 3)
+WVF_HD void dsd_state_init(DsdState &S, const BlockDesc &d, const uint8_t *blob, const uint8_t *tables,
+                           int32_t *ptable, const int32_t *ptables_all) {
+    S.data = blob + d.bits_off;  // data[byteptr] with byteptr == 0 here
+    S.dlen = d.dsd_data_len;
+    S.bp = 0;
+    S.kind = d.kind;
+    S.bins = d.dsd_history_bins;
+    S.prob = tables + d.dsd_table_off;
+    S.summed = (const uint16_t *)(tables + d.dsd_table_off + (size_t)S.bins * 256);
+    S.lookup = tables + d.dsd_table_off + (size_t)S.bins * 768;
+    S.vlook = (const int32_t *)(tables + d.dsd_table_off + (size_t)S.bins * 2048);
+    S.low = 0;
+    S.high = 0xFFFFFFFFu;
+    S.value = 0;
+    S.p0 = S.p1 = 0;
+    S.bytei[0] = S.bytei[1] = 0;
+    S.crc = -1;
+    S.mute = false;
     if (d.kind == KIND_DSD_FAST || d.kind == KIND_DSD_HIGH) {
-        for (int i = 0; i < 4; i++) value = (value << 8) | data[bp++];
+        for (int i = 0; i < 4; i++) S.value = (S.value << 8) | S.data[S.bp++];
     }
     if (d.kind == KIND_DSD_HIGH) {
         if (ptables_all) {  // the device's precomputed rows (g_dsd_ptables)
@@ -1219,13 +1235,41 @@ WVF_HD DsdResult decode_dsd_block(const BlockDesc &d, const uint8_t *blob, const
             dsd_ptable_init(d.dsd_rate_i, ptable, 0, 1);
         }
         for (int c = 0; c < 2; c++) {
-            F[c][0] = 0;
-            F[c][1] = 0;
-            for (int k = 0; k < 5; k++) F[c][2 + k] = d.dsd_filters[c][k];
-            F[c][7] = 0;  // filter6
-            F[c][8] = d.dsd_filters[c][5];  // factor
+            S.F[c][0] = 0;
+            S.F[c][1] = 0;
+            for (int k = 0; k < 5; k++) S.F[c][2 + k] = d.dsd_filters[c][k];
+            S.F[c][7] = 0;  // filter6
+            S.F[c][8] = d.dsd_filters[c][5];  // factor
         }
     }
+}
+
+// block d's calls (unpack_dsd_samples, DsdUtils.cs:56-136) from state S; d's own
+// header gives the layout, the frames and the crc to check
+template <class Store>
+WVF_HD DsdResult dsd_run(DsdState &S, const BlockDesc &d, int32_t *ptable, Store &out) {
+    using namespace wvf;
+    const uint32_t flags = d.flags;
+    const bool mono = (flags & MONO_DATA) != 0;
+    const bool fstereo = (flags & FALSE_STEREO) != 0;
+    const int wch = mono ? 1 : 2;
+    const int och = (flags & MONO_FLAG) ? 1 : 2;
+    const uint8_t *data = S.data;
+    const uint32_t dlen = S.dlen;
+    uint32_t bp = S.bp;
+    int32_t crc = S.crc;
+    DsdResult res = {0, 0};
+    bool mute = S.mute;
+    const int bins = S.bins;
+    const uint8_t *prob = S.prob;
+    const uint16_t *summed = S.summed;
+    const uint8_t *lookup = S.lookup;
+    const int32_t *vlook = S.vlook;
+    uint32_t low = S.low, high = S.high, value = S.value;
+    int p0 = S.p0, p1 = S.p1;
+    int32_t(&F)[2][9] = S.F;
+    int32_t *bytei = S.bytei;
+    const uint32_t kind = S.kind;
 
     uint32_t f = 0, chunk_len = d.first_chunk, ci = 0;
     while (f < d.nframes) {
@@ -1237,10 +1281,13 @@ WVF_HD DsdResult decode_dsd_block(const BlockDesc &d, const uint8_t *blob, const
                 int32_t v[2] = {0, 0};
                 for (int c = 0; c < wch; c++) {
                     int code;
-                    if (d.kind == KIND_DSD_RAW) {
+                    if (kind == KIND_DSD_RAW) {
+                        // (past the sub-block the reference leaves the caller's buffer as it
+                        // was: only a block continuing a consumed one gets there)
+                        if (bp >= dlen) res.status |= ST_NONDET;
                         code = bp < dlen ? data[bp] : 0;
                         bp++;
-                    } else if (d.kind == KIND_DSD_FAST) {
+                    } else if (kind == KIND_DSD_FAST) {
                         const int pi = p0 * 256;
                         uint32_t tot = summed[pi + 255];
                         if (tot == 0) { chunk_ok = false; break; }
@@ -1275,7 +1322,7 @@ WVF_HD DsdResult decode_dsd_block(const BlockDesc &d, const uint8_t *blob, const
                     v[c] = code;
                 }
                 if (!chunk_ok) break;
-                if (d.kind == KIND_DSD_HIGH) {
+                if (kind == KIND_DSD_HIGH) {
                     for (int c = 0; c < wch; c++) F[c][0] = add32(sub32(F[c][2], F[c][6]), mul32(F[c][7], F[c][8]) >> 2);
                     for (int bit = 0; bit < 8; bit++) {
                         for (int c = 0; c < wch; c++) {
@@ -1345,7 +1392,38 @@ WVF_HD DsdResult decode_dsd_block(const BlockDesc &d, const uint8_t *blob, const
         res.status |= ST_CRC_CHECKED;
         if (crc != d.crc) res.status |= ST_CRC_ERROR;
     }
+    S.bp = bp;
+    S.crc = crc;
+    S.mute = mute;
+    S.low = low;
+    S.high = high;
+    S.value = value;
+    S.p0 = p0;
+    S.p1 = p1;
     return res;
+}
+
+template <class Store>
+WVF_HD DsdResult decode_dsd_block(const BlockDesc &d, const uint8_t *blob, const uint8_t *tables, int32_t *ptable,
+                                  Store &out, const int32_t *ptables_all = nullptr) {
+    DsdState S;
+    dsd_state_init(S, d, blob, tables, ptable, ptables_all);
+    return dsd_run(S, d, ptable, out);
+}
+
+// a block of a DSD chain: the head starts from its descriptor, a member continues S
+// (unpack_init's crc / mute reset unless its header was read without unpack_init)
+template <class Store>
+WVF_HD DsdResult decode_dsd_chained(DsdState &S, const BlockDesc &d, bool head, const uint8_t *blob,
+                                    const uint8_t *tables, int32_t *ptable, Store &out,
+                                    const int32_t *ptables_all = nullptr) {
+    if (head) {
+        dsd_state_init(S, d, blob, tables, ptable, ptables_all);
+    } else if (!(d.inherit & INH_NOINIT)) {
+        S.crc = -1;
+        S.mute = false;
+    }
+    return dsd_run(S, d, ptable, out);
 }
 
 }  // namespace wvg

@@ -130,6 +130,7 @@ enum InheritBits : uint32_t {
     INH_DLT0 = 1u << 7,
     INH_DLT1 = 1u << 8,
     INH_NOINIT = 1u << 9,   // no unpack_init since the last decode: crc, crc_x, mute_error, bit register continue
+    INH_DSD = 1u << 10,     // DSD: no ID_DSD_BLOCK since the last decode -- its data, coder and filters continue
     INH_MEMBER = 1u << 31,  // decoded by the chain kernel after its predecessor
 };
 static_assert(sizeof(BlockDesc) % 16 == 0, "BlockDesc is loaded with 16-B alignment");

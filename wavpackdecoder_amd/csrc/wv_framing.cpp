@@ -792,7 +792,7 @@ class Framer {
         uint32_t inh = 0, inhp = 0;
         if (!inited_this_block && decoded_since_init) inh |= INH_NOINIT;
         if (flags & DSD_FLAG) {
-            if (!dsd.fresh) status |= ST_UNSUPPORTED;
+            if (!dsd.fresh) inh |= INH_DSD;  // continues a consumed DSD state (chained, frame_file)
             d.kind = dsd.mode == 0 ? KIND_DSD_RAW : dsd.mode == 1 ? KIND_DSD_FAST : KIND_DSD_HIGH;
             d.bits_off = blob_base + (uint64_t)dsd.data_off + (uint64_t)dsd.byteptr;
             d.dsd_data_len = (uint32_t)(dsd.data_len - dsd.byteptr);
@@ -889,8 +889,10 @@ class Framer {
             d.inherit = inh;
             d.inherit_passes = inhp;
             if (!inh && !inhp && !(d.wvx_state & 1)) attach_wvc(d);
-        } else if (inh & INH_NOINIT) {
-            status |= ST_UNSUPPORTED;  // a DSD block continuing the crc / mute state
+        } else {
+            // a DSD block continuing the DSD state and / or the crc / mute state of the block
+            // decoded before it (chained with it, decode_dsd_chained)
+            d.inherit = inh & (INH_DSD | INH_NOINIT);
         }
         if (status & ST_UNSUPPORTED) {
             d.kind = KIND_SKIP;
@@ -1166,17 +1168,20 @@ int compute_mode(const FileInfo &info) {  // WavPackUtils.cs:133-167 (fields cap
 
 // Blocks that inherit decode state (d.inherit) join the block decoded before
 // them into a chain, back to a block whose state is all in its descriptor; the
-// chain's first descriptor records the chain length.  A block whose
-// predecessor cannot be decoded on the device (a DSD or skipped block) stays
-// unsupported.
+// chain's first descriptor records the chain length.  PCM chains continue PCM
+// state, DSD chains DSD state; a block whose predecessor is of the other family
+// or was skipped stays unsupported (the state it continues was left by a block
+// further back: malformed files only).
 static void chain_blocks(FramingOutput &out, int64_t first, int64_t count) {
     int64_t head = -1;
+    auto family = [](uint32_t kind) { return kind == KIND_PCM ? 0 : (kind == KIND_SKIP ? 2 : 1); };
     for (int64_t k = first; k < first + count; k++) {
         BlockDesc &d = out.descs[(size_t)k];
-        if (d.kind != KIND_PCM || (d.inherit == 0 && d.inherit_passes == 0)) {
-            head = d.kind == KIND_PCM ? k : -1;
+        if (d.kind == KIND_SKIP || (d.inherit == 0 && d.inherit_passes == 0)) {
+            head = d.kind == KIND_SKIP ? -1 : k;
             continue;
         }
+        if (head >= 0 && family(out.descs[(size_t)head].kind) != family(d.kind)) head = -1;
         if (head < 0) {
             d.kind = KIND_SKIP;
             d.fstatus |= ST_UNSUPPORTED;

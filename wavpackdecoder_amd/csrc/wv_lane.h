@@ -239,7 +239,7 @@ struct CWin {
     const uint32_t *w;  // the stream's dword-aligned base
     uint64_t win;       // LSB = next bit
     int32_t nb;         // valid bits (>= 33 at every word start)
-    uint32_t q0, ld;    // the next dword, and the load of the one after (consumed a refill later)
+    uint32_t q0, q1, q2, ld;  // the next dwords, and the load of the one after (consumed three refills later)
     uint32_t ni;        // index of the dword in ld
     uint32_t used;      // bits consumed (checked against end at the block's end)
     uint32_t end;       // the stream's bits (from its first bit)
@@ -417,9 +417,10 @@ __device__ __forceinline__ void lhy_code(uint32_t x, uint32_t low, uint32_t mc, 
 
 // ---- .wvc correction stream (HY == 2; beyond the reference: WavPack 4's get_word) ----
 // A hybrid word the error limit left inexact (el != 0) reads its exact magnitude as
-// read_code(wvcbits, high - low) + low from the block's ID_WVC_BITSTREAM; the
-// parser hands the reconstruction exact-minus-lossy (corr), which it carries through
-// the passes (LPass::frame_wvc).  Each lane reads its correction stream through a
+// read_code(wvcbits, high - low) + low from the block's ID_WVC_BITSTREAM.  The parser
+// hands the reconstruction wave each word's final interval (LW.clo / cn); that wave
+// reads the correction, exact minus lossy, and carries it through the passes
+// (LPass::frame_wvc), off the parser's chain.  Each lane reads its correction stream through a
 // 64-bit register window merged from dwords loaded a refill ahead (global loads: the
 // stream is sparse beside the main one); a lane whose reads pass the stream's end
 // hands its block back (its bytes past the end would read 0xFF there).
@@ -430,40 +431,48 @@ __device__ __forceinline__ void cwin_init(CWin &c, const uint8_t *blob, uint64_t
     c.win = ((uint64_t)c.w[0] | ((uint64_t)c.w[1] << 32)) >> (8u * sh);
     c.nb = 64 - 8 * (int32_t)sh;
     c.q0 = c.w[2];
-    c.ld = c.w[3];
-    c.ni = 3;
+    c.q1 = c.w[3];
+    c.q2 = c.w[4];
+    c.ld = c.w[5];
+    c.ni = 5;
     c.used = 0;
     c.end = len * 8u;
 }
-__device__ __forceinline__ void cwin_merge(CWin &c) {  // keep >= 33 bits: merge q0 when 32 or fewer are left
+// keep >= 33 bits: merge q0 when 32 or fewer are left; the queue moves on, and the load
+// issued now is consumed three merges later (a lane's stream runs through a cache line
+// every 32 dwords: its first read waits for memory)
+__device__ __forceinline__ void cwin_merge(CWin &c) {
     const uint32_t mg = (uint32_t)((c.nb - 33) >> 31);  // ~0: merge
     const uint32_t sh = (uint32_t)c.nb;
     __builtin_assume(sh < 64u);
     c.win |= (uint64_t)(c.q0 & mg) << sh;
     c.nb += (int32_t)(mg & 32u);
-    c.q0 = mg ? c.ld : c.q0;
+    c.q0 = mg ? c.q1 : c.q0;
+    c.q1 = mg ? c.q2 : c.q1;
+    c.q2 = mg ? c.ld : c.q2;
     c.ni += mg & 1u;
-    c.ld = c.w[c.ni];  // (reads stay within 12 bytes past the stream: the blob's tail)
+    c.ld = c.w[c.ni];  // (reads stay within 24 bytes past the stream: the blob's tail)
 }
-// exact - lossy for a word of sign sg (0 / -1), lossy magnitude mid, final interval
-// (lo, n), error limit el (0: the word was exact, nothing is read)
-__device__ __forceinline__ int32_t cwin_corr(CWin &c, int32_t el, uint32_t mid, int32_t sg, uint32_t lo, uint32_t n) {
+// exact - lossy for a word of value v (sign and lossy magnitude) whose final interval
+// is [lo, lo + n - 1] (n 1: the word was exact, nothing is read, lo its magnitude)
+__device__ __forceinline__ int32_t cwin_corr(CWin &c, int32_t v, uint32_t lo, uint32_t n) {
+    const int32_t sg = v >> 31;
+    const uint32_t mid = (uint32_t)(v ^ sg);
     const uint32_t mc = n - 1u;  // high - low
     const uint32_t x = (uint32_t)c.win;
     const uint32_t z = (uint32_t)__builtin_clz(mc | 1u);
     const uint32_t ex = (0xFFFFFFFFu >> z) - mc;
     const uint32_t nbt = z ^ 31u;
-    const uint32_t v = __builtin_amdgcn_ubfe(x, 0, nbt);
-    const bool big = v >= ex;
-    const uint32_t code = big ? 2u * v + __builtin_amdgcn_ubfe(x, nbt, 1) - ex : v;
-    const uint32_t used = el != 0 ? nbt + (big ? 1u : 0u) : 0u;
+    const uint32_t vv = __builtin_amdgcn_ubfe(x, 0, nbt);
+    const bool big = vv >= ex;
+    const uint32_t code = big ? 2u * vv + __builtin_amdgcn_ubfe(x, nbt, 1) - ex : vv;
+    const uint32_t used = nbt + (big ? 1u : 0u);  // (0 for n == 1)
     c.win >>= used;
     c.nb -= (int32_t)used;
     c.used += used;
     cwin_merge(c);
     const uint32_t value = lo + code;
-    const uint32_t d = sg ? mid - value : value - mid;
-    return el != 0 ? (int32_t)d : 0;
+    return (int32_t)(sg ? mid - value : value - mid);
 }
 // slow_level after a word (HYBRID_BITRATE, :501-502): slow - (slow + SLO) >> SLS + mylog2(mid)
 // (mylog2, WordsUtils.cs:588-608: the 8 bits below the leading one index the table)
@@ -487,7 +496,7 @@ __device__ __forceinline__ int32_t lhy_decay(int32_t slow) {  // a zero-run zero
 struct LW {
     uint32_t x, low, mc;
     int32_t v;
-    int32_t corr;  // HY == 2: the .wvc's exact minus this lossy value
+    uint32_t clo, cn;  // HY == 2: the final interval [clo, clo + cn - 1] of an inexact hybrid word (cn 1: exact)
 };
 
 // get_words for one residual of channel C (WordsUtils.cs:290-503, lossless:
@@ -501,7 +510,7 @@ struct LW {
 // nothing, which leaves its state as it was -- and the checks it feeds are those
 // of the word that ends the run, which reads the same window with the same state.
 template <int C, int HY = false>
-__device__ __forceinline__ LW lword(LState &s, const uint8_t *ring, uint32_t rbase, CWin &cw) {
+__device__ __forceinline__ LW lword(LState &s, const uint8_t *ring, uint32_t rbase) {
     using namespace wvf;
     // zero-run mode (:304-352): both channels' median[0] < 2, nothing held
     const uint64_t h0m0 = lmask(s.keep == 0u), h1m0 = lmask(s.h1 != 0u);
@@ -591,8 +600,13 @@ __device__ __forceinline__ LW lword(LState &s, const uint8_t *ring, uint32_t rba
     w.x = vselm(zm, 0u, x);
     w.low = vselm(zm, 0u, low);
     w.mc = vselm(zm, 0u, mc);
-    w.corr = 0;
-    if constexpr (HY == 2) w.corr = cwin_corr(cw, zskip ? 0 : s.el[C], mid, sg, lo_f, n_f);
+    w.clo = vselm(zm, 0u, mid);
+    w.cn = 1u;
+    if constexpr (HY == 2) {
+        const bool inexact = !zskip && s.el[C] != 0;
+        w.clo = inexact ? lo_f : w.clo;
+        w.cn = inexact ? n_f : 1u;
+    }
     if constexpr (HY) s.slow[C] = zskip ? s.slow[C] : lhy_slow(s.slow[C], mid, ring);
     lrefill(s, ring, rbase);
     return w;
@@ -656,7 +670,8 @@ __device__ __forceinline__ LW lword_fast(LState &s, const uint8_t *ring, uint32_
     w.x = x & (zsk - 1u);
     w.low = low & (zsk - 1u);
     w.mc = mc & (zsk - 1u);
-    w.corr = 0;
+    w.clo = 0u;
+    w.cn = 1u;
     lrefill(s, ring, rbase);
     return w;
 }
@@ -690,7 +705,7 @@ __device__ __forceinline__ void lmerge(LState &s, const uint8_t *ring) {
 // W32: 32-bit products (C#'s int wrap) for groups whose medians pass the 24-bit
 // operands (pgroup_try: below 2^29 at the group's start, so none wraps in the group)
 template <int C, bool SPLIT, int HY = false, bool W32 = false>
-__device__ __forceinline__ LW lword_nz(LState &s, const uint8_t *ring, uint32_t rbase, CWin &cw) {
+__device__ __forceinline__ LW lword_nz(LState &s, const uint8_t *ring, uint32_t rbase) {
     static_assert(!HY || SPLIT, "a hybrid word's bisection bits follow a refill");
     using namespace wvf;
     const uint32_t lo = (uint32_t)s.win, hi = (uint32_t)(s.win >> 32);
@@ -765,9 +780,12 @@ __device__ __forceinline__ LW lword_nz(LState &s, const uint8_t *ring, uint32_t 
 #ifdef WV_LANE_WORD_BARRIER  // (experiment: words in program order, the ring read a word ahead of its use)
     __builtin_amdgcn_sched_barrier(WV_LANE_WORD_BARRIER);
 #endif
-    int32_t corr = 0;
-    if constexpr (HY == 2) corr = cwin_corr(cw, s.el[C], mid, sg, lo_f, n_f);
-    return LW{x, low, mc, (int32_t)(mid ^ (uint32_t)sg), corr};
+    uint32_t clo = mid, cn = 1u;
+    if constexpr (HY == 2) {
+        clo = s.el[C] != 0 ? lo_f : mid;
+        cn = s.el[C] != 0 ? n_f : 1u;
+    }
+    return LW{x, low, mc, (int32_t)(mid ^ (uint32_t)sg), clo, cn};
 }
 
 // ---------------------------------------------------------------------------
@@ -798,50 +816,50 @@ __device__ __forceinline__ uint32_t rpos(const LState &s) { return s.rp + (((s.r
 
 // the parser's verdict for its lane now (after the block's last frame)
 template <int HY>
-__device__ __forceinline__ uint32_t pverdict(const LState &s, uint32_t u0, const CWin &cw) {
-    uint32_t r = s.bad | (s.pmax >= 17u ? 16u : 0u) | (s.slack < 0 ? 32u : 0u) | (rpos(s) >= u0 * 4u ? 64u : 0u);
-    if constexpr (HY == 2) r |= cw.used > cw.end ? 1u : 0u;  // (a correction read past its stream)
+__device__ __forceinline__ uint32_t pverdict(const LState &s, uint32_t u0) {
+    const uint32_t r = s.bad | (s.pmax >= 17u ? 16u : 0u) | (s.slack < 0 ? 32u : 0u) | (rpos(s) >= u0 * 4u ? 64u : 0u);
     return 0x80000000u | r | ((s.bad0 ? s.bad0 : r) << 8);
 }
 
 // word kinds: WK_CHECKED lword, WK_FAST lword_fast, WK_NORUN / WK_NORUN_SPLIT lword_nz
 enum { WK_CHECKED = 0, WK_FAST = 1, WK_NORUN = 2, WK_NORUN_SPLIT = 3, WK_NORUN_SPLIT32 = 4 };
 template <int K, int C, int HY>
-__device__ __forceinline__ LW lword_k(LState &s, const uint8_t *ring, uint32_t rb, CWin &cw) {
-    if constexpr (K == WK_NORUN) return lword_nz<C, false, false>(s, ring, rb, cw);  // (not HY: pgroup_try)
-    else if constexpr (K == WK_NORUN_SPLIT) return lword_nz<C, true, HY>(s, ring, rb, cw);
-    else if constexpr (K == WK_NORUN_SPLIT32) return lword_nz<C, true, HY, true>(s, ring, rb, cw);
+__device__ __forceinline__ LW lword_k(LState &s, const uint8_t *ring, uint32_t rb) {
+    if constexpr (K == WK_NORUN) return lword_nz<C, false, false>(s, ring, rb);  // (not HY: pgroup_try)
+    else if constexpr (K == WK_NORUN_SPLIT) return lword_nz<C, true, HY>(s, ring, rb);
+    else if constexpr (K == WK_NORUN_SPLIT32) return lword_nz<C, true, HY, true>(s, ring, rb);
     else if constexpr (K == WK_FAST) return lword_fast<C>(s, ring, rb);
-    else return lword<C, HY>(s, ring, rb, cw);
+    else return lword<C, HY>(s, ring, rb);
 }
 template <int U, bool FULL, int FAST, bool MONO, int HY, bool CODES>
 __device__ __forceinline__ void pframe(LState &s, const uint8_t *ring, uint32_t rb, LShared &sh, uint32_t lane,
-                                       uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin, CWin &cw) {
+                                       uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin) {
     const uint32_t t = g0 + U;
     const uint32_t slot = (((g0 % (uint32_t)RF) + U) << 6) + lane;  // (GF divides RF: no wrap inside a group)
-    const LW w0 = lword_k<FAST, 0, HY>(s, ring, rb, cw);
-    LW w1 = {0u, 0u, 0u, 0};
-    if constexpr (!MONO) w1 = lword_k<FAST, 1, HY>(s, ring, rb, cw);
+    const LW w0 = lword_k<FAST, 0, HY>(s, ring, rb);
+    LW w1 = {0u, 0u, 0u, 0, 0u, 1u};
+    if constexpr (!MONO) w1 = lword_k<FAST, 1, HY>(s, ring, rb);
     if constexpr (CODES) {
         sh.rq[slot] = make_int4((int32_t)w0.x, (int32_t)w0.low, (int32_t)w1.x, (int32_t)w1.low);
         sh.rm[slot] = make_int2((int32_t)w0.mc, (int32_t)w1.mc);
     } else {
         sh.rm[slot] = make_int2(w0.v, w1.v);
-        if constexpr (HY == 2) *(int2 *)&sh.rq[slot] = make_int2(w0.corr, w1.corr);  // (rq is free without CODES)
+        if constexpr (HY == 2)  // (rq is free without CODES)
+            sh.rq[slot] = make_int4((int32_t)w0.clo, (int32_t)w0.cn, (int32_t)w1.clo, (int32_t)w1.cn);
     }
-    if (!FULL && t + 1u == nfr) pfin = pverdict<HY>(s, u0, cw);
+    if (!FULL && t + 1u == nfr) pfin = pverdict<HY>(s, u0);
 }
 template <bool FULL, int FAST, bool MONO, int HY, bool CODES>
 __device__ __forceinline__ void pgroup(LState &s, const uint8_t *ring, uint32_t rb, LShared &sh, uint32_t lane,
-                                       uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin, CWin &cw) {
-    pframe<0, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
-    pframe<1, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
-    pframe<2, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
-    pframe<3, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
-    pframe<4, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
-    pframe<5, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
-    pframe<6, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
-    pframe<7, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
+                                       uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin) {
+    pframe<0, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
+    pframe<1, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
+    pframe<2, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
+    pframe<3, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
+    pframe<4, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
+    pframe<5, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
+    pframe<6, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
+    pframe<7, FULL, FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
 }
 // a group: the fast words first -- the no-run words when no live lane can meet a
 // zero run in it (lword_nz), else lword_fast; if a live lane met a rare word, the
@@ -871,7 +889,7 @@ struct LCount {
 template <bool FULL, bool MONO, int HY, bool CODES>
 __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint32_t rb, LShared &sh, uint32_t lane,
                                            uint32_t g0, uint32_t nfr, uint32_t u0, uint32_t &pfin, uint32_t mm,
-                                           LCount &cnt, CWin &cw) {
+                                           LCount &cnt) {
     LCNT(cnt.groups++);
     // (every wave-wide test below is one compare of a lane value -- a compound
     // condition would go through SALU mask logic, ~20 cycles each way)
@@ -887,7 +905,7 @@ __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint3
         for (int u = 0; u < GF; u++) {
             const uint32_t slot = (((g0 % (uint32_t)RF) + u) << 6) + lane;
             if constexpr (CODES) sh.rq[slot] = make_int4(0, 0, 0, 0);
-            if constexpr (HY == 2) *(int2 *)&sh.rq[slot] = make_int2(0, 0);
+            if constexpr (HY == 2) sh.rq[slot] = make_int4(0, 1, 0, 1);
             sh.rm[slot] = make_int2(0, 0);
             if constexpr (HY) {  // every zero of a run decays its channel's slow_level
                 s.slow[0] = lhy_decay(s.slow[0]);
@@ -895,7 +913,7 @@ __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint3
             }
         }
         s.zacc -= WPG;
-        if (!FULL && livem && nfr <= g0 + GF) pfin = pverdict<HY>(s, u0, cw);
+        if (!FULL && livem && nfr <= g0 + GF) pfin = pverdict<HY>(s, u0);
         LCNT(cnt.bulk++);
         return;
     }
@@ -909,14 +927,12 @@ __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint3
     const bool allnr = lmask((runnable & livem) != 0u) == 0ull &&
                        !(HY && ((WV_LANE_HY_PATH == 1 && m26) || WV_LANE_HY_PATH == 2));
     if (__builtin_expect(m26 && !allnr, 0)) {
-        pgroup<FULL, WK_CHECKED, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
+        pgroup<FULL, WK_CHECKED, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
         s.bad |= s.slack < 0 ? 32u : 0u;
         LCNT(cnt.checked++);
         return;
     }
     const LState s0 = s;
-    CWin cw0;  // (copied only where it is used: a copy of the unused window went to scratch)
-    if constexpr (HY == 2) cw0 = cw;
     const uint32_t pfin0 = pfin;
     if (allnr) {
         // a word may count on 33 bits: 17 of unary count (16 ones are an escape) and a
@@ -925,35 +941,34 @@ __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint3
         // between a word's parts (a group with a longer word goes to the checked words)
         s.rmax = 0u;
         if (__builtin_expect(m26, 0)) {  // (medians below 2^29, none wraps in the group; or hybrid words)
-            pgroup<FULL, WK_NORUN_SPLIT32, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
+            pgroup<FULL, WK_NORUN_SPLIT32, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
             lmerge(s, ring);
             LCNT(cnt.split++);
         } else if (!HY && lmask(mml >= (1u << 17)) == 0ull) {
-            pgroup<FULL, WK_NORUN, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
+            pgroup<FULL, WK_NORUN, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
             LCNT(cnt.norun++);
         } else {
-            pgroup<FULL, WK_NORUN_SPLIT, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
+            pgroup<FULL, WK_NORUN_SPLIT, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
             lmerge(s, ring);  // (the next group's words start from >= 33 bits)
             LCNT(cnt.split++);
         }
         s.rare = s.rmax >> 4;  // (an escape: the checked words)
     } else if constexpr (HY) {  // (no run-aware fast words for hybrid blocks: the checked words)
         s.slack = 0;
-        pgroup<FULL, WK_CHECKED, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
+        pgroup<FULL, WK_CHECKED, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
         s.bad |= s.slack < 0 ? 32u : 0u;
         LCNT(cnt.checked++);
         return;
     } else {
         s.rare = 0u;
-        pgroup<FULL, WK_FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
+        pgroup<FULL, WK_FAST, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
         LCNT(cnt.fast++);
     }
     if (__builtin_expect(lmask(((s.rare | ((uint32_t)s.slack >> 31)) & livem) != 0u) != 0ull, 0)) {
         s = s0;
-        if constexpr (HY == 2) cw = cw0;
         pfin = pfin0;
         s.slack = 0;
-        pgroup<FULL, WK_CHECKED, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, cw);
+        pgroup<FULL, WK_CHECKED, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
         s.bad |= s.slack < 0 ? 32u : 0u;
         LCNT(cnt.replay++);
     }
@@ -1009,7 +1024,7 @@ __device__ __forceinline__ int32_t rdecode(uint32_t x, uint32_t low, uint32_t mc
 template <int U, bool FULL, bool MONO, int HY, bool CODES, int... Ts>
 __device__ __forceinline__ void rframe(LChain<Ts...> &ch, const LShared &shr, uint32_t lane, uint32_t g0, uint32_t nfr,
                                        bool joint, int32_t &mx, int32_t &mn, uint32_t &crc, uint32_t sh, int32_t *o,
-                                       uint32_t rbad, const LEnd &e, bool fst, const Fixup &fx) {
+                                       uint32_t rbad, const LEnd &e, bool fst, const Fixup &fx, CWin &cw) {
     const uint32_t t = g0 + U;
     const uint32_t slot = (((g0 % (uint32_t)RF) + U) << 6) + lane;
     const int2 r = shr.rm[slot];
@@ -1023,8 +1038,12 @@ __device__ __forceinline__ void rframe(LChain<Ts...> &ch, const LShared &shr, ui
         R = r.y;
     }
     if constexpr (HY == 2) {  // the exact values; the passes keep the lossy history
-        const int2 c = *(const int2 *)&shr.rq[slot];
-        int32_t cL = c.x, cR = c.y;
+        const int4 q = shr.rq[slot];
+        int32_t cL = 0, cR = 0;
+        if (FULL || t < nfr) {  // (a lane past its block reads nothing more)
+            cL = cwin_corr(cw, L, (uint32_t)q.x, (uint32_t)q.y);
+            cR = cwin_corr(cw, R, (uint32_t)q.z, (uint32_t)q.w);
+        }
         ch.template frame_wvc<U, MONO>(L, R, cL, cR);
         L = wvf::add32(L, cL);
         R = wvf::add32(R, cR);
@@ -1041,7 +1060,7 @@ __device__ __forceinline__ void rframe(LChain<Ts...> &ch, const LShared &shr, ui
             if (fst) st2(o + 2u * t, make_int2(v, v));
             else o[t] = v;
         }
-        if (!FULL && t + 1u == nfr) lane_finish(rbad, e, mx, mn, crc);
+        if (!FULL && t + 1u == nfr) lane_finish(rbad | (HY == 2 && cw.used > cw.end ? 1u : 0u), e, mx, mn, crc);
         return;
     }
     if (joint) {
@@ -1059,7 +1078,7 @@ __device__ __forceinline__ void rframe(LChain<Ts...> &ch, const LShared &shr, ui
         if (nfr) st2(o + 2u * t, v);  // (a lane without a block of its own stores nothing)
     } else {
         if (t < nfr) st2(o + 2u * t, v);
-        if (t + 1u == nfr) lane_finish(rbad, e, mx, mn, crc);
+        if (t + 1u == nfr) lane_finish(rbad | (HY == 2 && cw.used > cw.end ? 1u : 0u), e, mx, mn, crc);
     }
 }
 
@@ -1197,9 +1216,6 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
         s.el[c] = 0;
     }
     // (every field set in every instantiation: left undefined, they stay memory -- scratch)
-    CWin cw;  // the .wvc stream (HY == 2; a local of its own: in LState it went to scratch)
-    if constexpr (HY == 2) cwin_init(cw, blob, lb.ok ? d.wvc_off : 0u, lb.ok ? d.wvc_len : 0u);
-    else cw = CWin{(const uint32_t *)blob, 0ull, 0, 0u, 0u, 0u, 0u, 0u};
     uint32_t pfin = 0u;
     uint32_t cpre = 0u;  // the recon's consumed count, read a group ahead (a lower bound: it only grows)
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), lgkm/exp untouched: the loop's waits count only its own loads
@@ -1230,9 +1246,9 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
         fu = u0 + nld;
         const uint64_t tg0 = (WV_LANE_COUNTERS && dbg) ? __builtin_readcyclecounter() : 0;
         if (g0 + GF < lb.nmin)  // (strict: the group holding a block's last frame records its verdict)
-            pgroup_try<true, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, mm, cnt, cw);
+            pgroup_try<true, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, mm, cnt);
         else
-            pgroup_try<false, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, mm, cnt, cw);
+            pgroup_try<false, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin, mm, cnt);
         if (WV_LANE_COUNTERS && dbg) cnt.words += __builtin_readcyclecounter() - tg0;
         // the reader stayed inside the units written before this group
         s.rp = rpos(s);
@@ -1286,8 +1302,8 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
 
 template <bool MONO, int HY, int... Ts>
 __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
-                                           uint32_t n, int32_t *__restrict__ out, uint32_t *__restrict__ status,
-                                           LShared &sh, uint32_t grp, uint32_t lane) {
+                                           uint32_t n, const uint8_t *__restrict__ blob, int32_t *__restrict__ out,
+                                           uint32_t *__restrict__ status, LShared &sh, uint32_t grp, uint32_t lane) {
     using namespace wvf;
     constexpr bool CODES = lane_codes<HY, Ts...>();
     const LBlock lb = lane_block<MONO, HY, Ts...>(descs, list, n, grp, lane);
@@ -1303,6 +1319,11 @@ __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, 
     ch.init(d, 0);
     Fixup fx;
     if constexpr (HY) fixup_init(fx, d);
+    // the .wvc stream (HY == 2): this wave reads the corrections -- the parser hands over
+    // each word's final interval, off its own chain
+    CWin cw;
+    if constexpr (HY == 2) cwin_init(cw, blob, lb.ok ? d.wvc_off : 0u, lb.ok ? d.wvc_len : 0u);
+    else cw = CWin{(const uint32_t *)blob, 0ull, 0, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
     uint32_t crc = 0xFFFFFFFFu;
     int32_t mx = 0, mn = 0;
     uint32_t rbad = 0u;
@@ -1316,23 +1337,23 @@ __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, 
         }
         rbad |= ch.wbad() ? 4u : 0u;
         if (g0 + GF < lb.nmin) {
-            rframe<0, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<1, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<2, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<3, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<4, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<5, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<6, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<7, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<0, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
+            rframe<1, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
+            rframe<2, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
+            rframe<3, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
+            rframe<4, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
+            rframe<5, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
+            rframe<6, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
+            rframe<7, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
         } else {
-            rframe<0, false, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<1, false, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<2, false, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<3, false, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<4, false, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<5, false, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<6, false, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
-            rframe<7, false, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx);
+            rframe<0, false, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
+            rframe<1, false, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
+            rframe<2, false, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
+            rframe<3, false, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
+            rframe<4, false, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
+            rframe<5, false, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
+            rframe<6, false, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
+            rframe<7, false, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
         }
         // the group's residuals are read (DS ops of one wave complete in order)
         w2::lds_publish(&sh.consumed, g0 + GF);
@@ -1376,7 +1397,7 @@ __device__ __forceinline__ void lane_blocks(const BlockDesc *__restrict__ descs,
     if ((wave & 1u) == 0u)
         lane_parser<MONO, HY, Ts...>(descs, list, n, blob, sh, (uint8_t *)rings, pair, grp, lane, dbg);
     else
-        lane_recon<MONO, HY, Ts...>(descs, list, n, out, status, sh, grp, lane);
+        lane_recon<MONO, HY, Ts...>(descs, list, n, blob, out, status, sh, grp, lane);
 }
 
 }  // namespace lane
