@@ -191,7 +191,7 @@ def pmc_traffic(kernel_substr: str = "wv_pcm_2wave<17, 17>"):
 
 
 # the bench kernel's name as rocprofv3 reports it (profiles/<tag>_pmc.json "kernel")
-KERNEL_NAMES = {"lane": "wv_pcm_lane<false, false, 17, 17>", "two_wave": "wv_pcm_2wave<17, 17>"}
+KERNEL_NAMES = {"lane": "wv_pcm_lane<false, 0, 17, 17>", "two_wave": "wv_pcm_2wave<17, 17>"}
 
 
 def verify(batches, pcm) -> dict:

@@ -56,7 +56,7 @@ for x in ([json.loads(l) for l in open(p) if l.startswith('{')] if os.path.exist
     TAG=${TAG:-r04} bash scripts/profile.sh || exit 1 ;;
   pmc_sq)
     bash scripts/pmc_sq.sh > /dev/null || exit 1
-    python3 scripts/pmc_sq_sum.py "${KSUB:-wv_pcm_lane<false, false, 17, 17>}" > $G/pmc_sq.txt && cat $G/pmc_sq.txt ;;
+    python3 scripts/pmc_sq_sum.py "${KSUB:-wv_pcm_lane<false, 0, 17, 17>}" > $G/pmc_sq.txt && cat $G/pmc_sq.txt ;;
   micro)
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 scripts/micro/issue.hip -o $G/issue && timeout -k 10 120 $G/issue > $G/micro.log 2>&1 || fail micro $? $G/micro.log
     cat $G/micro.log ;;

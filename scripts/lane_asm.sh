@@ -1,4 +1,4 @@
-# gfx950 assembly of the C2 lane kernel alone (wv_pcm_lane<false, false, 17, 17>) and a
+# gfx950 assembly of the C2 lane kernel alone (wv_pcm_lane<false, 0, 17, 17>) and a
 # per-basic-block instruction census of it (the fast group is the largest block).
 # usage: bash scripts/lane_asm.sh [out.s]
 set -e
