@@ -159,6 +159,11 @@ int wvg_batch_add_files_device(wvg_batch *b, int n, const uint8_t *const *files,
 int wvg_batch_file_info(const wvg_batch *b, int file, wvg_file_info *info);
 /* Files of the batch framed on the device / by the host fallback at its uploads. */
 int wvg_batch_framing_stats(const wvg_batch *b, int64_t *device_files, int64_t *host_files);
+/* Diagnostics: which launch groups the last wvg_batch_decode ran on the lane / row
+ * kernels (bit t: PCM term-set group t, 0..7; bit 8: .wvc blocks; bit 9: DSD mode 3;
+ * bit 10: DSD mode 1) -- under WVG_KERNEL_AUTO the choice depends on whether other
+ * batches of the context overlapped within the last second.  No reference counterpart. */
+int wvg_batch_lane_groups(const wvg_batch *b, uint32_t *mask);
 
 /* Drop every file of the batch but keep its device and page-locked host
  * buffers (a decode server refills one batch per request). */

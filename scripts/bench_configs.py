@@ -174,6 +174,8 @@ def main():
     ap.add_argument("--c3-blocks", type=int, default=4096)
     ap.add_argument("--c3-copies", type=int, default=1)
     ap.add_argument("--c5-files", type=int, default=4000)
+    ap.add_argument("--list-blocks", type=int, default=1024, help="blocks per batch of the 'lists' config")
+    ap.add_argument("--lists", default="", help="'lists' config: comma-separated name prefixes (default all)")
     ap.add_argument("--dsd-files", type=int, default=64, help="files per DSD mode batch (one block each)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="also time the oracle on this many host threads")
     ap.add_argument("--inflight", type=int, default=1, help="also time this many copies of each batch in flight")
@@ -211,6 +213,21 @@ def main():
             run_wvc("C4 1024 x 22050 float32 hybrid+bitrate + .wvc (exact)", wv, wvc, exact=ref)
         elif c == "c5":
             run(f"C5 mixed corpus, files 0..{a.c5_files - 1}", corpora.c5(a.c5_files))
+        elif c == "lists":
+            # C2's shape (1,024 x 22,050-frame 16-bit stereo blocks) under term lists with and
+            # without a lane instantiation: the run-time list kernel (wv_pcm_lane_rt) against
+            # the compile-time ones on the same PCM
+            from synth import wvsynth as S
+            pcm = corpora.c2_pcm(a.list_blocks)
+            lists = {"default (instantiated)": S.TERMS_DEFAULT, "alt5 (run-time)": [18, 18, 2, 3, -1],
+                     "high16 (instantiated)": S.TERMS_HIGH,
+                     "alt16 (run-time)": [18, 18, 2, 3, -1, 18, 2, 4, 7, 5, 3, 6, 8, -2, 17, 2],
+                     "high10 (run-time)": S.TERMS_HIGH10}
+            for nm, t in lists.items():
+                if a.lists and not any(nm.startswith(x) for x in a.lists.split(",")):
+                    continue
+                data = S.encode_pcm_parallel(pcm, S.EncParams(terms=t, block_samples=22050, joint_stereo=True))
+                run(f"C2-shape {a.list_blocks} x 22050 16-bit stereo, list {nm}", [data], pcm)
         elif c.startswith("dsd"):  # dsd0 / dsd1 / dsd3: N stereo files of one 22,050-frame block in one mode
             from synth import wvsynth as S
             mode = int(c[3:])

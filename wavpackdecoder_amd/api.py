@@ -161,6 +161,13 @@ class DecodeBatch:
         self._check(self._L.wvg_batch_framing_stats(self._b, ctypes.byref(dev), ctypes.byref(host)))
         return int(dev.value), int(host.value)
 
+    def lane_groups(self) -> int:
+        """Diagnostics: the launch groups the last decode ran on lane / row kernels (bit t:
+        PCM term set t; 8 .wvc; 9 DSD mode 3; 10 DSD mode 1) -- wvg_batch_lane_groups."""
+        m = ctypes.c_uint32()
+        self._check(self._L.wvg_batch_lane_groups(self._b, ctypes.byref(m)))
+        return int(m.value)
+
     def upload(self):
         self._check(self._L.wvg_batch_upload(self._b))
         for i in range(len(self.infos)):  # device-framed files get their infos here

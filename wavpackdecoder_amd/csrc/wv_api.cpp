@@ -4,6 +4,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <cstddef>
 #include <chrono>
@@ -26,6 +27,7 @@ hipError_t launch_decode(const BlockDesc *descs, const uint32_t *pcm_list, uint3
                          int lane_mode_fast, uint32_t n_fast_mono, int lane_mode_wvc, uint32_t n_pcm_wvc);
 bool wvc_lane_candidate(const BlockDesc &d);
 int term_set_of(const BlockDesc &d, int prefer_pipe);
+bool lane_rt_group(int ts);  // the launch groups of the run-time list lane kernel (wv_pcm_lane_rt)
 hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, uint32_t n, const uint8_t *blob,
                         int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s, int lane_mode,
                         const uint32_t *lane_list, uint32_t lane_n, uint32_t *lane_dbg);
@@ -66,6 +68,10 @@ constexpr int kSide = kMaxTermSets + 3;  // term sets, generic PCM, DSD, DSD mod
 // DSD mode 1 and the PCM groups side by side, 54.6 ms, as with a lane per group).
 constexpr int kLanes = 3;
 constexpr size_t kAutoLaneMin = 2048;  // WVG_KERNEL_AUTO: larger groups decode on lanes even alone
+// how long a context keeps the lane kernels after batches last overlapped (a caller that
+// keeps several batches in flight issues its next decode well within it; one that went
+// back to a batch at a time gets the latency kernels again after it)
+constexpr double kConcurrentHoldMs = 1000.0;
 // The part of a device-framed descriptor the host reads (kind, flags, frames, the
 // call schedule, status, terms): everything up to and including term[].  The rest
 // (weights, histories, DSD, seek, sticky, .wvc, exact float) is zero or unused on
@@ -81,7 +87,9 @@ struct wvg_ctx {
     std::mutex mu;                   // guards `batches` and `side`
     std::vector<wvg_batch *> batches;  // live batches (a decode counts those still running)
     hipStream_t side[kLanes - 1] = {nullptr};  // side streams: lanes 1 .. kLanes - 1 of a decode
-    std::atomic<bool> concurrent{false};  // a decode was once issued while another batch ran (WVG_KERNEL_AUTO)
+    // when a decode last found another batch of this context running (now_ms; WVG_KERNEL_AUTO
+    // keeps the lane kernels for kConcurrentHoldMs after it)
+    std::atomic<double> concurrent_ms{-1e30};
 };
 
 // Page-locked, grow-only host buffer: the batch's file bytes live here from
@@ -179,6 +187,7 @@ struct wvg_batch {
     int lanes = kLanes;                                 // WVG_LANES: streams per decode (A/B of the queue mapping)
     bool lanes_env = false;                             // WVG_LANES given: no in-flight policy (wvg_batch_decode)
     int lane_mode = 1;                                  // term-set groups on the lane-per-block kernel (wvg_batch_set_kernel)
+    uint32_t lane_groups = 0;                           // the last decode's groups on lane kernels (wvg_batch_lane_groups)
     bool kernel_auto = true;                            // WVG_KERNEL_AUTO: lane_mode chosen per decode and group
     bool log_decodes = false;                           // WVG_DECODE_LOG=1: each decode's streams and kernels on stderr
     std::vector<uint32_t> h_status, h_aux;
@@ -918,6 +927,12 @@ int wvg_batch_file_info(const wvg_batch *b, int file, wvg_file_info *info) {
     return b->finfo[(size_t)file].open_ok ? WVG_OK : WVG_ERR_OPEN;
 }
 
+int wvg_batch_lane_groups(const wvg_batch *b, uint32_t *mask) {
+    if (!b || !mask) return WVG_ERR_ARG;
+    *mask = b->lane_groups;
+    return WVG_OK;
+}
+
 int wvg_batch_framing_stats(const wvg_batch *b, int64_t *device_files, int64_t *host_files) {
     if (!b) return WVG_ERR_ARG;
     if (device_files) *device_files = b->framed_dev;
@@ -947,16 +962,41 @@ static void build_lane_orders(wvg_batch *b) {
     auto pad = [](std::vector<uint32_t> &v) {
         while (v.size() & 63u) v.push_back(kLaneGap);
     };
-    std::vector<uint32_t> rest;
+    // The run-time list kernel's groups (lane_rt_group) are ordered by list first --
+    // mono / stereo, length, terms -- each list in waves of its own: a wave decodes the
+    // list of its first block and hands back any other.
+    auto lkey = [&](uint32_t k) {
+        const BlockDesc &d = b->fo.descs[k];
+        std::array<int8_t, MAXP + 2> key{};
+        key[0] = (d.flags & wvf::MONO_DATA) ? 1 : 0;
+        key[1] = (int8_t)d.num_terms;
+        for (int i = 0; i < d.num_terms && i < MAXP; i++) key[2 + i] = d.term[i];
+        return key;
+    };
+    std::vector<uint32_t> rest, part;
     for (int t = 0; t < kMaxTermSets; t++) {
         std::vector<uint32_t> &L = b->ts_list[t], &LL = b->ts_lane[t];
         LL.clear();
         if (L.empty()) continue;
         std::sort(L.begin(), L.end(), by_len_density);
-        rest.clear();
-        for (uint32_t k : L) (silent(k) ? LL : rest).push_back(k);
-        if (!LL.empty() && !rest.empty()) pad(LL);
-        LL.insert(LL.end(), rest.begin(), rest.end());
+        std::vector<uint32_t> order = L;
+        if (lane_rt_group(t))
+            std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return lkey(x) < lkey(y); });
+        for (size_t i = 0; i < order.size();) {
+            size_t j = i + 1;
+            if (lane_rt_group(t))
+                while (j < order.size() && lkey(order[j]) == lkey(order[i])) j++;
+            else
+                j = order.size();
+            part.clear();
+            rest.clear();
+            for (size_t k = i; k < j; k++) (silent(order[k]) ? part : rest).push_back(order[k]);
+            if (!part.empty() && !rest.empty()) pad(part);
+            part.insert(part.end(), rest.begin(), rest.end());
+            if (!LL.empty()) pad(LL);
+            LL.insert(LL.end(), part.begin(), part.end());
+            i = j;
+        }
         while (!LL.empty() && LL.back() == kLaneGap) LL.pop_back();
     }
 }
@@ -1167,20 +1207,23 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
     // on one per launch group (profiles/r04_c5_streams.txt).
     // (asked only when it decides something: a multi-group decode's streams, or the
     // default kernel choice before the context has seen batches overlap)
-    const bool ask = (!b->lanes_env && b->lanes > 1 && n > 1) || (b->kernel_auto && !c->concurrent);
+    const double t_now = now_ms();
+    const bool held = t_now - c->concurrent_ms.load() < kConcurrentHoldMs;
+    const bool ask = (!b->lanes_env && b->lanes > 1 && n > 1) || (b->kernel_auto && !held);
     const bool running = ask && others_running(b);
     int nlanes = b->lanes;
     if (!b->lanes_env && nlanes > 1 && running) nlanes = 1;
     // WVG_KERNEL_AUTO: in a context that has had batches in flight together, the lane
-    // kernels (throughput); in one that decodes a batch at a time, a group of at most
+    // kernels (throughput) -- for kConcurrentHoldMs after a decode last found another
+    // batch running; in one that decodes a batch at a time, a group of at most
     // kAutoLaneMin blocks on the one-workgroup / one-wave-per-block kernels, whose chains
     // run faster than a lane's (C2 alone: 6.5 vs 7.5 ms; C4 15.4 vs 24.4; DSD mode 3 34 vs
     // 56), larger ones on lanes (C3's 4,096 blocks: 24.8 vs 37.7 ms).  (Not per decode: a
     // lane workgroup needs a whole CU's LDS, and a two-wave decode among lane decodes
     // leaves CUs partly taken -- C4 at 20 in flight fell from 16,000 to 8,200 Mframes/s
     // when the first decode of each round ran alone on the two-wave kernel.)
-    if (running) c->concurrent = true;
-    const bool lanes_now = c->concurrent;
+    if (running) c->concurrent_ms = t_now;
+    const bool lanes_now = running || held;
     auto mode_of = [&](size_t nblocks) -> int {
         if (!b->kernel_auto) return b->lane_mode;
         return (lanes_now || nblocks > kAutoLaneMin) ? 1 : 0;
@@ -1256,6 +1299,15 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
                             // (.wvc blocks: the lane kernel even alone -- 35.8 against the generic
                             // kernel's 130 ms for C4's 1,024 blocks, profiles/r05_c4wvc_rates.jsonl)
                             b->kernel_auto ? 1 : b->lane_mode, b->pcm_wvc_n));
+    {   // the launch groups this decode gave to lane / row kernels (wvg_batch_lane_groups)
+        uint32_t m = 0;
+        for (int t = 0; t < kMaxTermSets; t++)
+            if (!b->ts_list[t].empty() && mode_of(b->ts_list[t].size())) m |= 1u << t;
+        if (b->pcm_wvc_n && (b->kernel_auto || b->lane_mode)) m |= 1u << kPcm;
+        if (b->dsd_list.size() > b->dsd_high_lo && mode_of(b->dsd_list.size() - b->dsd_high_lo)) m |= 1u << kDsd;
+        if (b->dsd_fast_n && mode_of(b->dsd_fast_n)) m |= 1u << kDsd1;
+        b->lane_groups = m;
+    }
     HIPCHK(c, mark(kDsd));
     HIPCHK(c, mark(kDsd1));
     HIPCHK(c, mark(kPcm));

@@ -1252,6 +1252,8 @@ static const bool kLaneSetNeg12[kNumLaneSets] = {true, false};
 // which two-wave kernel decodes this block (-1: the generic wave kernel, for
 // int32 + wvx, .wvc, exact-float and chained blocks).  prefer_pipe 2: every list goes to the pipelined kernel
 // (A/B tests)
+bool lane_rt_group(int ts) { return ts == kPipe || ts == kPipe + 1; }
+
 int term_set_of(const BlockDesc &d, int prefer_pipe) {
     using namespace wvf;
     if (d.kind != KIND_PCM) return -1;
@@ -1346,6 +1348,18 @@ hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, ui
             if (lane_mode != 2)  // 2: the lane kernel alone (diagnostics: ST_REDO stays in the status)
                 hipLaunchKernelGGL((wv_pcm_2wave_redo<WVG_TS_M5>), g, b, 0, s, descs, list, blob, out, status, aux);
             break;
+        }
+        return hipGetLastError();
+    }
+    if (lane_mode && (ts == kPipe || ts == kPipe + 1)) {
+        // every other lossless list of up to 16 terms: the run-time list lane kernel (the
+        // host orders its lane list by list, wv_api.cpp build_lane_orders), then the
+        // pipelined kernel over its hand-backs
+        dim3 gl((lane_n + 64 * lane::LPAIRS - 1) / (64 * lane::LPAIRS)), bl(64 * lane::LPAIRS * 2);
+        if (hipError_t e = launch_lane(LANE_RT, gl, bl, s, descs, lane_list, lane_n, blob, out, status, lane_dbg); e != hipSuccess) return e;
+        if (lane_mode != 2) {
+            if (ts == kPipe + 1) hipLaunchKernelGGL((wv_pcm_pipe_redo<true>), g, b, 0, s, descs, list, blob, out, status, aux);
+            else hipLaunchKernelGGL((wv_pcm_pipe_redo<false>), g, b, 0, s, descs, list, blob, out, status, aux);
         }
         return hipGetLastError();
     }

@@ -45,6 +45,68 @@ __device__ __forceinline__ int32_t aw(int32_t w, int32_t s) {  // apply_weight (
     return (int32_t)(((int64_t)w * (int64_t)s + 512) >> 10);
 }
 
+// frame t (t % 8 == U): the sample-major form of decorr_stereo_pass
+// (pass_stereo, wv_decode_core.h; the ring of terms 1..8 read at t & 7, written at (t + T) & 7);
+// MONO: decorr_mono_pass (UnpackUtils.cs:1085-1154), channel A alone
+template <int T, int U, bool MONO>
+__device__ __forceinline__ void lp_frame(int32_t &wA, int32_t &wB, const int32_t dl, int32_t *hA, int32_t *hB, int32_t &L,
+                                         int32_t &R) {
+    using namespace wvf;
+    static_assert(!MONO || T > 0, "mono lists have positive terms only");
+    if constexpr (T == 17 || T == 18) {
+        const int32_t sa = T == 17 ? sub32(mul32(2, hA[0]), hA[1]) : (sub32(mul32(3, hA[0]), hA[1]) >> 1);
+        const int32_t oa = add32(aw(wA, sa), L);
+        wA = w2::vupd(wA, sa, L, dl);
+        hA[1] = hA[0];
+        hA[0] = oa;
+        L = oa;
+        if constexpr (MONO) return;
+        const int32_t sb = T == 17 ? sub32(mul32(2, hB[0]), hB[1]) : (sub32(mul32(3, hB[0]), hB[1]) >> 1);
+        const int32_t ob = add32(aw(wB, sb), R);
+        wB = w2::vupd(wB, sb, R, dl);
+        hB[1] = hB[0];
+        hB[0] = ob;
+        R = ob;
+    } else if constexpr (T >= 1 && T <= 8) {
+        const int32_t sa = hA[U & 7];
+        const int32_t oa = add32(aw(wA, sa), L);
+        wA = w2::vupd(wA, sa, L, dl);
+        hA[(U + T) & 7] = oa;
+        L = oa;
+        if constexpr (MONO) return;
+        const int32_t sb = hB[U & 7];
+        const int32_t ob = add32(aw(wB, sb), R);
+        wB = w2::vupd(wB, sb, R, dl);
+        hB[(U + T) & 7] = ob;
+        R = ob;
+    } else if constexpr (T == -1) {
+        const int32_t sa = add32(L, aw(wA, hA[0]));
+        wA = w2::vupdc(wA, hA[0], L, dl);
+        L = sa;
+        const int32_t o = add32(R, aw(wB, sa));
+        wB = w2::vupdc(wB, sa, R, dl);
+        R = o;
+        hA[0] = o;
+    } else if constexpr (T == -2) {
+        const int32_t sb = add32(R, aw(wB, hB[0]));
+        wB = w2::vupdc(wB, hB[0], R, dl);
+        R = sb;
+        const int32_t o = add32(L, aw(wA, sb));
+        wA = w2::vupdc(wA, sb, L, dl);
+        L = o;
+        hB[0] = o;
+    } else if constexpr (T == -3) {
+        const int32_t sa = add32(L, aw(wA, hA[0]));
+        wA = w2::vupdc(wA, hA[0], L, dl);
+        const int32_t sb = add32(R, aw(wB, hB[0]));
+        wB = w2::vupdc(wB, hB[0], R, dl);
+        hB[0] = sa;
+        hA[0] = sb;
+        L = sa;
+        R = sb;
+    }
+}
+
 // one decorrelation pass, both channels in the lane (decoder order, as BlockDesc.term)
 template <int T>
 struct LPass {
@@ -62,65 +124,10 @@ struct LPass {
             hB[i] = d.samples_B[p][i];
         }
     }
-    // frame t (t % 8 == U): the sample-major form of decorr_stereo_pass
-    // (pass_stereo, wv_decode_core.h; the ring of terms 1..8 read at t & 7, written at (t + T) & 7);
-    // MONO: decorr_mono_pass (UnpackUtils.cs:1085-1154), channel A alone
+    // frame t (t % 8 == U): lp_frame
     template <int U, bool MONO>
     __device__ __forceinline__ void frame(int32_t &L, int32_t &R) {
-        using namespace wvf;
-        static_assert(!MONO || T > 0, "mono lists have positive terms only");
-        if constexpr (T == 17 || T == 18) {
-            const int32_t sa = T == 17 ? sub32(mul32(2, hA[0]), hA[1]) : (sub32(mul32(3, hA[0]), hA[1]) >> 1);
-            const int32_t oa = add32(aw(wA, sa), L);
-            wA = w2::vupd(wA, sa, L, dl);
-            hA[1] = hA[0];
-            hA[0] = oa;
-            L = oa;
-            if constexpr (MONO) return;
-            const int32_t sb = T == 17 ? sub32(mul32(2, hB[0]), hB[1]) : (sub32(mul32(3, hB[0]), hB[1]) >> 1);
-            const int32_t ob = add32(aw(wB, sb), R);
-            wB = w2::vupd(wB, sb, R, dl);
-            hB[1] = hB[0];
-            hB[0] = ob;
-            R = ob;
-        } else if constexpr (T >= 1 && T <= 8) {
-            const int32_t sa = hA[U & 7];
-            const int32_t oa = add32(aw(wA, sa), L);
-            wA = w2::vupd(wA, sa, L, dl);
-            hA[(U + T) & 7] = oa;
-            L = oa;
-            if constexpr (MONO) return;
-            const int32_t sb = hB[U & 7];
-            const int32_t ob = add32(aw(wB, sb), R);
-            wB = w2::vupd(wB, sb, R, dl);
-            hB[(U + T) & 7] = ob;
-            R = ob;
-        } else if constexpr (T == -1) {
-            const int32_t sa = add32(L, aw(wA, hA[0]));
-            wA = w2::vupdc(wA, hA[0], L, dl);
-            L = sa;
-            const int32_t o = add32(R, aw(wB, sa));
-            wB = w2::vupdc(wB, sa, R, dl);
-            R = o;
-            hA[0] = o;
-        } else if constexpr (T == -2) {
-            const int32_t sb = add32(R, aw(wB, hB[0]));
-            wB = w2::vupdc(wB, hB[0], R, dl);
-            R = sb;
-            const int32_t o = add32(L, aw(wA, sb));
-            wA = w2::vupdc(wA, sb, L, dl);
-            L = o;
-            hB[0] = o;
-        } else if constexpr (T == -3) {
-            const int32_t sa = add32(L, aw(wA, hA[0]));
-            wA = w2::vupdc(wA, hA[0], L, dl);
-            const int32_t sb = add32(R, aw(wB, hB[0]));
-            wB = w2::vupdc(wB, hB[0], R, dl);
-            hB[0] = sa;
-            hA[0] = sb;
-            L = sa;
-            R = sb;
-        }
+        lp_frame<T, U, MONO>(wA, wB, dl, hA, hB, L, R);
     }
     // .wvc (HY == 2): the frame with the exact-minus-lossy differences cL / cR carried
     // along (pass_stereo_wvc, wv_decode_core.h): a pass predicting from history moves
@@ -181,6 +188,100 @@ struct LChain<T, Ts...> {
         rest.template frame_wvc<U, MONO>(L, R, cL, cR);
     }
     __device__ __forceinline__ bool wbad() const { return p.wbad() || rest.wbad(); }
+};
+
+// A term list read at run time (lane kernels with Ts = {LANE_RT, NS}): up to NS passes,
+// the list of the pair's first block, which every lane of the pair shares (lane_block;
+// a block with another list is handed back).  The passes run pass-major over a group's
+// GF frames: one wave-uniform branch on a slot's term per group, each term's frames
+// with the compile-time register indices of lp_frame (a slot holds every term's
+// registers: LPass<1>'s two 8-entry rings).  UnpackUtils.cs:156-187 (any list of
+// -3..-1, 1..8, 17, 18), :688-1154 (the passes).
+constexpr int LANE_RT = 99;
+template <int... Ts>
+struct LaneRt {
+    static constexpr int NS = 0;
+};
+template <int N>
+struct LaneRt<LANE_RT, N> {
+    static constexpr int NS = N;
+};
+static_assert(offsetof(BlockDesc, term) % 4 == 0, "lane_block reads a list as dwords");
+template <int NS>
+struct RChain {
+    LPass<1> p[NS];
+    uint32_t tw[4];  // the terms, four to a dword (wave-uniform)
+    int32_t nt;      // (wave-uniform)
+    __device__ __forceinline__ void init(const BlockDesc &d, const uint32_t *ptw, int32_t pnt) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) tw[k] = ptw[k];
+        nt = pnt;
+#pragma unroll
+        for (int i = 0; i < NS; i++) {
+            p[i].init(d, i);
+            if (i >= nt) p[i].wA = p[i].wB = p[i].dl = 0;  // (wbad: a slot past the list)
+        }
+    }
+    __device__ __forceinline__ int term(int i) const { return (int32_t)(int8_t)(tw[i >> 2] >> (8 * (i & 3))); }
+    template <int T, bool MONO>
+    __device__ __forceinline__ static void run(LPass<1> &q, int32_t (&L)[GF], int32_t (&R)[GF]) {
+        if constexpr (MONO && T < 0) {
+            return;  // (lane_ok: a mono list has positive terms only)
+        } else {
+            lp_frame<T, 0, MONO>(q.wA, q.wB, q.dl, q.hA, q.hB, L[0], R[0]);
+            lp_frame<T, 1, MONO>(q.wA, q.wB, q.dl, q.hA, q.hB, L[1], R[1]);
+            lp_frame<T, 2, MONO>(q.wA, q.wB, q.dl, q.hA, q.hB, L[2], R[2]);
+            lp_frame<T, 3, MONO>(q.wA, q.wB, q.dl, q.hA, q.hB, L[3], R[3]);
+            lp_frame<T, 4, MONO>(q.wA, q.wB, q.dl, q.hA, q.hB, L[4], R[4]);
+            lp_frame<T, 5, MONO>(q.wA, q.wB, q.dl, q.hA, q.hB, L[5], R[5]);
+            lp_frame<T, 6, MONO>(q.wA, q.wB, q.dl, q.hA, q.hB, L[6], R[6]);
+            lp_frame<T, 7, MONO>(q.wA, q.wB, q.dl, q.hA, q.hB, L[7], R[7]);
+        }
+    }
+    // the group's GF frames through passes I.. (frame t of the group at index t % GF;
+    // template recursion: every slot's registers at compile-time indices)
+    template <int I, bool MONO>
+    __device__ __forceinline__ void group_from(int32_t (&L)[GF], int32_t (&R)[GF]) {
+        if constexpr (I < NS) {
+            if (I >= nt) return;
+            switch (term(I)) {
+            case 1: run<1, MONO>(p[I], L, R); break;
+            case 2: run<2, MONO>(p[I], L, R); break;
+            case 3: run<3, MONO>(p[I], L, R); break;
+            case 4: run<4, MONO>(p[I], L, R); break;
+            case 5: run<5, MONO>(p[I], L, R); break;
+            case 6: run<6, MONO>(p[I], L, R); break;
+            case 7: run<7, MONO>(p[I], L, R); break;
+            case 8: run<8, MONO>(p[I], L, R); break;
+            case 17: run<17, MONO>(p[I], L, R); break;
+            case 18: run<18, MONO>(p[I], L, R); break;
+            case -1: run<-1, MONO>(p[I], L, R); break;
+            case -2: run<-2, MONO>(p[I], L, R); break;
+            default: run<-3, MONO>(p[I], L, R); break;
+            }
+            group_from<I + 1, MONO>(L, R);
+        }
+    }
+    template <bool MONO>
+    __device__ __forceinline__ void group(int32_t (&L)[GF], int32_t (&R)[GF]) {
+        group_from<0, MONO>(L, R);
+    }
+    // (negative terms' weights stay within +-1024: the test holds for them too)
+    __device__ __forceinline__ bool wbad() const {
+        bool b = false;
+#pragma unroll
+        for (int i = 0; i < NS; i++) b |= p[i].wbad();
+        return b;
+    }
+};
+
+template <int... Ts>
+struct ChainOf {
+    using type = LChain<Ts...>;
+};
+template <int N>
+struct ChainOf<LANE_RT, N> {
+    using type = RChain<N>;
 };
 
 // The 64 lanes' rings are interleaved by dword: dword k of a lane's stream (a count
@@ -1021,14 +1122,11 @@ __device__ __forceinline__ int32_t rdecode(uint32_t x, uint32_t low, uint32_t mc
     const int32_t sg = __builtin_amdgcn_sbfe((int32_t)x, used, 1);
     return (int32_t)(add3(low, v, big ? t : 0u) ^ (uint32_t)sg);
 }
-template <int U, bool FULL, bool MONO, int HY, bool CODES, int... Ts>
-__device__ __forceinline__ void rframe(LChain<Ts...> &ch, const LShared &shr, uint32_t lane, uint32_t g0, uint32_t nfr,
-                                       bool joint, int32_t &mx, int32_t &mn, uint32_t &crc, uint32_t sh, int32_t *o,
-                                       uint32_t rbad, const LEnd &e, bool fst, const Fixup &fx, CWin &cw) {
-    const uint32_t t = g0 + U;
+// frame t = g0 + U's two word values from the parser's slot
+template <int U, bool MONO, bool CODES>
+__device__ __forceinline__ void rin(const LShared &shr, uint32_t lane, uint32_t g0, int32_t &L, int32_t &R) {
     const uint32_t slot = (((g0 % (uint32_t)RF) + U) << 6) + lane;
     const int2 r = shr.rm[slot];
-    int32_t L, R;
     if constexpr (CODES) {
         const int4 q = shr.rq[slot];
         L = rdecode((uint32_t)q.x, (uint32_t)q.y, (uint32_t)r.x);
@@ -1037,19 +1135,14 @@ __device__ __forceinline__ void rframe(LChain<Ts...> &ch, const LShared &shr, ui
         L = r.x;
         R = r.y;
     }
-    if constexpr (HY == 2) {  // the exact values; the passes keep the lossy history
-        const int4 q = shr.rq[slot];
-        int32_t cL = 0, cR = 0;
-        if (FULL || t < nfr) {  // (a lane past its block reads nothing more)
-            cL = cwin_corr(cw, L, (uint32_t)q.x, (uint32_t)q.y);
-            cR = cwin_corr(cw, R, (uint32_t)q.z, (uint32_t)q.w);
-        }
-        ch.template frame_wvc<U, MONO>(L, R, cL, cR);
-        L = wvf::add32(L, cL);
-        R = wvf::add32(R, cR);
-    } else {
-        ch.template frame<U, MONO>(L, R);
-    }
+}
+// frame t = g0 + U after the passes: joint stereo, the mute bound, the CRC, the fixup,
+// the stores, and the block's verdict after its last frame
+template <int U, bool FULL, bool MONO, int HY>
+__device__ __forceinline__ void rout(int32_t L, int32_t R, uint32_t g0, uint32_t nfr, bool joint, int32_t &mx,
+                                     int32_t &mn, uint32_t &crc, uint32_t sh, int32_t *o, uint32_t rbad, const LEnd &e,
+                                     bool fst, const Fixup &fx, const CWin &cw) {
+    const uint32_t t = g0 + U;
     if constexpr (MONO) {
         mx = max(mx, L);
         mn = min(mn, L);
@@ -1081,6 +1174,52 @@ __device__ __forceinline__ void rframe(LChain<Ts...> &ch, const LShared &shr, ui
         if (t + 1u == nfr) lane_finish(rbad | (HY == 2 && cw.used > cw.end ? 1u : 0u), e, mx, mn, crc);
     }
 }
+template <int U, bool FULL, bool MONO, int HY, bool CODES, int... Ts>
+__device__ __forceinline__ void rframe(LChain<Ts...> &ch, const LShared &shr, uint32_t lane, uint32_t g0, uint32_t nfr,
+                                       bool joint, int32_t &mx, int32_t &mn, uint32_t &crc, uint32_t sh, int32_t *o,
+                                       uint32_t rbad, const LEnd &e, bool fst, const Fixup &fx, CWin &cw) {
+    const uint32_t t = g0 + U;
+    int32_t L, R;
+    rin<U, MONO, CODES>(shr, lane, g0, L, R);
+    if constexpr (HY == 2) {  // the exact values; the passes keep the lossy history
+        const int4 q = shr.rq[(((g0 % (uint32_t)RF) + U) << 6) + lane];
+        int32_t cL = 0, cR = 0;
+        if (FULL || t < nfr) {  // (a lane past its block reads nothing more)
+            cL = cwin_corr(cw, L, (uint32_t)q.x, (uint32_t)q.y);
+            cR = cwin_corr(cw, R, (uint32_t)q.z, (uint32_t)q.w);
+        }
+        ch.template frame_wvc<U, MONO>(L, R, cL, cR);
+        L = wvf::add32(L, cL);
+        R = wvf::add32(R, cR);
+    } else {
+        ch.template frame<U, MONO>(L, R);
+    }
+    rout<U, FULL, MONO, HY>(L, R, g0, nfr, joint, mx, mn, crc, sh, o, rbad, e, fst, fx, cw);
+}
+// a group of a run-time list (RChain): the frames' values, the passes pass-major, the frames' tails
+template <bool FULL, bool MONO, bool CODES, int NS>
+__device__ __forceinline__ void rgroup_rt(RChain<NS> &ch, const LShared &shr, uint32_t lane, uint32_t g0, uint32_t nfr,
+                                          bool joint, int32_t &mx, int32_t &mn, uint32_t &crc, uint32_t sh, int32_t *o,
+                                          uint32_t rbad, const LEnd &e, bool fst, const Fixup &fx, const CWin &cw) {
+    int32_t L[GF], R[GF];
+    rin<0, MONO, CODES>(shr, lane, g0, L[0], R[0]);
+    rin<1, MONO, CODES>(shr, lane, g0, L[1], R[1]);
+    rin<2, MONO, CODES>(shr, lane, g0, L[2], R[2]);
+    rin<3, MONO, CODES>(shr, lane, g0, L[3], R[3]);
+    rin<4, MONO, CODES>(shr, lane, g0, L[4], R[4]);
+    rin<5, MONO, CODES>(shr, lane, g0, L[5], R[5]);
+    rin<6, MONO, CODES>(shr, lane, g0, L[6], R[6]);
+    rin<7, MONO, CODES>(shr, lane, g0, L[7], R[7]);
+    ch.template group<MONO>(L, R);
+    rout<0, FULL, MONO, 0>(L[0], R[0], g0, nfr, joint, mx, mn, crc, sh, o, rbad, e, fst, fx, cw);
+    rout<1, FULL, MONO, 0>(L[1], R[1], g0, nfr, joint, mx, mn, crc, sh, o, rbad, e, fst, fx, cw);
+    rout<2, FULL, MONO, 0>(L[2], R[2], g0, nfr, joint, mx, mn, crc, sh, o, rbad, e, fst, fx, cw);
+    rout<3, FULL, MONO, 0>(L[3], R[3], g0, nfr, joint, mx, mn, crc, sh, o, rbad, e, fst, fx, cw);
+    rout<4, FULL, MONO, 0>(L[4], R[4], g0, nfr, joint, mx, mn, crc, sh, o, rbad, e, fst, fx, cw);
+    rout<5, FULL, MONO, 0>(L[5], R[5], g0, nfr, joint, mx, mn, crc, sh, o, rbad, e, fst, fx, cw);
+    rout<6, FULL, MONO, 0>(L[6], R[6], g0, nfr, joint, mx, mn, crc, sh, o, rbad, e, fst, fx, cw);
+    rout<7, FULL, MONO, 0>(L[7], R[7], g0, nfr, joint, mx, mn, crc, sh, o, rbad, e, fst, fx, cw);
+}
 
 // CODES: the parser hands the reconstruction wave each word's (x, low, mc) and the
 // reconstruction computes the value (rdecode), taking ~13 instructions a word off
@@ -1088,7 +1227,7 @@ __device__ __forceinline__ void rframe(LChain<Ts...> &ch, const LShared &shr, ui
 // lists' passes already load it more than the words load the parser); hybrid words
 // (bisection) hand over values
 template <int HY, int... Ts>
-constexpr bool lane_codes() { return !HY && sizeof...(Ts) <= 5; }
+constexpr bool lane_codes() { return !HY && (LaneRt<Ts...>::NS ? LaneRt<Ts...>::NS : (int)sizeof...(Ts)) <= 5; }
 
 // can this lane decode block d exactly (else ST_REDO)?
 template <bool MONO, int HY, int... Ts>
@@ -1105,6 +1244,16 @@ __device__ __forceinline__ bool lane_ok(const BlockDesc &d) {
     if (((d.flags & MONO_DATA) != 0) != MONO) return false;
     if ((d.wvc_len != 0) != (HY == 2)) return false;  // HY 2: hybrid blocks with their .wvc stream
     if (d.inherit || d.chain_len >= 2 || d.wvx_state || d.xfloat || d.pre_end || d.fstatus) return false;
+    if constexpr (LaneRt<Ts...>::NS != 0) {  // a run-time list: its length and terms (lane_block: the pair's list)
+        static_assert(!HY, "run-time lists: lossless");
+        if (d.num_terms < 0 || d.num_terms > LaneRt<Ts...>::NS) return false;
+        for (int i = 0; i < d.num_terms; i++) {
+            const int t = d.term[i];
+            // (term 0: pass_stereo's call-position rule, the generic kernel; mono: positive terms)
+            if (!((t >= 1 && t <= 8) || t == 17 || t == 18 || (!MONO && t < 0 && t >= -3))) return false;
+        }
+        return true;
+    }
     if (d.num_terms != (int32_t)sizeof...(Ts)) return false;
     constexpr int8_t terms[sizeof...(Ts) + 1] = {(int8_t)Ts..., 0};
     for (int i = 0; i < (int)sizeof...(Ts); i++)
@@ -1116,6 +1265,8 @@ __device__ __forceinline__ bool lane_ok(const BlockDesc &d) {
 struct LBlock {
     uint32_t bi, nfr, nmax, nmin;
     bool ok, inl;
+    uint32_t tw[4];  // run-time lists: the pair's terms (wave-uniform)
+    int32_t nt;
 };
 template <bool MONO, int HY, int... Ts>
 __device__ __forceinline__ LBlock lane_block(const BlockDesc *descs, const uint32_t *list, uint32_t n, uint32_t grp,
@@ -1127,6 +1278,30 @@ __device__ __forceinline__ LBlock lane_block(const BlockDesc *descs, const uint3
     b.inl = li < n && list[li] != kLaneGap;
     b.bi = b.inl ? list[li] : 0u;
     b.ok = b.inl && lane_ok<MONO, HY, Ts...>(descs[b.bi]);
+    b.tw[0] = b.tw[1] = b.tw[2] = b.tw[3] = 0u;
+    b.nt = 0;
+    if constexpr (LaneRt<Ts...>::NS != 0) {
+        // the pair's list: its first decodable block's; a block with another list is handed back
+        // (the host orders the lane list by list, in waves of their own)
+        const uint64_t m = lmask(b.ok);
+        if (m != 0ull) {
+            const uint32_t f = (uint32_t)__builtin_ctzll(m);
+            const BlockDesc &d = descs[b.bi];
+            const uint32_t *tp = (const uint32_t *)d.term;
+            const int32_t nt = d.num_terms;
+            b.nt = __builtin_amdgcn_readlane(nt, f);
+            bool same = nt == b.nt;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t w = tp[k];
+                b.tw[k] = __builtin_amdgcn_readlane(w, f);
+                const int32_t nb = min(max(b.nt - 4 * k, 0), 4);  // this dword's bytes inside the list
+                const uint32_t bm = nb >= 4 ? ~0u : ((1u << (8 * nb)) - 1u);
+                same = same && ((w ^ b.tw[k]) & bm) == 0u;
+            }
+            b.ok = b.ok && same;
+        }
+    }
     b.nfr = b.ok ? descs[b.bi].nframes : 0u;
     // the wave runs to its longest block; groups inside every block skip the per-frame end tests
     uint32_t nmax = b.nfr, nmin = b.nfr ? b.nfr : 0xFFFFFFFFu;
@@ -1315,8 +1490,10 @@ __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, 
     const uint32_t sh_ = (uint32_t)d.shift & 31u;
     const int32_t ml = d.mute_limit;
     int32_t *o = out + d.out_off;
-    LChain<Ts...> ch;
-    ch.init(d, 0);
+    constexpr int NS = LaneRt<Ts...>::NS;
+    typename ChainOf<Ts...>::type ch;
+    if constexpr (NS != 0) ch.init(d, lb.tw, lb.nt);
+    else ch.init(d, 0);
     Fixup fx;
     if constexpr (HY) fixup_init(fx, d);
     // the .wvc stream (HY == 2): this wave reads the corrections -- the parser hands over
@@ -1336,7 +1513,12 @@ __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, 
             return;
         }
         rbad |= ch.wbad() ? 4u : 0u;
-        if (g0 + GF < lb.nmin) {
+        if constexpr (NS != 0) {
+            if (g0 + GF < lb.nmin)
+                rgroup_rt<true, MONO, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
+            else
+                rgroup_rt<false, MONO, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
+        } else if (g0 + GF < lb.nmin) {
             rframe<0, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
             rframe<1, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
             rframe<2, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
@@ -1400,6 +1582,49 @@ __device__ __forceinline__ void lane_blocks(const BlockDesc *__restrict__ descs,
         lane_recon<MONO, HY, Ts...>(descs, list, n, blob, out, status, sh, grp, lane);
 }
 
+// run-time term lists (RChain): each pair takes the variant of its first listed block --
+// mono or stereo, up to 5 terms (CODES: the reconstruction computes the word values) or
+// up to 16 -- and the list of its first decodable block (lane_block)
+__device__ __forceinline__ void lane_blocks_rt(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
+                                               uint32_t n, const uint8_t *__restrict__ blob, int32_t *__restrict__ out,
+                                               uint32_t *__restrict__ status, uint32_t *__restrict__ dbg) {
+    __shared__ LShared shp[LPAIRS];
+    __shared__ uint32_t rings[(LPAIRS * RING_BYTES + LDS_AFTER_RINGS) / 4];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint32_t pair = wave >> 1, grp = blockIdx.x * LPAIRS + pair;
+    LShared &sh = shp[pair];
+    if (lane == 0 && (wave & 1u) == 0u) {
+        sh.produced = 0u;
+        sh.consumed = 0u;
+        sh.abort = 0u;
+    }
+    __syncthreads();
+    if (grp * 64u >= n) return;  // (both waves of the pair: uniform)
+    const uint32_t li = grp * 64u + lane;
+    const bool inl = li < n && list[li] != kLaneGap;
+    const uint64_t m = lmask(inl);
+    if (m == 0ull) return;
+    const uint32_t f = (uint32_t)__builtin_ctzll(m);
+    const BlockDesc &d0 = descs[inl ? list[li] : 0u];
+    const uint32_t fl = __builtin_amdgcn_readlane(d0.flags, f);
+    const int32_t nt = __builtin_amdgcn_readlane(d0.num_terms, f);
+    uint8_t *rg = (uint8_t *)rings;
+    const bool parser = (wave & 1u) == 0u;
+#define WV_RT_PAIR(MONO_, NS_)                                                                       \
+    do {                                                                                           \
+        if (parser) lane_parser<MONO_, 0, LANE_RT, NS_>(descs, list, n, blob, sh, rg, pair, grp, lane, dbg); \
+        else lane_recon<MONO_, 0, LANE_RT, NS_>(descs, list, n, blob, out, status, sh, grp, lane);       \
+    } while (0)
+    if (fl & wvf::MONO_DATA) {
+        if (nt <= 5) WV_RT_PAIR(true, 5);
+        else WV_RT_PAIR(true, 16);
+    } else {
+        if (nt <= 5) WV_RT_PAIR(false, 5);
+        else WV_RT_PAIR(false, 16);
+    }
+#undef WV_RT_PAIR
+}
+
 }  // namespace lane
 
 // the term lists with a lane instantiation (decoder order, the reverse of the
@@ -1410,7 +1635,7 @@ __device__ __forceinline__ void lane_blocks(const BlockDesc *__restrict__ descs,
 #define WVG_TS_M5 18, 3, 2, 18, 18
 #define WVG_TS_HIGH16 2, 18, -1, 8, 6, 3, 5, 7, 4, 2, 18, -2, 3, 2, 18, 18
 #define WVG_TS_MONO_HIGH16 1, 17, 2, 18, 8, 6, 3, 5, 7, 4, 2, 18, 3, 2, 18, 18
-enum LaneList { LANE_FAST = 0, LANE_DEFAULT, LANE_M5, LANE_HIGH16, LANE_MONO_HIGH16, LANE_HY_DEFAULT, LANE_HY_WVC };
+enum LaneList { LANE_FAST = 0, LANE_DEFAULT, LANE_M5, LANE_HIGH16, LANE_MONO_HIGH16, LANE_HY_DEFAULT, LANE_HY_WVC, LANE_RT };
 // the lane kernel of one list over n blocks (wv_lane.hip)
 // dbg (nullptr: off): per parser wave 16 words (cycles, groups by path, wait cycles: LCount)
 hipError_t launch_lane(int which, dim3 grid, dim3 block, hipStream_t s, const BlockDesc *descs, const uint32_t *list,

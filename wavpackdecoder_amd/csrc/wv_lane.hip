@@ -25,6 +25,10 @@ __global__ void __launch_bounds__(256) WV_LANE_ATTR wv_pcm_lane(const BlockDesc 
     lane::lane_blocks<MONO, HY, Ts...>(descs, list, n, blob, out, status, dbg);
 }
 
+// (wv_lane_rt.hip)
+hipError_t launch_lane_rt(dim3 grid, dim3 block, hipStream_t s, const BlockDesc *descs, const uint32_t *list, uint32_t n,
+                          const uint8_t *blob, int32_t *out, uint32_t *status, uint32_t *dbg);
+
 hipError_t launch_lane(int which, dim3 gl, dim3 bl, hipStream_t s, const BlockDesc *descs, const uint32_t *list,
                        uint32_t n, const uint8_t *blob, int32_t *out, uint32_t *status, uint32_t *dbg) {
     switch (which) {
@@ -36,6 +40,7 @@ hipError_t launch_lane(int which, dim3 gl, dim3 bl, hipStream_t s, const BlockDe
     case LANE_MONO_HIGH16: hipLaunchKernelGGL((wv_pcm_lane<true, 0, WVG_TS_MONO_HIGH16>), gl, bl, 0, s, descs, list, n, blob, out, status, dbg); break;
     case LANE_HY_DEFAULT: hipLaunchKernelGGL((wv_pcm_lane<false, 1, WVG_TS_DEFAULT>), gl, bl, 0, s, descs, list, n, blob, out, status, dbg); break;
     case LANE_HY_WVC: hipLaunchKernelGGL((wv_pcm_lane<false, 2, WVG_TS_DEFAULT>), gl, bl, 0, s, descs, list, n, blob, out, status, dbg); break;
+    case LANE_RT: return launch_lane_rt(gl, bl, s, descs, list, n, blob, out, status, dbg);
 #endif
     default: return hipErrorInvalidValue;
     }

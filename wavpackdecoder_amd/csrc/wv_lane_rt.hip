@@ -1,0 +1,25 @@
+// wv_lane_rt.hip -- the lane-per-block PCM kernel for term lists read at run time
+// (wv_lane.h: RChain, lane_blocks_rt): lossless blocks, mono or stereo, any list of up
+// to 16 terms of -3..-1, 1..8, 17, 18 (UnpackUtils.cs:156-187) -- the lists without a
+// compile-time instantiation (wv_lane.hip).  Its own translation unit: it builds in
+// parallel with the others.
+#include <hip/hip_runtime.h>
+
+#include "wv_lane.h"
+
+namespace wvg {
+
+__global__ void __launch_bounds__(256) wv_pcm_lane_rt(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
+                                                      uint32_t n, const uint8_t *__restrict__ blob,
+                                                      int32_t *__restrict__ out, uint32_t *__restrict__ status,
+                                                      uint32_t *__restrict__ dbg) {
+    lane::lane_blocks_rt(descs, list, n, blob, out, status, dbg);
+}
+
+hipError_t launch_lane_rt(dim3 gl, dim3 bl, hipStream_t s, const BlockDesc *descs, const uint32_t *list, uint32_t n,
+                          const uint8_t *blob, int32_t *out, uint32_t *status, uint32_t *dbg) {
+    hipLaunchKernelGGL(wv_pcm_lane_rt, gl, bl, 0, s, descs, list, n, blob, out, status, dbg);
+    return hipGetLastError();
+}
+
+}  // namespace wvg
