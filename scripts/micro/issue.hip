@@ -64,6 +64,17 @@ BENCH(k_dswrite64, "v_mov_b32 v20, 0\n v_mov_b32 v22, 0\n v_mov_b32 v23, 0\n", "
 BENCH(k_pk_add_f32, "v_mov_b32 v20, 0\n v_mov_b32 v21, 0\n v_mov_b32 v22, 0\n v_mov_b32 v23, 0\n",
       "v_pk_add_f32 v[20:21], v[20:21], v[22:23]\n")
 
+// the decorr passes' apply_weight: a 64-bit product then the 10-bit shift
+BENCH(k_madi64_dep, "v_mov_b32 v20, 3\n v_mov_b32 v21, 0\n v_mov_b32 v22, 5\n",
+      "v_mad_i64_i32 v[20:21], s[20:21], v20, v22, 0\n")
+BENCH(k_madi64_ind, "v_mov_b32 v20, 3\n v_mov_b32 v21, 0\n v_mov_b32 v22, 5\n",
+      "v_mad_i64_i32 v[24:25], s[20:21], v20, v22, 0\n v_mad_i64_i32 v[26:27], s[22:23], v20, v22, 0\n")
+BENCH(k_aw64_chain, "v_mov_b32 v20, 3\n v_mov_b32 v21, 0\n v_mov_b32 v22, 5\n",
+      "v_mad_i64_i32 v[24:25], s[20:21], v20, v22, 0\n v_alignbit_b32 v20, v25, v24, 10\n")
+BENCH(k_aw24_chain, "v_mov_b32 v20, 3\n v_mov_b32 v21, 0\n v_mov_b32 v22, 5\n s_movk_i32 s24, 0x200\n",
+      "v_ashrrev_i32 v24, 12, v20\n v_and_b32 v25, 0xfff, v20\n v_mul_i32_i24 v24, v22, v24\n v_mad_i32_i24 v25, v22, v25, s24\n v_ashrrev_i32 v25, 10, v25\n v_lshl_add_u32 v20, v24, 2, v25\n")
+BENCH(k_cbranch_taken, "s_cmp_eq_u32 0, 0\n", "s_cbranch_scc1 0\n")
+
 typedef void (*kfn)(long long *);
 int main() {
     long long *d;
@@ -77,7 +88,9 @@ int main() {
         {"v_bitop3 dep", k_bitop3_dep}, {"v_add3 dep", k_add3_dep}, {"v_bfe_u32 dep", k_bfe_dep},
         {"v_ffbl dep", k_ffbl_dep}, {"v_ffbh dep", k_ffbh_dep}, {"v_min_u32 dep", k_min_dep}, {"v_med3 dep", k_med3_dep},
         {"v_mul_u32_u24 dep", k_mul24_dep}, {"v_mad_i32_i24 dep", k_mad24_dep}, {"v_mul_lo_u32 dep", k_mullo_dep},
-        {"v_mul_lo_u32 ind x2", k_mullo_ind}, {"v_cmp->v_cndmask vcc", k_cmp_cnd_vcc},
+        {"v_mul_lo_u32 ind x2", k_mullo_ind}, {"v_mad_i64_i32 dep", k_madi64_dep}, {"v_mad_i64_i32 ind x2", k_madi64_ind},
+        {"aw: mad_i64+alignbit chain", k_aw64_chain}, {"aw: 24-bit split chain (6)", k_aw24_chain},
+        {"s_cbranch taken", k_cbranch_taken}, {"v_cmp->v_cndmask vcc", k_cmp_cnd_vcc},
         {"v_cmp->v_cndmask sgpr", k_cmp_cnd_sgpr}, {"v_cmp->v_addc vcc", k_cmp_addc},
         {"v_cmp->s_and->v_cndmask", k_cmp_sand_cnd}, {"v_sub,v_ashr,v_and", k_ashr_mask},
         {"ds_read dep", k_ds_dep}, {"ds_read + 16 v_add", k_ds_hidden}, {"ds_write_b32", k_dswrite},

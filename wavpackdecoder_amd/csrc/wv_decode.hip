@@ -33,6 +33,8 @@
 // blocks the block frame of the residual whose decode raised the reference's
 // C# exception (with ST_EXCEPTION).
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
+#include <string.h>
 #include <vector>
 
 #include "wv_decode_core.h"
@@ -1312,7 +1314,13 @@ hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, ui
             return hipGetLastError();
         }
         dim3 gl((lane_n + 64 * lane::LPAIRS - 1) / (64 * lane::LPAIRS)), bl(64 * lane::LPAIRS * 2);
-        if (hipError_t e = launch_lane(ts - kLaneBase == 0 ? LANE_HIGH16 : LANE_MONO_HIGH16, gl, bl, s, descs, lane_list, lane_n, blob, out, status, lane_dbg); e != hipSuccess) return e;
+        // the 16-term lists on the run-time list kernel (wv_pcm_lane_rt3): its reconstruction
+        // pipeline of three waves beats the one-wave compile-time chain -- C3 (1,024 blocks, 20
+        // in flight) 32,700 vs 28,900 Mframes/s, 22.1 vs 24.8 ms alone (profiles/r05_lists_rates.jsonl);
+        // WVG_LANE_HIGH16=ct: the compile-time instantiations (A/B)
+        static const bool high_rt = !(getenv("WVG_LANE_HIGH16") && strcmp(getenv("WVG_LANE_HIGH16"), "ct") == 0);
+        const int which = high_rt ? LANE_RT : (ts - kLaneBase == 0 ? LANE_HIGH16 : LANE_MONO_HIGH16);
+        if (hipError_t e = launch_lane(which, gl, bl, s, descs, lane_list, lane_n, blob, out, status, lane_dbg); e != hipSuccess) return e;
         if (lane_mode != 2) {
             if (neg12) hipLaunchKernelGGL((wv_pcm_pipe_redo<true>), g, b, 0, s, descs, list, blob, out, status, aux);
             else hipLaunchKernelGGL((wv_pcm_pipe_redo<false>), g, b, 0, s, descs, list, blob, out, status, aux);

@@ -212,13 +212,26 @@ struct RChain {
     LPass<1> p[NS];
     uint32_t tw[4];  // the terms, four to a dword (wave-uniform)
     int32_t nt;      // (wave-uniform)
-    __device__ __forceinline__ void init(const BlockDesc &d, const uint32_t *ptw, int32_t pnt) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) tw[k] = ptw[k];
-        nt = pnt;
+    // passes [first, first + count) of the list ptw (wave-uniform; count <= NS)
+    __device__ __forceinline__ void init(const BlockDesc &d, const uint32_t *ptw, int32_t first, int32_t count) {
+        // the terms from `first` on: the 16-byte list shifted down by `first` bytes (first <= 8)
+        uint64_t a = (uint64_t)ptw[0] | ((uint64_t)ptw[1] << 32), b = (uint64_t)ptw[2] | ((uint64_t)ptw[3] << 32);
+        const uint32_t sh = 8u * (uint32_t)first;
+        if (sh >= 64u) {
+            a = b >> (sh - 64u);
+            b = 0;
+        } else if (sh) {
+            a = (a >> sh) | (b << (64u - sh));
+            b >>= sh;
+        }
+        tw[0] = (uint32_t)a;
+        tw[1] = (uint32_t)(a >> 32);
+        tw[2] = (uint32_t)b;
+        tw[3] = (uint32_t)(b >> 32);
+        nt = count;
 #pragma unroll
         for (int i = 0; i < NS; i++) {
-            p[i].init(d, i);
+            p[i].init(d, min(first + i, MAXP - 1));
             if (i >= nt) p[i].wA = p[i].wB = p[i].dl = 0;  // (wbad: a slot past the list)
         }
     }
@@ -910,6 +923,10 @@ struct LShared {
     int2 rm[RF * 64];
     uint32_t pflag[64];                    // parser -> recon: the block's parse verdict (bit 31: final)
     uint32_t produced, consumed, abort;    // frames; abort: a wait ran out
+    // (wv_pcm_lane_rt3: reconstruction role h -> h + 1 through ring h, int2 slots in the free
+    // rq region: frames handed on / taken; role h's weight verdicts per lane)
+    uint32_t hop_out[3], hop_in[3];
+    uint32_t rbh[2][64];
 };
 
 // the index of the stream dword merged next (< 128 advances since the group's start)
@@ -1492,7 +1509,7 @@ __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, 
     int32_t *o = out + d.out_off;
     constexpr int NS = LaneRt<Ts...>::NS;
     typename ChainOf<Ts...>::type ch;
-    if constexpr (NS != 0) ch.init(d, lb.tw, lb.nt);
+    if constexpr (NS != 0) ch.init(d, lb.tw, 0, lb.nt);
     else ch.init(d, 0);
     Fixup fx;
     if constexpr (HY) fixup_init(fx, d);
@@ -1545,6 +1562,126 @@ __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, 
         status[lb.bi] = (d.block_samples == 0u) ? ST_CRC_CHECKED | ((int32_t)0xFFFFFFFFu != d.crc ? ST_CRC_ERROR : 0u) : 0u;
 }
 
+// Run-time lists of 6..16 terms (wv_pcm_lane_rt3): NW reconstruction waves per pair in
+// a pipeline -- role r runs its share of the passes and hands each frame on through ring r
+// (int2 slots in the rq region, free without CODES), the last role runs the rest and the
+// frame tails -- so that each holds at most RS passes' registers and shares its SIMD
+// with another chain (lane_blocks_rt3).
+template <int NW>
+struct RSplit {
+    static constexpr int RS = NW == 2 ? 8 : 6;  // passes per role, at most
+    static_assert(NW * RS >= MAXP, "the roles cover every list");
+    // role r's passes [first, first + count) of nt (the last role also runs the tails: one more share)
+    __device__ __forceinline__ static void share(int32_t nt, int role, int32_t &first, int32_t &count) {
+        const int32_t q = min((nt + 1 + NW - 1) / NW, (int32_t)RS);
+        first = min(q * (role - 1), nt);
+        count = role < NW ? min(q, nt - first) : nt - first;
+    }
+};
+template <bool MONO>
+__device__ __forceinline__ void rin2(const int2 *ring2, uint32_t lane, uint32_t g0, int32_t (&L)[GF], int32_t (&R)[GF]) {
+#pragma unroll
+    for (int u = 0; u < GF; u++) {
+        const int2 r = ring2[(((g0 % (uint32_t)RF) + u) << 6) + lane];
+        L[u] = r.x;
+        R[u] = MONO ? 0 : r.y;
+    }
+}
+template <bool MONO, int ROLE, int NW>
+__device__ __forceinline__ void lane_recon_split(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
+                                                 uint32_t n, int32_t *__restrict__ out, uint32_t *__restrict__ status,
+                                                 LShared &sh, uint32_t grp, uint32_t lane) {
+    using namespace wvf;
+    static_assert(ROLE >= 1 && ROLE <= NW && NW <= 3, "roles");
+    const LBlock lb = lane_block<MONO, 0, LANE_RT, 16>(descs, list, n, grp, lane);
+    const BlockDesc &d = descs[lb.bi];
+    const uint32_t nfr = lb.nfr;
+    int32_t first, count;
+    RSplit<NW>::share(lb.nt, ROLE, first, count);
+    RChain<RSplit<NW>::RS> ch;
+    ch.init(d, lb.tw, first, count);
+    int2 *const rings2 = (int2 *)sh.rq;  // ring h (1 .. NW - 1) at rings2 + (h - 1) * RF * 64
+    static_assert(sizeof(LShared::rq) >= 2 * RF * 64 * sizeof(int2), "two hop rings in rq");
+    uint32_t rbad = 0u;
+    int32_t L[GF], R[GF];
+    if constexpr (ROLE < NW) {
+        int2 *const rout2 = rings2 + (ROLE - 1) * RF * 64;
+        uint32_t cpre = 0u;  // the next role's consumed count, read a group ahead
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        for (uint32_t g0 = 0; g0 < lb.nmax; g0 += GF) {
+            if (!lwait(ROLE == 1 ? &sh.produced : &sh.hop_out[ROLE - 1], g0 + GF, &sh.abort)) return;
+            const uint32_t need = g0 + GF > (uint32_t)RF ? g0 + GF - RF : 0u;
+            if (w2::uni(cpre) < need && !lwait(&sh.hop_in[ROLE], need, &sh.abort)) return;
+            rbad |= ch.wbad() ? 4u : 0u;
+            if constexpr (ROLE == 1) {
+                rin<0, MONO, false>(sh, lane, g0, L[0], R[0]);
+                rin<1, MONO, false>(sh, lane, g0, L[1], R[1]);
+                rin<2, MONO, false>(sh, lane, g0, L[2], R[2]);
+                rin<3, MONO, false>(sh, lane, g0, L[3], R[3]);
+                rin<4, MONO, false>(sh, lane, g0, L[4], R[4]);
+                rin<5, MONO, false>(sh, lane, g0, L[5], R[5]);
+                rin<6, MONO, false>(sh, lane, g0, L[6], R[6]);
+                rin<7, MONO, false>(sh, lane, g0, L[7], R[7]);
+            } else {
+                rin2<MONO>(rings2 + (ROLE - 2) * RF * 64, lane, g0, L, R);
+                rbad |= sh.rbh[ROLE - 2][lane];
+            }
+            ch.template group<MONO>(L, R);
+#pragma unroll
+            for (int u = 0; u < GF; u++) rout2[(((g0 % (uint32_t)RF) + u) << 6) + lane] = make_int2(L[u], R[u]);
+            sh.rbh[ROLE - 1][lane] = rbad;
+            // (DS ops of one wave complete in order: the input slots are read, the frames written)
+            w2::lds_publish(ROLE == 1 ? &sh.consumed : &sh.hop_in[ROLE - 1], g0 + GF);
+            w2::lds_publish(&sh.hop_out[ROLE], g0 + GF);
+            cpre = __hip_atomic_load(&sh.hop_in[ROLE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    } else {
+        const bool fst = (d.flags & FALSE_STEREO) != 0;
+        if (lb.inl && !lb.ok) status[lb.bi] = ST_REDO | (1u << 16);
+        const bool joint = (d.flags & JOINT_STEREO) != 0;
+        const uint32_t sh_ = (uint32_t)d.shift & 31u;
+        int32_t *o = out + d.out_off;
+        Fixup fx;
+        const CWin cw = CWin{nullptr, 0ull, 0, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+        uint32_t crc = 0xFFFFFFFFu;
+        int32_t mx = 0, mn = 0;
+        const LEnd le = {status + lb.bi, d.mute_limit, d.nframes == d.block_samples, d.crc, sh.pflag, lane};
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        for (uint32_t g0 = 0; g0 < lb.nmax; g0 += GF) {
+            if (!lwait(&sh.hop_out[NW - 1], g0 + GF, &sh.abort)) {
+                if (lb.ok && nfr > g0) status[lb.bi] = ST_REDO | (128u << 16);
+                return;
+            }
+            rbad |= ch.wbad() ? 4u : 0u;
+            rin2<MONO>(rings2 + (NW - 2) * RF * 64, lane, g0, L, R);
+            const uint32_t rb = rbad | sh.rbh[NW - 2][lane];
+            ch.template group<MONO>(L, R);
+            if (g0 + GF < lb.nmin) {
+                rout<0, true, MONO, 0>(L[0], R[0], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<1, true, MONO, 0>(L[1], R[1], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<2, true, MONO, 0>(L[2], R[2], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<3, true, MONO, 0>(L[3], R[3], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<4, true, MONO, 0>(L[4], R[4], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<5, true, MONO, 0>(L[5], R[5], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<6, true, MONO, 0>(L[6], R[6], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<7, true, MONO, 0>(L[7], R[7], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+            } else {
+                rout<0, false, MONO, 0>(L[0], R[0], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<1, false, MONO, 0>(L[1], R[1], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<2, false, MONO, 0>(L[2], R[2], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<3, false, MONO, 0>(L[3], R[3], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<4, false, MONO, 0>(L[4], R[4], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<5, false, MONO, 0>(L[5], R[5], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<6, false, MONO, 0>(L[6], R[6], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<7, false, MONO, 0>(L[7], R[7], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+            }
+            w2::lds_publish(&sh.hop_in[NW - 1], g0 + GF);
+        }
+        if (lb.ok && nfr == 0u)
+            status[lb.bi] = (d.block_samples == 0u) ? ST_CRC_CHECKED | ((int32_t)0xFFFFFFFFu != d.crc ? ST_CRC_ERROR : 0u) : 0u;
+    }
+}
+
 // LPAIRS (parser, recon) wave pairs per workgroup, each pair 64 blocks: the 4 waves
 // of a workgroup take the 4 SIMDs of one CU.  Its LDS (2 x ~50 KiB: the 32-unit
 // payload rings) is more than half a CU's 160 KiB, so no second workgroup -- of
@@ -1582,9 +1719,12 @@ __device__ __forceinline__ void lane_blocks(const BlockDesc *__restrict__ descs,
         lane_recon<MONO, HY, Ts...>(descs, list, n, blob, out, status, sh, grp, lane);
 }
 
+#ifndef WV_RT_SPLIT16  // (0: A/B builds with every run-time list on the two-wave layout)
+#define WV_RT_SPLIT16 1
+#endif
 // run-time term lists (RChain): each pair takes the variant of its first listed block --
-// mono or stereo, up to 5 terms (CODES: the reconstruction computes the word values) or
-// up to 16 -- and the list of its first decodable block (lane_block)
+// mono or stereo, up to 5 terms (CODES: the reconstruction computes the word values; longer
+// lists: lane_blocks_rt3) -- and the list of its first decodable block (lane_block)
 __device__ __forceinline__ void lane_blocks_rt(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
                                                uint32_t n, const uint8_t *__restrict__ blob, int32_t *__restrict__ out,
                                                uint32_t *__restrict__ status, uint32_t *__restrict__ dbg) {
@@ -1615,6 +1755,11 @@ __device__ __forceinline__ void lane_blocks_rt(const BlockDesc *__restrict__ des
         if (parser) lane_parser<MONO_, 0, LANE_RT, NS_>(descs, list, n, blob, sh, rg, pair, grp, lane, dbg); \
         else lane_recon<MONO_, 0, LANE_RT, NS_>(descs, list, n, blob, out, status, sh, grp, lane);       \
     } while (0)
+#if WV_RT_SPLIT16  // lists of 6..16 terms: wv_pcm_lane_rt3
+    if (nt > 5) return;
+    if (fl & wvf::MONO_DATA) WV_RT_PAIR(true, 5);
+    else WV_RT_PAIR(false, 5);
+#else  // (A/B builds: every run-time list on one reconstruction wave)
     if (fl & wvf::MONO_DATA) {
         if (nt <= 5) WV_RT_PAIR(true, 5);
         else WV_RT_PAIR(true, 16);
@@ -1622,7 +1767,66 @@ __device__ __forceinline__ void lane_blocks_rt(const BlockDesc *__restrict__ des
         if (nt <= 5) WV_RT_PAIR(false, 5);
         else WV_RT_PAIR(false, 16);
     }
+#endif
 #undef WV_RT_PAIR
+}
+
+
+// wv_pcm_lane_rt3: the pairs of run-time lists of 6..16 terms (lane_blocks_rt takes the
+// others), 1 + RT3_NW waves each -- the parser and RT3_NW reconstruction waves
+// (lane_recon_split).  A workgroup's wave w runs on SIMD w % 4; the roles are placed so
+// that no SIMD holds two parsers and the reconstruction load spreads: with three
+// reconstruction waves, SIMD 0 holds both pairs' first, SIMD 1 both seconds, SIMDs 2 / 3
+// a parser each with its pair's last (the lightest: it ends with the tails); with two,
+// SIMDs 0 / 1 one pair's two each and SIMDs 2 / 3 the parsers.
+#ifndef RT3_NW
+#define RT3_NW 3
+#endif
+constexpr int RT3_THREADS = 64 * (1 + RT3_NW) * LPAIRS;
+__device__ __forceinline__ void lane_blocks_rt3(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
+                                                uint32_t n, const uint8_t *__restrict__ blob, int32_t *__restrict__ out,
+                                                uint32_t *__restrict__ status, uint32_t *__restrict__ dbg) {
+    static_assert(LPAIRS == 2, "wave roles");
+    __shared__ LShared shp[LPAIRS];
+    __shared__ uint32_t rings[(LPAIRS * RING_BYTES + LDS_AFTER_RINGS) / 4];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    // (pair, role) of wave w: role 0 the parser, 1..RT3_NW the reconstruction pipeline
+#if RT3_NW == 3
+    constexpr uint8_t kPair[8] = {0, 0, 0, 1, 1, 1, 0, 1}, kRole[8] = {1, 2, 0, 0, 1, 2, 3, 3};
+#else
+    constexpr uint8_t kPair[6] = {0, 1, 0, 1, 0, 1}, kRole[6] = {1, 1, 0, 0, 2, 2};
+#endif
+    const uint32_t role = kRole[wave], pair = kPair[wave], grp = blockIdx.x * LPAIRS + pair;
+    LShared &sh = shp[pair];
+    if (lane == 0 && role == 0u) {
+        sh.produced = 0u;
+        sh.consumed = 0u;
+        sh.abort = 0u;
+#pragma unroll
+        for (int h = 0; h < 3; h++) sh.hop_out[h] = sh.hop_in[h] = 0u;
+    }
+    __syncthreads();
+    if (grp * 64u >= n) return;
+    const uint32_t li = grp * 64u + lane;
+    const bool inl = li < n && list[li] != kLaneGap;
+    const uint64_t m = lmask(inl);
+    if (m == 0ull) return;
+    const uint32_t f = (uint32_t)__builtin_ctzll(m);
+    const BlockDesc &d0 = descs[inl ? list[li] : 0u];
+    const uint32_t fl = __builtin_amdgcn_readlane(d0.flags, f);
+    const int32_t nt = __builtin_amdgcn_readlane(d0.num_terms, f);
+    if (nt <= 5) return;  // (lane_blocks_rt's pair)
+    uint8_t *rg = (uint8_t *)rings;
+#define WV_RT3_ROLES(MONO_)                                                                          \
+    do {                                                                                           \
+        if (role == 0u) lane_parser<MONO_, 0, LANE_RT, 16>(descs, list, n, blob, sh, rg, pair, grp, lane, dbg); \
+        else if (role == 1u) lane_recon_split<MONO_, 1, RT3_NW>(descs, list, n, out, status, sh, grp, lane);  \
+        else if (role == 2u) lane_recon_split<MONO_, 2, RT3_NW>(descs, list, n, out, status, sh, grp, lane);  \
+        else if constexpr (RT3_NW == 3) lane_recon_split<MONO_, 3, 3>(descs, list, n, out, status, sh, grp, lane); \
+    } while (0)
+    if (fl & wvf::MONO_DATA) WV_RT3_ROLES(true);
+    else WV_RT3_ROLES(false);
+#undef WV_RT3_ROLES
 }
 
 }  // namespace lane
