@@ -364,7 +364,9 @@ def run_rank(args) -> None:
     multi = len(slices) > 1
 
     L = _lib.lib()
-    api._ctx = L.wvg_open(local)
+    # (WVG_BENCH_SAME_DEVICE=1: every rank on device 0 -- the multi-rank path rehearsed on a
+    # one-GPU box, tests/test_gpu_ranks.py; the driver's N-GPU runs leave it unset)
+    api._ctx = L.wvg_open(0 if os.environ.get("WVG_BENCH_SAME_DEVICE") == "1" else local)
     if not api._ctx:
         raise SystemExit("no GPU")
 

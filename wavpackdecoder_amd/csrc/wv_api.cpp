@@ -963,12 +963,12 @@ static void build_lane_orders(wvg_batch *b) {
         while (v.size() & 63u) v.push_back(kLaneGap);
     };
     // The run-time list kernel's groups (lane_rt_group) are ordered by list first --
-    // mono / stereo, length, terms -- each list in waves of its own: a wave decodes the
-    // list of its first block and hands back any other.
+    // mono / stereo, lossless / hybrid, length, terms -- each list in waves of its own: a
+    // wave decodes the list (and kind) of its first block and hands back any other.
     auto lkey = [&](uint32_t k) {
         const BlockDesc &d = b->fo.descs[k];
         std::array<int8_t, MAXP + 2> key{};
-        key[0] = (d.flags & wvf::MONO_DATA) ? 1 : 0;
+        key[0] = (int8_t)(((d.flags & wvf::MONO_DATA) ? 1 : 0) | ((d.flags & wvf::HYBRID_FLAG) ? 2 : 0));
         key[1] = (int8_t)d.num_terms;
         for (int i = 0; i < d.num_terms && i < MAXP; i++) key[2 + i] = d.term[i];
         return key;

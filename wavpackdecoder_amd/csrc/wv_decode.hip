@@ -1254,7 +1254,9 @@ static const bool kLaneSetNeg12[kNumLaneSets] = {true, false};
 // which two-wave kernel decodes this block (-1: the generic wave kernel, for
 // int32 + wvx, .wvc, exact-float and chained blocks).  prefer_pipe 2: every list goes to the pipelined kernel
 // (A/B tests)
-bool lane_rt_group(int ts) { return ts == kPipe || ts == kPipe + 1; }
+// the launch groups whose lane kernel reads the list at run time (wv_pcm_lane_rt / _rt3): the
+// pipelined kernel's lists and the 16-term lists (the host orders their lane lists by list)
+bool lane_rt_group(int ts) { return ts == kPipe || ts == kPipe + 1 || (ts >= kLaneBase && ts < kLaneBase + kNumLaneSets); }
 
 int term_set_of(const BlockDesc &d, int prefer_pipe) {
     using namespace wvf;
@@ -1285,8 +1287,13 @@ int term_set_of(const BlockDesc &d, int prefer_pipe) {
             if (mono && t < 0) ok = false;
         }
         if (ok) {
-            const uint32_t hy = d.flags & (HYBRID_FLAG | HYBRID_BITRATE | HYBRID_BALANCE | INT32_DATA);
-            if (s == 1 && !mono && hy == (HYBRID_FLAG | HYBRID_BITRATE)) return kHyDefault;
+            if (d.flags & HYBRID_FLAG) {
+                // hybrid: stereo default-list blocks with HYBRID_BITRATE on their own lane kernel
+                // (kHyDefault), every other one with the run-time list lanes (or the pipelined kernel)
+                const uint32_t hy = d.flags & (HYBRID_FLAG | HYBRID_BITRATE | INT32_DATA);
+                if (s == 1 && !mono && hy == (HYBRID_FLAG | HYBRID_BITRATE)) return kHyDefault;
+                return pipe;
+            }
             return s;
         }
     }

@@ -377,6 +377,7 @@ struct LState {
     int32_t slack;   // least window bits left after a word (< 0: a word past the window)
     uint32_t bad;
     uint32_t bad0;   // (diagnostics) the reasons of the first group that set any: status bits 24-31
+    uint32_t bal;    // hybrid stereo with HYBRID_BALANCE: ~0 (lhy_errlim), else 0
     // hybrid words (HYBRID_FLAG | HYBRID_BITRATE): slow_level, bitrate_acc/delta, error limit per channel
     int32_t slow[2];
     int64_t acc[2], dlt[2];
@@ -468,24 +469,43 @@ constexpr uint32_t TAB_EXP2 = LPAIRS * RING_BYTES, TAB_LOG2 = TAB_EXP2 + 256u;
 // (4 slots of 64 lanes: every lane's put_unit_at stays branch-free)
 constexpr uint32_t RING_DUMMY = TAB_LOG2 + 256u, LDS_AFTER_RINGS = 512u + 1024u;
 // exp2s(L) for L > 0 (WordsUtils.cs:633-646): value (9 bits) scaled by 2^(e - 9) as
-// one shift pair, exact for e <= 22 (else the lane hands its block back); 0 for L <= 0
+// one shift pair, exact for e <= 22 (else the lane hands its block back); 0 for L <= 0.
+// L = slow_log - bitrate + 0x100: unsigned, [0x1700, 2^31 + 0x100) holds every e > 22 and
+// the sums whose + 0x100 wrapped past INT_MAX (the reference's exp2s of a negative):
+// one compare hands both back
 __device__ __forceinline__ int32_t lexp2s_pos(int32_t L, const uint8_t *ring, uint32_t &bad) {
     const uint32_t e = (uint32_t)L >> 8;
     const uint32_t v = (uint32_t)ring[TAB_EXP2 + ((uint32_t)L & 0xFFu)] | 0x100u;
-    bad |= (L > 0 && e > 22u) ? 2u : 0u;
+    bad |= ((uint32_t)L - 0x1700u < 0x80000100u - 0x1700u) ? 2u : 0u;
     return L > 0 ? (int32_t)((v << (e & 31u)) >> 9) : 0;
 }
-// update_error_limit (WordsUtils.cs:195-261; stereo, HYBRID_BITRATE, no HYBRID_BALANCE):
-// before the first word of a frame, in lanes where that word is not a zero-run zero
+// update_error_limit (WordsUtils.cs:195-261; HYBRID_BITRATE): before the first word of a
+// frame, in lanes where that word is not a zero-run zero.  Stereo with HYBRID_BALANCE
+// (:222-241) moves bitrate between the channels by their slow levels (a wave-uniform branch:
+// some lane balances); mono and false stereo (:199-209) use channel 0 alone -- the lane
+// computes channel 1 too, unused (its descriptor values are zero)
 __device__ __forceinline__ void lhy_errlim(LState &s, const uint8_t *ring, bool apply) {
     using namespace wvf;
+    int64_t acc[2];
+    int32_t br[2], sl[2];
 #pragma unroll
     for (int c = 0; c < 2; c++) {
-        const int64_t acc = s.acc[c] + s.dlt[c];
-        const int32_t br = (int32_t)(acc >> 16);
-        const int32_t sl = add32(s.slow[c], SLO) >> SLS;
-        const int32_t el = lexp2s_pos(add32(sub32(sl, br), 0x100), ring, s.bad);
-        s.acc[c] = apply ? acc : s.acc[c];
+        acc[c] = s.acc[c] + s.dlt[c];
+        br[c] = (int32_t)(acc[c] >> 16);
+        sl[c] = add32(s.slow[c], SLO) >> SLS;
+    }
+    if (lmask(s.bal != 0u) != 0ull) {
+        const int32_t bl = add32(add32(sub32(sl[1], sl[0]), br[1]), 1) >> 1;
+        const bool up = bl > br[0], dn = sub32(0, bl) > br[0];
+        const int32_t n1 = up ? mul32(br[0], 2) : (dn ? 0 : add32(br[0], bl));
+        const int32_t n0 = up ? 0 : (dn ? mul32(br[0], 2) : sub32(br[0], bl));
+        br[1] = s.bal ? n1 : br[1];
+        br[0] = s.bal ? n0 : br[0];
+    }
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+        const int32_t el = lexp2s_pos(add32(sub32(sl[c], br[c]), 0x100), ring, s.bad);
+        s.acc[c] = apply ? acc[c] : s.acc[c];
         s.el[c] = apply ? el : s.el[c];
     }
 }
@@ -1214,7 +1234,7 @@ __device__ __forceinline__ void rframe(LChain<Ts...> &ch, const LShared &shr, ui
     rout<U, FULL, MONO, HY>(L, R, g0, nfr, joint, mx, mn, crc, sh, o, rbad, e, fst, fx, cw);
 }
 // a group of a run-time list (RChain): the frames' values, the passes pass-major, the frames' tails
-template <bool FULL, bool MONO, bool CODES, int NS>
+template <bool FULL, bool MONO, bool CODES, int NS, int HY = 0>
 __device__ __forceinline__ void rgroup_rt(RChain<NS> &ch, const LShared &shr, uint32_t lane, uint32_t g0, uint32_t nfr,
                                           bool joint, int32_t &mx, int32_t &mn, uint32_t &crc, uint32_t sh, int32_t *o,
                                           uint32_t rbad, const LEnd &e, bool fst, const Fixup &fx, const CWin &cw) {
@@ -1228,14 +1248,14 @@ __device__ __forceinline__ void rgroup_rt(RChain<NS> &ch, const LShared &shr, ui
     rin<6, MONO, CODES>(shr, lane, g0, L[6], R[6]);
     rin<7, MONO, CODES>(shr, lane, g0, L[7], R[7]);
     ch.template group<MONO>(L, R);
-    rout<0, FULL, MONO, 0>(L[0], R[0], g0, nfr, joint, mx, mn, crc, sh, o, rbad, e, fst, fx, cw);
-    rout<1, FULL, MONO, 0>(L[1], R[1], g0, nfr, joint, mx, mn, crc, sh, o, rbad, e, fst, fx, cw);
-    rout<2, FULL, MONO, 0>(L[2], R[2], g0, nfr, joint, mx, mn, crc, sh, o, rbad, e, fst, fx, cw);
-    rout<3, FULL, MONO, 0>(L[3], R[3], g0, nfr, joint, mx, mn, crc, sh, o, rbad, e, fst, fx, cw);
-    rout<4, FULL, MONO, 0>(L[4], R[4], g0, nfr, joint, mx, mn, crc, sh, o, rbad, e, fst, fx, cw);
-    rout<5, FULL, MONO, 0>(L[5], R[5], g0, nfr, joint, mx, mn, crc, sh, o, rbad, e, fst, fx, cw);
-    rout<6, FULL, MONO, 0>(L[6], R[6], g0, nfr, joint, mx, mn, crc, sh, o, rbad, e, fst, fx, cw);
-    rout<7, FULL, MONO, 0>(L[7], R[7], g0, nfr, joint, mx, mn, crc, sh, o, rbad, e, fst, fx, cw);
+    rout<0, FULL, MONO, HY>(L[0], R[0], g0, nfr, joint, mx, mn, crc, sh, o, rbad, e, fst, fx, cw);
+    rout<1, FULL, MONO, HY>(L[1], R[1], g0, nfr, joint, mx, mn, crc, sh, o, rbad, e, fst, fx, cw);
+    rout<2, FULL, MONO, HY>(L[2], R[2], g0, nfr, joint, mx, mn, crc, sh, o, rbad, e, fst, fx, cw);
+    rout<3, FULL, MONO, HY>(L[3], R[3], g0, nfr, joint, mx, mn, crc, sh, o, rbad, e, fst, fx, cw);
+    rout<4, FULL, MONO, HY>(L[4], R[4], g0, nfr, joint, mx, mn, crc, sh, o, rbad, e, fst, fx, cw);
+    rout<5, FULL, MONO, HY>(L[5], R[5], g0, nfr, joint, mx, mn, crc, sh, o, rbad, e, fst, fx, cw);
+    rout<6, FULL, MONO, HY>(L[6], R[6], g0, nfr, joint, mx, mn, crc, sh, o, rbad, e, fst, fx, cw);
+    rout<7, FULL, MONO, HY>(L[7], R[7], g0, nfr, joint, mx, mn, crc, sh, o, rbad, e, fst, fx, cw);
 }
 
 // CODES: the parser hands the reconstruction wave each word's (x, low, mc) and the
@@ -1251,10 +1271,9 @@ template <bool MONO, int HY, int... Ts>
 __device__ __forceinline__ bool lane_ok(const BlockDesc &d) {
     using namespace wvf;
     if (d.kind != KIND_PCM) return false;
-    if constexpr (HY) {  // hybrid with HYBRID_BITRATE, no HYBRID_BALANCE; integer or float (float_values)
-        static_assert(!MONO, "hybrid lanes: stereo");
-        if ((d.flags & (HYBRID_FLAG | HYBRID_BITRATE | HYBRID_BALANCE | INT32_DATA)) != (HYBRID_FLAG | HYBRID_BITRATE))
-            return false;
+    if constexpr (HY) {  // hybrid with HYBRID_BITRATE (HYBRID_BALANCE too); integer or float (float_values)
+        static_assert(!MONO || HY == 1, "hybrid .wvc lanes: stereo");
+        if ((d.flags & (HYBRID_FLAG | HYBRID_BITRATE | INT32_DATA)) != (HYBRID_FLAG | HYBRID_BITRATE)) return false;
     } else if (d.flags & (HYBRID_FLAG | FLOAT_DATA | INT32_DATA)) {
         return false;
     }
@@ -1262,7 +1281,7 @@ __device__ __forceinline__ bool lane_ok(const BlockDesc &d) {
     if ((d.wvc_len != 0) != (HY == 2)) return false;  // HY 2: hybrid blocks with their .wvc stream
     if (d.inherit || d.chain_len >= 2 || d.wvx_state || d.xfloat || d.pre_end || d.fstatus) return false;
     if constexpr (LaneRt<Ts...>::NS != 0) {  // a run-time list: its length and terms (lane_block: the pair's list)
-        static_assert(!HY, "run-time lists: lossless");
+        static_assert(HY <= 1, "run-time lists: lossless or hybrid without .wvc");
         if (d.num_terms < 0 || d.num_terms > LaneRt<Ts...>::NS) return false;
         for (int i = 0; i < d.num_terms; i++) {
             const int t = d.term[i];
@@ -1396,6 +1415,7 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
     s.slack = 0;
     s.bad = 0u;
     s.bad0 = 0u;
+    s.bal = (HY && !MONO && (d.flags & HYBRID_BALANCE)) ? ~0u : 0u;
 #pragma unroll
     for (int c = 0; c < 2; c++) {
 #pragma unroll
@@ -1532,9 +1552,9 @@ __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, 
         rbad |= ch.wbad() ? 4u : 0u;
         if constexpr (NS != 0) {
             if (g0 + GF < lb.nmin)
-                rgroup_rt<true, MONO, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
+                rgroup_rt<true, MONO, CODES, NS, HY>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
             else
-                rgroup_rt<false, MONO, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
+                rgroup_rt<false, MONO, CODES, NS, HY>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
         } else if (g0 + GF < lb.nmin) {
             rframe<0, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
             rframe<1, true, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
@@ -1587,13 +1607,13 @@ __device__ __forceinline__ void rin2(const int2 *ring2, uint32_t lane, uint32_t 
         R[u] = MONO ? 0 : r.y;
     }
 }
-template <bool MONO, int ROLE, int NW>
+template <bool MONO, int ROLE, int NW, int HY>
 __device__ __forceinline__ void lane_recon_split(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
                                                  uint32_t n, int32_t *__restrict__ out, uint32_t *__restrict__ status,
                                                  LShared &sh, uint32_t grp, uint32_t lane) {
     using namespace wvf;
     static_assert(ROLE >= 1 && ROLE <= NW && NW <= 3, "roles");
-    const LBlock lb = lane_block<MONO, 0, LANE_RT, 16>(descs, list, n, grp, lane);
+    const LBlock lb = lane_block<MONO, HY, LANE_RT, 16>(descs, list, n, grp, lane);
     const BlockDesc &d = descs[lb.bi];
     const uint32_t nfr = lb.nfr;
     int32_t first, count;
@@ -1642,6 +1662,7 @@ __device__ __forceinline__ void lane_recon_split(const BlockDesc *__restrict__ d
         const uint32_t sh_ = (uint32_t)d.shift & 31u;
         int32_t *o = out + d.out_off;
         Fixup fx;
+        if constexpr (HY) fixup_init(fx, d);
         const CWin cw = CWin{nullptr, 0ull, 0, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
         uint32_t crc = 0xFFFFFFFFu;
         int32_t mx = 0, mn = 0;
@@ -1657,23 +1678,23 @@ __device__ __forceinline__ void lane_recon_split(const BlockDesc *__restrict__ d
             const uint32_t rb = rbad | sh.rbh[NW - 2][lane];
             ch.template group<MONO>(L, R);
             if (g0 + GF < lb.nmin) {
-                rout<0, true, MONO, 0>(L[0], R[0], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
-                rout<1, true, MONO, 0>(L[1], R[1], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
-                rout<2, true, MONO, 0>(L[2], R[2], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
-                rout<3, true, MONO, 0>(L[3], R[3], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
-                rout<4, true, MONO, 0>(L[4], R[4], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
-                rout<5, true, MONO, 0>(L[5], R[5], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
-                rout<6, true, MONO, 0>(L[6], R[6], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
-                rout<7, true, MONO, 0>(L[7], R[7], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<0, true, MONO, HY>(L[0], R[0], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<1, true, MONO, HY>(L[1], R[1], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<2, true, MONO, HY>(L[2], R[2], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<3, true, MONO, HY>(L[3], R[3], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<4, true, MONO, HY>(L[4], R[4], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<5, true, MONO, HY>(L[5], R[5], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<6, true, MONO, HY>(L[6], R[6], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<7, true, MONO, HY>(L[7], R[7], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
             } else {
-                rout<0, false, MONO, 0>(L[0], R[0], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
-                rout<1, false, MONO, 0>(L[1], R[1], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
-                rout<2, false, MONO, 0>(L[2], R[2], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
-                rout<3, false, MONO, 0>(L[3], R[3], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
-                rout<4, false, MONO, 0>(L[4], R[4], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
-                rout<5, false, MONO, 0>(L[5], R[5], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
-                rout<6, false, MONO, 0>(L[6], R[6], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
-                rout<7, false, MONO, 0>(L[7], R[7], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<0, false, MONO, HY>(L[0], R[0], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<1, false, MONO, HY>(L[1], R[1], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<2, false, MONO, HY>(L[2], R[2], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<3, false, MONO, HY>(L[3], R[3], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<4, false, MONO, HY>(L[4], R[4], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<5, false, MONO, HY>(L[5], R[5], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<6, false, MONO, HY>(L[6], R[6], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
+                rout<7, false, MONO, HY>(L[7], R[7], g0, nfr, joint, mx, mn, crc, sh_, o, rb, le, fst, fx, cw);
             }
             w2::lds_publish(&sh.hop_in[NW - 1], g0 + GF);
         }
@@ -1738,6 +1759,13 @@ __device__ __forceinline__ void lane_blocks_rt(const BlockDesc *__restrict__ des
         sh.consumed = 0u;
         sh.abort = 0u;
     }
+    {   // the exp2 / log2 tables of the hybrid words (a pair of hybrid blocks may come)
+        if (threadIdx.x < 128u) {
+            const uint32_t i = threadIdx.x & 63u;
+            const auto *tab = (const __attribute__((address_space(4))) uint32_t *)(threadIdx.x < 64u ? c_exp2_table : c_log2_table);
+            rings[(threadIdx.x < 64u ? TAB_EXP2 : TAB_LOG2) / 4u + i] = tab[i];
+        }
+    }
     __syncthreads();
     if (grp * 64u >= n) return;  // (both waves of the pair: uniform)
     const uint32_t li = grp * 64u + lane;
@@ -1750,22 +1778,28 @@ __device__ __forceinline__ void lane_blocks_rt(const BlockDesc *__restrict__ des
     const int32_t nt = __builtin_amdgcn_readlane(d0.num_terms, f);
     uint8_t *rg = (uint8_t *)rings;
     const bool parser = (wave & 1u) == 0u;
-#define WV_RT_PAIR(MONO_, NS_)                                                                       \
+#define WV_RT_PAIR(MONO_, NS_, HY_)                                                                  \
     do {                                                                                           \
-        if (parser) lane_parser<MONO_, 0, LANE_RT, NS_>(descs, list, n, blob, sh, rg, pair, grp, lane, dbg); \
-        else lane_recon<MONO_, 0, LANE_RT, NS_>(descs, list, n, blob, out, status, sh, grp, lane);       \
+        if (parser) lane_parser<MONO_, HY_, LANE_RT, NS_>(descs, list, n, blob, sh, rg, pair, grp, lane, dbg); \
+        else lane_recon<MONO_, HY_, LANE_RT, NS_>(descs, list, n, blob, out, status, sh, grp, lane);       \
     } while (0)
 #if WV_RT_SPLIT16  // lists of 6..16 terms: wv_pcm_lane_rt3
     if (nt > 5) return;
-    if (fl & wvf::MONO_DATA) WV_RT_PAIR(true, 5);
-    else WV_RT_PAIR(false, 5);
+    if (fl & wvf::HYBRID_FLAG) {  // (hybrid lanes: HYBRID_BITRATE, lane_ok)
+        if (fl & wvf::MONO_DATA) WV_RT_PAIR(true, 5, 1);
+        else WV_RT_PAIR(false, 5, 1);
+    } else if (fl & wvf::MONO_DATA) {
+        WV_RT_PAIR(true, 5, 0);
+    } else {
+        WV_RT_PAIR(false, 5, 0);
+    }
 #else  // (A/B builds: every run-time list on one reconstruction wave)
     if (fl & wvf::MONO_DATA) {
-        if (nt <= 5) WV_RT_PAIR(true, 5);
-        else WV_RT_PAIR(true, 16);
+        if (nt <= 5) WV_RT_PAIR(true, 5, 0);
+        else WV_RT_PAIR(true, 16, 0);
     } else {
-        if (nt <= 5) WV_RT_PAIR(false, 5);
-        else WV_RT_PAIR(false, 16);
+        if (nt <= 5) WV_RT_PAIR(false, 5, 0);
+        else WV_RT_PAIR(false, 16, 0);
     }
 #endif
 #undef WV_RT_PAIR
@@ -1805,8 +1839,15 @@ __device__ __forceinline__ void lane_blocks_rt3(const BlockDesc *__restrict__ de
 #pragma unroll
         for (int h = 0; h < 3; h++) sh.hop_out[h] = sh.hop_in[h] = 0u;
     }
+    {   // the exp2 / log2 tables of the hybrid words (a pair of hybrid blocks may come)
+        if (threadIdx.x < 128u) {
+            const uint32_t i = threadIdx.x & 63u;
+            const auto *tab = (const __attribute__((address_space(4))) uint32_t *)(threadIdx.x < 64u ? c_exp2_table : c_log2_table);
+            rings[(threadIdx.x < 64u ? TAB_EXP2 : TAB_LOG2) / 4u + i] = tab[i];
+        }
+    }
     __syncthreads();
-    if (grp * 64u >= n) return;
+    if (grp * 64u >= n) return;  // (both waves of the pair: uniform)
     const uint32_t li = grp * 64u + lane;
     const bool inl = li < n && list[li] != kLaneGap;
     const uint64_t m = lmask(inl);
@@ -1817,15 +1858,21 @@ __device__ __forceinline__ void lane_blocks_rt3(const BlockDesc *__restrict__ de
     const int32_t nt = __builtin_amdgcn_readlane(d0.num_terms, f);
     if (nt <= 5) return;  // (lane_blocks_rt's pair)
     uint8_t *rg = (uint8_t *)rings;
-#define WV_RT3_ROLES(MONO_)                                                                          \
+#define WV_RT3_ROLES(MONO_, HY_)                                                                     \
     do {                                                                                           \
-        if (role == 0u) lane_parser<MONO_, 0, LANE_RT, 16>(descs, list, n, blob, sh, rg, pair, grp, lane, dbg); \
-        else if (role == 1u) lane_recon_split<MONO_, 1, RT3_NW>(descs, list, n, out, status, sh, grp, lane);  \
-        else if (role == 2u) lane_recon_split<MONO_, 2, RT3_NW>(descs, list, n, out, status, sh, grp, lane);  \
-        else if constexpr (RT3_NW == 3) lane_recon_split<MONO_, 3, 3>(descs, list, n, out, status, sh, grp, lane); \
+        if (role == 0u) lane_parser<MONO_, HY_, LANE_RT, 16>(descs, list, n, blob, sh, rg, pair, grp, lane, dbg); \
+        else if (role == 1u) lane_recon_split<MONO_, 1, RT3_NW, HY_>(descs, list, n, out, status, sh, grp, lane);  \
+        else if (role == 2u) lane_recon_split<MONO_, 2, RT3_NW, HY_>(descs, list, n, out, status, sh, grp, lane);  \
+        else if constexpr (RT3_NW == 3) lane_recon_split<MONO_, 3, 3, HY_>(descs, list, n, out, status, sh, grp, lane); \
     } while (0)
-    if (fl & wvf::MONO_DATA) WV_RT3_ROLES(true);
-    else WV_RT3_ROLES(false);
+    if (fl & wvf::HYBRID_FLAG) {
+        if (fl & wvf::MONO_DATA) WV_RT3_ROLES(true, 1);
+        else WV_RT3_ROLES(false, 1);
+    } else if (fl & wvf::MONO_DATA) {
+        WV_RT3_ROLES(true, 0);
+    } else {
+        WV_RT3_ROLES(false, 0);
+    }
 #undef WV_RT3_ROLES
 }
 
