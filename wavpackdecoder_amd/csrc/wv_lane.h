@@ -350,11 +350,17 @@ __device__ __forceinline__ uint4 ff_unit(uint4 v, uint32_t u, uint32_t e) {
 
 // .wvc correction stream window (HY == 2; cwin_init / cwin_merge / cwin_corr below)
 struct CWin {
-    const uint32_t *w;  // the stream's dword-aligned base
+    const uint4 *src;   // the stream's 16-B aligned base
+    uint8_t *lds;       // the correction rings (WRING_OFF)
+    uint32_t col;       // this lane's column of its pair's ring (byte offset from lds)
     uint64_t win;       // LSB = next bit
     int32_t nb;         // valid bits (>= 33 at every word start)
-    uint32_t q0, q1, q2, ld;  // the next dwords, and the load of the one after (consumed three refills later)
-    uint32_t ni;        // index of the dword in ld
+    uint32_t rd;        // index of the dword merged next (its value read ahead in nxt)
+    uint32_t nxt;
+    uint32_t lu;        // units (16 B) staged in the ring so far; dwords below 4 lu are readable
+    uint32_t ulast;     // the stream's last unit (units past it re-read it)
+    uint32_t lim;       // 4 lu at the group's start: a merge of dword rd >= lim is an underrun
+    uint32_t ovf;       // an underrun happened (the block goes back)
     uint32_t used;      // bits consumed (checked against end at the block's end)
     uint32_t end;       // the stream's bits (from its first bit)
 };
@@ -555,37 +561,85 @@ __device__ __forceinline__ void lhy_code(uint32_t x, uint32_t low, uint32_t mc, 
 // hands the reconstruction wave each word's final interval (LW.clo / cn); that wave
 // reads the correction, exact minus lossy, and carries it through the passes
 // (LPass::frame_wvc), off the parser's chain.  Each lane reads its correction stream through a
-// 64-bit register window merged from dwords loaded a refill ahead (global loads: the
-// stream is sparse beside the main one); a lane whose reads pass the stream's end
-// hands its block back (its bytes past the end would read 0xFF there).
+// 64-bit register window refilled from an LDS ring (below); a lane whose reads pass the
+// stream's end, or the units staged so far, hands its block back.
 
-__device__ __forceinline__ void cwin_init(CWin &c, const uint8_t *blob, uint64_t off, uint32_t len) {
-    const uint32_t sh = (uint32_t)(off & 3u);
-    c.w = (const uint32_t *)(blob + (off - sh));
-    c.win = ((uint64_t)c.w[0] | ((uint64_t)c.w[1] << 32)) >> (8u * sh);
-    c.nb = 64 - 8 * (int32_t)sh;
-    c.q0 = c.w[2];
-    c.q1 = c.w[3];
-    c.q2 = c.w[4];
-    c.ld = c.w[5];
-    c.ni = 5;
+// The stream is staged in LDS like the parser's payload, in a ring of WRU 16-B units per
+// lane (dword k of lane l at ((k mod 4 WRU) * 64 + l) * 4: every lane's read hits bank l):
+// a group issues the loads of up to WNL next units at its start and writes them at its end,
+// so a load has a group's time to arrive and the window's refills read LDS (a register
+// queue of global loads left each load's latency on the word after it: 31.4 ms for C4).
+constexpr uint32_t WRU = 8, WNL = 4;
+constexpr uint32_t WRING_BYTES = WRU * 16u * 64u;
+constexpr uint32_t WRING_OFF = LPAIRS * RING_BYTES + LDS_AFTER_RINGS;  // (HY == 2 kernels: lane_blocks)
+__device__ __forceinline__ uint32_t cw_addr(const CWin &c, uint32_t k) { return c.col + ((k & (WRU * 4u - 1u)) << 8); }
+__device__ __forceinline__ void cw_put(CWin &c, uint32_t u, uint4 v) {
+    uint32_t *d = (uint32_t *)(c.lds + cw_addr(c, 4u * u));  // (the unit's four dwords: consecutive slots)
+    d[0] = v.x;
+    d[64] = v.y;
+    d[128] = v.z;
+    d[192] = v.w;
+}
+__device__ __forceinline__ void cwin_init(CWin &c, const uint8_t *blob, uint8_t *lds, uint32_t pair, uint32_t lane,
+                                          uint64_t off, uint32_t len) {
+    const uint32_t skip = (uint32_t)(off & 15u);
+    c.src = (const uint4 *)(blob + (off - skip));
+    c.lds = lds;
+    c.col = WRING_OFF + pair * WRING_BYTES + lane * 4u;
+    const uint32_t eu = (skip + len + 15u) >> 4;
+    c.ulast = eu > 0u ? eu - 1u : 0u;
+#pragma unroll
+    for (uint32_t u = 0; u < WRU; u++) cw_put(c, u, c.src[min(u, c.ulast)]);
+    c.lu = WRU;
+    c.lim = 4u * WRU;
+    c.ovf = 0u;
+    const uint32_t k = skip >> 2, sb = (skip & 3u) * 8u;
+    c.win = ((uint64_t)*(const uint32_t *)(c.lds + cw_addr(c, k)) |
+             ((uint64_t)*(const uint32_t *)(c.lds + cw_addr(c, k + 1u)) << 32)) >> sb;
+    c.nb = 64 - (int32_t)sb;
+    c.rd = k + 2u;
+    c.nxt = *(const uint32_t *)(c.lds + cw_addr(c, c.rd));
     c.used = 0;
     c.end = len * 8u;
 }
-// keep >= 33 bits: merge q0 when 32 or fewer are left; the queue moves on, and the load
-// issued now is consumed three merges later (a lane's stream runs through a cache line
-// every 32 dwords: its first read waits for memory)
+// keep >= 33 bits: merge the dword read ahead when 32 or fewer are left, then read the next
 __device__ __forceinline__ void cwin_merge(CWin &c) {
     const uint32_t mg = (uint32_t)((c.nb - 33) >> 31);  // ~0: merge
     const uint32_t sh = (uint32_t)c.nb;
     __builtin_assume(sh < 64u);
-    c.win |= (uint64_t)(c.q0 & mg) << sh;
+    c.win |= (uint64_t)(c.nxt & mg) << sh;
     c.nb += (int32_t)(mg & 32u);
-    c.q0 = mg ? c.q1 : c.q0;
-    c.q1 = mg ? c.q2 : c.q1;
-    c.q2 = mg ? c.ld : c.q2;
-    c.ni += mg & 1u;
-    c.ld = c.w[c.ni];  // (reads stay within 24 bytes past the stream: the blob's tail)
+    c.ovf |= mg & (c.rd >= c.lim ? 1u : 0u);
+    c.rd += mg & 1u;
+    c.nxt = *(const uint32_t *)(c.lds + cw_addr(c, c.rd));
+}
+// a group's staging: the loads of the units after lu that fit in the ring (the dwords
+// below rd are merged), issued at the group's start ...
+struct CStage {
+    uint4 v0, v1, v2, v3;
+    uint32_t n;
+};
+__device__ __forceinline__ CStage cwin_issue(CWin &c) {
+    CStage st;
+    c.lim = 4u * c.lu;
+    const uint32_t room = (c.rd >> 2) + WRU - c.lu;
+    st.n = room < WNL ? room : WNL;
+    st.v0 = c.src[min(c.lu, c.ulast)];
+    st.v1 = c.src[min(c.lu + 1u, c.ulast)];
+    st.v2 = c.src[min(c.lu + 2u, c.ulast)];
+    st.v3 = c.src[min(c.lu + 3u, c.ulast)];
+    return st;
+}
+// ... and written at its end (a unit without room to the dummy slots past the rings)
+__device__ __forceinline__ void cwin_stage(CWin &c, const CStage &st, uint32_t lane) {
+    const uint32_t dummy = RING_DUMMY + lane * 4u;
+    CWin d = c;
+    d.col = dummy;  // (cw_addr of a dummy: its 4 slots of 64 lanes at RING_DUMMY)
+    if (st.n > 0u) cw_put(c, c.lu, st.v0); else cw_put(d, 0u, st.v0);
+    if (st.n > 1u) cw_put(c, c.lu + 1u, st.v1); else cw_put(d, 0u, st.v1);
+    if (st.n > 2u) cw_put(c, c.lu + 2u, st.v2); else cw_put(d, 0u, st.v2);
+    if (st.n > 3u) cw_put(c, c.lu + 3u, st.v3); else cw_put(d, 0u, st.v3);
+    c.lu += st.n;
 }
 // exact - lossy for a word of value v (sign and lossy magnitude) whose final interval
 // is [lo, lo + n - 1] (n 1: the word was exact, nothing is read, lo its magnitude)
@@ -1190,7 +1244,7 @@ __device__ __forceinline__ void rout(int32_t L, int32_t R, uint32_t g0, uint32_t
             if (fst) st2(o + 2u * t, make_int2(v, v));
             else o[t] = v;
         }
-        if (!FULL && t + 1u == nfr) lane_finish(rbad | (HY == 2 && cw.used > cw.end ? 1u : 0u), e, mx, mn, crc);
+        if (!FULL && t + 1u == nfr) lane_finish(rbad | (HY == 2 && (cw.used > cw.end || cw.ovf) ? 1u : 0u), e, mx, mn, crc);
         return;
     }
     if (joint) {
@@ -1208,7 +1262,7 @@ __device__ __forceinline__ void rout(int32_t L, int32_t R, uint32_t g0, uint32_t
         if (nfr) st2(o + 2u * t, v);  // (a lane without a block of its own stores nothing)
     } else {
         if (t < nfr) st2(o + 2u * t, v);
-        if (t + 1u == nfr) lane_finish(rbad | (HY == 2 && cw.used > cw.end ? 1u : 0u), e, mx, mn, crc);
+        if (t + 1u == nfr) lane_finish(rbad | (HY == 2 && (cw.used > cw.end || cw.ovf) ? 1u : 0u), e, mx, mn, crc);
     }
 }
 template <int U, bool FULL, bool MONO, int HY, bool CODES, int... Ts>
@@ -1515,7 +1569,8 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
 template <bool MONO, int HY, int... Ts>
 __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
                                            uint32_t n, const uint8_t *__restrict__ blob, int32_t *__restrict__ out,
-                                           uint32_t *__restrict__ status, LShared &sh, uint32_t grp, uint32_t lane) {
+                                           uint32_t *__restrict__ status, LShared &sh, uint8_t *lds, uint32_t pair,
+                                           uint32_t grp, uint32_t lane) {
     using namespace wvf;
     constexpr bool CODES = lane_codes<HY, Ts...>();
     const LBlock lb = lane_block<MONO, HY, Ts...>(descs, list, n, grp, lane);
@@ -1536,8 +1591,8 @@ __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, 
     // the .wvc stream (HY == 2): this wave reads the corrections -- the parser hands over
     // each word's final interval, off its own chain
     CWin cw;
-    if constexpr (HY == 2) cwin_init(cw, blob, lb.ok ? d.wvc_off : 0u, lb.ok ? d.wvc_len : 0u);
-    else cw = CWin{(const uint32_t *)blob, 0ull, 0, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    if constexpr (HY == 2) cwin_init(cw, blob, lds, pair, lane, lb.ok ? d.wvc_off : 0u, lb.ok ? d.wvc_len : 0u);
+    else cw = CWin{nullptr, nullptr, 0u, 0ull, 0, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
     uint32_t crc = 0xFFFFFFFFu;
     int32_t mx = 0, mn = 0;
     uint32_t rbad = 0u;
@@ -1550,6 +1605,8 @@ __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, 
             return;
         }
         rbad |= ch.wbad() ? 4u : 0u;
+        CStage cst;
+        if constexpr (HY == 2) cst = cwin_issue(cw);  // (the next units of the .wvc stream)
         if constexpr (NS != 0) {
             if (g0 + GF < lb.nmin)
                 rgroup_rt<true, MONO, CODES, NS, HY>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
@@ -1574,6 +1631,7 @@ __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, 
             rframe<6, false, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
             rframe<7, false, MONO, HY, CODES>(ch, sh, lane, g0, nfr, joint, mx, mn, crc, sh_, o, rbad, le, fst, fx, cw);
         }
+        if constexpr (HY == 2) cwin_stage(cw, cst, lane);
         // the group's residuals are read (DS ops of one wave complete in order)
         w2::lds_publish(&sh.consumed, g0 + GF);
     }
@@ -1663,7 +1721,7 @@ __device__ __forceinline__ void lane_recon_split(const BlockDesc *__restrict__ d
         int32_t *o = out + d.out_off;
         Fixup fx;
         if constexpr (HY) fixup_init(fx, d);
-        const CWin cw = CWin{nullptr, 0ull, 0, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+        const CWin cw = CWin{nullptr, nullptr, 0u, 0ull, 0, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
         uint32_t crc = 0xFFFFFFFFu;
         int32_t mx = 0, mn = 0;
         const LEnd le = {status + lb.bi, d.mute_limit, d.nframes == d.block_samples, d.crc, sh.pflag, lane};
@@ -1715,8 +1773,9 @@ __device__ __forceinline__ void lane_blocks(const BlockDesc *__restrict__ descs,
                                             uint32_t n, const uint8_t *__restrict__ blob, int32_t *__restrict__ out,
                                             uint32_t *__restrict__ status, uint32_t *__restrict__ dbg) {
     __shared__ LShared shp[LPAIRS];
-    // the parsers' payload rings (put_unit, ring_step), the exp2 / log2 tables (HY), the dummy unit slots
-    __shared__ uint32_t rings[(LPAIRS * RING_BYTES + LDS_AFTER_RINGS) / 4];
+    // the parsers' payload rings (put_unit, ring_step), the exp2 / log2 tables (HY), the dummy unit
+    // slots, and with .wvc streams (HY == 2) the reconstruction waves' correction rings (CWin)
+    __shared__ uint32_t rings[(LPAIRS * RING_BYTES + LDS_AFTER_RINGS + (HY == 2 ? LPAIRS * WRING_BYTES : 0u)) / 4];
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     const uint32_t pair = wave >> 1, grp = blockIdx.x * LPAIRS + pair;
     LShared &sh = shp[pair];
@@ -1737,7 +1796,7 @@ __device__ __forceinline__ void lane_blocks(const BlockDesc *__restrict__ descs,
     if ((wave & 1u) == 0u)
         lane_parser<MONO, HY, Ts...>(descs, list, n, blob, sh, (uint8_t *)rings, pair, grp, lane, dbg);
     else
-        lane_recon<MONO, HY, Ts...>(descs, list, n, blob, out, status, sh, grp, lane);
+        lane_recon<MONO, HY, Ts...>(descs, list, n, blob, out, status, sh, (uint8_t *)rings, pair, grp, lane);
 }
 
 #ifndef WV_RT_SPLIT16  // (0: A/B builds with every run-time list on the two-wave layout)
@@ -1781,7 +1840,7 @@ __device__ __forceinline__ void lane_blocks_rt(const BlockDesc *__restrict__ des
 #define WV_RT_PAIR(MONO_, NS_, HY_)                                                                  \
     do {                                                                                           \
         if (parser) lane_parser<MONO_, HY_, LANE_RT, NS_>(descs, list, n, blob, sh, rg, pair, grp, lane, dbg); \
-        else lane_recon<MONO_, HY_, LANE_RT, NS_>(descs, list, n, blob, out, status, sh, grp, lane);       \
+        else lane_recon<MONO_, HY_, LANE_RT, NS_>(descs, list, n, blob, out, status, sh, rg, pair, grp, lane); \
     } while (0)
 #if WV_RT_SPLIT16  // lists of 6..16 terms: wv_pcm_lane_rt3
     if (nt > 5) return;
