@@ -1876,6 +1876,8 @@ __device__ __forceinline__ void lane_blocks_rt(const BlockDesc *__restrict__ des
 #define RT3_NW 3
 #endif
 constexpr int RT3_THREADS = 64 * (1 + RT3_NW) * LPAIRS;
+// (HYK: the lossless pairs (0) or the hybrid ones (1): two kernels, two translation units)
+template <int HYK>
 __device__ __forceinline__ void lane_blocks_rt3(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
                                                 uint32_t n, const uint8_t *__restrict__ blob, int32_t *__restrict__ out,
                                                 uint32_t *__restrict__ status, uint32_t *__restrict__ dbg) {
@@ -1924,14 +1926,9 @@ __device__ __forceinline__ void lane_blocks_rt3(const BlockDesc *__restrict__ de
         else if (role == 2u) lane_recon_split<MONO_, 2, RT3_NW, HY_>(descs, list, n, out, status, sh, grp, lane);  \
         else if constexpr (RT3_NW == 3) lane_recon_split<MONO_, 3, 3, HY_>(descs, list, n, out, status, sh, grp, lane); \
     } while (0)
-    if (fl & wvf::HYBRID_FLAG) {
-        if (fl & wvf::MONO_DATA) WV_RT3_ROLES(true, 1);
-        else WV_RT3_ROLES(false, 1);
-    } else if (fl & wvf::MONO_DATA) {
-        WV_RT3_ROLES(true, 0);
-    } else {
-        WV_RT3_ROLES(false, 0);
-    }
+    if (((fl & wvf::HYBRID_FLAG) != 0) != (HYK != 0)) return;  // (the other kernel's pair)
+    if (fl & wvf::MONO_DATA) WV_RT3_ROLES(true, HYK);
+    else WV_RT3_ROLES(false, HYK);
 #undef WV_RT3_ROLES
 }
 
