@@ -1680,11 +1680,17 @@ __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, 
 // with another chain (lane_blocks_rt3).
 template <int NW>
 struct RSplit {
-    static constexpr int RS = NW == 2 ? 8 : 6;  // passes per role, at most
+#ifndef WV_RT3_RS  // (A/B builds: the passes per role, and the frame tails' weight in passes)
+#define WV_RT3_RS 6
+#endif
+#ifndef WV_RT3_TAILW
+#define WV_RT3_TAILW 1
+#endif
+    static constexpr int RS = NW == 2 ? 8 : WV_RT3_RS;  // passes per role, at most
     static_assert(NW * RS >= MAXP, "the roles cover every list");
     // role r's passes [first, first + count) of nt (the last role also runs the tails: one more share)
     __device__ __forceinline__ static void share(int32_t nt, int role, int32_t &first, int32_t &count) {
-        const int32_t q = min((nt + 1 + NW - 1) / NW, (int32_t)RS);
+        const int32_t q = min((nt + WV_RT3_TAILW + NW - 1) / NW, (int32_t)RS);
         first = min(q * (role - 1), nt);
         count = role < NW ? min(q, nt - first) : nt - first;
     }
