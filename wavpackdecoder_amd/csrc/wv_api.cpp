@@ -982,13 +982,28 @@ static void build_lane_orders(wvg_batch *b) {
         LL.clear();
         if (L.empty()) continue;
         std::sort(L.begin(), L.end(), by_len_density);
+        // (the keys once per block, then a stable sort of positions by key: the list order --
+        // longest first -- stays within each list)
+        const bool rt = lane_rt_group(t);
+        std::vector<std::array<int8_t, MAXP + 2>> keys;
         std::vector<uint32_t> order = L;
-        if (lane_rt_group(t))
-            std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return lkey(x) < lkey(y); });
+        if (rt) {
+            keys.reserve(L.size());
+            for (uint32_t k : L) keys.push_back(lkey(k));
+            std::vector<uint32_t> pos(L.size());
+            for (size_t i = 0; i < pos.size(); i++) pos[i] = (uint32_t)i;
+            std::stable_sort(pos.begin(), pos.end(), [&](uint32_t x, uint32_t y) { return keys[x] < keys[y]; });
+            std::vector<std::array<int8_t, MAXP + 2>> sk(pos.size());
+            for (size_t i = 0; i < pos.size(); i++) {
+                order[i] = L[pos[i]];
+                sk[i] = keys[pos[i]];
+            }
+            keys.swap(sk);
+        }
         for (size_t i = 0; i < order.size();) {
             size_t j = i + 1;
-            if (lane_rt_group(t))
-                while (j < order.size() && lkey(order[j]) == lkey(order[i])) j++;
+            if (rt)
+                while (j < order.size() && keys[j] == keys[i]) j++;
             else
                 j = order.size();
             part.clear();
