@@ -194,6 +194,18 @@ def pmc_traffic(kernel_substr: str = "wv_pcm_2wave<17, 17>"):
 KERNEL_NAMES = {"lane": "wv_pcm_lane<false, 0, 17, 17>", "two_wave": "wv_pcm_2wave<17, 17>"}
 
 
+# C5: batches in flight the copies aim at (each batch takes up to 3 streams while others
+# run, within the process's hardware queues: wv_api.cpp wvg_batch_decode)
+C5_BATCHES_IN_FLIGHT = 8
+
+
+def c5_copies(args, nslices: int) -> int:
+    """Copies of a rank's C5 batches: --c5-copies, else enough that about
+    C5_BATCHES_IN_FLIGHT batches are in flight (at least 1, at most --steps)."""
+    c = args.c5_copies if args.c5_copies else max(1, C5_BATCHES_IN_FLIGHT // max(1, nslices))
+    return max(1, min(c, args.steps))
+
+
 def verify(batches, pcm) -> dict:
     """Download every batch copy and check what its last decode produced: C2's
     int32 output equals the generator's PCM, no CRC error in any file
@@ -352,18 +364,25 @@ def run_rank(args) -> None:
     else:
         from wavpackdecoder_amd import shard
         costs = [corpora.c5_cost(i) for i in range(args.c5_files)]
-        mine = shard.partition([int(c) for c in costs], ws)[rank]
+        # (--c5-share N:r: decode rank r's share of an N-way split in this one process --
+        # the per-rank times of an N-GPU run measured one share at a time on one GPU,
+        # scripts/c5_scaling.py)
+        pw, pr = (int(x) for x in args.c5_share.split(":")) if args.c5_share else (ws, rank)
+        mine = shard.partition(costs, pw)[pr]
         t_gen = time.perf_counter()
         files = corpora.c5_files(mine, progress=rank == 0)
         print(f"bench: C5 rank {rank}: {len(files)} files generated in {time.perf_counter() - t_gen:.1f} s",
               file=sys.stderr, flush=True)
         workload = f"C5: files 0..{args.c5_files - 1} of the mixed corpus, LPT file partition over {ws} GPU(s)"
+        if args.c5_share:
+            workload += f"; share {pr} of an {pw}-way split (--c5-share)"
         scaling = "strong"
-    # the rank's files in slices of at most --c5-batch files (one batch each); a single
-    # slice is decoded as `inflight` copies, several slices are all decoded every step
-    slices = [files[k:k + args.c5_batch] for k in range(0, len(files), args.c5_batch)] if args.workload == "c5" \
-        else [files]
-    multi = len(slices) > 1
+    # C5: the rank's files in slices of at most --c5-batch files (one batch each), and
+    # --c5-copies copies of that set of batches; step k decodes every slice of copy
+    # k % copies, so consecutive steps overlap on the device (each step is still one
+    # complete decode of the rank's files).  C2: --inflight copies of the one batch.
+    multi = args.workload == "c5"
+    slices = [files[k:k + args.c5_batch] for k in range(0, len(files), args.c5_batch)] if multi else [files]
 
     L = _lib.lib()
     # (WVG_BENCH_SAME_DEVICE=1: every rank on device 0 -- the multi-rank path rehearsed on a
@@ -376,26 +395,29 @@ def run_rank(args) -> None:
     # step k decodes copy k % inflight, so consecutive steps overlap on the device
     # the way a decode server keeps several batches in flight (every step is still
     # one complete decode of the whole batch into its own output)
-    inflight = args.inflight if args.inflight else (20 if args.kernel == "lane" else 3)
-    inflight = max(1, min(inflight, args.steps))
-    batches = []
-    for k in range(len(slices) if multi else inflight):
-        bb = DecodeBatch(4096)
-        bb.set_kernel(args.kernel)
-        bb.add_files(slices[k] if multi else files)  # host framing on worker threads
-        bb.upload()
-        batches.append(bb)
+    if multi:
+        copies = c5_copies(args, len(slices))
+    else:
+        copies = args.inflight if args.inflight else (20 if args.kernel == "lane" else 3)
+        copies = max(1, min(copies, args.steps))
+    sets = []
+    for _ in range(copies):
+        cur = []
+        for sl in slices:
+            bb = DecodeBatch(4096)
+            bb.set_kernel(args.kernel)
+            bb.add_files(sl)  # host framing on worker threads
+            bb.upload()
+            cur.append(bb)
+        sets.append(cur)
+    batches = [bb for cur in sets for bb in cur]
     b = batches[0]
-    frames_rank = sum(bb.frames for bb in batches) if multi else b.frames
+    frames_rank = sum(bb.frames for bb in sets[0])
     alg_bytes = sum(algorithmic_bytes(f) for f in files)
-    # (several slices: a step decodes every slice, all issued back to back; else step k
-    # decodes copy k % inflight)
+
     def step(k):
-        if multi:
-            for bb in batches:
-                bb.decode()
-        else:
-            batches[k % len(batches)].decode()
+        for bb in sets[k % copies]:
+            bb.decode()
     extras = not multi and not args.timed_only  # the one-batch legs beside `value`
 
     # setup, untimed: one decode of every copy binds its stream to a hardware queue
@@ -480,6 +502,7 @@ def run_rank(args) -> None:
         auto_ms = b.time(3)
         b.set_kernel(args.kernel)
     dt = _reduce(pg, t1 - t0, "max")
+    dt_all = _gather(pg, t1 - t0, ws)
     frames_total = _reduce(pg, float(frames_rank), "sum")
     kms_all = _gather(pg, kernel_ms, ws)
     value = frames_total * args.steps / dt / 1e6
@@ -500,7 +523,9 @@ def run_rank(args) -> None:
                                "frames_total": int(frames_total),
                                "parallelism": f"file-shard x{ws}, no collectives"},
                     "kernel_ms": round(kernel_ms, 4), "per_rank_kernel_ms": [round(x, 4) for x in kms_all],
-                    "batches_in_flight": len(batches), "kernel": args.kernel, "verified": ver,
+                    "per_rank_ms_per_step": [round(x * 1e3 / args.steps, 4) for x in dt_all],
+                    "batches_in_flight": len(batches), "c5_copies": copies if multi else None,
+                    "kernel": args.kernel, "verified": ver,
                     "cpu_baseline": cpu}
             if multi:
                 line["vs_cpu"] = None if cpu is None else {
@@ -711,8 +736,13 @@ def main():
     ap.add_argument("--blocks", type=int, default=1024)
     ap.add_argument("--block-frames", type=int, default=22050)
     ap.add_argument("--c5-files", type=int, default=4000)
-    ap.add_argument("--c5-batch", type=int, default=4000,
+    ap.add_argument("--c5-batch", type=int, default=12500,
                     help="C5: files per batch; a rank with more files decodes all its batches every step")
+    ap.add_argument("--c5-share", default=None,
+                    help="C5: N:r -- decode rank r's share of an N-way file split (one process)")
+    ap.add_argument("--c5-copies", type=int, default=0,
+                    help="C5: copies of the rank's batches, step k decoding copy k %% copies (0: as many as "
+                         "keep about C5_BATCHES_IN_FLIGHT batches in flight)")
     ap.add_argument("--inflight", type=int, default=None,
                     help="batch copies decoding concurrently (own buffers and streams); 1 = one batch at a time "
                          "(default: 20 for the lane kernel, 3 for the two-wave kernel, at most --steps)")

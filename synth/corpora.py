@@ -160,11 +160,10 @@ def c5_file(i: int) -> bytes:
     return S.encode_dsd(dd, S.DsdParams(nch=2, mode=mode, block_samples=B))
 
 
-# relative device cost per frame of a block of each C5 kind (one serial chain per
-# block; DESIGN.md §6 per-mode timings): used to balance a strong-scaling split
-# (round 5: from the kinds' in-flight rates on the lane kernels -- C2 56,000, C3 57,000,
-# DSD mode 0 212,000, mode 1 7,350, mode 3 9,330 Mframes/s; mono about twice stereo)
-C5_COST = {"stereo16": 1.0, "mono16": 0.5, "stereo24": 1.0, "mono24": 0.6, "dsd0": 0.3, "dsd1": 7.6, "dsd3": 6.0}
+# relative device cost per frame of a block of each C5 kind: shard.KIND_COST, the table
+# shard.file_cost applies to a file's own header (the same cost in bench.py's split and
+# in shard.run_rank)
+from wavpackdecoder_amd.shard import KIND_COST as C5_COST  # noqa: E402
 
 
 def c5_meta(i: int):

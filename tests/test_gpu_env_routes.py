@@ -4,7 +4,11 @@ in a child process), against the oracle bit for bit:
 * WVG_LANE_HIGH16=ct -- WavPack's 16-term lists on their compile-time lane instantiations
   (the default runs them on the run-time list pipeline, wv_pcm_lane_rt3);
 * WVG_DSD_STREAM=1 -- a mixed batch's DSD groups on a second stream of its own while other
-  batches of the context run (batches in flight together, C5-style files)."""
+  batches of the context run (batches in flight together, C5-style files);
+* the default own-stream policy -- a batch's launch groups on up to three streams of its own
+  while others run, as far as the hardware-queue budget (GPU_MAX_HW_QUEUES) leaves each batch
+  in flight -- and WVG_DSD_STREAM=0, which keeps every group on the batch's one stream.
+The routes are read from the decodes' WVG_DECODE_LOG lines (streams taken, own streams)."""
 import json
 import os
 import subprocess
@@ -71,7 +75,14 @@ def _child(case, env_extra):
     r = subprocess.run([sys.executable, "-c", code, case], env=env, capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, r.stderr[-2000:]
     print(r.stdout[-400:])
-    return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    # WVG_DECODE_LOG=1: "wvg decode <p>: groups G, others running R, streams S, own O, auto A"
+    d["decodes"] = []
+    for ln in r.stderr.splitlines():
+        if ln.startswith("wvg decode "):
+            kv = dict(x.strip().rsplit(" ", 1) for x in ln.split(":", 1)[1].split(","))
+            d["decodes"].append({k: int(v) for k, v in kv.items()})
+    return d
 
 
 @pytest.mark.timeout(300)
@@ -83,6 +94,26 @@ def test_high16_compile_time_route():
 
 @pytest.mark.timeout(300)
 def test_dsd_own_stream_route():
-    d = _child("c5", {"WVG_DSD_STREAM": "1"})
+    d = _child("c5", {"WVG_DSD_STREAM": "1", "WVG_DECODE_LOG": "1"})
     assert d["compared"] == d["files"] * d["copies"] and d["frames"] > 0
     assert d["mismatches"] == 0
+    # the route was taken: a decode that found others running, on two streams of its own
+    assert any(x["others running"] >= 1 and x["own"] == 1 and x["streams"] == 2 for x in d["decodes"]), d["decodes"]
+
+
+@pytest.mark.timeout(300)
+def test_own_streams_queue_budget_route():
+    """The default policy: with 24 hardware queues and 3 batches in flight each decode that
+    finds the others running takes 3 streams of its own (24 / 3 >= kLanes); with 4 queues
+    (HIP's default) it keeps one."""
+    d = _child("c5", {"GPU_MAX_HW_QUEUES": "24", "WVG_DECODE_LOG": "1"})
+    assert d["mismatches"] == 0 and d["compared"] == d["files"] * d["copies"]
+    assert any(x["others running"] >= 1 and x["own"] == 1 and x["streams"] == 3 for x in d["decodes"]), d["decodes"]
+    d = _child("c5", {"GPU_MAX_HW_QUEUES": "4", "WVG_DECODE_LOG": "1"})
+    assert d["mismatches"] == 0
+    run = [x for x in d["decodes"] if x["others running"] >= 1]
+    assert run and all(x["streams"] <= max(1, 4 // (x["others running"] + 1)) for x in run), d["decodes"]
+    d = _child("c5", {"GPU_MAX_HW_QUEUES": "24", "WVG_DSD_STREAM": "0", "WVG_DECODE_LOG": "1"})
+    assert d["mismatches"] == 0
+    run = [x for x in d["decodes"] if x["others running"] >= 1]
+    assert run and all(x["streams"] == 1 and x["own"] == 0 for x in run), d["decodes"]

@@ -90,6 +90,12 @@ struct wvg_ctx {
     // when a decode last found another batch of this context running (now_ms; WVG_KERNEL_AUTO
     // keeps the lane kernels for kConcurrentHoldMs after it)
     std::atomic<double> concurrent_ms{-1e30};
+    // the process's hardware queues (GPU_MAX_HW_QUEUES as the process started; HIP's default
+    // 4): the stream budget the batches in flight share (wvg_batch_decode's own-stream policy)
+    int hw_queues = 4;
+    // WVG_DSD_STREAM: 0 never give a batch streams of its own while others run, 1 always
+    // (two), unset: as many as the queue budget leaves each batch in flight (up to kLanes)
+    int own_streams = -1;
 };
 
 // Page-locked, grow-only host buffer: the batch's file bytes live here from
@@ -144,7 +150,7 @@ struct wvg_batch {
     int chunk = 4096;
     hipStream_t stream = nullptr;          // the batch's own stream (default for decode/format/download)
     hipEvent_t fork = nullptr, join[kLanes - 1] = {nullptr};  // lanes 1 .. (the context's side streams)
-    hipStream_t dstream[2] = {nullptr, nullptr};  // the batch's own side streams while others run (split_dsd)
+    hipStream_t dstream[2] = {nullptr, nullptr};  // the batch's own side streams while others run (own_side)
     hipEvent_t done = nullptr;             // end of the last decode/format, on whatever stream it ran
     bool timing = false;                   // wvg_batch_set_timing: an event pair around every decode
     std::vector<hipEvent_t> tev;           // pending (start, end) pairs, folded into t_sum/t_cnt
@@ -272,6 +278,10 @@ wvg_ctx *wvg_open(int device) {
     if (upload_dsd_ptables() != hipSuccess) return nullptr;  // DSD mode 3's starting tables, per device
     wvg_ctx *c = new wvg_ctx();
     c->device = device;
+    const char *q = getenv("GPU_MAX_HW_QUEUES");
+    if (q && atoi(q) >= 1) c->hw_queues = atoi(q);
+    const char *ds = getenv("WVG_DSD_STREAM");
+    if (ds && (ds[0] == '0' || ds[0] == '1')) c->own_streams = ds[0] - '0';
     return c;
 }
 
@@ -1178,12 +1188,13 @@ static hipError_t fold_timing(wvg_batch *b, int pairs) {
     return hipSuccess;
 }
 
-// another batch of b's context with a decode or format still running
-static bool others_running(wvg_batch *b) {
+// the other batches of b's context with a decode or format still running
+static int others_running(wvg_batch *b) {
     std::lock_guard<std::mutex> g(b->ctx->mu);
+    int k = 0;
     for (wvg_batch *o : b->ctx->batches)
-        if (o != b && o->done && hipEventQuery(o->done) == hipErrorNotReady) return true;
-    return false;
+        if (o != b && o->done && hipEventQuery(o->done) == hipErrorNotReady) k++;
+    return k;
 }
 
 int wvg_batch_decode(wvg_batch *b, void *stream) {
@@ -1203,12 +1214,12 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
         HIPCHK(c, hipEventRecord(e0, s));
     }
     // The non-empty launch groups (DSD, DSD mode 1, generic PCM, term sets 0..7)
-    // each go onto a stream of their own (lanes: the batch stream and side
-    // streams).  Streams beyond the process's hardware queues (GPU_MAX_HW_QUEUES,
-    // raised to 16 by wvg_open) share a queue, whose kernels then run one after
-    // another -- a PCM group queued behind the DSD group (its mode-3 blocks are
-    // the batch's longest serial chains) waits for all of it.  With fewer lanes
-    // than groups (WVG_LANES, A/B) the DSD groups keep lanes of their own and the
+    // each go onto a stream of their own when the decode is issued alone (its
+    // batch's stream and the context's side streams).  Streams beyond the process's
+    // hardware queues (GPU_MAX_HW_QUEUES, the host's choice) share a queue, whose
+    // kernels then run one after another -- a PCM group queued behind the DSD group
+    // (its mode-3 blocks are the batch's longest serial chains) waits for all of it.
+    // With fewer lanes than groups the DSD groups keep lanes of their own and the
     // PCM groups share the rest, the largest first onto the least loaded.
     const int kDsd = kMaxTermSets + 1, kDsd1 = kMaxTermSets + 2, kPcm = kMaxTermSets;
     int used[kSide], n = 0;
@@ -1218,28 +1229,38 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
     for (int t = 0; t < kMaxTermSets; t++)
         if (!b->ts_list[t].empty()) used[n++] = t;
     int lane_of[kSide];
-    // With other batches of this context still running, a decode keeps its groups
-    // on its own stream (in order on it; the batches in flight fill the device);
-    // alone, it spreads them over the context's side streams for its own latency
-    // (kLanes).  C5 at 20 in flight: 10,600 Mframes/s on one stream per batch, 6,500
-    // on one per launch group (profiles/r04_c5_streams.txt).
-    // (asked only when it decides something: a multi-group decode's streams, or the
-    // default kernel choice before the context has seen batches overlap)
+    // With other batches of this context running, a decode's groups share the
+    // hardware queues with theirs: it takes streams of its own (its stream and up to
+    // kLanes - 1 side streams of the batch) only as far as the queue budget leaves
+    // each batch in flight, else everything goes in order onto its one stream (the
+    // batches in flight fill the device).  One stream per batch: C5's 4,000-file
+    // slice at 20 in flight 10,600 Mframes/s against 6,500 on one stream per group
+    // (profiles/r04_c5_streams.txt); 25 slices on 24 queues with a second stream
+    // each for the DSD groups: 7,446 -> 9,337 Msamples/s, but the 4,000-file slice at
+    // 20 in flight 13,174 -> 11,148 (40 streams on 24 queues,
+    // profiles/r05_c5_streams.jsonl) -- hence the budget.
+    // (asked when it decides something: a multi-group decode's streams, or the default
+    // kernel choice -- also while the hold is on, so that batches that keep overlapping
+    // keep renewing it: the hold is a sliding window over the last overlap seen)
     const double t_now = now_ms();
     const bool held = t_now - c->concurrent_ms.load() < kConcurrentHoldMs;
-    const bool ask = (!b->lanes_env && b->lanes > 1 && n > 1) || (b->kernel_auto && !held);
-    const bool running = ask && others_running(b);
+    const bool ask = (!b->lanes_env && b->lanes > 1 && n > 1) || b->kernel_auto;
+    const int others = ask ? others_running(b) : 0;
+    const bool running = others > 0;
     int nlanes = b->lanes;
-    // (WVG_DSD_STREAM=1: while others run, a batch with DSD and PCM groups puts its DSD groups on a
-    // second stream of its own, so that its DSD mode-3 chains overlap its PCM groups.  The full C5
-    // corpus as 25 slices decoded every step: 7,446 -> 9,337 Msamples/s; one slice as 20 copies
-    // in flight: 13,174 -> 11,148 -- two streams per batch share the hardware queues; off by
-    // default, profiles/r05_c5_streams.jsonl)
-    static const bool dsd_own = getenv("WVG_DSD_STREAM") && getenv("WVG_DSD_STREAM")[0] == '1';
     bool has_pcm = !b->pcm_list.empty();
     for (int t = 0; t < kMaxTermSets; t++) has_pcm |= !b->ts_list[t].empty();
-    const bool split_dsd = dsd_own && running && !b->dsd_list.empty() && has_pcm && !b->lanes_env;
-    if (!b->lanes_env && nlanes > 1 && running) nlanes = split_dsd ? 2 : 1;
+    int own = 1;  // streams of its own while others run
+    if (running && !b->lanes_env && n > 1) {
+        if (c->own_streams < 0) {
+            own = c->hw_queues / (others + 1);
+            own = own < 1 ? 1 : (own > kLanes ? kLanes : own);
+        } else if (c->own_streams == 1 && !b->dsd_list.empty() && has_pcm) {
+            own = 2;  // (WVG_DSD_STREAM=1: the DSD groups on a second stream whatever the budget)
+        }
+    }
+    const bool own_side = running && own > 1;
+    if (!b->lanes_env && nlanes > 1 && running) nlanes = own;
     // WVG_KERNEL_AUTO: in a context that has had batches in flight together, the lane
     // kernels (throughput) -- for kConcurrentHoldMs after a decode last found another
     // batch running; in one that decodes a batch at a time, a group of at most
@@ -1256,35 +1277,40 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
         return (lanes_now || nblocks > kAutoLaneMin) ? 1 : 0;
     };
     if (b->log_decodes)
-        fprintf(stderr, "wvg decode %p: groups %d, others running %d, streams %d, auto %d\n", (void *)b, n,
-                (int)running, nlanes < n ? nlanes : n, (int)b->kernel_auto);
+        fprintf(stderr, "wvg decode %p: groups %d, others running %d, streams %d, own %d, auto %d\n", (void *)b, n,
+                others, nlanes < n ? nlanes : n, (int)own_side, (int)b->kernel_auto);
     const int nl = n < nlanes ? n : nlanes;
     if (n <= nlanes) {
         for (int i = 0; i < n; i++) lane_of[used[i]] = i;
     } else {
         int64_t load[kSide] = {0};
         int first = 0;  // lanes before it are reserved for the DSD groups
-        // (one lane left for the PCM groups; with a single lane everything is on it)
-        for (int i = 0; i < n; i++)
-            if (used[i] == kDsd || used[i] == kDsd1) {
-                lane_of[used[i]] = first < nl - 1 ? first : 0;
-                if (first < nl - 1) first++;
-            }
+        // (DSD mode 3 first -- the batch's longest chains -- then mode 1, each while a lane
+        // is left for the rest; a DSD group without a lane of its own joins the PCM
+        // groups' pool, placed first; with a single lane everything is on it)
+        bool pooled[kSide] = {false};
+        for (int g : {kDsd, kDsd1})
+            for (int i = 0; i < n; i++)
+                if (used[i] == g) {
+                    if (first < nl - 1) lane_of[g] = first++;
+                    else pooled[g] = true;
+                }
         int pcm[kSide], np = 0;
         for (int i = 0; i < n; i++)
-            if (used[i] != kDsd && used[i] != kDsd1) pcm[np++] = used[i];
-        std::sort(pcm, pcm + np, [&](int x, int y) { return b->gframes[x] > b->gframes[y]; });
+            if ((used[i] != kDsd && used[i] != kDsd1) || pooled[used[i]]) pcm[np++] = used[i];
+        auto load_of = [&](int g) -> int64_t { return (g == kDsd || g == kDsd1) ? INT64_MAX / 4 : b->gframes[g]; };
+        std::sort(pcm, pcm + np, [&](int x, int y) { return load_of(x) > load_of(y); });
         for (int i = 0; i < np; i++) {
             int best = first;
             for (int l = first; l < nl; l++)
                 if (load[l] < load[best]) best = l;
             lane_of[pcm[i]] = best;
-            load[best] += b->gframes[pcm[i]];
+            load[best] += load_of(pcm[i]);
         }
     }
     hipStream_t side[kLanes - 1] = {nullptr};
     for (int l = 1; l < nl; l++) {
-        if (split_dsd) {  // (the batch's own side streams, not the context's shared ones)
+        if (own_side) {  // (the batch's own side streams, not the context's shared ones)
             if (!b->dstream[l - 1]) HIPCHK(c, hipStreamCreateWithFlags(&b->dstream[l - 1], hipStreamNonBlocking));
             side[l - 1] = b->dstream[l - 1];
         } else {
@@ -1526,7 +1552,8 @@ static int64_t exception_call_frame(const wvg_batch *b, const FileInfo &fi, cons
 // the status word a block contributes to the file result
 static uint32_t block_verdict(const wvg_batch *b, int64_t k) {
     const BlockDesc &d = b->fo.descs[(size_t)k];
-    uint32_t st = b->h_status[(size_t)k] & ~(uint32_t)ST_REDONE;  // (which kernel decoded it is not a result)
+    // (which kernel decoded it is not a result, nor is the poison bit of wvg_batch_poison)
+    uint32_t st = b->h_status[(size_t)k] & ~((uint32_t)ST_REDONE | (uint32_t)WVG_ST_UNWRITTEN);
     // a block decoded from state the device cannot see (only in malformed
     // files): the reference decodes garbage and its CRC check fails
     if ((st & ST_UNSUPPORTED) && d.nframes == d.block_samples) st |= ST_CRC_CHECKED | ST_CRC_ERROR;

@@ -78,7 +78,14 @@ __device__ __noinline__ void decode_chain(const BlockDesc *__restrict__ descs, u
             status[bi] = r;
             aux[bi] = exc;
         }
-        if (r & ST_EXCEPTION) break;
+        if (r & ST_EXCEPTION) {
+            // the members after it are never decoded (the reference stops here): their
+            // status is the framing's, as the upload stored it (a poisoned status --
+            // wvg_batch_poison's WVG_ST_UNWRITTEN -- must not survive the decode)
+            if (lead)
+                for (uint32_t j = k + 1; j < n; j++) status[head + j] = descs[head + j].fstatus;
+            break;
+        }
     }
 }
 

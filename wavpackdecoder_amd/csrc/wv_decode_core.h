@@ -1279,12 +1279,16 @@ WVF_HD DsdResult dsd_run(DsdState &S, const BlockDesc &d, int32_t *ptable, Store
         if (!mute) {
             for (uint32_t j = 0; j < n && chunk_ok; j++) {
                 int32_t v[2] = {0, 0};
+                bool past[2] = {false, false};
                 for (int c = 0; c < wch; c++) {
                     int code;
                     if (kind == KIND_DSD_RAW) {
-                        // (past the sub-block the reference leaves the caller's buffer as it
-                        // was: only a block continuing a consumed one gets there)
-                        if (bp >= dlen) res.status |= ST_NONDET;
+                        // (past the sub-block the reference clamps the count, DsdUtils.cs:73-82:
+                        // neither the caller's buffer nor the crc sees those values -- the
+                        // buffer keeps what it held; only a block continuing a consumed one
+                        // gets there)
+                        past[c] = bp >= dlen;
+                        if (past[c]) res.status |= ST_NONDET;
                         code = bp < dlen ? data[bp] : 0;
                         bp++;
                     } else if (kind == KIND_DSD_FAST) {
@@ -1361,16 +1365,19 @@ WVF_HD DsdResult dsd_run(DsdState &S, const BlockDesc &d, int32_t *ptable, Store
                         F[c][8] = sub32(F[c][8], add32(F[c][8], 512) >> 10);
                     }
                 }
-                for (int c = 0; c < wch; c++) crc = add32(crc, add32(shl32(crc, 1), v[c]));
+                for (int c = 0; c < wch; c++)
+                    if (!past[c]) crc = add32(crc, add32(shl32(crc, 1), v[c]));
                 uint64_t o = (uint64_t)(f + j) * och;
                 if (mono && !fstereo) {
-                    out.put(o, v[0]);
+                    if (!past[0]) out.put(o, v[0]);
                 } else if (fstereo) {
-                    out.put(o, v[0]);
-                    out.put(o + 1, v[0]);
+                    if (!past[0]) {
+                        out.put(o, v[0]);
+                        out.put(o + 1, v[0]);
+                    }
                 } else {
-                    out.put(o, v[0]);
-                    out.put(o + 1, v[1]);
+                    if (!past[0]) out.put(o, v[0]);
+                    if (!past[1]) out.put(o + 1, v[1]);
                 }
             }
             if (!chunk_ok) {
