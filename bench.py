@@ -194,6 +194,77 @@ def pmc_traffic(kernel_substr: str = "wv_pcm_2wave<17, 17>"):
 KERNEL_NAMES = {"lane": "wv_pcm_lane<false, 0, 17, 17>", "two_wave": "wv_pcm_2wave<17, 17>"}
 
 
+def c5_end_to_end(sets, slices) -> dict:
+    """C5 end to end on warm batches: per slice, host framing into the page-locked blob
+    (wvg_batch_add_files, the library's framing threads), the upload, the decode,
+    WavpackFormatSamples on the device and the PCM download into page-locked memory.
+    `serial`: one slice at a time, each phase timed (synchronised after each).
+    `pipelined`: one host thread per slice batch of the first copy set, two batches each
+    when a second copy exists (the next slice framed, uploaded and decoding before the
+    current one's format + download), every slice of the rank once; the wall time of
+    the whole pass.  Reported beside `value` (device-resident), never as it."""
+    import threading
+    bats = sets[0]
+    ph = {"framing": 0.0, "upload": 0.0, "decode": 0.0, "format_download": 0.0}
+    frames = 0
+    t_all = time.perf_counter()
+    for bb, sl in zip(bats, slices):
+        t0 = time.perf_counter()
+        bb.reset()
+        bb.add_files(sl)
+        t1 = time.perf_counter()
+        bb.upload()
+        t2 = time.perf_counter()
+        bb.decode()
+        bb.sync()
+        t3 = time.perf_counter()
+        bb.format()
+        bb.download_pcm(pinned=True)
+        t4 = time.perf_counter()
+        for k, v in zip(ph, (t1 - t0, t2 - t1, t3 - t2, t4 - t3)):
+            ph[k] += v
+        frames += bb.frames
+    t_serial = time.perf_counter() - t_all
+    pcm_bytes = sum(int(bb._L.wvg_batch_pcm_bytes(bb._b)) for bb in bats)
+    in_bytes = sum(bb.bytes_in for bb in bats)
+    # pipelined: thread i serves slices i, i + T, ... with its one or two batches
+    T = len(bats)
+    spare = sets[1] if len(sets) > 1 else [None] * T
+
+    def serve(i):
+        mine = list(range(i, len(slices), T))
+        pair = (bats[i], spare[i]) if spare[i] is not None else (bats[i],)
+
+        def start(b, j):
+            b.reset()
+            b.add_files(slices[j])
+            b.upload()
+            b.decode()
+        start(pair[0], mine[0])
+        for k, j in enumerate(mine):
+            if k + 1 < len(mine) and len(pair) > 1:
+                start(pair[(k + 1) % 2], mine[k + 1])
+            cur = pair[k % len(pair)]
+            cur.format()
+            cur.download_pcm(pinned=True)
+            if k + 1 < len(mine) and len(pair) == 1:
+                start(pair[0], mine[k + 1])
+    th = [threading.Thread(target=serve, args=(i,)) for i in range(T)]
+    t0 = time.perf_counter()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    t_pipe = time.perf_counter() - t0
+    return {"frames": int(frames), "compressed_bytes": int(in_bytes), "pcm_bytes": int(pcm_bytes),
+            "serial": {"Msamples_s": round(frames / t_serial / 1e6, 1), "ms": round(t_serial * 1e3, 2),
+                       "phase_ms": {k: round(v * 1e3, 2) for k, v in ph.items()}},
+            "pipelined": {"Msamples_s": round(frames / t_pipe / 1e6, 1), "ms": round(t_pipe * 1e3, 2),
+                          "threads": T, "batches_per_thread": 2 if len(sets) > 1 else 1},
+            "what": "warm batches: host framing (wvg_batch_add_files) + upload + decode + device "
+                    "WavpackFormatSamples + PCM download into page-locked memory, every slice once"}
+
+
 # C5: batches in flight the copies aim at (each batch takes up to 3 streams while others
 # run, within the process's hardware queues: wv_api.cpp wvg_batch_decode)
 C5_BATCHES_IN_FLIGHT = 8
@@ -513,13 +584,14 @@ def run_rank(args) -> None:
         cpu = None
         if multi and rank == 0 and not args.no_cpu:
             cpu = cpu_baseline_c5(files, args.cpu_threads)
+        e2e5 = c5_end_to_end(sets, slices) if multi and args.c5_e2e else None
         if rank == 0:
             line = {"metric": METRIC, "value": round(value, 2), "unit": "Msamples/s", "n_gpus": ws,
                     "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
                     "higher_is_better": True, "scaling": scaling, "dtype": "int32",
                     "data": "synthetic (repo encoder; C5 seeds per file index)",
                     "config": {"workload": workload, "files_rank0": len(files), "slices_rank0": len(slices),
-                               "blocks_rank0": sum(bb.num_blocks for bb in batches), "frames_rank0": int(frames_rank),
+                               "blocks_rank0": sum(bb.num_blocks for bb in sets[0]), "frames_rank0": int(frames_rank),
                                "frames_total": int(frames_total),
                                "parallelism": f"file-shard x{ws}, no collectives"},
                     "kernel_ms": round(kernel_ms, 4), "per_rank_kernel_ms": [round(x, 4) for x in kms_all],
@@ -528,6 +600,7 @@ def run_rank(args) -> None:
                     "kernel": args.kernel, "verified": ver,
                     "cpu_baseline": cpu}
             if multi:
+                line["end_to_end"] = e2e5
                 line["vs_cpu"] = None if cpu is None else {
                     "measured": round(value / cpu["value"], 2),
                     "per_gpu_vs_socket_scaled": round(value / ws / cpu["socket_scaled"], 2)}
@@ -738,6 +811,8 @@ def main():
     ap.add_argument("--c5-files", type=int, default=4000)
     ap.add_argument("--c5-batch", type=int, default=12500,
                     help="C5: files per batch; a rank with more files decodes all its batches every step")
+    ap.add_argument("--c5-e2e", type=int, default=1,
+                    help="C5: also time the end-to-end pass (framing, upload, decode, format, download)")
     ap.add_argument("--c5-share", default=None,
                     help="C5: N:r -- decode rank r's share of an N-way file split (one process)")
     ap.add_argument("--c5-copies", type=int, default=0,

@@ -6,9 +6,9 @@ profiles/<tag>_pmc.json: per-launch HBM bytes of the bench kernel from the
 separate FETCH_SIZE / WRITE_SIZE passes (unit KiB).  MI355X_MICROARCH.md: on
 gfx950 FETCH_SIZE counts half the bytes of 16-B-per-lane vector streaming reads
 and other widths are uncalibrated.  The bench kernel reads its payload with
-scalar s_load_dwordx2 (no vector reads), and the raw FETCH_SIZE equals the
-known bytes it must read (compressed payload + block descriptors, each read
-once) -- so the scale is 1 (FETCH_SCALE=2 for the old dwordx4 LDS staging).
+scalar s_load_dwordx2 for the two-wave kernel (scale 1: the raw FETCH_SIZE equals
+the known bytes it must read) and global_load_dwordx4 for the lane kernels' LDS
+staging (FETCH_SCALE=2, the guide's gfx950 correction for 16-B-per-lane reads).
 bench.py reports `roofline.traffic` from it.
 usage: [FETCH_SCALE=1] python scripts/pmc_to_profile.py <tag> [kernel-substring]
 """
@@ -44,6 +44,12 @@ stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(dst, f"{tag}_ker
 st = next(v for k, v in stats.items() if kern in k)
 fetch_kib = sum(fetch) / len(fetch)
 scale = float(os.environ.get("FETCH_SCALE", "1"))
+NOTE_X1 = ("FETCH_SIZE/WRITE_SIZE in KiB. Payload read by scalar s_load_dwordx2 (the two-wave kernel): raw FETCH_SIZE "
+           "calibrated against the known read bytes (compressed payload + block descriptors) -> scale 1; WRITE from "
+           "dword-per-lane stores equals the int32 output byte count")
+NOTE_X2 = ("FETCH_SIZE/WRITE_SIZE in KiB. Payload read by global_load_dwordx4 (16 B per lane: the lane kernels' LDS "
+           "staging), which gfx950's FETCH_SIZE counts at half (MI355X_MICROARCH.md) -> scale 2; WRITE from "
+           "dword-per-lane stores equals the int32 output byte count")
 write_kib = sum(write) / len(write)
 out = {
     "kernel": name,
@@ -54,9 +60,7 @@ out = {
     "fetch_bytes_per_launch": fetch_kib * 1024 * scale,
     "write_bytes_per_launch": write_kib * 1024,
     "traffic_bytes_per_launch": fetch_kib * 1024 * scale + write_kib * 1024,
-    "note": os.environ.get("PMC_NOTE", "FETCH_SIZE/WRITE_SIZE in KiB. Payload read by scalar s_load_dwordx2: raw "
-            "FETCH_SIZE calibrated against the known read bytes (compressed payload + 1,392-B block descriptors) -> "
-            "scale 1; WRITE from dword-per-lane stores equals the int32 output byte count"),
+    "note": os.environ.get("PMC_NOTE", NOTE_X2 if scale == 2 else NOTE_X1),
 }
 with open(os.path.join(dst, f"{tag}_pmc.json"), "w") as f:
     json.dump(out, f, indent=1)

@@ -1,12 +1,13 @@
 """GPU: BASELINE config 5 at its own size -- the 100,000-file mixed corpus on one GPU
-(VERDICT r04 "Next round" #6).  Runs only when asked (WVG_C5_FULL=<files>, e.g. 100000:
-the corpus takes minutes to generate), so the round-end `pytest -m gpu` skips it.
+(VERDICT r05 "Next round" #3: in the driver's run by default; WVG_C5_FULL=<files> picks
+another size, 0 skips it).
 
-The files are decoded as bench.py's C5 workload decodes them: slices of 4,000 files, one
-batch each, every batch issued before any finishes (WVG_KERNEL_AUTO: the lane kernels
-once batches overlap).  Every file must decode with no CRC error and no exception, and
-an evenly spaced sample of files (WVG_C5_SAMPLE, default 3,000, plus every DSD mode-1
-and mode-3 file among the first 20,000) must equal the oracle bit for bit.  Reference:
+The files are decoded as bench.py's C5 workload decodes them at N = 1: slices of 12,500
+files, one batch each, every batch issued before any finishes (WVG_KERNEL_AUTO: the lane
+kernels once batches overlap; each batch's launch groups on streams of its own within the
+hardware-queue budget).  Every file must decode with no CRC error and no exception, and
+an evenly spaced sample of files (WVG_C5_SAMPLE, default 3,000, plus every DSD mode-1 and
+mode-3 file among the first 20,000) must equal the oracle bit for bit.  Reference:
 WavPackUtils.cs:200-282 per file."""
 import json
 import os
@@ -16,18 +17,18 @@ import numpy as np
 import pytest
 
 from oracle import oracle as O
-from wavpackdecoder_amd._lib import WVG_ST_REDONE, WVG_ST_TIMEOUT
+from wavpackdecoder_amd._lib import WVG_ST_REDONE, WVG_ST_TIMEOUT, WVG_ST_UNWRITTEN
 
-pytestmark = [pytest.mark.gpu,
-              pytest.mark.skipif(not os.environ.get("WVG_C5_FULL"), reason="WVG_C5_FULL=<files> runs the full corpus")]
+N_FILES = int(os.environ.get("WVG_C5_FULL", "100000"))
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(N_FILES <= 0, reason="WVG_C5_FULL=0")]
 
 
 @pytest.mark.timeout(1500)
 def test_c5_full_corpus_one_gpu():
     from synth import corpora
     from wavpackdecoder_amd.api import DecodeBatch
-    n = int(os.environ["WVG_C5_FULL"])
-    per = 4000
+    n = N_FILES
+    per = int(os.environ.get("WVG_C5_BATCH", "12500"))
     t0 = time.perf_counter()
     files = corpora.c5_files(range(n), progress=True)
     t_gen = time.perf_counter() - t0
@@ -58,6 +59,7 @@ def test_c5_full_corpus_one_gpu():
     for k, b in enumerate(batches):
         out = b.download()
         st = b.block_status()
+        assert not np.any(st & WVG_ST_UNWRITTEN)
         redone += int(np.count_nonzero(st & WVG_ST_REDONE))
         blocks += int(st.size)
         for i in range(len(b.infos)):

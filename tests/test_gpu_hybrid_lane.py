@@ -105,3 +105,55 @@ def test_hybrid_lanes_chunks(chunk):
     # the caller's chunk schedule does not change a block's words (crc / mute at the block end)
     files = [_hy(9000, 61, block=4000), _hy(9000, 62, flt=True, block=3000)]
     _check(files, [f"chunk{chunk}#{k}" for k in range(len(files))], chunk)
+
+
+def _enc(x, nch=2, **kw):
+    p = dict(terms=S.TERMS_DEFAULT if nch == 2 else S.TERMS_MONO_HIGH, block_samples=4000, nch=nch)
+    p.update(kw)
+    return S.encode_pcm(x, S.EncParams(**p))
+
+
+def test_hybrid_lanes_without_bitrate():
+    """Hybrid blocks without HYBRID_BITRATE (error limit exp2s(bitrate) alone, WordsUtils.cs:209,
+    256-258) on the lanes: stereo on the default list (kHyDefault) and on run-time lists, mono;
+    16 / 24 bit and float; bitrates 1 to 8 bits per sample."""
+    files, names = [], []
+    for k in range(24):
+        bits = 24 if k % 3 == 1 else 16
+        flt = k % 3 == 2
+        nch = 1 if k % 4 == 3 else 2
+        x = S.audio_like(int(3000 + 700 * k), nch, bits, seed=900 + k, kind="noise" if k % 5 == 4 else "music")
+        terms = (S.TERMS_DEFAULT, S.TERMS_HIGH, S.TERMS_FAST)[k % 3] if nch == 2 else S.TERMS_MONO_HIGH[: 5 + k % 3]
+        kw = dict(terms=terms, hybrid=True, hybrid_bitrate=False, bitrate_x256=256 + 96 * k)
+        if flt:
+            files.append(_enc(S.float_mantissas(x.astype(np.float32) / 32768.0), nch, bytes_per_sample=4,
+                              float_data=True, **kw))
+        else:
+            files.append(_enc(x, nch, bytes_per_sample=bits // 8, **kw))
+        names.append(f"nobr#{k}_{'f' if flt else bits}_{nch}ch")
+    st = _check(files, names)
+    assert int(np.count_nonzero(st & WVG_ST_REDONE)) <= max(1, len(st) // 20)
+
+
+def test_int32_blocks_on_lanes():
+    """INT32_DATA blocks without a wvx stream: hybrid (fixup_tail: zeros / ones / dups, or the
+    sent_bits shift, then the 4-byte clip; UnpackUtils.cs:1318-1393) on the hybrid lanes, and
+    lossless ones whose fixup is a shift (sent_bits) on the lossless lanes."""
+    from tests import vectors as V
+    x = S.audio_like(9000, 2, 16, seed=77)
+    m = S.audio_like(9000, 1, 16, seed=78)
+    files, names = [], []
+    for k, lay in enumerate((dict(zeros=3), dict(ones=2), dict(dups=4), dict(sent_bits=5), dict(sent_bits=9))):
+        y = S.int32_layout(x, seed=80 + k, **lay)
+        kw = {("int32_" + a): v for a, v in lay.items()}
+        for br in (True, False):
+            files.append(_enc(y, bytes_per_sample=4, hybrid=True, hybrid_bitrate=br, bitrate_x256=700, **kw))
+            names.append(f"int32_hy_{list(lay)[0]}_br{int(br)}")
+        ym = S.int32_layout(m, seed=90 + k, **lay)
+        files.append(_enc(ym, nch=1, bytes_per_sample=4, hybrid=True, hybrid_bitrate=True, bitrate_x256=700, **kw))
+        names.append(f"int32_hy_mono_{list(lay)[0]}")
+    for k, sb in enumerate((4, 11)):  # lossless, the fixup a shift (no wvx: its bits are lost)
+        files.append(V.int32_file(x, sent_bits=sb, seed=95 + k))
+        names.append(f"int32_ll_sent{sb}")
+    st = _check(files, names)
+    assert int(np.count_nonzero(st & WVG_ST_REDONE)) <= max(1, len(st) // 20)

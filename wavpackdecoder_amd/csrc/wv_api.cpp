@@ -1276,6 +1276,9 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
         if (!b->kernel_auto) return b->lane_mode;
         return (lanes_now || nblocks > kAutoLaneMin) ? 1 : 0;
     };
+    // (WVG_DSD3_WAVE=1: DSD mode 3 on the wave-per-block kernel whatever the PCM groups use -- A/B)
+    static const bool dsd3_wave = getenv("WVG_DSD3_WAVE") && getenv("WVG_DSD3_WAVE")[0] == '1';
+    const int dsd3_mode = dsd3_wave ? 0 : mode_of(b->dsd_list.size() - b->dsd_high_lo);
     if (b->log_decodes)
         fprintf(stderr, "wvg decode %p: groups %d, others running %d, streams %d, own %d, auto %d\n", (void *)b, n,
                 others, nlanes < n ? nlanes : n, (int)own_side, (int)b->kernel_auto);
@@ -1350,7 +1353,7 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
     };
     HIPCHK(c, launch_decode(b->d_descs, b->d_pcml, (uint32_t)b->pcm_list.size(), b->d_dsd, (uint32_t)b->dsd_list.size(),
                             b->dsd_fast_lo, b->dsd_fast_n, b->d_blob, b->d_tables, b->d_out, b->d_status, b->d_mute,
-                            slot(kPcm), slot(kDsd), slot(kDsd1), mode_of(b->dsd_list.size() - b->dsd_high_lo),
+                            slot(kPcm), slot(kDsd), slot(kDsd1), dsd3_mode,
                             b->dsd_high_lo, b->dsd_high_mono, mode_of(b->dsd_fast_n), b->dsd_fast_mono,
                             // (.wvc blocks: the lane kernel even alone -- 35.8 against the generic
                             // kernel's 130 ms for C4's 1,024 blocks, profiles/r05_c4wvc_rates.jsonl)
@@ -1360,7 +1363,7 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
         for (int t = 0; t < kMaxTermSets; t++)
             if (!b->ts_list[t].empty() && mode_of(b->ts_list[t].size())) m |= 1u << t;
         if (b->pcm_wvc_n && (b->kernel_auto || b->lane_mode)) m |= 1u << kPcm;
-        if (b->dsd_list.size() > b->dsd_high_lo && mode_of(b->dsd_list.size() - b->dsd_high_lo)) m |= 1u << kDsd;
+        if (b->dsd_list.size() > b->dsd_high_lo && dsd3_mode) m |= 1u << kDsd;
         if (b->dsd_fast_n && mode_of(b->dsd_fast_n)) m |= 1u << kDsd1;
         b->lane_groups = m;
     }

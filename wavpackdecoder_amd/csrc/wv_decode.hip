@@ -1295,10 +1295,10 @@ int term_set_of(const BlockDesc &d, int prefer_pipe) {
         }
         if (ok) {
             if (d.flags & HYBRID_FLAG) {
-                // hybrid: stereo default-list blocks with HYBRID_BITRATE on their own lane kernel
-                // (kHyDefault), every other one with the run-time list lanes (or the pipelined kernel)
-                const uint32_t hy = d.flags & (HYBRID_FLAG | HYBRID_BITRATE | INT32_DATA);
-                if (s == 1 && !mono && hy == (HYBRID_FLAG | HYBRID_BITRATE)) return kHyDefault;
+                // hybrid: stereo default-list blocks on their own lane kernel (kHyDefault; with or
+                // without HYBRID_BITRATE, integer, float or int32 without wvx), every other one
+                // with the run-time list lanes (or the pipelined kernel)
+                if (s == 1 && !mono) return kHyDefault;
                 return pipe;
             }
             return s;

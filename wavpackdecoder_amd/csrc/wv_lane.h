@@ -384,6 +384,7 @@ struct LState {
     uint32_t bad;
     uint32_t bad0;   // (diagnostics) the reasons of the first group that set any: status bits 24-31
     uint32_t bal;    // hybrid stereo with HYBRID_BALANCE: ~0 (lhy_errlim), else 0
+    uint32_t nobr;   // hybrid without HYBRID_BITRATE: ~0 (the error limit is exp2s(bitrate) alone), else 0
     // hybrid words (HYBRID_FLAG | HYBRID_BITRATE): slow_level, bitrate_acc/delta, error limit per channel
     int32_t slow[2];
     int64_t acc[2], dlt[2];
@@ -485,11 +486,13 @@ __device__ __forceinline__ int32_t lexp2s_pos(int32_t L, const uint8_t *ring, ui
     bad |= ((uint32_t)L - 0x1700u < 0x80000100u - 0x1700u) ? 2u : 0u;
     return L > 0 ? (int32_t)((v << (e & 31u)) >> 9) : 0;
 }
-// update_error_limit (WordsUtils.cs:195-261; HYBRID_BITRATE): before the first word of a
-// frame, in lanes where that word is not a zero-run zero.  Stereo with HYBRID_BALANCE
-// (:222-241) moves bitrate between the channels by their slow levels (a wave-uniform branch:
-// some lane balances); mono and false stereo (:199-209) use channel 0 alone -- the lane
-// computes channel 1 too, unused (its descriptor values are zero)
+// update_error_limit (WordsUtils.cs:195-261): before the first word of a frame, in lanes
+// where that word is not a zero-run zero.  HYBRID_BITRATE: exp2s(slow_log - bitrate + 0x100);
+// stereo with HYBRID_BALANCE (:222-241) moves bitrate between the channels by their slow
+// levels (a wave-uniform branch: some lane balances).  Without HYBRID_BITRATE (s.nobr):
+// exp2s(bitrate) (:209, :256-258) -- a negative bitrate (the reference's exp2s of a negative:
+// a negative error limit) hands the block back.  Mono and false stereo (:199-209) use
+// channel 0 alone -- the lane computes channel 1 too, unused (its descriptor values are zero)
 __device__ __forceinline__ void lhy_errlim(LState &s, const uint8_t *ring, bool apply) {
     using namespace wvf;
     int64_t acc[2];
@@ -510,7 +513,9 @@ __device__ __forceinline__ void lhy_errlim(LState &s, const uint8_t *ring, bool 
     }
 #pragma unroll
     for (int c = 0; c < 2; c++) {
-        const int32_t el = lexp2s_pos(add32(sub32(sl[c], br[c]), 0x100), ring, s.bad);
+        const int32_t L = s.nobr ? br[c] : add32(sub32(sl[c], br[c]), 0x100);
+        s.bad |= s.nobr & ((uint32_t)br[c] >> 30) & 2u;  // (bit 31: a negative bitrate)
+        const int32_t el = lexp2s_pos(L, ring, s.bad);
         s.acc[c] = apply ? acc[c] : s.acc[c];
         s.el[c] = apply ? el : s.el[c];
     }
@@ -1353,16 +1358,34 @@ __device__ __forceinline__ void rgroup_rt(RChain<NS> &ch, const LShared &shr, ui
 template <int HY, int... Ts>
 constexpr bool lane_codes() { return !HY && (LaneRt<Ts...>::NS ? LaneRt<Ts...>::NS : (int)sizeof...(Ts)) <= 5; }
 
+// the lossless lanes' fixup shift (UnpackUtils.cs:1251-1404): the header's, plus an int32
+// block's zeros + sent_bits + ones + dups when those reduce to a shift (:1344-1345)
+__device__ __forceinline__ uint32_t lane_shift(const BlockDesc &d) {
+    int32_t sh = d.shift;
+    if (d.flags & wvf::INT32_DATA) sh += d.int32_zeros + d.int32_sent_bits + d.int32_ones + d.int32_dups;
+    return (uint32_t)sh & 31u;
+}
+
 // can this lane decode block d exactly (else ST_REDO)?
 template <bool MONO, int HY, int... Ts>
 __device__ __forceinline__ bool lane_ok(const BlockDesc &d) {
     using namespace wvf;
     if (d.kind != KIND_PCM) return false;
-    if constexpr (HY) {  // hybrid with HYBRID_BITRATE (HYBRID_BALANCE too); integer or float (float_values)
-        static_assert(!MONO || HY == 1, "hybrid .wvc lanes: stereo");
+    if constexpr (HY == 2) {  // hybrid with its .wvc stream: HYBRID_BITRATE (HYBRID_BALANCE too), not int32
+        static_assert(!MONO, "hybrid .wvc lanes: stereo");
         if ((d.flags & (HYBRID_FLAG | HYBRID_BITRATE | INT32_DATA)) != (HYBRID_FLAG | HYBRID_BITRATE)) return false;
-    } else if (d.flags & (HYBRID_FLAG | FLOAT_DATA | INT32_DATA)) {
+    } else if constexpr (HY) {
+        // hybrid, with or without HYBRID_BITRATE (and HYBRID_BALANCE); integer, float (float_values)
+        // or int32 without a wvx stream (fixup_tail: zeros / ones / dups, or the shift, then the clip)
+        if (!(d.flags & HYBRID_FLAG) || (d.wvx_state & 0x100)) return false;
+    } else if (d.flags & (HYBRID_FLAG | FLOAT_DATA)) {
         return false;
+    } else if (d.flags & INT32_DATA) {
+        // lossless int32 without a wvx stream whose fixup is a shift (UnpackUtils.cs:1318-1345:
+        // sent_bits or no zeros / ones / dups -- lane_shift); the wvx read and the zeros / ones /
+        // dups map go to the two-wave / generic kernels
+        if ((d.wvx_state & 0x100) || (d.int32_sent_bits == 0 && (d.int32_zeros | d.int32_ones | d.int32_dups) != 0))
+            return false;
     }
     if (((d.flags & MONO_DATA) != 0) != MONO) return false;
     if ((d.wvc_len != 0) != (HY == 2)) return false;  // HY 2: hybrid blocks with their .wvc stream
@@ -1502,7 +1525,8 @@ __device__ __forceinline__ void lane_parser(const BlockDesc *__restrict__ descs,
     s.slack = 0;
     s.bad = 0u;
     s.bad0 = 0u;
-    s.bal = (HY && !MONO && (d.flags & HYBRID_BALANCE)) ? ~0u : 0u;
+    s.nobr = (HY && !(d.flags & HYBRID_BITRATE)) ? ~0u : 0u;
+    s.bal = (HY && !MONO && (d.flags & HYBRID_BALANCE) && !s.nobr) ? ~0u : 0u;
 #pragma unroll
     for (int c = 0; c < 2; c++) {
 #pragma unroll
@@ -1612,7 +1636,7 @@ __device__ __forceinline__ void lane_recon(const BlockDesc *__restrict__ descs, 
     const bool fst = (d.flags & FALSE_STEREO) != 0;
     if (lb.inl && !lb.ok) status[lb.bi] = ST_REDO | (1u << 16);
     const bool joint = (d.flags & JOINT_STEREO) != 0;
-    const uint32_t sh_ = (uint32_t)d.shift & 31u;
+    const uint32_t sh_ = lane_shift(d);
     const int32_t ml = d.mute_limit;
     int32_t *o = out + d.out_off;
     constexpr int NS = LaneRt<Ts...>::NS;
@@ -1756,7 +1780,7 @@ __device__ __forceinline__ void lane_recon_split(const BlockDesc *__restrict__ d
         const bool fst = (d.flags & FALSE_STEREO) != 0;
         if (lb.inl && !lb.ok) status[lb.bi] = ST_REDO | (1u << 16);
         const bool joint = (d.flags & JOINT_STEREO) != 0;
-        const uint32_t sh_ = (uint32_t)d.shift & 31u;
+        const uint32_t sh_ = lane_shift(d);
         int32_t *o = out + d.out_off;
         Fixup fx;
         if constexpr (HY) fixup_init(fx, d);
