@@ -327,23 +327,43 @@ def test_poison_then_decode_stores_every_status(gpu_batch_cls):
     must store every block's status -- including the members of a sticky-state chain
     after a block that raises the reference's exception, which are never decoded
     (decode_chain gives them back the framing's status) -- and produce the same
-    output, statuses and file results as a decode of the unpoisoned batch."""
-    from wavpackdecoder_amd._lib import WVG_ST_UNWRITTEN
+    statuses, file results and output as a decode of the unpoisoned batch (the output
+    over each file's defined frames: up to the call that throws, and nothing of a file
+    whose output reads the caller's stale buffer, WVG_ST_NONDET)."""
+    from wavpackdecoder_amd._lib import WVG_ST_NONDET, WVG_ST_UNWRITTEN
     sticky = [c[1] for c in V.sticky_cases()]
     files = sticky + [V.corrupt(f, 700 + k, nflips=6) for k, f in enumerate(sticky)]
     b = gpu_batch_cls(4096)
     idx = [b.add_file(f) for f in files]
     b.decode()
     out0, st0 = b.download().copy(), b.block_status().copy()
-    res0 = [(r.frames, r.crc_errors, r.exception, r.status_or) for r in (b.result(i) for i in idx if i >= 0)]
+
+    def results():
+        rs = []
+        for i in idx:
+            if i < 0:
+                continue
+            r = b.result(i)
+            rs.append((r.frames, r.crc_errors, r.exception, r.exception_frame, r.status_or))
+        return rs
+    res0 = results()
     b.poison(0x7F)
     b.decode()
     out1, st1 = b.download(), b.block_status()
-    res1 = [(r.frames, r.crc_errors, r.exception, r.status_or) for r in (b.result(i) for i in idx if i >= 0)]
+    res1 = results()
+    infos = [b.infos[i] for i in idx if i >= 0]
     b.close()
     assert not np.any(st1 & WVG_ST_UNWRITTEN)
     np.testing.assert_array_equal(st1, st0)
-    np.testing.assert_array_equal(out1, out0)
     assert res1 == res0
-    assert all(not (r[3] & WVG_ST_UNWRITTEN) for r in res1)
+    assert all(not (r[4] & WVG_ST_UNWRITTEN) for r in res1)
     assert sum(r[2] for r in res0) >= 1, "no file raised the reference's exception: the chain case is not exercised"
+    compared = 0
+    for r, info in zip(res1, infos):
+        if r[4] & WVG_ST_NONDET:
+            continue
+        n = (r[3] if r[2] else r[0]) * info.reduced_channels
+        a, z = info.out_offset, info.out_offset + n
+        np.testing.assert_array_equal(out1[a:z], out0[a:z])
+        compared += 1
+    assert compared >= len(res1) // 2

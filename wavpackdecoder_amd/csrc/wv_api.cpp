@@ -32,6 +32,7 @@ hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, ui
                         int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s, int lane_mode,
                         const uint32_t *lane_list, uint32_t lane_n, uint32_t *lane_dbg);
 hipError_t launch_format(const FormatSeg *segs, uint32_t nseg, const int32_t *in, uint8_t *out, int dsd, hipStream_t s);
+hipError_t launch_zero_fill(const ZeroSeg *segs, uint32_t nseg, int32_t *out, hipStream_t s);
 hipError_t upload_dsd_ptables();
 hipError_t launch_dsd_fill(const BlockDesc *descs, const uint32_t *dsd_list, uint32_t n_dsd, uint32_t *status,
                            const uint32_t *aux, int32_t *out, hipStream_t s);
@@ -209,6 +210,9 @@ struct wvg_batch {
     MetaItem *d_items = nullptr;  // deferred metadata values (wv_meta.h), applied once per upload
     MetaJob *d_jobs = nullptr;
     FormatSeg *d_segs = nullptr;
+    ZeroSeg *d_zeros = nullptr;  // the framing's gap zero-fills (FramingOutput::zeros), written by each decode
+    size_t cap_zeros = 0;
+    uint32_t nzeros = 0;
     int32_t *d_out = nullptr;
     uint32_t *d_status = nullptr, *d_mute = nullptr, *d_pcml = nullptr, *d_dsd = nullptr;
     bool uploaded = false, downloaded = false, formatted = false;
@@ -374,6 +378,7 @@ static void free_dev(wvg_batch *b) {
     hipFree(b->d_items);
     hipFree(b->d_jobs);
     hipFree(b->d_segs);
+    hipFree(b->d_zeros);
     hipFree(b->d_out);
     hipFree(b->d_status);
     hipFree(b->d_mute);
@@ -407,6 +412,8 @@ static void free_dev(wvg_batch *b) {
     b->d_items = nullptr;
     b->d_jobs = nullptr;
     b->d_segs = nullptr;
+    b->d_zeros = nullptr;
+    b->cap_zeros = 0;
     b->d_out = nullptr;
     b->d_status = b->d_mute = b->d_pcml = b->d_dsd = nullptr;
     b->cap_blob = b->cap_descs = b->cap_items = b->cap_jobs = b->cap_tables = b->cap_out = b->cap_st = 0;
@@ -665,6 +672,10 @@ static int merge_framed(wvg_batch *b, FramingOutput &f, FileInfo &fi, size_t len
     if (!f.tables.empty()) {
         b->fo.tables.resize(t0);
         b->fo.tables.insert(b->fo.tables.end(), f.tables.begin(), f.tables.end());
+    }
+    for (ZeroSeg z : f.zeros) {
+        z.off += ob;
+        b->fo.zeros.push_back(z);
     }
     fi.first_desc += d0;
     return commit_file(b, fi, len, info, at);
@@ -1138,6 +1149,11 @@ int wvg_batch_upload(wvg_batch *b) {
     HIPCHK(c, ensure(b->d_pcml, b->cap_pcml, sizeof(uint32_t) * (np ? np : 1)));
     HIPCHK(c, ensure(b->d_dsd, b->cap_dsd, sizeof(uint32_t) * (ns ? ns : 1)));
     HIPCHK(c, put(b->d_pcml, b->pcm_list.data(), sizeof(uint32_t) * np));
+    b->nzeros = (uint32_t)b->fo.zeros.size();
+    if (b->nzeros) {
+        HIPCHK(c, ensure(b->d_zeros, b->cap_zeros, sizeof(ZeroSeg) * b->nzeros));
+        HIPCHK(c, put(b->d_zeros, b->fo.zeros.data(), sizeof(ZeroSeg) * b->nzeros));
+    }
     HIPCHK(c, put(b->d_dsd, b->dsd_list.data(), sizeof(uint32_t) * ns));
     for (int t = 0; t < kMaxTermSets; t++) {
         const std::vector<uint32_t> &L = b->ts_list[t], &LL = b->ts_lane[t];
@@ -1329,6 +1345,8 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
             if (used[i] == g) return lane(lane_of[g]);
         return s;  // (an empty group launches nothing)
     };
+    // the gap zero-fills (WavPackUtils.cs:227-251) are part of the decode's output
+    if (b->nzeros) HIPCHK(c, launch_zero_fill(b->d_zeros, b->nzeros, b->d_out, s));
     if (nl > 1) {
         HIPCHK(c, hipEventRecord(b->fork, s));
         for (int l = 1; l < nl; l++) HIPCHK(c, hipStreamWaitEvent(lane(l), b->fork, 0));

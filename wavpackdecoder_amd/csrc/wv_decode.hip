@@ -1488,6 +1488,18 @@ hipError_t launch_meta(BlockDesc *descs, const MetaJob *jobs, uint32_t njobs, co
     return hipGetLastError();
 }
 
+// the gap zero-fills of a decode (ZeroSeg, wv_framing.h): one workgroup per segment
+__global__ void __launch_bounds__(256) wv_zero_fill(const ZeroSeg *__restrict__ segs, int32_t *__restrict__ out) {
+    const ZeroSeg z = segs[blockIdx.x];
+    for (uint64_t i = threadIdx.x; i < z.n; i += 256) out[z.off + i] = 0;
+}
+
+hipError_t launch_zero_fill(const ZeroSeg *segs, uint32_t nseg, int32_t *out, hipStream_t s) {
+    if (!nseg) return hipSuccess;
+    hipLaunchKernelGGL(wv_zero_fill, dim3(nseg), dim3(256), 0, s, segs, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_format(const FormatSeg *segs, uint32_t nseg, const int32_t *in, uint8_t *out, int dsd, hipStream_t s) {
     if (!nseg) return hipSuccess;
     hipLaunchKernelGGL(wv_format_pcm, dim3(nseg), dim3(256), 0, s, segs, in, out, dsd);

@@ -153,4 +153,13 @@ struct FormatSeg {
     uint32_t bps;      // bytes per sample of the file (WavpackGetBytesPerSample)
 };
 
+// An output range the reference zero-fills itself: a gap between the frames already
+// returned and the next block's first frame (WavPackUtils.cs:227-251).  The framing
+// records it (FramingOutput::zeros) and every decode writes it (wv_zero_fill), so a
+// decode's output never depends on the buffer's earlier contents.
+struct ZeroSeg {
+    uint64_t off;  // first int
+    uint64_t n;    // ints
+};
+
 }  // namespace wvg

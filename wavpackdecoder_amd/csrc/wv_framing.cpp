@@ -1290,9 +1290,12 @@ void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t ou
                 Hdr &hh = F.wphdr;
                 if (hh.block_samples == 0 || !(hh.flags & INITIAL_BLOCK) || F.sample_index >= hh.block_index + hh.block_samples)
                     continue;
-                if (F.sample_index < hh.block_index) {  // gap: zero fill (output is pre-zeroed)
+                if (F.sample_index < hh.block_index) {  // gap: zero fill (the decode writes it, ZeroSeg)
                     int64_t n = hh.block_index - F.sample_index;
                     if (n > samples) n = samples;
+                    // (a fill that runs past the caller's buffer throws below, and the call returns nothing)
+                    if (!disc_call && n > 0 && buf_idx + n * nch <= (int64_t)chunk * nch)
+                        out.zeros.push_back({out_base_ints + (uint64_t)((out_frames + unpacked) * nch), (uint64_t)(n * nch)});
                     F.sample_index += n;
                     unpacked += n;
                     samples -= n;

@@ -50,6 +50,7 @@ struct FileInfo {
 
 // DSD fast/high tables live in a side area (bytes) appended per block.
 struct FramingOutput {
+    std::vector<ZeroSeg> zeros;   // gap zero-fills (ZeroSeg)
     std::vector<BlockDesc> descs;
     std::vector<uint8_t> tables;  // DSD tables (see BlockDesc::dsd_table_off)
     // defer_values: the decorr weight/sample and entropy/hybrid values are left
