@@ -1066,7 +1066,8 @@ int wvg_batch_upload(wvg_batch *b) {
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     size_t need = al(sizeof(BlockDesc) * nd) + al(sizeof(MetaItem) * b->fo.items.size()) +
                   al(sizeof(MetaJob) * b->fo.jobs.size()) + al(b->fo.tables.size()) + al(sizeof(uint32_t) * (nd + 1)) +
-                  al(sizeof(uint32_t) * b->pcm_list.size()) + al(sizeof(uint32_t) * b->dsd_list.size());
+                  al(sizeof(uint32_t) * b->pcm_list.size()) + al(sizeof(uint32_t) * b->dsd_list.size()) +
+                  al(sizeof(ZeroSeg) * b->fo.zeros.size());
     build_lane_orders(b);
     for (int t = 0; t < kMaxTermSets; t++)
         need += al(sizeof(uint32_t) * b->ts_list[t].size()) + al(sizeof(uint32_t) * b->ts_lane[t].size());
@@ -1074,6 +1075,10 @@ int wvg_batch_upload(wvg_batch *b) {
     size_t soff = 0;
     auto put = [&](void *dst, const void *src, size_t bytes) -> hipError_t {
         if (!bytes) return hipSuccess;
+        if (soff + bytes > need) {  // (cannot happen: `need` covers every put; never write past the stage)
+            soff = need + 1;
+            return hipErrorInvalidValue;
+        }
         uint8_t *h = b->stage.data() + soff;
         memcpy(h, src, bytes);
         soff += al(bytes);
@@ -1162,7 +1167,10 @@ int wvg_batch_upload(wvg_batch *b) {
         HIPCHK(c, put(b->d_ts[t], L.data(), sizeof(uint32_t) * L.size()));
         HIPCHK(c, put(b->d_ts[t] + L.size(), LL.data(), sizeof(uint32_t) * LL.size()));
     }
-    if (soff > need) return WVG_ERR_SPACE;  // (cannot happen: the sizes above cover every put)
+    if (soff > need) {  // (cannot happen: the sizes above cover every put)
+        c->err = "upload: staging buffer undersized";
+        return WVG_ERR_HIP;
+    }
     // frames per launch group: the load the decode's lane assignment balances
     auto frames_of = [&](const std::vector<uint32_t> &L) {
         int64_t f = 0;
