@@ -676,35 +676,37 @@ def run_rank(args) -> None:
         e2e_pipe = pipelined(False)
         e2e_pcm = pipelined(True)
 
-        # the same 4 request threads, each with two batches: a request's framing, upload
-        # and decode are issued before the previous request's format + PCM download, so
-        # the host side of one overlaps the device side of the other
-        def serve2(b0, b1, rounds=rounds):
-            bb = (b0, b1)
+        # request threads each with a ring of batches: a request's framing, upload and
+        # decode are issued before the previous requests' format + PCM download, so the
+        # host side of one overlaps the device side and the PCIe download of the others
+        def serve_ring(bb, rounds=rounds):
+            D = len(bb)
 
             def start(x):
                 x.reset()
                 x.add_files(files)
                 x.upload()
                 x.decode()
-            start(bb[0])
+            for k in range(min(D - 1, rounds)):
+                start(bb[k % D])
             for k in range(rounds):
-                if k + 1 < rounds:
-                    start(bb[(k + 1) % 2])
-                bb[k % 2].format()
-                bb[k % 2].download_pcm(pinned=True)
+                if k + D - 1 < rounds:
+                    start(bb[(k + D - 1) % D])
+                bb[k % D].format()
+                bb[k % D].download_pcm(pinned=True)
 
-        if len(batches) >= 8:
-            pairs = [(batches[2 * i], batches[2 * i + 1]) for i in range(4)]
-            for b0, b1 in pairs:  # (page-locked landing buffers of the second batches: untimed)
-                serve2(b0, b1, 2)
-            th = [threading.Thread(target=serve2, args=p) for p in pairs]
+        T, D = args.pipe_threads, args.pipe_depth
+        if len(batches) >= T * D and D >= 2:
+            rings = [batches[D * i:D * i + D] for i in range(T)]
+            for r in rings:  # (page-locked landing buffers of every batch: untimed)
+                serve_ring(r, D)
+            th = [threading.Thread(target=serve_ring, args=(r, 6)) for r in rings]
             t_p = time.perf_counter()
             for t in th:
                 t.start()
             for t in th:
                 t.join()
-            e2e_pcm2 = frames_rank * rounds * len(pairs) / (time.perf_counter() - t_p) / 1e6
+            e2e_pcm2 = frames_rank * 6 * len(rings) / (time.perf_counter() - t_p) / 1e6
 
     if kernel_ms <= 0:  # (timing off: the launch time of one batch alone stands in)
         kernel_ms = solo_ms if solo_ms > 0 else b.time(3)
@@ -776,9 +778,10 @@ def run_rank(args) -> None:
                                "pipelined_what": "the same request served by one host thread per batch copy (at most 4) "
                                                  "(4 requests each), framing/copies/decode of different batches "
                                                  "overlapping; _pcm: formatted on the device (WavpackFormatSamples) "
-                                                 "and downloaded as PCM bytes; _pcm_2buf: the 4 threads with two "
-                                                 "batches each, the next request framed, uploaded and decoding "
-                                                 "before the current one's PCM download"},
+                                                 "and downloaded as PCM bytes; _pcm_2buf: pipe_threads threads with "
+                                                 "a ring of pipe_depth batches each, the next requests framed, "
+                                                 "uploaded and decoding before the current one's PCM download",
+                               "pipe_threads": args.pipe_threads, "pipe_depth": args.pipe_depth},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": None if traffic is None else int(traffic),
@@ -823,6 +826,9 @@ def main():
                          "(default: 20 for the lane kernel, 3 for the two-wave kernel, at most --steps)")
     ap.add_argument("--kernel", choices=("lane", "two_wave"), default="lane",
                     help="PCM kernel (wvg_batch_set_kernel): lane-per-block or one workgroup per block")
+    ap.add_argument("--pipe-threads", type=int, default=8,
+                    help="pcie_inclusive.pipelined_pcm_2buf: request threads (each with --pipe-depth batches)")
+    ap.add_argument("--pipe-depth", type=int, default=2)
     ap.add_argument("--cpu-threads", type=int, default=None, help="override the socket/lease-derived thread count")
     ap.add_argument("--cpu-reps", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")

@@ -1,10 +1,10 @@
-"""bench.py's `pipelined_pcm_2buf` request stream (T request threads, two batches each:
-the next request framed, uploaded and decoding before the current one's format + PCM
-download) with every call of every request timed in its thread, so the phase that keeps
-the stream below the PCIe bound shows.
+"""bench.py's pipelined PCM request stream (T request threads, a ring of D batches
+each: the next D-1 requests framed, uploaded and decoding before the current one's
+format + PCM download) with every call of every request timed in its thread, so the
+phase that keeps the stream below the PCIe bound shows.
 
-usage: python3 scripts/pipe2_probe.py [--threads 1,2,4,6] [--rounds 6] [--kernel auto]
-       [--device-framing]"""
+usage: python3 scripts/pipe2_probe.py [--threads 1,2,4,6] [--depth 2,3] [--rounds 6]
+       [--kernel auto] [--device-framing]"""
 import argparse
 import json
 import os
@@ -19,8 +19,10 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 PHASES = ("reset", "add_files", "upload", "decode_issue", "format_issue", "download_pcm")
 
 
-def serve2(b0, b1, files, rounds, rec, dev):
-    bb = (b0, b1)
+def serve_ring(bb, files, rounds, rec, dev):
+    """Requests 0..rounds-1 on the ring bb (request k on bb[k % D]): requests k+1..k+D-1
+    are started before request k's format + download."""
+    D = len(bb)
 
     def start(x, t):
         t.append(time.perf_counter())
@@ -37,15 +39,16 @@ def serve2(b0, b1, files, rounds, rec, dev):
         t.append(time.perf_counter())
 
     ts = [[] for _ in range(rounds)]
-    start(bb[0], ts[0])
+    for k in range(min(D - 1, rounds)):
+        start(bb[k % D], ts[k])
     for k in range(rounds):
-        if k + 1 < rounds:
-            start(bb[(k + 1) % 2], ts[k + 1])
+        if k + D - 1 < rounds:
+            start(bb[(k + D - 1) % D], ts[k + D - 1])
         t = ts[k]
         t0 = time.perf_counter()
-        bb[k % 2].format()
+        bb[k % D].format()
         t1 = time.perf_counter()
-        bb[k % 2].download_pcm(pinned=True)
+        bb[k % D].download_pcm(pinned=True)
         t2 = time.perf_counter()
         rec.append(list(np.diff(t)) + [t1 - t0, t2 - t1])
 
@@ -53,6 +56,7 @@ def serve2(b0, b1, files, rounds, rec, dev):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", default="1,2,4,6")
+    ap.add_argument("--depth", default="2")
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--kernel", default="auto")
     ap.add_argument("--device-framing", action="store_true")
@@ -62,31 +66,33 @@ def main():
     _, c2 = corpora.c2(return_pcm=True)
     files = [c2]
     nts = [int(x) for x in a.threads.split(",")]
+    depths = [int(x) for x in a.depth.split(",")]
     batches = []
-    for _ in range(2 * max(nts)):
+    for _ in range(max(depths) * max(nts)):
         b = DecodeBatch(4096)
         b.set_kernel(a.kernel)
         batches.append(b)
     frames = None
     for i in range(0, len(batches), 2):  # warm: buffers and page-locked landing areas
-        serve2(batches[i], batches[i + 1], files, 2, [], a.device_framing)
+        serve_ring(batches[i:i + 2], files, 2, [], a.device_framing)
         frames = batches[i].frames
-    for nt in nts:
-        recs = [[] for _ in range(nt)]
-        th = [threading.Thread(target=serve2, args=(batches[2 * i], batches[2 * i + 1], files, a.rounds, recs[i],
-                                                    a.device_framing)) for i in range(nt)]
-        t0 = time.perf_counter()
-        for t in th:
-            t.start()
-        for t in th:
-            t.join()
-        dt = time.perf_counter() - t0
-        allr = np.array([r for rr in recs for r in rr]) * 1e3
-        print(json.dumps({"threads": nt, "kernel": a.kernel, "device_framing": a.device_framing,
-                          "Msamples_per_s": round(frames * a.rounds * nt / dt / 1e6, 1),
-                          "ms_per_request": round(dt * 1e3 / (a.rounds * nt), 3),
-                          "phase_ms_mean": {k: round(float(v), 3) for k, v in zip(PHASES, allr.mean(axis=0))}}),
-              flush=True)
+    for D in depths:
+        for nt in nts:
+            recs = [[] for _ in range(nt)]
+            th = [threading.Thread(target=serve_ring, args=(batches[D * i:D * i + D], files, a.rounds, recs[i],
+                                                            a.device_framing)) for i in range(nt)]
+            t0 = time.perf_counter()
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            dt = time.perf_counter() - t0
+            allr = np.array([r for rr in recs for r in rr]) * 1e3
+            print(json.dumps({"threads": nt, "depth": D, "kernel": a.kernel, "device_framing": a.device_framing,
+                              "Msamples_per_s": round(frames * a.rounds * nt / dt / 1e6, 1),
+                              "ms_per_request": round(dt * 1e3 / (a.rounds * nt), 3),
+                              "phase_ms_mean": {k: round(float(v), 3) for k, v in zip(PHASES, allr.mean(axis=0))}}),
+                  flush=True)
     for b in batches:
         b.close()
 

@@ -20,6 +20,7 @@
 // ST_REDO and decoded again right after by the wave-per-block kernel, so results
 // are exactly the wave kernel's, which the GPU tests hold against the oracle.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 
 #include "wv_desc.h"
 #include "wv_format.h"
@@ -252,7 +253,222 @@ __device__ __forceinline__ void dsd3_lanes(const BlockDesc *__restrict__ descs, 
     status[bi] = st;
 }
 
+// ---------------------------------------------------------------------------
+// Stereo blocks on lane pairs (round 6): lane 2j runs channel 0 of block j, lane
+// 2j + 1 channel 1.  The range coder (low / high / value, the payload window) is
+// one serial chain through both channels' decisions, so both lanes of a pair run
+// it -- the same instructions, in parallel -- while each lane runs only its own
+// channel's filter update, which in the one-lane kernel was half of a bit pair's
+// instructions.  The pair's two table entries come from one LDS read (each lane
+// reads its channel's entry, DPP quad_perm broadcasts give both lanes both), and
+// each lane writes back its channel's updated entry (channel 0's when both chose
+// the same entry is superseded by channel 1's, so both lanes write that one).
+// ---------------------------------------------------------------------------
+
+// quad_perm DPP moves within a lane pair: [1,0,3,2] swap, [0,0,2,2] even, [1,1,3,3] odd
+__device__ __forceinline__ int32_t qp_swap(int32_t x) { return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false); }
+__device__ __forceinline__ int32_t qp_even(int32_t x) { return __builtin_amdgcn_mov_dpp(x, 0xA0, 0xF, 0xF, false); }
+__device__ __forceinline__ int32_t qp_odd(int32_t x) { return __builtin_amdgcn_mov_dpp(x, 0xF5, 0xF, 0xF, false); }
+
+// The payload window of a pair: as Win, with the valid byte count kept as
+// base8 + left8 (bits; both fall by the same shift at every decision, so only the
+// bits left in the block are counted per decision and the window's fill is
+// recovered at each refill).
+struct Win8 {
+    const uint32_t *w;
+    uint64_t win;
+    int32_t base8;
+    uint32_t ni, nxt, nxt2;
+    __device__ __forceinline__ void init(const uint8_t *p, uint32_t left8) {
+        const uint32_t sh = (uint32_t)((uintptr_t)p & 3u);
+        w = (const uint32_t *)(p - sh);
+        win = (uint64_t)bswap(w[0]) << (32u + 8u * sh);
+        base8 = 8 * (4 - (int32_t)sh) - (int32_t)left8;
+        nxt = w[1];
+        nxt2 = w[2];
+        ni = 3;
+        refill(left8);
+    }
+    // returns the valid bits before the refill (< 0: the window ran dry since the last one)
+    __device__ __forceinline__ int32_t refill(uint32_t left8) {
+        const int32_t av = base8 + (int32_t)left8;
+        const bool m = av <= 32;
+        const uint32_t sh = (uint32_t)(32 - (m ? av : 0)) & 63u;
+        win |= m ? (uint64_t)bswap(nxt) << sh : 0ull;
+        base8 += m ? 32 : 0;
+        const uint32_t nn = w[ni];  // (inside the blob's tail: ni stops advancing once left8 is 0)
+        nxt = m ? nxt2 : nxt;
+        nxt2 = m ? nn : nxt2;
+        ni += m ? 1u : 0u;
+        return av;
+    }
+};
+
+// decide() with the shift in bits and only left8 counted (see Win8); p16 = the entry >> 16
+__device__ __forceinline__ bool decide8p(uint64_t &lowp, uint32_t &high, uint32_t &value, uint64_t &win,
+                                         uint32_t &left8, uint32_t p16) {
+    // lowp: low in its low half, the high half undefined (the shift below leaves its
+    // low 32 bits right whatever it holds, so no register pair is rebuilt per decision)
+    uint32_t low = (uint32_t)lowp;
+    const uint32_t split = low + __umul24((high - low) >> 8, p16);
+    const bool zero = value <= split;
+    high = zero ? split : high;
+    low = zero ? low : split + 1u;
+    uint32_t lz;
+    asm("v_ffbh_u32 %0, %1" : "=v"(lz) : "v"(high ^ low));
+    const uint32_t s = min(min(lz & ~7u, 32u), left8);  // (ffbh of 0 is ~0: 32 after the cap)
+    value = (uint32_t)(((((uint64_t)value << 32) | (win >> 32)) << s) >> 32);
+    high = (uint32_t)(((((uint64_t)high << 32) | 0xFFFFFFFFull) << s) >> 32);
+    lowp = (lowp & 0xFFFFFFFF00000000ull) | low;
+    asm("v_lshlrev_b64 %0, %1, %0" : "+v"(lowp) : "v"(s));
+    win <<= s;
+    left8 -= s;
+    return zero;
+}
+
+// a * b + c on 24-bit signed operands (v_mad_i32_i24: the compiler would take the
+// non-negative filters' products as 64-bit multiply-adds)
+__device__ __forceinline__ int32_t vmad24(int32_t a, int32_t b, int32_t c) {
+    int32_t r;
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// the filter update (DsdUtils.cs:431-441) of one channel after its decision (zero:
+// filter0 = -1).  `q += (y - q) >> k` is written `q = (y + (2^k - 1) q) >> k` (the
+// same floor), one 24-bit multiply-add and a shift (filter0 = f0): filters 1-5 stay in [0, 2^20],
+// filter6 within 2^16 (Filt / fupd above).
+__device__ __forceinline__ void fupd8(Filt &f, int32_t f0) {
+    const int32_t v = f.q0 + (f.q7 << 3);
+    const int32_t t = f.q0 - (f.q7 << 3);
+    f.byte = (f.byte << 1) | (f0 & 1);
+    f.q8 += (((v ^ f0) >> 31) | 1) & ((v ^ t) >> 31);
+    const int32_t x = f0 & (1 << 20);
+    f.q2 = vmad24(f.q2, 63, x) >> 6;
+    f.q3 = vmad24(f.q3, 15, x) >> 4;
+    f.q4 = vmad24(f.q4, 15, f.q3) >> 4;
+    f.q5 = vmad24(f.q5, 15, f.q4) >> 4;
+    const int32_t dd = (f.q5 - f.q6) >> 4;
+    f.q6 += dd;
+    f.q7 = vmad24(f.q7, 7, dd) >> 3;
+    f.q0 = fval(f);
+}
+
+// One workgroup = two waves = 64 stereo blocks; the waves share a 64 KiB table
+// array (entry e of the block of lane pair j of wave w at (e * 64 + 2j + w) * 4: the
+// address a filter value selects is one v_and_or), so two workgroups fit a CU.
+__device__ __forceinline__ void dsd3_pairs(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
+                                           uint32_t n, const uint8_t *__restrict__ blob,
+                                           const int32_t *__restrict__ ptables, int32_t *__restrict__ out,
+                                           uint32_t *__restrict__ status) {
+    using namespace wvf;
+    __shared__ int32_t pt[256 * 64];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t wv = tid >> 6, lane = tid & 63u, ch = lane & 1u, j = lane >> 1;
+    const uint32_t li = blockIdx.x * 64u + wv * 32u + j;
+    const bool inl = li < n;
+    const uint32_t bi = inl ? list[li] : 0u;
+    const BlockDesc &d = descs[bi];
+    const bool ok = inl && dsd3_ok<2>(d);
+    if (inl && !ok && ch == 0u) status[bi] = ST_REDO | (1u << 16);
+    const uint32_t nfr = ok ? d.nframes : 0u;
+    uint32_t nmax = nfr;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) nmax = max(nmax, (uint32_t)__shfl_xor((int)nmax, off));
+    nmax = __builtin_amdgcn_readfirstlane(nmax);
+    uint8_t *ptb = (uint8_t *)pt;
+    const uint32_t col = (2u * j + wv) * 4u;
+    const int32_t chm = -(int32_t)ch;
+    {   // the block's starting row (init_ptable for its rate_i), half of it by each lane of the pair
+        const int32_t *row = ptables + (uint32_t)(ok ? (d.dsd_rate_i & 255) : 0) * 256u;
+        for (uint32_t e = ch; e < 256u; e += 2u) *(int32_t *)(ptb + (e << 8) + col) = row[e];
+    }
+    __syncthreads();
+    if (nmax == 0u) return;
+    uint32_t left8 = ok ? 8u * d.dsd_data_len : 32u;
+    Win8 src;
+    src.init(blob + (ok ? d.bits_off : 0), left8);
+    uint64_t low = 0u;  // (decide8p: low in the low half)
+    uint32_t high = 0xFFFFFFFFu;
+    uint32_t value = (uint32_t)(src.win >> 32);  // init_dsd_block_high's 4 value bytes
+    src.win <<= 32;
+    left8 -= 32u;
+    int32_t dry = src.refill(left8);
+    Filt f;
+    f.q2 = d.dsd_filters[ch][0];
+    f.q3 = d.dsd_filters[ch][1];
+    f.q4 = d.dsd_filters[ch][2];
+    f.q5 = d.dsd_filters[ch][3];
+    f.q6 = d.dsd_filters[ch][4];
+    f.q7 = 0;
+    f.q8 = d.dsd_filters[ch][5];
+    f.q0 = fval(f);
+    f.byte = 0;
+    int32_t *o = out + d.out_off + ch;
+    int32_t crc = -1;
+    for (uint32_t t = 0; t < nmax; t++) {
+        const bool live = t < nfr;
+#pragma unroll
+        for (int bit = 0; bit < 8; bit++) {
+            if ((bit & 1) == 0 && bit != 0) {
+                const int32_t av = src.refill(left8);
+                dry = min(dry, live ? av : 0);
+            }
+            const uint32_t a = ((uint32_t)f.q0 & 0xFF00u) | col;
+            const int32_t pv = *(const int32_t *)(ptb + a);
+            const bool eq = a == (uint32_t)qp_swap((int32_t)a);
+            // channel 0's entry p0, channel 1's p1 -- or the entry channel 0 just updated when
+            // both chose it
+            const int32_t p0 = qp_even(pv);
+            int32_t p1;
+            asm("v_mov_b32_dpp %0, %1 quad_perm:[1,1,3,3] row_mask:0xf bank_mask:0xf" : "=v"(p1) : "v"(pv));
+            const bool z0 = decide8p(low, high, value, src.win, left8, (uint32_t)p0 >> 16);
+            const int32_t nv0 = p0 + (((z0 ? kUp : kDown) - p0) >> 8);
+            p1 = eq ? nv0 : p1;
+            const bool z1 = decide8p(low, high, value, src.win, left8, (uint32_t)p1 >> 16);
+            const int32_t nv1 = p1 + (((z1 ? kUp : kDown) - p1) >> 8);
+            *(int32_t *)(ptb + a) = (ch || eq) ? nv1 : nv0;
+            int32_t f0a = z0 ? -1 : 0, f0b = z1 ? -1 : 0, f0;
+            asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(f0) : "v"(chm), "v"(f0b), "v"(f0a));
+            fupd8(f, f0);
+        }
+        {
+            const int32_t av = src.refill(left8);
+            dry = min(dry, live ? av : 0);
+        }
+        // the frame's bytes, CRC (crc += 2 crc + v per value, channel 0 first), factor decay (:482-489)
+        const int32_t v = f.byte & 0xFF;
+        const int32_t v0 = qp_even(v), v1 = qp_odd(v);
+        crc = live ? (crc * 3 + v0) * 3 + v1 : crc;
+        f.q8 -= (f.q8 + 512) >> 10;
+        f.q0 = fval(f);
+        if (live) o[2u * t] = v;
+    }
+    if (!ok || ch) return;
+    if (dry < 0) {
+        status[bi] = ST_REDO | (64u << 16);
+        return;
+    }
+    uint32_t st = 0;
+    if (d.nframes == d.block_samples) {
+        st |= ST_CRC_CHECKED;
+        if (crc != d.crc) {  // (the final call's mute: decoded again on the wave kernel, as dsd3_lanes)
+            status[bi] = ST_REDO | (8u << 16);
+            return;
+        }
+    }
+    status[bi] = st;
+}
+
 }  // namespace dlane
+
+__global__ void __launch_bounds__(128) wv_dsd3_pair(const BlockDesc *__restrict__ descs,
+                                                    const uint32_t *__restrict__ list, uint32_t n,
+                                                    const uint8_t *__restrict__ blob,
+                                                    const int32_t *__restrict__ ptables, int32_t *__restrict__ out,
+                                                    uint32_t *__restrict__ status) {
+    dlane::dsd3_pairs(descs, list, n, blob, ptables, out, status);
+}
 
 template <int CH>
 __global__ void __launch_bounds__(64) wv_dsd3_lane(const BlockDesc *__restrict__ descs, const uint32_t *__restrict__ list,
@@ -270,9 +486,14 @@ hipError_t launch_dsd3_lane(const BlockDesc *descs, const uint32_t *list, uint32
     if (!n) return hipSuccess;
     // list order: the stereo blocks first, then n_mono mono blocks (the host sorts them)
     const uint32_t ns = n - n_mono;
-    if (ns)
+    // (WVG_DSD3_PAIR=0: stereo blocks one lane each, the round-4 kernel -- A/B)
+    static const bool one_lane = getenv("WVG_DSD3_PAIR") && getenv("WVG_DSD3_PAIR")[0] == '0';
+    if (ns && one_lane)
         hipLaunchKernelGGL((wv_dsd3_lane<2>), dim3((ns + 63) / 64), dim3(64), 0, s, descs, list, ns, blob, ptables, out,
                            status, mute_chunk);
+    else if (ns)
+        hipLaunchKernelGGL(wv_dsd3_pair, dim3((ns + 63) / 64), dim3(128), 0, s, descs, list, ns, blob, ptables, out,
+                           status);
     if (n_mono)
         hipLaunchKernelGGL((wv_dsd3_lane<1>), dim3((n_mono + 63) / 64), dim3(64), 0, s, descs, list + ns, n_mono, blob,
                            ptables, out, status, mute_chunk);
