@@ -153,6 +153,7 @@ struct wvg_batch {
     hipEvent_t fork = nullptr, join[kLanes - 1] = {nullptr};  // lanes 1 .. (the context's side streams)
     hipStream_t dstream[2] = {nullptr, nullptr};  // the batch's own side streams while others run (own_side)
     hipEvent_t done = nullptr;             // end of the last decode/format, on whatever stream it ran
+    hipEvent_t up = nullptr;               // end of the last upload's copies (on the batch stream)
     bool timing = false;                   // wvg_batch_set_timing: an event pair around every decode
     std::vector<hipEvent_t> tev;           // pending (start, end) pairs, folded into t_sum/t_cnt
     std::vector<hipEvent_t> tfree;         // event objects of folded pairs, reused
@@ -307,6 +308,7 @@ static void free_streams(wvg_batch *b) {
         if (b->join[i]) hipEventDestroy(b->join[i]);
     if (b->fork) hipEventDestroy(b->fork);
     if (b->done) hipEventDestroy(b->done);
+    if (b->up) hipEventDestroy(b->up);
     if (b->stream) hipStreamDestroy(b->stream);
     for (hipStream_t &d : b->dstream)
         if (d) hipStreamDestroy(d);
@@ -329,7 +331,8 @@ wvg_batch *wvg_batch_new(wvg_ctx *c, int chunk_frames) {
     // (GPU_MAX_HW_QUEUES), and batches in flight should each get their own
     bool ok = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&b->fork, hipEventDisableTiming) == hipSuccess &&
-              hipEventCreateWithFlags(&b->done, hipEventDisableTiming) == hipSuccess;
+              hipEventCreateWithFlags(&b->done, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&b->up, hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         free_streams(b);
         delete b;
@@ -1067,7 +1070,7 @@ int wvg_batch_upload(wvg_batch *b) {
     size_t need = al(sizeof(BlockDesc) * nd) + al(sizeof(MetaItem) * b->fo.items.size()) +
                   al(sizeof(MetaJob) * b->fo.jobs.size()) + al(b->fo.tables.size()) + al(sizeof(uint32_t) * (nd + 1)) +
                   al(sizeof(uint32_t) * b->pcm_list.size()) + al(sizeof(uint32_t) * b->dsd_list.size()) +
-                  al(sizeof(ZeroSeg) * b->fo.zeros.size());
+                  al(sizeof(ZeroSeg) * b->fo.zeros.size()) + al(sizeof(FormatSeg) * b->segs.size());
     build_lane_orders(b);
     for (int t = 0; t < kMaxTermSets; t++)
         need += al(sizeof(uint32_t) * b->ts_list[t].size()) + al(sizeof(uint32_t) * b->ts_lane[t].size());
@@ -1167,6 +1170,9 @@ int wvg_batch_upload(wvg_batch *b) {
         HIPCHK(c, put(b->d_ts[t], L.data(), sizeof(uint32_t) * L.size()));
         HIPCHK(c, put(b->d_ts[t] + L.size(), LL.data(), sizeof(uint32_t) * LL.size()));
     }
+    // the WavpackFormatSamples segments (wvg_batch_format), so a format issues no copy of its own
+    HIPCHK(c, ensure(b->d_segs, b->cap_segs, sizeof(FormatSeg) * (b->segs.empty() ? 1 : b->segs.size())));
+    HIPCHK(c, put(b->d_segs, b->segs.data(), sizeof(FormatSeg) * b->segs.size()));
     if (soff > need) {  // (cannot happen: the sizes above cover every put)
         c->err = "upload: staging buffer undersized";
         return WVG_ERR_HIP;
@@ -1179,8 +1185,15 @@ int wvg_batch_upload(wvg_batch *b) {
     };
     for (int t = 0; t < kMaxTermSets; t++) b->gframes[t] = frames_of(b->ts_list[t]);
     b->gframes[kMaxTermSets] = frames_of(b->pcm_list);
-    HIPCHK(c, hipStreamSynchronize(s));  // the blob may change after this call
-    if (trace) fprintf(stderr, "upload: %.3f ms (%zu blocks)\n", now_ms() - t_up0, nd);
+    HIPCHK(c, hipEventRecord(b->up, s));  // (a decode on a caller's stream waits for it)
+    // No wait for the copies: their sources are the page-locked blob and staging
+    // buffers, which change only after a quiesce (reset, the next upload) or, for a
+    // blob that must grow, after the copies finished (blob_resize).  The caller's
+    // thread goes on to its next request while this one's DMA runs.
+    if (trace) {
+        HIPCHK(c, hipStreamSynchronize(s));
+        fprintf(stderr, "upload: %.3f ms (%zu blocks)\n", now_ms() - t_up0, nd);
+    }
     b->uploaded = true;
     b->downloaded = false;
     b->segs_uploaded = false;
@@ -1226,6 +1239,7 @@ int wvg_batch_decode(wvg_batch *b, void *stream) {
     wvg_ctx *c = b->ctx;
     HIPCHK(c, hipSetDevice(c->device));  // side streams and events belong to the batch's device, whatever the calling thread
     hipStream_t s = stream ? (hipStream_t)stream : b->stream;
+    if (s != b->stream) HIPCHK(c, hipStreamWaitEvent(s, b->up, 0));  // the upload's copies (not waited for)
     if (b->timing) {
         // a bounded number of pairs stays pending: the oldest is folded into the
         // running sum (it finished long ago) and its events are reused
@@ -1726,16 +1740,12 @@ int wvg_batch_format(wvg_batch *b, int dsd, void *stream) {
     wvg_ctx *c = b->ctx;
     HIPCHK(c, hipSetDevice(c->device));  // d_pcm is allocated on the batch's device
     hipStream_t s = stream ? (hipStream_t)stream : b->stream;
+    if (s != b->stream) HIPCHK(c, hipStreamWaitEvent(s, b->up, 0));  // the segments come with the upload
     HIPCHK(c, hipStreamWaitEvent(s, b->done, 0));
-    if (!b->segs_uploaded) {  // once per upload (the file set may have changed)
+    if (!b->segs_uploaded) {  // once per upload (the segments came with it)
         const size_t pb = (size_t)(b->pcm_bytes ? b->pcm_bytes : 1);
         HIPCHK(c, ensure(b->d_pcm, b->cap_pcm, pb));
         HIPCHK(c, hipMemsetAsync(b->d_pcm, 0, pb, s));
-        HIPCHK(c, ensure(b->d_segs, b->cap_segs, sizeof(FormatSeg) * (b->segs.empty() ? 1 : b->segs.size())));
-        if (!b->segs.empty())
-            HIPCHK(c, hipMemcpyAsync(b->d_segs, b->segs.data(), sizeof(FormatSeg) * b->segs.size(),
-                                     hipMemcpyHostToDevice, s));
-        HIPCHK(c, hipStreamSynchronize(s));  // b->segs may change after this call
         b->segs_uploaded = true;
     }
     HIPCHK(c, launch_format(b->d_segs, (uint32_t)b->segs.size(), b->d_out, b->d_pcm, dsd ? 1 : 0, s));
