@@ -676,9 +676,11 @@ def run_rank(args) -> None:
         e2e_pipe = pipelined(False)
         e2e_pcm = pipelined(True)
 
-        # request threads each with a ring of batches: a request's framing, upload and
-        # decode are issued before the previous requests' format + PCM download, so the
-        # host side of one overlaps the device side and the PCIe download of the others
+        # request threads each with a ring of D batches: requests k+1 .. k+D-1 are framed,
+        # uploaded and decoding before request k's format + PCM download, so the host
+        # side of one overlaps the device side and the PCIe transfers of the others.
+        # (Every call of a request issued back to back with wvg_batch_download_pcm_async
+        # measured lower: profiles/r06_pipe_async.jsonl.)
         def serve_ring(bb, rounds=rounds):
             D = len(bb)
 
@@ -780,7 +782,8 @@ def run_rank(args) -> None:
                                                  "overlapping; _pcm: formatted on the device (WavpackFormatSamples) "
                                                  "and downloaded as PCM bytes; _pcm_2buf: pipe_threads threads with "
                                                  "a ring of pipe_depth batches each, the next requests framed, "
-                                                 "uploaded and decoding before the current one's PCM download",
+                                                 "uploaded and decoding before the current one's format + PCM "
+                                                 "download",
                                "pipe_threads": args.pipe_threads, "pipe_depth": args.pipe_depth},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6),
@@ -826,7 +829,7 @@ def main():
                          "(default: 20 for the lane kernel, 3 for the two-wave kernel, at most --steps)")
     ap.add_argument("--kernel", choices=("lane", "two_wave"), default="lane",
                     help="PCM kernel (wvg_batch_set_kernel): lane-per-block or one workgroup per block")
-    ap.add_argument("--pipe-threads", type=int, default=8,
+    ap.add_argument("--pipe-threads", type=int, default=10,
                     help="pcie_inclusive.pipelined_pcm_2buf: request threads (each with --pipe-depth batches)")
     ap.add_argument("--pipe-depth", type=int, default=2)
     ap.add_argument("--cpu-threads", type=int, default=None, help="override the socket/lease-derived thread count")

@@ -275,6 +275,14 @@ uint8_t *wvg_batch_device_pcm(wvg_batch *b);                 /* device pointer t
  * rate), read through wvg_batch_host_pcm until the next such download. */
 int wvg_batch_download_pcm(wvg_batch *b, uint8_t *host, int64_t cap);
 uint8_t *wvg_batch_host_pcm(wvg_batch *b);
+/* The same download into the batch's page-locked buffer, queued behind the format
+ * on the batch stream without waiting for it: a decode server issues a request's
+ * upload, decode, format and download back to back and takes the PCM
+ * (wvg_batch_host_pcm) after wvg_batch_sync -- the next reset/upload of the batch
+ * waits for it too.  (The reference's WavpackUnpackSamples + WavpackFormatSamples
+ * calls, WavPackUtils.cs:200-341, return the PCM synchronously; this is their
+ * batched, overlapped form.) */
+int wvg_batch_download_pcm_async(wvg_batch *b);
 
 /* WvDemo.Main (WvDemo.cs:15-168) for one file of a formatted batch built with
  * chunk_frames 4096: the .wav bytes it writes (stored RIFF header or the

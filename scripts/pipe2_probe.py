@@ -53,6 +53,32 @@ def serve_ring(bb, files, rounds, rec, dev):
         rec.append(list(np.diff(t)) + [t1 - t0, t2 - t1])
 
 
+def serve_async(bb, files, rounds, rec, dev):
+    """bench.py's ring: every call of request k issued back to back (the PCM download
+    queued, wvg_batch_download_pcm_async); the thread waits only for request k - D."""
+    D = len(bb)
+    for k in range(rounds):
+        x = bb[k % D]
+        t = [time.perf_counter()]
+        if k >= D:
+            x.sync()
+        t.append(time.perf_counter())
+        x.reset()
+        (x.add_files_device if dev else x.add_files)(files)
+        t.append(time.perf_counter())
+        x.upload()
+        t.append(time.perf_counter())
+        x.decode()
+        t.append(time.perf_counter())
+        x.format()
+        t.append(time.perf_counter())
+        x.download_pcm_async()
+        t.append(time.perf_counter())
+        rec.append(list(np.diff(t)))
+    for k in range(max(0, rounds - D), rounds):
+        bb[k % D].sync()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", default="1,2,4,6")
@@ -60,6 +86,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--kernel", default="auto")
     ap.add_argument("--device-framing", action="store_true")
+    ap.add_argument("--async-download", action="store_true", help="bench.py's ring (serve_async)")
     a = ap.parse_args()
     from synth import corpora
     from wavpackdecoder_amd.api import DecodeBatch
@@ -79,8 +106,9 @@ def main():
     for D in depths:
         for nt in nts:
             recs = [[] for _ in range(nt)]
-            th = [threading.Thread(target=serve_ring, args=(batches[D * i:D * i + D], files, a.rounds, recs[i],
-                                                            a.device_framing)) for i in range(nt)]
+            fn = serve_async if a.async_download else serve_ring
+            th = [threading.Thread(target=fn, args=(batches[D * i:D * i + D], files, a.rounds, recs[i],
+                                                    a.device_framing)) for i in range(nt)]
             t0 = time.perf_counter()
             for t in th:
                 t.start()
@@ -88,10 +116,13 @@ def main():
                 t.join()
             dt = time.perf_counter() - t0
             allr = np.array([r for rr in recs for r in rr]) * 1e3
+            names = ("wait", "reset+add_files", "upload", "decode", "format", "download_issue") if a.async_download \
+                else PHASES
             print(json.dumps({"threads": nt, "depth": D, "kernel": a.kernel, "device_framing": a.device_framing,
+                              "async_download": a.async_download,
                               "Msamples_per_s": round(frames * a.rounds * nt / dt / 1e6, 1),
                               "ms_per_request": round(dt * 1e3 / (a.rounds * nt), 3),
-                              "phase_ms_mean": {k: round(float(v), 3) for k, v in zip(PHASES, allr.mean(axis=0))}}),
+                              "phase_ms_mean": {k: round(float(v), 3) for k, v in zip(names, allr.mean(axis=0))}}),
                   flush=True)
     for b in batches:
         b.close()

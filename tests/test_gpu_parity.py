@@ -237,6 +237,9 @@ def test_format_epilogue_matches_oracle(gpu_batch_cls, dsd):
     b.format(dsd=bool(dsd))
     pcm = b.download_pcm()
     np.testing.assert_array_equal(b.download_pcm(pinned=True), pcm)  # the page-locked path, same bytes
+    b.download_pcm_async()  # queued behind the format; the bytes are there after sync
+    b.sync()
+    np.testing.assert_array_equal(b.host_pcm(), pcm)
     out = b.download()
     offs = [b.pcm_offset(i) for i in idx]
     infos = list(b.infos)

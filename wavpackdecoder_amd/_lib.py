@@ -124,6 +124,7 @@ def lib():
         "wvg_batch_device_pcm": (vp, [vp]),
         "wvg_batch_download_pcm": (i32, [vp, vp, i64]),
         "wvg_batch_host_pcm": (vp, [vp]),
+        "wvg_batch_download_pcm_async": (i32, [vp]),
         "wvg_batch_wav": (i32, [vp, i32, vp, i64, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32)]),
         "wvg_stream_open": (vp, [vp, ctypes.c_char_p, ctypes.c_size_t, u32, i64, ctypes.POINTER(WvgFileInfo)]),
         "wvg_stream_unpack": (i64, [vp, vp, i64]),
@@ -153,5 +154,6 @@ EXPORTED = ("wvg_open", "wvg_close", "wvg_last_error", "wvg_batch_new", "wvg_bat
             "wvg_batch_num_blocks", "wvg_batch_bytes_in", "wvg_batch_frames", "wvg_batch_download", "wvg_batch_host_out",
             "wvg_batch_file_result", "wvg_batch_block_status", "wvg_batch_lane_counters", "wvg_batch_file_blocks", "wvg_batch_time", "wvg_decode_file",
             "wvg_probe_file", "wvg_format_samples", "wvg_batch_format", "wvg_batch_pcm_bytes", "wvg_batch_pcm_offset",
-            "wvg_batch_device_pcm", "wvg_batch_download_pcm", "wvg_batch_host_pcm", "wvg_batch_wav",
+            "wvg_batch_device_pcm", "wvg_batch_download_pcm", "wvg_batch_host_pcm", "wvg_batch_download_pcm_async",
+            "wvg_batch_wav",
             "wvg_stream_open", "wvg_stream_unpack", "wvg_stream_set_sample", "wvg_stream_state", "wvg_stream_close")

@@ -293,6 +293,19 @@ class DecodeBatch:
     def pcm_offset(self, i: int) -> int:
         return int(self._L.wvg_batch_pcm_offset(self._b, int(i)))
 
+    def download_pcm_async(self):
+        """Queue the PCM download into the batch's page-locked buffer behind the format
+        (wvg_batch_download_pcm_async); after sync(), host_pcm() is the image."""
+        self._check(self._L.wvg_batch_download_pcm_async(self._b))
+
+    def host_pcm(self) -> np.ndarray:
+        """The page-locked PCM image of the last pinned / async download (a view)."""
+        n = int(self._L.wvg_batch_pcm_bytes(self._b))
+        p = self._L.wvg_batch_host_pcm(self._b)
+        if not p or n == 0:
+            return np.zeros(0, dtype=np.uint8)
+        return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint8)), shape=(n,))
+
     def download_pcm(self, pinned: bool = False) -> np.ndarray:
         """The formatted PCM bytes.  pinned=True: DMA into the batch's page-locked
         buffer and return a view of it (valid until the next such download or close)."""

@@ -32,6 +32,7 @@ hipError_t launch_2wave(int ts, const BlockDesc *descs, const uint32_t *list, ui
                         int32_t *out, uint32_t *status, uint32_t *aux, hipStream_t s, int lane_mode,
                         const uint32_t *lane_list, uint32_t lane_n, uint32_t *lane_dbg);
 hipError_t launch_format(const FormatSeg *segs, uint32_t nseg, const int32_t *in, uint8_t *out, int dsd, hipStream_t s);
+hipError_t launch_copy_to_host(const uint8_t *src, uint8_t *dst, size_t n, hipStream_t s);
 hipError_t launch_zero_fill(const ZeroSeg *segs, uint32_t nseg, int32_t *out, hipStream_t s);
 hipError_t upload_dsd_ptables();
 hipError_t launch_dsd_fill(const BlockDesc *descs, const uint32_t *dsd_list, uint32_t n_dsd, uint32_t *status,
@@ -1779,6 +1780,27 @@ int wvg_batch_download_pcm(wvg_batch *b, uint8_t *host, int64_t cap) {
     if (b->pcm_bytes)
         HIPCHK(c, hipMemcpyAsync(host, b->d_pcm, (size_t)b->pcm_bytes, hipMemcpyDeviceToHost, b->stream));
     HIPCHK(c, hipStreamSynchronize(b->stream));
+    return WVG_OK;
+}
+
+int wvg_batch_download_pcm_async(wvg_batch *b) {
+    if (!b || !b->formatted) return WVG_ERR_ARG;
+    wvg_ctx *c = b->ctx;
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t nb = (size_t)(b->pcm_bytes ? b->pcm_bytes : 1);
+    if (nb > b->hpcm.cap) HIPCHK(c, quiesce(b));  // (a grown buffer is a new one: no DMA may still land in the old)
+    if (!b->hpcm.resize(nb)) return WVG_ERR_SPACE;
+    HIPCHK(c, hipStreamWaitEvent(b->stream, b->done, 0));
+    if (b->pcm_bytes) {
+        // (WVG_PCM_DMA=1: the DMA-engine copy instead of the copy kernel -- A/B)
+        static const bool dma = getenv("WVG_PCM_DMA") && getenv("WVG_PCM_DMA")[0] == '1';
+        void *hdev = nullptr;
+        if (!dma && b->hpcm.pinned && hipHostGetDevicePointer(&hdev, b->hpcm.data(), 0) == hipSuccess && hdev)
+            HIPCHK(c, launch_copy_to_host(b->d_pcm, (uint8_t *)hdev, (size_t)b->pcm_bytes, b->stream));
+        else
+            HIPCHK(c, hipMemcpyAsync(b->hpcm.data(), b->d_pcm, (size_t)b->pcm_bytes, hipMemcpyDeviceToHost, b->stream));
+    }
+    HIPCHK(c, hipEventRecord(b->done, b->stream));  // (wvg_batch_sync and the next quiesce wait for it)
     return WVG_OK;
 }
 

@@ -1506,4 +1506,27 @@ hipError_t launch_format(const FormatSeg *segs, uint32_t nseg, const int32_t *in
     return hipGetLastError();
 }
 
+// n bytes from HBM into page-locked host memory by the CUs (16 B per lane, the
+// stores crossing PCIe as full lines): the async PCM download, a kernel in the
+// batch stream's order rather than a DMA-engine copy, whose dependency on the
+// format kernel the runtime resolves on the host (pipe2_probe: a thread issuing
+// request k+1 blocked for milliseconds behind request k's queued copy)
+extern "C" __global__ void __launch_bounds__(256) wv_copy_to_host(const uint4 *__restrict__ src, uint4 *__restrict__ dst,
+                                                                  uint64_t n16, const uint8_t *__restrict__ tsrc,
+                                                                  uint8_t *__restrict__ tdst, uint32_t ntail) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) dst[i] = src[i];
+    if (blockIdx.x == 0 && threadIdx.x < ntail) tdst[threadIdx.x] = tsrc[threadIdx.x];
+}
+
+hipError_t launch_copy_to_host(const uint8_t *src, uint8_t *dst, size_t n, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const uint64_t n16 = n / 16;
+    const uint32_t ntail = (uint32_t)(n - n16 * 16);
+    // 1,024 workgroups (4 per CU): enough stores in flight to cover the PCIe round trip
+    hipLaunchKernelGGL(wv_copy_to_host, dim3(1024), dim3(256), 0, s, (const uint4 *)src, (uint4 *)dst, n16,
+                       src + n16 * 16, dst + n16 * 16, ntail);
+    return hipGetLastError();
+}
+
 }  // namespace wvg
