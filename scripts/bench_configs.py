@@ -228,6 +228,26 @@ def main():
                     continue
                 data = S.encode_pcm_parallel(pcm, S.EncParams(terms=t, block_samples=22050, joint_stereo=True))
                 run(f"C2-shape {a.list_blocks} x 22050 16-bit stereo, list {nm}", [data], pcm)
+        elif c == "hykinds":
+            # C2's PCM (--list-blocks x 22,050 frames, 16-bit stereo, default terms) as the PCM kinds
+            # the round-6 lanes added, beside their neighbours: lossless (C2), hybrid with and without
+            # HYBRID_BITRATE, INT32 hybrid (zeros) and INT32 lossless with a shift-only fixup
+            from synth import wvsynth as S
+            pcm = corpora.c2_pcm(a.list_blocks)
+            base = dict(terms=S.TERMS_DEFAULT, block_samples=22050, joint_stereo=True)
+            kinds = {"lossless (C2)": (pcm, dict()),
+                     "hybrid + bitrate": (pcm, dict(hybrid=True, hybrid_bitrate=True, bitrate_x256=896)),
+                     "hybrid, no bitrate": (pcm, dict(hybrid=True, hybrid_bitrate=False, bitrate_x256=896)),
+                     "int32 hybrid zeros=3": (S.int32_layout(pcm, zeros=3, seed=5),
+                                              dict(bytes_per_sample=4, hybrid=True, hybrid_bitrate=True,
+                                                   bitrate_x256=896, int32_zeros=3)),
+                     "int32 lossless shift=4": (S.int32_layout(pcm, zeros=4, seed=6),
+                                                dict(bytes_per_sample=4, int32_zeros=4))}
+            for nm, (x, kw) in kinds.items():
+                if a.lists and not any(nm.startswith(y) for y in a.lists.split(",")):
+                    continue
+                data = S.encode_pcm_parallel(x, S.EncParams(**base, **kw))
+                run(f"{a.list_blocks} x 22050 16-bit stereo as {nm}", [data], x if not kw.get("hybrid") else None)
         elif c.startswith("dsd"):  # dsd0 / dsd1 / dsd3: N stereo files of one 22,050-frame block in one mode
             from synth import wvsynth as S
             mode = int(c[3:])
