@@ -155,5 +155,8 @@ def test_int32_blocks_on_lanes():
     for k, sb in enumerate((4, 11)):  # lossless, the fixup a shift (no wvx: its bits are lost)
         files.append(V.int32_file(x, sent_bits=sb, seed=95 + k))
         names.append(f"int32_ll_sent{sb}")
+    for k, z in enumerate((3, 12)):  # lossless, zeros alone: `<<= zeros` ahead of the header shift
+        files.append(V.int32_file(x, zeros=z, seed=97 + k))
+        names.append(f"int32_ll_zeros{z}")
     st = _check(files, names)
     assert int(np.count_nonzero(st & WVG_ST_REDONE)) <= max(1, len(st) // 20)

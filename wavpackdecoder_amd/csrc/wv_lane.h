@@ -1359,10 +1359,13 @@ template <int HY, int... Ts>
 constexpr bool lane_codes() { return !HY && (LaneRt<Ts...>::NS ? LaneRt<Ts...>::NS : (int)sizeof...(Ts)) <= 5; }
 
 // the lossless lanes' fixup shift (UnpackUtils.cs:1251-1404): the header's, plus an int32
-// block's zeros + sent_bits + ones + dups when those reduce to a shift (:1344-1345)
+// block's zeros + sent_bits + ones + dups when sent_bits is set (:1344-1345), or its zeros
+// alone when it is not (:1327-1330: `<<= zeros` ahead of the header shift; lane_ok keeps
+// the two shifts' sum below 32, where the two shifts compose into one)
 __device__ __forceinline__ uint32_t lane_shift(const BlockDesc &d) {
     int32_t sh = d.shift;
-    if (d.flags & wvf::INT32_DATA) sh += d.int32_zeros + d.int32_sent_bits + d.int32_ones + d.int32_dups;
+    if (d.flags & wvf::INT32_DATA)
+        sh += d.int32_sent_bits ? d.int32_zeros + d.int32_sent_bits + d.int32_ones + d.int32_dups : d.int32_zeros;
     return (uint32_t)sh & 31u;
 }
 
@@ -1382,10 +1385,11 @@ __device__ __forceinline__ bool lane_ok(const BlockDesc &d) {
         return false;
     } else if (d.flags & INT32_DATA) {
         // lossless int32 without a wvx stream whose fixup is a shift (UnpackUtils.cs:1318-1345:
-        // sent_bits or no zeros / ones / dups -- lane_shift); the wvx read and the zeros / ones /
-        // dups map go to the two-wave / generic kernels
-        if ((d.wvx_state & 0x100) || (d.int32_sent_bits == 0 && (d.int32_zeros | d.int32_ones | d.int32_dups) != 0))
-            return false;
+        // sent_bits, zeros -- which the reference applies before ones / dups -- or none of them;
+        // lane_shift); the wvx read and the ones / dups maps go to the two-wave / generic kernels
+        if (d.wvx_state & 0x100) return false;
+        if (d.int32_sent_bits == 0 && d.int32_zeros == 0 && (d.int32_ones | d.int32_dups) != 0) return false;
+        if (d.int32_sent_bits == 0 && d.int32_zeros != 0 && d.int32_zeros + (d.shift & 31) > 31) return false;
     }
     if (((d.flags & MONO_DATA) != 0) != MONO) return false;
     if ((d.wvc_len != 0) != (HY == 2)) return false;  // HY 2: hybrid blocks with their .wvc stream
