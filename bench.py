@@ -679,39 +679,61 @@ def run_rank(args) -> None:
         e2e_pipe = pipelined(False)
         e2e_pcm = pipelined(True)
 
-        # request threads each with a ring of D batches: requests k+1 .. k+D-1 are framed,
-        # uploaded and decoding before request k's format + PCM download, so the host
-        # side of one overlaps the device side and the PCIe transfers of the others.
-        # (Every call of a request issued back to back with wvg_batch_download_pcm_async
-        # measured lower: profiles/r06_pipe_async.jsonl.)
-        def serve_ring(bb, rounds=rounds):
-            D = len(bb)
+        # a decode server: producer threads take a free batch and frame, upload, decode and
+        # format a request on it (no call waits for the device), consumer threads download
+        # the queued requests' PCM in order (page-locked, blocking) and free the batches --
+        # the PCIe download, the request's bound, stays busy while the producers' host work
+        # and uploads overlap it (round 6; a thread per request ring measured 7,700-8,800,
+        # profiles/r06_pipe_pc.jsonl)
+        import queue
 
-            def start(x):
-                x.reset()
-                x.add_files(files)
-                x.upload()
-                x.decode()
-            for k in range(min(D - 1, rounds)):
-                start(bb[k % D])
-            for k in range(rounds):
-                if k + D - 1 < rounds:
-                    start(bb[(k + D - 1) % D])
-                bb[k % D].format()
-                bb[k % D].download_pcm(pinned=True)
+        def serve_pc(pool, total, producers, consumers):
+            free, ready = queue.Queue(), queue.Queue()
+            for x in pool:
+                free.put(x)
+            left = [total]
+            lock = threading.Lock()
 
-        T, D = args.pipe_threads, args.pipe_depth
-        if len(batches) >= T * D and D >= 2:
-            rings = [batches[D * i:D * i + D] for i in range(T)]
-            for r in rings:  # (page-locked landing buffers of every batch: untimed)
-                serve_ring(r, D)
-            th = [threading.Thread(target=serve_ring, args=(r, 6)) for r in rings]
+            def produce():
+                while True:
+                    with lock:
+                        if left[0] == 0:
+                            return
+                        left[0] -= 1
+                    x = free.get()
+                    x.reset()
+                    x.add_files(files)
+                    x.upload()
+                    x.decode()
+                    x.format()
+                    ready.put(x)
+
+            def consume():
+                while True:
+                    x = ready.get()
+                    if x is None:
+                        return
+                    x.download_pcm(pinned=True)
+                    free.put(x)
+            ps = [threading.Thread(target=produce) for _ in range(producers)]
+            cs = [threading.Thread(target=consume) for _ in range(consumers)]
             t_p = time.perf_counter()
-            for t in th:
+            for t in ps + cs:
                 t.start()
-            for t in th:
+            for t in ps:
                 t.join()
-            e2e_pcm2 = frames_rank * 6 * len(rings) / (time.perf_counter() - t_p) / 1e6
+            for _ in cs:
+                ready.put(None)
+            for t in cs:
+                t.join()
+            return time.perf_counter() - t_p
+
+        N = min(args.pipe_pool, len(batches))
+        if N >= 2:
+            pool = batches[:N]
+            serve_pc(pool, N, min(args.pipe_producers, N), args.pipe_consumers)  # (landing buffers: untimed)
+            reqs = 4 * N
+            e2e_pcm2 = frames_rank * reqs / serve_pc(pool, reqs, min(args.pipe_producers, N), args.pipe_consumers) / 1e6
 
     if kernel_ms <= 0:  # (timing off: the launch time of one batch alone stands in)
         kernel_ms = solo_ms if solo_ms > 0 else b.time(3)
@@ -783,11 +805,15 @@ def run_rank(args) -> None:
                                "pipelined_what": "the same request served by one host thread per batch copy (at most 4) "
                                                  "(4 requests each), framing/copies/decode of different batches "
                                                  "overlapping; _pcm: formatted on the device (WavpackFormatSamples) "
-                                                 "and downloaded as PCM bytes; _pcm_2buf: pipe_threads threads with "
-                                                 "a ring of pipe_depth batches each, the next requests framed, "
-                                                 "uploaded and decoding before the current one's format + PCM "
-                                                 "download",
-                               "pipe_threads": args.pipe_threads, "pipe_depth": args.pipe_depth},
+                                                 "and downloaded as PCM bytes; _pcm_2buf: a decode server over a "
+                                                 "pool of pipe_pool batches -- pipe_producers threads frame, upload, "
+                                                 "decode and format requests without waiting, pipe_consumers threads "
+                                                 "download the queued PCM in order and free the batches (4 x "
+                                                 "pipe_pool requests timed)",
+                               "pipe_producers": args.pipe_producers, "pipe_consumers": args.pipe_consumers,
+                               "pipe_pool": args.pipe_pool,
+                               "link_bound_Msamples_s": "~14,200 (90.3 MB of PCM16 down at the box's 56.7 GB/s D2H, "
+                                                        "scripts/micro/pcie_kernel.hip)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": None if traffic is None else int(traffic),
@@ -832,9 +858,10 @@ def main():
                          "(default: 20 for the lane kernel, 3 for the two-wave kernel, at most --steps)")
     ap.add_argument("--kernel", choices=("lane", "two_wave"), default="lane",
                     help="PCM kernel (wvg_batch_set_kernel): lane-per-block or one workgroup per block")
-    ap.add_argument("--pipe-threads", type=int, default=10,
-                    help="pcie_inclusive.pipelined_pcm_2buf: request threads (each with --pipe-depth batches)")
-    ap.add_argument("--pipe-depth", type=int, default=2)
+    ap.add_argument("--pipe-producers", type=int, default=6,
+                    help="pcie_inclusive.pipelined_pcm_2buf: producer threads of the decode server")
+    ap.add_argument("--pipe-consumers", type=int, default=1, help="its PCM download threads")
+    ap.add_argument("--pipe-pool", type=int, default=16, help="its batches (at most --inflight)")
     ap.add_argument("--cpu-threads", type=int, default=None, help="override the socket/lease-derived thread count")
     ap.add_argument("--cpu-reps", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")

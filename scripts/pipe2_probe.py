@@ -79,6 +79,58 @@ def serve_async(bb, files, rounds, rec, dev):
         bb[k % D].sync()
 
 
+def serve_pc(pool, files, total, producers, consumers):
+    """Producer/consumer server: `producers` threads take a free batch, frame, upload, decode
+    and format a request on it (no call waits for the device) and queue it; `consumers`
+    threads take the queued batches in order and download their PCM (page-locked, blocking),
+    then free the batch.  Returns (wall seconds, requests)."""
+    import queue
+    free, ready = queue.Queue(), queue.Queue()
+    for b in pool:
+        free.put(b)
+    left = [total]
+    lock = threading.Lock()
+
+    def produce():
+        while True:
+            with lock:
+                if left[0] == 0:
+                    return
+                left[0] -= 1
+            x = free.get()
+            x.reset()
+            x.add_files(files)
+            x.upload()
+            x.decode()
+            x.format()
+            ready.put(x)
+
+    done = [0]
+
+    def consume():
+        while True:
+            x = ready.get()
+            if x is None:
+                return
+            x.download_pcm(pinned=True)
+            with lock:
+                done[0] += 1
+            free.put(x)
+
+    ps = [threading.Thread(target=produce) for _ in range(producers)]
+    cs = [threading.Thread(target=consume) for _ in range(consumers)]
+    t0 = time.perf_counter()
+    for t in ps + cs:
+        t.start()
+    for t in ps:
+        t.join()
+    for _ in cs:
+        ready.put(None)
+    for t in cs:
+        t.join()
+    return time.perf_counter() - t0, done[0]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", default="1,2,4,6")
@@ -86,7 +138,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--kernel", default="auto")
     ap.add_argument("--device-framing", action="store_true")
-    ap.add_argument("--async-download", action="store_true", help="bench.py's ring (serve_async)")
+    ap.add_argument("--async-download", action="store_true", help="every call back to back (serve_async)")
+    ap.add_argument("--pc", default="", help="producer/consumer server: comma list of P:C:pool configs")
     a = ap.parse_args()
     from synth import corpora
     from wavpackdecoder_amd.api import DecodeBatch
@@ -103,6 +156,19 @@ def main():
     for i in range(0, len(batches), 2):  # warm: buffers and page-locked landing areas
         serve_ring(batches[i:i + 2], files, 2, [], a.device_framing)
         frames = batches[i].frames
+    for cfg in [x for x in a.pc.split(",") if x]:
+        P, C, N = (int(v) for v in cfg.split(":"))
+        while len(batches) < N:
+            b = DecodeBatch(4096)
+            b.set_kernel(a.kernel)
+            serve_ring([b], files, 1, [], a.device_framing)
+            batches.append(b)
+        dt, nreq = serve_pc(batches[:N], files, a.rounds * N, P, C)
+        print(json.dumps({"producers": P, "consumers": C, "pool": N, "kernel": a.kernel, "requests": nreq,
+                          "Msamples_per_s": round(frames * nreq / dt / 1e6, 1),
+                          "ms_per_request": round(dt * 1e3 / nreq, 3)}), flush=True)
+    if a.pc:
+        return
     for D in depths:
         for nt in nts:
             recs = [[] for _ in range(nt)]
