@@ -140,7 +140,10 @@ def main():
     ap.add_argument("--device-framing", action="store_true")
     ap.add_argument("--async-download", action="store_true", help="every call back to back (serve_async)")
     ap.add_argument("--pc", default="", help="producer/consumer server: comma list of P:C:pool configs")
+    ap.add_argument("--switch", type=float, default=0.0, help="sys.setswitchinterval (0: Python's default)")
     a = ap.parse_args()
+    if a.switch > 0:
+        sys.setswitchinterval(a.switch)
     from synth import corpora
     from wavpackdecoder_amd.api import DecodeBatch
     _, c2 = corpora.c2(return_pcm=True)
