@@ -75,6 +75,15 @@ def _context():
     return _ctx
 
 
+def _file_arrays(files):
+    """(the files as bytes objects, a c_char_p array of them, their lengths as a uint64
+    array) for the C-ABI's file-array calls; bytes inputs are passed as they are."""
+    bufs = files if all(type(f) is bytes for f in files) else [bytes(f) for f in files]
+    ptrs = (ctypes.c_char_p * len(bufs))(*bufs)
+    lens = np.fromiter(map(len, bufs), dtype=np.uint64, count=len(bufs))
+    return bufs, ptrs, lens
+
+
 class DecodeBatch:
     """A batch of .wv files decoded together on one GPU (files shard across GPUs)."""
 
@@ -84,6 +93,7 @@ class DecodeBatch:
         if not self._b:
             raise RuntimeError("wvg_batch_new failed")
         self.infos: list = []
+        self._dev_infos: list = []  # indices of device-framed files (their infos come with the upload)
         self._uploaded = False
         self._data: list = []
 
@@ -115,6 +125,7 @@ class DecodeBatch:
         """Drop every file, keep the device and page-locked buffers (wvg_batch_reset)."""
         self._check(self._L.wvg_batch_reset(self._b))
         self.infos = []
+        self._dev_infos = []
         self._uploaded = False
 
     def add_files(self, files, open_flags: int = 0, threads: int = 0):
@@ -122,19 +133,17 @@ class DecodeBatch:
         n = len(files)
         if n == 0:
             return []
-        bufs = [bytes(f) for f in files]
-        ptrs = (ctypes.c_char_p * n)(*bufs)
-        lens = (ctypes.c_size_t * n)(*[len(f) for f in bufs])
+        bufs, ptrs, lens = _file_arrays(files)
         infos = (_L.WvgFileInfo * n)()
-        idx = (ctypes.c_int32 * n)()
-        rc = self._L.wvg_batch_add_files(self._b, n, ctypes.cast(ptrs, ctypes.c_void_p),
-                                         ctypes.cast(lens, ctypes.c_void_p), int(open_flags), int(threads),
-                                         ctypes.cast(infos, ctypes.c_void_p), ctypes.cast(idx, ctypes.c_void_p))
+        idx = np.empty(n, dtype=np.int32)
+        rc = self._L.wvg_batch_add_files(self._b, n, ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data,
+                                         int(open_flags), int(threads), ctypes.cast(infos, ctypes.c_void_p),
+                                         idx.ctypes.data)
         if rc < 0:
             self._check(rc)
-        self.infos.extend(infos[i] for i in range(n))
+        self.infos.extend(infos)
         self._uploaded = False
-        return [int(idx[i]) for i in range(n)]
+        return idx.tolist()
 
     def add_files_device(self, files):
         """Queue files for device-side framing at the next upload
@@ -143,17 +152,16 @@ class DecodeBatch:
         n = len(files)
         if n == 0:
             return []
-        bufs = [bytes(f) for f in files]
-        ptrs = (ctypes.c_char_p * n)(*bufs)
-        lens = (ctypes.c_size_t * n)(*[len(f) for f in bufs])
-        idx = (ctypes.c_int32 * n)()
-        rc = self._L.wvg_batch_add_files_device(self._b, n, ctypes.cast(ptrs, ctypes.c_void_p),
-                                                ctypes.cast(lens, ctypes.c_void_p), ctypes.cast(idx, ctypes.c_void_p))
+        bufs, ptrs, lens = _file_arrays(files)
+        idx = np.empty(n, dtype=np.int32)
+        rc = self._L.wvg_batch_add_files_device(self._b, n, ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data,
+                                                idx.ctypes.data)
         if rc < 0:
             self._check(rc)
+        self._dev_infos.extend(range(len(self.infos), len(self.infos) + n))
         self.infos.extend(_L.WvgFileInfo() for _ in range(n))
         self._uploaded = False
-        return [int(idx[i]) for i in range(n)]
+        return idx.tolist()
 
     def framing_stats(self):
         """(files framed on the device, files framed by the host fallback)"""
@@ -170,7 +178,7 @@ class DecodeBatch:
 
     def upload(self):
         self._check(self._L.wvg_batch_upload(self._b))
-        for i in range(len(self.infos)):  # device-framed files get their infos here
+        for i in self._dev_infos:  # device-framed files get their infos here
             self._L.wvg_batch_file_info(self._b, i, ctypes.byref(self.infos[i]))
         self._uploaded = True
 

@@ -529,23 +529,25 @@ int wvg_probe_file(const uint8_t *file, size_t len, uint32_t open_flags, int chu
 // WavpackFormatSamples segments and its blocks' launch groups.  `fi` refers to
 // descriptors already in b->fo.
 // `at` >= 0: the file's slot was reserved when it was added (device framing).
-static int commit_file(wvg_batch *b, const FileInfo &fi, size_t len, wvg_file_info *info, int at = -1) {
+static int commit_file(wvg_batch *b, FileInfo &fin, size_t len, wvg_file_info *info, int at = -1) {
     wvg_file_info wi;
-    fill_info(fi, wi);
+    fill_info(fin, wi);
     wi.out_offset = b->out_ints;
-    wi.header_off = fi.header_off;
-    wi.header_len = fi.header_len;
-    wi.trailer_off = fi.trailer_off;
-    wi.trailer_len = fi.trailer_len;
+    wi.header_off = fin.header_off;
+    wi.header_len = fin.header_len;
+    wi.trailer_off = fin.trailer_off;
+    wi.trailer_len = fin.trailer_len;
+    // (the FileInfo moves into the batch: its call cuts and error text are not copied)
     if (at < 0) {
         at = (int)b->infos.size();
-        b->finfo.push_back(fi);
+        b->finfo.push_back(std::move(fin));
         b->infos.push_back(wi);
         b->pcm_off.push_back(-1);
     } else {
-        b->finfo[(size_t)at] = fi;
+        b->finfo[(size_t)at] = std::move(fin);
         b->infos[(size_t)at] = wi;
     }
+    const FileInfo &fi = b->finfo[(size_t)at];
     if (info) *info = wi;
     if (!fi.open_ok) return WVG_ERR_OPEN;
     // the file's WavpackFormatSamples image: frames x reduced channels x bytes per sample, 16-B aligned
@@ -591,6 +593,7 @@ static int add_file(wvg_batch *b, const uint8_t *file, size_t len, uint32_t open
     }
     if (len) memcpy(b->blob.data() + base, file, len);
     FileInfo fi;
+    b->fo.chain_tables_only = true;  // (the device builds every unchained mode-1 block's tables)
     frame_file(b->blob.data() + base, len, base, (uint64_t)b->out_ints, open_flags, b->chunk, b->fo, fi, seek_to);
     return commit_file(b, fi, len, info);
 }
@@ -643,7 +646,10 @@ static void frame_threaded(wvg_batch *b, const std::vector<size_t> &base, const 
     if (threads > n) threads = n > 0 ? n : 1;
     fos.assign((size_t)n, FramingOutput());
     fis.assign((size_t)n, FileInfo());
-    for (auto &f : fos) f.defer_values = b->fo.defer_values;
+    for (auto &f : fos) {
+        f.defer_values = b->fo.defer_values;
+        f.chain_tables_only = true;  // (the device builds every unchained mode-1 block's tables)
+    }
     std::atomic<int> next(0);
     auto work = [&]() {
         for (int i; (i = next.fetch_add(1)) < n;)
@@ -659,6 +665,8 @@ static void frame_threaded(wvg_batch *b, const std::vector<size_t> &base, const 
 // The files' bytes into the page-locked blob on host threads, in pieces of up to 4 MiB
 // (one thread copies a 53 MB file at ~15 GB/s: 3.4 ms of a C2 request's host time, and a
 // 12,500-file C5 slice's 540 MB took ~50 of its ~70 ms of framing)
+static double now_ms();
+
 static void parallel_copy(uint8_t *blob, const uint8_t *const *files, const size_t *lens,
                           const std::vector<size_t> &base, int n, int threads) {
     constexpr size_t kPiece = (size_t)4 << 20;
@@ -739,13 +747,18 @@ int wvg_batch_add_files(wvg_batch *b, int n, const uint8_t *const *files, const 
         b->ctx->err = "out of host memory";
         return WVG_ERR_ARG;
     }
+    static const bool trace = getenv("WVG_ADD_TRACE") && getenv("WVG_ADD_TRACE")[0] == '1';
+    const double t0 = trace ? now_ms() : 0.0;
     parallel_copy(b->blob.data(), files, lens, base, n, threads);
+    const double t1 = trace ? now_ms() : 0.0;
     HIPCHK(b->ctx, hipSetDevice(b->ctx->device));
     HIPCHK(b->ctx, blob_push(b));  // the DMA runs while the host threads frame the files
     std::vector<size_t> ln(lens, lens + n);
     std::vector<FramingOutput> fos;
     std::vector<FileInfo> fis;
+    const double t2 = trace ? now_ms() : 0.0;
     frame_threaded(b, base, ln, open_flags, threads, fos, fis);
+    const double t3 = trace ? now_ms() : 0.0;
     {   // (the merge appends every file's records: one allocation each, not a doubling series)
         size_t nd = b->fo.descs.size(), ni = b->fo.items.size(), nj = b->fo.jobs.size(), nz = b->fo.zeros.size();
         for (const FramingOutput &f : fos) {
@@ -758,11 +771,18 @@ int wvg_batch_add_files(wvg_batch *b, int n, const uint8_t *const *files, const 
         b->fo.items.reserve(ni);
         b->fo.jobs.reserve(nj);
         b->fo.zeros.reserve(nz);
+        const size_t nf = b->finfo.size() + (size_t)n;
+        b->finfo.reserve(nf);
+        b->infos.reserve(nf);
+        b->pcm_off.reserve(nf);
     }
     for (int i = 0; i < n; i++) {
         const int idx = merge_framed(b, fos[(size_t)i], fis[(size_t)i], lens[i], infos ? &infos[i] : nullptr, -1);
         if (indices) indices[i] = idx;
     }
+    if (trace)
+        fprintf(stderr, "wvg add_files: %d files, copy %.2f ms, push %.2f, frame %.2f, merge %.2f\n", n, t1 - t0,
+                t2 - t1, t3 - t2, now_ms() - t3);
     return n;
 }
 
@@ -782,6 +802,7 @@ int wvg_batch_add_file_wvc(wvg_batch *b, const uint8_t *file, size_t len, const 
     if (len) memcpy(b->blob.data() + base, file, len);
     if (wvc_len) memcpy(b->blob.data() + cbase, wvc, wvc_len);
     FileInfo fi;
+    b->fo.chain_tables_only = true;
     frame_file(b->blob.data() + base, len, base, (uint64_t)b->out_ints, open_flags, b->chunk, b->fo, fi, -1,
                wvc_len ? b->blob.data() + cbase : nullptr, wvc_len, cbase);
     return commit_file(b, fi, len + wvc_len, info);

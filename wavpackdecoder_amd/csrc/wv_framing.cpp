@@ -1209,6 +1209,7 @@ void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t ou
     info = FileInfo();
     info.first_desc = (int64_t)out.descs.size();
     info.blob_base = blob_base;
+    const size_t tables0 = out.tables.size();
     try {
         std::string err;
         if (!open_input(F, open_flags, err)) {
@@ -1410,6 +1411,25 @@ void frame_file(const uint8_t *file, size_t len, uint64_t blob_base, uint64_t ou
     info.num_desc = (int64_t)out.descs.size() - info.first_desc;
     (void)cur;
     chain_blocks(out, info.first_desc, info.num_desc);
+    if (out.chain_tables_only && out.tables.size() > tables0) {
+        // this file's mode-1 table areas, compacted to the chained blocks' (same layout
+        // and 16-B alignment as snapshot's); the others' offsets are never read
+        size_t w = tables0;
+        for (int64_t k = info.first_desc; k < info.first_desc + info.num_desc; k++) {
+            BlockDesc &d = out.descs[(size_t)k];
+            if (d.kind != KIND_DSD_FAST || d.dsd_table_off < tables0) continue;
+            if (d.chain_len >= 2 || (d.inherit & INH_MEMBER)) {
+                const size_t bins = (size_t)d.dsd_history_bins, n = bins * 2052 + 16;
+                w = (w + 15) & ~(size_t)15;
+                memmove(out.tables.data() + w, out.tables.data() + d.dsd_table_off, n);
+                d.dsd_table_off = w;
+                w += n;
+            } else {
+                d.dsd_table_off = 0;
+            }
+        }
+        out.tables.resize(w);
+    }
     for (int64_t k = info.first_desc; k < info.first_desc + info.num_desc; k++) {
         BlockDesc &d = out.descs[(size_t)k];
         if (d.wvc_len && (d.kind != KIND_PCM || d.chain_len || (d.inherit & INH_MEMBER))) {

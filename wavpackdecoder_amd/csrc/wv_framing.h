@@ -57,6 +57,11 @@ struct FramingOutput {
     // to meta_apply (wv_meta.h) -- the device parse kernel, or apply_meta_jobs on
     // the host; until then those descriptor fields hold the older stream values
     bool defer_values = false;
+    // chain_tables_only: keep the DSD mode-1 tables only for blocks in a decode chain
+    // (the device's decode_dsd_chain reads them; every other mode-1 block has its tables
+    // built on the device, dsd_fast_tables / wv_dsd1_lane), so a batch does not copy and
+    // upload ~2 KB per history bin of every mode-1 block
+    bool chain_tables_only = false;
     std::vector<MetaItem> items;  // offsets into the batch blob
     std::vector<MetaJob> jobs;
 };
