@@ -644,7 +644,7 @@ def run_rank(args) -> None:
     # the same request stream served by one host thread per batch copy, so one
     # batch's framing, upload, decode and download overlap the others' (ctypes
     # drops the GIL inside the library; each batch has its own stream)
-    e2e_pipe = e2e_pcm = e2e_pcm2 = None
+    e2e_pipe = e2e_pcm = e2e_pcm2 = pipe_ok = None
     if len(batches) > 1:
         import threading
         rounds = 4
@@ -732,8 +732,14 @@ def run_rank(args) -> None:
         if N >= 2:
             pool = batches[:N]
             serve_pc(pool, N, min(args.pipe_producers, N), args.pipe_consumers)  # (landing buffers: untimed)
+            for x in pool:  # the page-locked PCM every timed request lands in, poisoned
+                x.host_pcm()[:] = 0x7F
             reqs = 4 * N
             e2e_pcm2 = frames_rank * reqs / serve_pc(pool, reqs, min(args.pipe_producers, N), args.pipe_consumers) / 1e6
+            if pcm is not None:  # each batch's last request: WavpackFormatSamples' 16-bit image of the generator's PCM
+                want = np.ascontiguousarray(pcm.reshape(-1).astype("<i2")).view(np.uint8)
+                pipe_ok = all(np.array_equal(x.host_pcm(), want) for x in pool)
+                assert pipe_ok, "a pipelined request's PCM differs from the generator's"
 
     if kernel_ms <= 0:  # (timing off: the launch time of one batch alone stands in)
         kernel_ms = solo_ms if solo_ms > 0 else b.time(3)
@@ -810,6 +816,7 @@ def run_rank(args) -> None:
                                                  "decode and format requests without waiting, pipe_consumers threads "
                                                  "download the queued PCM in order and free the batches (4 x "
                                                  "pipe_pool requests timed)",
+                               "pipelined_pcm_2buf_verified": pipe_ok,
                                "pipe_producers": args.pipe_producers, "pipe_consumers": args.pipe_consumers,
                                "pipe_pool": args.pipe_pool,
                                "link_bound_Msamples_s": "~14,200 (90.3 MB of PCM16 down at the box's 56.7 GB/s D2H, "
