@@ -234,13 +234,13 @@ def c5_end_to_end(sets, slices) -> dict:
     T = len(bats)
     spare = sets[1] if len(sets) > 1 else [None] * T
 
-    def serve(i):
+    def serve(i, dev=False):
         mine = list(range(i, len(slices), T))
         pair = (bats[i], spare[i]) if spare[i] is not None else (bats[i],)
 
         def start(b, j):
             b.reset()
-            b.add_files(slices[j])
+            (b.add_files_device if dev else b.add_files)(slices[j])
             b.upload()
             b.decode()
         start(pair[0], mine[0])
@@ -252,18 +252,23 @@ def c5_end_to_end(sets, slices) -> dict:
             cur.download_pcm(pinned=True)
             if k + 1 < len(mine) and len(pair) == 1:
                 start(pair[0], mine[k + 1])
-    th = [threading.Thread(target=serve, args=(i,)) for i in range(T)]
-    t0 = time.perf_counter()
-    for t in th:
-        t.start()
-    for t in th:
-        t.join()
-    t_pipe = time.perf_counter() - t0
+    def pipelined(dev):
+        th = [threading.Thread(target=serve, args=(i, dev)) for i in range(T)]
+        t0 = time.perf_counter()
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        return time.perf_counter() - t0
+    t_pipe = pipelined(False)
+    t_pipe_dev = pipelined(True)  # the header / sub-block walk in kernels (wvg_batch_add_files_device)
     return {"frames": int(frames), "compressed_bytes": int(in_bytes), "pcm_bytes": int(pcm_bytes),
             "serial": {"Msamples_s": round(frames / t_serial / 1e6, 1), "ms": round(t_serial * 1e3, 2),
                        "phase_ms": {k: round(v * 1e3, 2) for k, v in ph.items()}},
             "pipelined": {"Msamples_s": round(frames / t_pipe / 1e6, 1), "ms": round(t_pipe * 1e3, 2),
                           "threads": T, "batches_per_thread": 2 if len(sets) > 1 else 1},
+            "pipelined_device_framing": {"Msamples_s": round(frames / t_pipe_dev / 1e6, 1),
+                                         "ms": round(t_pipe_dev * 1e3, 2)},
             "what": "warm batches: host framing (wvg_batch_add_files) + upload + decode + device "
                     "WavpackFormatSamples + PCM download into page-locked memory, every slice once"}
 

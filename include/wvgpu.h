@@ -157,6 +157,9 @@ int wvg_batch_add_files_device(wvg_batch *b, int n, const uint8_t *const *files,
                                int32_t *indices);
 /* A file's info (after the upload for device-framed files); WVG_ERR_OPEN if it did not open. */
 int wvg_batch_file_info(const wvg_batch *b, int file, wvg_file_info *info);
+/* Files [first, first + n) at once (one call for a whole device-framed slice); returns how
+ * many were copied (fewer when the batch has fewer files). */
+int wvg_batch_file_infos(const wvg_batch *b, int first, int n, wvg_file_info *infos);
 /* Files of the batch framed on the device / by the host fallback at its uploads. */
 int wvg_batch_framing_stats(const wvg_batch *b, int64_t *device_files, int64_t *host_files);
 /* Diagnostics: which launch groups the last wvg_batch_decode ran on the lane / row

@@ -90,6 +90,7 @@ def lib():
         "wvg_batch_add_file_wvc": (i32, [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, u32,
                                          ctypes.POINTER(WvgFileInfo)]),
         "wvg_batch_file_info": (i32, [vp, i32, ctypes.POINTER(WvgFileInfo)]),
+        "wvg_batch_file_infos": (i32, [vp, i32, i32, vp]),
         "wvg_batch_framing_stats": (i32, [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
         "wvg_batch_lane_groups": (i32, [vp, ctypes.POINTER(ctypes.c_uint32)]),
         "wvg_batch_upload": (i32, [vp]),
@@ -147,7 +148,8 @@ def lib():
 
 
 EXPORTED = ("wvg_open", "wvg_close", "wvg_last_error", "wvg_batch_new", "wvg_batch_free", "wvg_batch_add_file",
-            "wvg_batch_add_file_at", "wvg_batch_add_files", "wvg_batch_add_files_device", "wvg_batch_file_info", "wvg_batch_add_file_wvc",
+            "wvg_batch_add_file_at", "wvg_batch_add_files", "wvg_batch_add_files_device", "wvg_batch_file_info", "wvg_batch_file_infos",
+            "wvg_batch_add_file_wvc",
             "wvg_batch_framing_stats", "wvg_batch_lane_groups",
             "wvg_batch_upload", "wvg_batch_reset", "wvg_batch_decode", "wvg_batch_sync", "wvg_batch_stream", "wvg_batch_poison", "wvg_batch_set_timing", "wvg_batch_set_kernel",
             "wvg_batch_timed", "wvg_batch_group_times", "wvg_batch_out_ints", "wvg_batch_device_out",

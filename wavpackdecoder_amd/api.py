@@ -178,8 +178,14 @@ class DecodeBatch:
 
     def upload(self):
         self._check(self._L.wvg_batch_upload(self._b))
-        for i in self._dev_infos:  # device-framed files get their infos here
-            self._L.wvg_batch_file_info(self._b, i, ctypes.byref(self.infos[i]))
+        if self._dev_infos:  # device-framed files get their infos here (one call for the lot)
+            lo, hi = min(self._dev_infos), max(self._dev_infos) + 1
+            arr = (_L.WvgFileInfo * (hi - lo))()
+            got = self._L.wvg_batch_file_infos(self._b, lo, hi - lo, ctypes.cast(arr, ctypes.c_void_p))
+            for i in self._dev_infos:
+                if i - lo < got:
+                    self.infos[i] = arr[i - lo]
+            self._dev_infos = []
         self._uploaded = True
 
     def decode(self, stream=None):

@@ -833,17 +833,22 @@ int wvg_batch_add_files_device(wvg_batch *b, int n, const uint8_t *const *files,
         return WVG_ERR_ARG;
     }
     HIPCHK(b->ctx, hipSetDevice(b->ctx->device));
+    // the bytes on host threads (parallel_copy), then one DMA of them: a 12,500-file C5 slice's
+    // 540 MB took 36 ms on this thread, piece by piece behind the pushes
+    parallel_copy(b->blob.data(), files, lens, base, n, 0);
+    HIPCHK(b->ctx, blob_push(b));
+    FileInfo fi0;
+    fi0.error = "not framed yet (wvg_batch_upload frames it)";
+    wvg_file_info wi;
+    fill_info(fi0, wi);
+    const size_t nf = b->finfo.size() + (size_t)n;
+    b->finfo.reserve(nf);
+    b->infos.reserve(nf);
+    b->pcm_off.reserve(nf);
+    b->dfiles.reserve(b->dfiles.size() + (size_t)n);
     for (int i = 0; i < n; i++) {
-        if (lens[i]) memcpy(b->blob.data() + base[(size_t)i], files[i], lens[i]);
-        // send every few MiB: the DMA of the first files overlaps the copying of the rest
-        if (base[(size_t)i] + lens[i] >= b->blob_dev + ((size_t)8 << 20))
-            HIPCHK(b->ctx, blob_push(b, base[(size_t)i] + lens[i]));
         const int idx = (int)b->infos.size();
-        FileInfo fi;
-        fi.error = "not framed yet (wvg_batch_upload frames it)";
-        wvg_file_info wi;
-        fill_info(fi, wi);
-        b->finfo.push_back(fi);
+        b->finfo.push_back(fi0);
         b->infos.push_back(wi);
         b->pcm_off.push_back(-1);
         b->dfiles.push_back({base[(size_t)i], lens[i], idx});
@@ -1022,6 +1027,14 @@ int wvg_batch_file_info(const wvg_batch *b, int file, wvg_file_info *info) {
     if (!b || !info || file < 0 || file >= (int)b->infos.size()) return WVG_ERR_ARG;
     *info = b->infos[(size_t)file];
     return b->finfo[(size_t)file].open_ok ? WVG_OK : WVG_ERR_OPEN;
+}
+
+int wvg_batch_file_infos(const wvg_batch *b, int first, int n, wvg_file_info *infos) {
+    if (!b || !infos || first < 0 || n < 0) return WVG_ERR_ARG;
+    const int have = (int)b->infos.size();
+    const int m = first >= have ? 0 : (n < have - first ? n : have - first);
+    if (m > 0) memcpy(infos, b->infos.data() + first, sizeof(wvg_file_info) * (size_t)m);
+    return m;
 }
 
 int wvg_batch_lane_groups(const wvg_batch *b, uint32_t *mask) {
