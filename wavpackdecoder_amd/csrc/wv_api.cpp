@@ -2129,7 +2129,13 @@ int64_t wvg_stream_unpack(wvg_stream *s, int32_t *buffer, int64_t samples) {
     }
     if (s->pos >= s->limit) return s->throws ? WVG_ERR_EXCEPTION : 0;
     int64_t n = std::min(samples, s->limit - s->pos);
-    // a call the reference ends early (its loop breaks on a header / unpack_init failure)
+    // a call the reference ends early (its loop breaks on a header / unpack_init failure).
+    // The cuts are output positions: a break falls where a block's header or unpack_init
+    // fails, whatever the request size, so they hold after the caller changes its size too
+    // (schedule_changed); the file-end cut is the limit itself.  What a size change can
+    // move is a break landing exactly on a call boundary, which returns 0 frames (the end
+    // of a WvDemo-style loop) under one schedule and a short call under another -- such a
+    // stream is served from its first schedule, and wvg_stream_state reports it.
     const std::vector<int64_t> &cuts = s->b->finfo[0].call_cuts;
     auto cut = std::upper_bound(cuts.begin(), cuts.end(), s->pos);
     if (cut != cuts.end() && *cut - s->pos < n) n = *cut - s->pos;
