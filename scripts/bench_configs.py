@@ -55,6 +55,8 @@ def run(name, files, pcm=None, iters=5, fmt=False):
         group_ms = {g: round(float(np.median([t[g] for t in gts])), 3) for g in gts[0]}
     out = b.download()
     crc = sum(b.result(i).crc_errors for i in range(len(files)) if b.infos[i].open_ok)
+    from wavpackdecoder_amd import _lib as _LL
+    redone = int(np.count_nonzero(b.block_status() & _LL.WVG_ST_REDONE))
     ok = None
     if pcm is not None:
         ok = bool(np.array_equal(out, pcm.reshape(-1)))
@@ -67,7 +69,7 @@ def run(name, files, pcm=None, iters=5, fmt=False):
         fmt_ms = (time.perf_counter() - t) / iters * 1e3
     line = {"config": name, "files": len(files), "blocks": b.num_blocks, "frames": b.frames,
             "compressed_bytes": b.bytes_in, "kernel_ms": round(ms, 3),
-            "Mframes_per_s": round(b.frames / ms / 1e3, 1), "crc_errors": int(crc),
+            "Mframes_per_s": round(b.frames / ms / 1e3, 1), "crc_errors": int(crc), "redone_blocks": redone,
             "lossless_roundtrip": ok, "host_framing_s": round(t_frame, 3), "group_end_ms": group_ms}
     if INFLIGHT > 1:
         # the same batch as INFLIGHT copies on their own streams, decodes issued

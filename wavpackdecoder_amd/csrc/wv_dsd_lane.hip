@@ -408,6 +408,8 @@ __device__ __forceinline__ void dsd3_pairs(const BlockDesc *__restrict__ descs, 
     int32_t crc = -1;
     for (uint32_t t = 0; t < nmax; t++) {
         const bool live = t < nfr;
+        // (a refill every 2 bit pairs: every 4 after the first 64 frames handed 832 of 1,024
+        // blocks back dry, profiles/r06_sched_ab.txt)
 #pragma unroll
         for (int bit = 0; bit < 8; bit++) {
             if ((bit & 1) == 0 && bit != 0) {
