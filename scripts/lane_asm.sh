@@ -4,7 +4,7 @@
 set -e
 OUT=${1:-/tmp/wv_lane_fast.s}
 /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -mllvm -structurizecfg-skip-uniform-regions=true -mllvm -amdgpu-sched-strategy=max-ilp \
-  -DWV_LANE_ONLY_FAST --cuda-device-only -S -o "$OUT" "$(dirname "$0")/../wavpackdecoder_amd/csrc/wv_lane.hip"
+  -DWV_LANE_ONLY_FAST $LANE_DEFS --cuda-device-only -S -o "$OUT" "$(dirname "$0")/../wavpackdecoder_amd/csrc/wv_lane.hip"
 python3 - "$OUT" <<'PY'
 import re, sys
 lines = open(sys.argv[1]).read().split("\n")

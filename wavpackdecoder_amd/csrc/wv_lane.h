@@ -380,6 +380,7 @@ struct LState {
     uint32_t pmax;   // 17: a bits error or a count too long for the lane (else smaller)
     uint32_t rare;   // fast words: nonzero when a word needed the checked path (escape, run length)
     uint32_t rmax;   // no-run words: the largest raw unary count (16: an escape -> the checked path)
+    uint32_t r0;     // plain no-run words (WV_LANE_SPEC): the next word's raw unary count
     int32_t slack;   // least window bits left after a word (< 0: a word past the window)
     uint32_t bad;
     uint32_t bad0;   // (diagnostics) the reasons of the first group that set any: status bits 24-31
@@ -930,12 +931,28 @@ __device__ __forceinline__ void lmerge(LState &s, const uint8_t *ring) {
 // past it shows as slack < 0, and the group is replayed by the checked words)
 // W32: 32-bit products (C#'s int wrap) for groups whose medians pass the 24-bit
 // operands (pgroup_try: below 2^29 at the group's start, so none wraps in the group)
+// SPEC (the plain no-run word): the next word's unary count is taken before this
+// word's refill.  E = the window with the read-ahead dword placed at nb (its low 64
+// bits; nb >= 33 at a word start, so only E's high half changes) holds stream bits
+// [0, 64) exactly, and the next word's unary bits [tot, tot + 17) lie in it whether
+// the refill merges or not (tot <= 47); so s.r0 = ctz over E >> tot, and the
+// refill (compare, mask, 64-bit shift, or) leaves the word-to-word chain.
+#ifndef WV_LANE_SPEC
+#define WV_LANE_SPEC 0
+#endif
 template <int C, bool SPLIT, int HY = false, bool W32 = false>
 __device__ __forceinline__ LW lword_nz(LState &s, const uint8_t *ring, uint32_t rbase) {
     static_assert(!HY || SPLIT, "a hybrid word's bisection bits follow a refill");
     using namespace wvf;
+    constexpr bool SPEC = WV_LANE_SPEC && !SPLIT && !HY && !W32;
     const uint32_t lo = (uint32_t)s.win, hi = (uint32_t)(s.win >> 32);
-    const uint32_t raw0 = (uint32_t)__builtin_ctz(~lo | 0x10000u);  // unary ones, capped at 16
+    // unary ones, capped at 16
+    const uint32_t raw0 = SPEC ? s.r0 : (uint32_t)__builtin_ctz(~lo | 0x10000u);
+    uint32_t ehi = 0u;
+    if constexpr (SPEC) {
+        const uint32_t sft = (uint32_t)(s.nb - 32) & 63u;  // 1..32 at a word start
+        ehi = hi | (uint32_t)((uint64_t)s.nxt << sft);
+    }
     s.rmax = max(s.rmax, raw0);
     const uint32_t raw = raw0 & s.keep;          // a held zero: no unary count (ones 0, holding_one clear)
     const uint32_t ones = (raw >> 1) + s.h1;
@@ -998,6 +1015,7 @@ __device__ __forceinline__ LW lword_nz(LState &s, const uint8_t *ring, uint32_t 
     const int32_t sg = __builtin_amdgcn_sbfe((int32_t)x, used, 1);  // 0 or -1
     const uint32_t tot = SPLIT ? used + 1u : add3(q, used, 1u);
     __builtin_assume(tot < 64u);
+    if constexpr (SPEC) s.r0 = (uint32_t)__builtin_ctz(~(uint32_t)((((uint64_t)ehi << 32) | lo) >> tot) | 0x10000u);
     s.win >>= tot;
     s.nb -= (int32_t)tot;
     s.slack = min(s.slack, s.nb);
@@ -1175,6 +1193,7 @@ __device__ __forceinline__ void pgroup_try(LState &s, const uint8_t *ring, uint3
             lmerge(s, ring);
             LCNT(cnt.split++);
         } else if (!HY && lmask(mml >= (1u << 17)) == 0ull) {
+            if constexpr (WV_LANE_SPEC) s.r0 = (uint32_t)__builtin_ctz(~(uint32_t)s.win | 0x10000u);
             pgroup<FULL, WK_NORUN, MONO, HY, CODES>(s, ring, rb, sh, lane, g0, nfr, u0, pfin);
             LCNT(cnt.norun++);
         } else {
