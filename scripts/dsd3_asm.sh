@@ -3,7 +3,7 @@
 # usage: bash scripts/dsd3_asm.sh [out.s]
 set -e
 OUT=${1:-/tmp/wv_dsd_lane.s}
-/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -mllvm -amdgpu-sched-strategy=max-ilp \
+/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -mllvm -amdgpu-sched-strategy=${SCHED:-iterative-ilp} \
   --cuda-device-only -S -o "$OUT" "$(dirname "$0")/../wavpackdecoder_amd/csrc/wv_dsd_lane.hip"
 python3 - "$OUT" <<'PY'
 import re, sys

@@ -381,6 +381,10 @@ __device__ __forceinline__ void dsd3_pairs(const BlockDesc *__restrict__ descs, 
     const int32_t chm = -(int32_t)ch;
     {   // the block's starting row (init_ptable for its rate_i), half of it by each lane of the pair
         const int32_t *row = ptables + (uint32_t)(ok ? (d.dsd_rate_i & 255) : 0) * 256u;
+        // (fully unrolled: 128 loads in flight, 512 registers and a few spills here, once per
+        // block; unrolled by 8 the kernel takes 129 VGPRs and no scratch, but its frame loop
+        // is scheduled differently and measured 35.1 against 34.3 ms per batch, also with
+        // the allocation pinned to one wave per SIMD -- profiles/r06_dsd3_regs_ab.txt)
         for (uint32_t e = ch; e < 256u; e += 2u) *(int32_t *)(ptb + (e << 8) + col) = row[e];
     }
     __syncthreads();
