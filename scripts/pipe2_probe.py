@@ -79,7 +79,7 @@ def serve_async(bb, files, rounds, rec, dev):
         bb[k % D].sync()
 
 
-def serve_pc(pool, files, total, producers, consumers):
+def serve_pc(pool, files, total, producers, consumers, add_threads=0):
     """Producer/consumer server: `producers` threads take a free batch, frame, upload, decode
     and format a request on it (no call waits for the device) and queue it; `consumers`
     threads take the queued batches in order and download their PCM (page-locked, blocking),
@@ -99,7 +99,7 @@ def serve_pc(pool, files, total, producers, consumers):
                 left[0] -= 1
             x = free.get()
             x.reset()
-            x.add_files(files)
+            x.add_files(files, threads=add_threads)
             x.upload()
             x.decode()
             x.format()
@@ -160,14 +160,15 @@ def main():
         serve_ring(batches[i:i + 2], files, 2, [], a.device_framing)
         frames = batches[i].frames
     for cfg in [x for x in a.pc.split(",") if x]:
-        P, C, N = (int(v) for v in cfg.split(":"))
+        P, C, N, *T = (int(v) for v in cfg.split(":"))  # (P:C:pool[:add_files threads, 0: the library's])
         while len(batches) < N:
             b = DecodeBatch(4096)
             b.set_kernel(a.kernel)
             serve_ring([b], files, 1, [], a.device_framing)
             batches.append(b)
-        dt, nreq = serve_pc(batches[:N], files, a.rounds * N, P, C)
-        print(json.dumps({"producers": P, "consumers": C, "pool": N, "kernel": a.kernel, "requests": nreq,
+        dt, nreq = serve_pc(batches[:N], files, a.rounds * N, P, C, T[0] if T else 0)
+        print(json.dumps({"producers": P, "consumers": C, "pool": N, "add_threads": T[0] if T else 0,
+                          "kernel": a.kernel, "requests": nreq,
                           "Msamples_per_s": round(frames * nreq / dt / 1e6, 1),
                           "ms_per_request": round(dt * 1e3 / nreq, 3)}), flush=True)
     if a.pc:
