@@ -873,7 +873,7 @@ def main():
     ap.add_argument("--pipe-producers", type=int, default=6,
                     help="pcie_inclusive.pipelined_pcm_2buf: producer threads of the decode server")
     ap.add_argument("--pipe-consumers", type=int, default=2, help="its PCM download threads")
-    ap.add_argument("--pipe-pool", type=int, default=16, help="its batches (at most --inflight)")
+    ap.add_argument("--pipe-pool", type=int, default=20, help="its batches (at most --inflight)")
     ap.add_argument("--cpu-threads", type=int, default=None, help="override the socket/lease-derived thread count")
     ap.add_argument("--cpu-reps", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
