@@ -618,6 +618,13 @@ def run_rank(args) -> None:
         if pg is not None:
             pg.destroy_process_group()
         return
+    if rank != 0:  # (the PCIe-inclusive legs below are rank 0's report: no collective follows, and the
+        # other ranks' framing threads and page-locked buffers would only contend with rank 0's host)
+        for bb in batches:
+            bb.close()
+        if pg is not None:
+            pg.destroy_process_group()
+        return
     # a decode server's request on a warm batch: reset, frame the files on the host,
     # upload (page-locked), decode, download into page-locked memory; median of 3
     be = batches[-1]
@@ -825,7 +832,9 @@ def run_rank(args) -> None:
                                "pipe_producers": args.pipe_producers, "pipe_consumers": args.pipe_consumers,
                                "pipe_pool": args.pipe_pool,
                                "link_bound_Msamples_s": "~14,200 (90.3 MB of PCM16 down at the box's 56.7 GB/s D2H, "
-                                                        "scripts/micro/pcie_kernel.hip)"},
+                                                        "scripts/micro/pcie_kernel.hip); ~12,000 with each "
+                                                        "request's 52.9 MB upload sharing the link (~97 GB/s "
+                                                        "both ways)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": None if traffic is None else int(traffic),
